@@ -1,0 +1,417 @@
+"""MATLAB-named host mirror of the reference hot path over the C ABI.
+
+Each function keeps the reference's name, argument meaning, defaults and
+error behaviour (file:line cited per function) and calls the HIP library; a
+sparse ``A`` is uploaded once and kept resident in HBM for every later call
+with the same matrix object (the "two tiers" boundary of SURVEY §8b).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import weakref
+from dataclasses import dataclass, field
+
+import numpy as np
+import scipy.sparse as sp
+
+from . import _lib
+from ._lib import CalError, check, dp, f64, iptr, lib, ptr
+from .matrices import to_csr
+
+
+class Context:
+    """A device context (``cal_ctx``): one HIP stream, the resident matrix and
+    the device-resident CA-Lanczos state."""
+
+    def __init__(self, device: int | None = None):
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        h = ctypes.c_void_p()
+        st = lib.cal_create(device, ctypes.byref(h))
+        if st != 0:
+            raise CalError(st, "cal_create(device=%d) failed: no usable HIP device" % device)
+        self.h = h
+        self.device = device
+        self.n = None
+        self._keep = []
+
+    def close(self):
+        if self.h:
+            lib.cal_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- matrix ---------------------------------------------------------------
+    def set_matrix(self, A):
+        A = to_csr(A)
+        if A.shape[0] != A.shape[1]:
+            raise ValueError("A must be square")
+        rowptr = np.ascontiguousarray(A.indptr, dtype=np.int64)
+        col = np.ascontiguousarray(A.indices, dtype=np.int32)
+        val = np.ascontiguousarray(A.data, dtype=np.float64)
+        check(self.h, lib.cal_set_matrix_csr(self.h, A.shape[0], rowptr.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                             col.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ptr(val)),
+              "set_matrix")
+        self.n = A.shape[0]
+        return self
+
+    def set_matrix_slab(self, n_global, row0, A_rows):
+        """Distributed: rows [row0, row0+nlocal) of A (global column ids)."""
+        A_rows = sp.csr_matrix(A_rows)
+        A_rows.sort_indices()
+        rowptr = np.ascontiguousarray(A_rows.indptr, dtype=np.int64)
+        col = np.ascontiguousarray(A_rows.indices, dtype=np.int64)
+        val = np.ascontiguousarray(A_rows.data, dtype=np.float64)
+        check(self.h, lib.cal_set_matrix_csr_dist(
+            self.h, n_global, row0, A_rows.shape[0], rowptr.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+            col.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), ptr(val)), "set_matrix_slab")
+        self.n = A_rows.shape[0]
+        return self
+
+    def matrix_info(self):
+        v = [ctypes.c_int64() for _ in range(4)]
+        check(self.h, lib.cal_matrix_info(self.h, *[ctypes.byref(x) for x in v]))
+        return dict(n_local=v[0].value, nnz_local=v[1].value, n_global=v[2].value, nghost=v[3].value)
+
+    # -- timers ---------------------------------------------------------------
+    def timer_enable(self, on=True):
+        check(self.h, lib.cal_timer_enable(self.h, 1 if on else 0))
+
+    def timer_reset(self):
+        check(self.h, lib.cal_timer_reset(self.h))
+
+    def timer_read(self, kind="spmv"):
+        cnt = ctypes.c_int64()
+        tot = ctypes.c_double()
+        check(self.h, lib.cal_timer_read(self.h, kind.encode(), ctypes.byref(cnt), ctypes.byref(tot)))
+        return cnt.value, tot.value
+
+    def synchronize(self):
+        check(self.h, lib.cal_synchronize(self.h))
+
+    # -- communicators ----------------------------------------------------------
+    def comm_init_rccl(self, nranks, rank, uid: bytes):
+        buf = ctypes.create_string_buffer(uid, 128)
+        check(self.h, lib.cal_comm_init_rccl(self.h, nranks, rank, buf), "comm_init_rccl")
+
+    def comm_init_host(self, nranks, rank, allreduce, exchange):
+        """allreduce(np.ndarray) sums in place; exchange(peer, send, recv) fills recv."""
+        def _ar(user, buf, count):
+            try:
+                a = np.ctypeslib.as_array(buf, shape=(count,))
+                allreduce(a)
+                return 0
+            except Exception:  # pragma: no cover - reported as CAL_ERR_COMM
+                return -1
+
+        def _ex(user, peer, send, ns, recv, nr):
+            try:
+                s = np.ctypeslib.as_array(send, shape=(ns,)) if ns > 0 else np.zeros(0)
+                r = np.ctypeslib.as_array(recv, shape=(nr,)) if nr > 0 else np.zeros(0)
+                exchange(peer, s, r)
+                return 0
+            except Exception:  # pragma: no cover
+                return -1
+
+        cb = (_lib.ALLREDUCE_FN(_ar), _lib.EXCHANGE_FN(_ex))
+        self._keep.append(cb)
+        check(self.h, lib.cal_comm_init_host(self.h, nranks, rank, cb[0], cb[1], None), "comm_init_host")
+
+    # -- step-wise CA-Lanczos ---------------------------------------------------
+    def lanczos_begin(self, r, s, max_outer, basis="newton", orth="local"):
+        r = f64(r)
+        check(self.h, lib.cal_lanczos_begin(self.h, ptr(r), s, max_outer, basis.encode(), orth.encode()),
+              "lanczos_begin")
+        self._lz = dict(s=s, max_outer=max_outer)
+
+    def lanczos_step(self, diagnostics=False):
+        return check(self.h, lib.cal_lanczos_step(self.h, 1 if diagnostics else 0), "lanczos_step")
+
+    def lanczos_state(self):
+        k, s, re = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(self.h, lib.cal_lanczos_state(self.h, ctypes.byref(k), ctypes.byref(s), ctypes.byref(re)))
+        return k.value, s.value, re.value
+
+    def lanczos_get(self):
+        k, s, _ = self.lanczos_state()
+        sk = s * k
+        T = np.zeros((sk, sk), order="F")
+        rn = np.zeros((k, sk), order="F")
+        oe = np.zeros(k)
+        fl = np.zeros(k, dtype=np.int32)
+        info = _lib.LanczosInfo()
+        check(self.h, lib.cal_lanczos_get(self.h, ptr(T), max(sk, 1), ptr(rn), ptr(oe), iptr(fl),
+                                          ctypes.byref(info)))
+        return T, rn, oe, fl, info
+
+    def lanczos_get_Q(self, col0, ncols):
+        Q = np.zeros((self.n, ncols), order="F")
+        check(self.h, lib.cal_lanczos_get_Q(self.h, col0, ncols, ptr(Q)))
+        return Q
+
+    def lanczos_end(self):
+        check(self.h, lib.cal_lanczos_end(self.h))
+
+
+# ---------------------------------------------------------------------------
+# context cache: one resident copy per matrix object (MATLAB passes A by value
+# on every call; the device copy is the "persistent state" of SURVEY §8b)
+# ---------------------------------------------------------------------------
+_default_ctx: Context | None = None
+_matrix_ctx: dict = {}
+
+
+def default_context() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context()
+    return _default_ctx
+
+
+def context_for(A) -> Context:
+    key = id(A)
+    hit = _matrix_ctx.get(key)
+    if hit is not None and hit[0]() is A:
+        return hit[1]
+    ctx = Context().set_matrix(A)
+    try:
+        ref = weakref.ref(A)
+    except TypeError:  # pragma: no cover
+        ref = lambda: A  # noqa: E731
+    _matrix_ctx[key] = (ref, ctx)
+    return ctx
+
+
+# ---------------------------------------------------------------------------
+# a1-a4
+# ---------------------------------------------------------------------------
+def SpMV(A, v):
+    """``Av = SpMV(A,v)`` -- SpMV.m:6-8."""
+    ctx = context_for(A)
+    v = f64(v).ravel()
+    out = np.empty_like(v)
+    check(ctx.h, lib.cal_spmv(ctx.h, ptr(v), ptr(out)), "SpMV")
+    return out
+
+
+def matrix_powers_monomial(A, q, s):
+    """``V = matrix_powers_monomial(A,q,s)`` (n x s) -- matrix_powers_monomial.m:6-12."""
+    ctx = context_for(A)
+    q = f64(q).ravel()
+    V = np.zeros((len(q), s), order="F")
+    check(ctx.h, lib.cal_matrix_powers_monomial(ctx.h, ptr(q), s, ptr(V)), "matrix_powers_monomial")
+    return V
+
+
+def matrix_powers_newton(A, v, s, lam, modifiedp=0):
+    """``V = matrix_powers_newton(A,v,s,lambda,modifiedp)`` (n x (s+1)) -- matrix_powers_newton.m:15-54."""
+    ctx = context_for(A)
+    v = f64(v).ravel()
+    lam = np.asarray(lam)
+    lre = f64(np.real(lam)).ravel()
+    lim = f64(np.imag(lam)).ravel() if np.iscomplexobj(lam) else None
+    V = np.zeros((len(v), s + 1), order="F")
+    check(ctx.h, lib.cal_matrix_powers_newton(ctx.h, ptr(v), s, ptr(lre), ptr(lim), int(modifiedp), ptr(V)),
+          "matrix_powers_newton")
+    return V
+
+
+# ---------------------------------------------------------------------------
+# a5-a9
+# ---------------------------------------------------------------------------
+def tsqr(A):
+    """``[Q,R] = tsqr(A)`` -- tsqr.m:7-12 (R upper, diag(R) >= 0)."""
+    ctx = default_context()
+    A = f64(A)
+    n, m = A.shape
+    Q = np.zeros((n, m), order="F")
+    R = np.zeros((m, m), order="F")
+    check(ctx.h, lib.cal_tsqr(ctx.h, n, m, ptr(A), ptr(Q), ptr(R)), "tsqr")
+    return Q, R
+
+
+def cholqr(X):
+    """``[Q,R] = cholqr(X)`` -- cholqr.m:3-8 (one Cholesky-QR pass)."""
+    ctx = default_context()
+    X = f64(X)
+    n, m = X.shape
+    Q = np.zeros((n, m), order="F")
+    R = np.zeros((m, m), order="F")
+    check(ctx.h, lib.cal_cholqr(ctx.h, n, m, ptr(X), ptr(Q), ptr(R)), "cholqr")
+    return Q, R
+
+
+def _blocks(Q):
+    if not isinstance(Q, (list, tuple)):
+        raise TypeError("Input Q (arg 1) to project() must be cell (block) array.")
+    blocks = [f64(b) if (b is not None and np.size(b) > 0) else None for b in Q]
+    widths = np.array([0 if b is None else b.shape[1] for b in blocks], dtype=np.int32)
+    arr = (dp * max(len(blocks), 1))(*[ptr(b) if b is not None else None for b in blocks])
+    return blocks, widths, arr
+
+
+def project(Q, X, doreorth=False):
+    """``[X,R] = project(Q,X,doreorth)`` -- project.m:7-58."""
+    if isinstance(X, (list, tuple)):
+        raise TypeError("Input X (arg 2) project() must be a column matrix.")
+    if len(Q) == 0:
+        return np.array(X, dtype=np.float64), []
+    ctx = default_context()
+    X = f64(X)
+    n, m = X.shape
+    blocks, widths, arr = _blocks(Q)
+    R = [np.zeros((int(w), m), order="F") for w in widths]
+    Rarr = (dp * len(R))(*[ptr(r) for r in R])
+    Xout = np.zeros((n, m), order="F")
+    check(ctx.h, lib.cal_project(ctx.h, n, len(blocks), arr, iptr(widths), m, ptr(X), 1 if doreorth else 0,
+                                 ptr(Xout), Rarr), "project")
+    return Xout, R
+
+
+def normalize(X, opt="None", tol=1.0e-8):
+    """``[Q,R,rank] = normalize(X,opt,tol)`` -- normalize.m:3-36."""
+    if str(opt).lower() == "randomizenullspace":
+        raise NotImplementedError("normalize(...,'randomizeNullSpace') is not on the hot path")
+    ctx = default_context()
+    X = f64(X)
+    n, m = X.shape
+    Q = np.zeros((n, m), order="F")
+    R = np.zeros((m, m), order="F")
+    rank = ctypes.c_int()
+    check(ctx.h, lib.cal_normalize(ctx.h, n, m, ptr(X), tol, ptr(Q), ptr(R), ctypes.byref(rank)), "normalize")
+    return Q, R, rank.value
+
+
+def projectAndNormalize_ex(Q, X, doreorth=True):
+    """projectAndNormalize.m:3-90, also returning (reorth flag, rank)."""
+    ctx = default_context()
+    X = f64(X)
+    n, m = X.shape
+    blocks, widths, arr = _blocks(Q)
+    RZ = [np.zeros((int(w), m), order="F") for w in widths] + [np.zeros((m, m), order="F")]
+    RZarr = (dp * len(RZ))(*[ptr(r) for r in RZ])
+    QZ = np.zeros((n, m), order="F")
+    re, rk = ctypes.c_int(), ctypes.c_int()
+    check(ctx.h, lib.cal_project_and_normalize(ctx.h, n, len(blocks), arr, iptr(widths), m, ptr(X),
+                                               1 if doreorth else 0, ptr(QZ), RZarr, ctypes.byref(re),
+                                               ctypes.byref(rk)), "projectAndNormalize")
+    return QZ, RZ, bool(re.value), rk.value
+
+
+def projectAndNormalize(Q, X, doreorth=True):
+    """``[QZ,RZ] = projectAndNormalize(Q,X,doreorth)`` -- projectAndNormalize.m:3-90."""
+    QZ, RZ, _, _ = projectAndNormalize_ex(Q, X, doreorth)
+    return QZ, RZ
+
+
+# ---------------------------------------------------------------------------
+# a13 host routines
+# ---------------------------------------------------------------------------
+def leja(x, which=None):
+    """``[y,idx] = leja(x,'nonmodified')`` -> real_leja -> modified_leja (leja.m:23-31)."""
+    if which is None:
+        raise NotImplementedError("nonmodified_leja is not on the ca_lanczos path")
+    x = np.asarray(x).ravel()
+    n = len(x)
+    xr = f64(np.real(x))
+    xi = f64(np.imag(x)) if np.iscomplexobj(x) else None
+    yr, yi = np.zeros(n), np.zeros(n)
+    idx = np.zeros(n, dtype=np.int32)
+    st = lib.cal_leja(n, ptr(xr), ptr(xi), ptr(yr), ptr(yi), iptr(idx))
+    if st != 0:
+        raise CalError(st, "leja: modified Leja ordering failed")
+    y = yr + 1j * yi if np.any(yi != 0) else yr
+    return y, idx.astype(np.int64)
+
+
+def newton_basis_matrix(lam, s, modifiedp=0):
+    """``B_ = newton_basis_matrix(lambda,s,modifiedp)`` -- newton_basis_matrix.m:13-60."""
+    lam = np.asarray(lam)
+    lr = f64(np.real(lam)).ravel()
+    li = f64(np.imag(lam)).ravel() if np.iscomplexobj(lam) else None
+    B = np.zeros((s + 1, s), order="F")
+    st = lib.cal_newton_basis_matrix(s, ptr(lr), ptr(li), int(modifiedp), ptr(B))
+    if st != 0:
+        raise CalError(st, "newton_basis_matrix failed")
+    return B
+
+
+def eig(T):
+    """``[V,D] = eig(T)`` as used by ca_lanczos.m:229 -> (w complex/real, V)."""
+    T = f64(T)
+    n = T.shape[0]
+    wr, wi = np.zeros(n), np.zeros(n)
+    V = np.zeros((n, n), order="F")
+    st = lib.cal_eig(n, ptr(T), n, ptr(wr), ptr(wi), ptr(V))
+    if st != 0:
+        raise CalError(st, "eig did not converge")
+    if np.any(wi != 0):
+        Vc = V.astype(complex)
+        j = 0
+        while j < n:
+            if wi[j] > 0:
+                Vc[:, j] = V[:, j] + 1j * V[:, j + 1]
+                Vc[:, j + 1] = V[:, j] - 1j * V[:, j + 1]
+                j += 2
+            else:
+                j += 1
+        return wr + 1j * wi, Vc
+    return wr, V
+
+
+# ---------------------------------------------------------------------------
+# a14: the driver
+# ---------------------------------------------------------------------------
+@dataclass
+class CALanczosOutput:
+    T: np.ndarray
+    Q: np.ndarray | None
+    ritz_rnorm: np.ndarray
+    orth_err: np.ndarray
+    reorth: np.ndarray
+    shifts: np.ndarray
+    info: dict = field(default_factory=dict)
+
+
+def ca_lanczos_ex(A, r, s, iter, basis, orth="local", diagnostics=True, return_Q=True, ctx=None):
+    """ca_lanczos.m:24-86 with the extra outputs (flags, shifts, timings)."""
+    o = orth.lower() if isinstance(orth, str) else str(orth)
+    if o not in ("local", "full", "selective", "periodic"):
+        raise ValueError("ca_lanczos.m: Invalid option value for orth: %s" % orth)
+    ctx = ctx or context_for(A)
+    r = f64(r).ravel()
+    t = int(math.ceil(iter / s))
+    n = len(r)
+    T = np.zeros((s * t, s * t), order="F")
+    Q = np.zeros((n, s * t), order="F") if return_Q else None
+    rn = np.zeros((t, s * t), order="F")
+    oe = np.zeros(t)
+    fl = np.zeros(t, dtype=np.int32)
+    info = _lib.LanczosInfo()
+    st = lib.cal_ca_lanczos(ctx.h, ptr(r), s, iter, basis.encode(), orth.encode(), 1 if diagnostics else 0,
+                            ptr(T), ptr(Q), ptr(rn), ptr(oe), iptr(fl), ctypes.byref(info))
+    check(ctx.h, st, "ca_lanczos")
+    k = info.t
+    sk = s * k
+    shifts = np.array(info.shifts[: 2 * s]) if basis.lower() == "newton" else np.zeros(0)
+    if np.any(np.array(info.shifts_im[: 2 * s]) != 0):
+        shifts = shifts + 1j * np.array(info.shifts_im[: 2 * s])
+    return CALanczosOutput(
+        T=np.array(T[:sk, :sk]), Q=None if Q is None else np.array(Q[:, :sk]),
+        ritz_rnorm=np.array(rn[:k, :sk]), orth_err=oe[:k].copy(), reorth=fl[:k].copy(), shifts=shifts,
+        info=dict(t=k, n_reorth=info.n_reorth, n_rank_deficient=info.n_rank_deficient,
+                  breakdown=info.breakdown, prologue_ms=info.prologue_ms, loop_ms=info.loop_ms,
+                  diag_ms=info.diag_ms, status=st))
+
+
+def ca_lanczos(A, r, s, iter, basis, orth="local"):
+    """``[T,Q,ritz_rnorm,orth_err] = ca_lanczos(A,r,s,iter,basis,orth)`` -- ca_lanczos.m:24-86."""
+    out = ca_lanczos_ex(A, r, s, iter, basis, orth, diagnostics=True, return_Q=True)
+    return out.T, out.Q, out.ritz_rnorm, out.orth_err

@@ -1,0 +1,324 @@
+// api.cpp -- tier-1 (host-pointer) entry points of the C ABI: each call
+// stages its column-major inputs into HBM, runs the device kernels and copies
+// the outputs back (SURVEY §8b "two tiers").  These are what a MEX shim of
+// SpMV.m, matrix_powers_*.m, tsqr.m, cholqr.m, project.m, normalize.m and
+// projectAndNormalize.m binds; the device-resident tier is lanczos.cpp.
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "cal_internal.hpp"
+#include "dense.hpp"
+
+using namespace cal;
+
+namespace {
+
+int64_t ld_for(int64_t n) {
+    int64_t ld = ((n + 63) / 64) * 64;
+    return ld > 0 ? ld : 64;
+}
+
+// upload host column-major (n x m, ld n) into device (ld dld)
+int upload(cal_ctx* c, double* d, int64_t dld, const double* h, int64_t n, int m) {
+    if (m <= 0 || n <= 0) return 0;
+    CAL_HIP(c, hipMemcpy2DAsync(d, dld * sizeof(double), h, n * sizeof(double), n * sizeof(double), m,
+                                hipMemcpyHostToDevice, c->stream));
+    return 0;
+}
+
+int download(cal_ctx* c, double* h, const double* d, int64_t dld, int64_t n, int m) {
+    if (m <= 0 || n <= 0) return 0;
+    CAL_HIP(c, hipMemcpy2DAsync(h, n * sizeof(double), d, dld * sizeof(double), n * sizeof(double), m,
+                                hipMemcpyDeviceToHost, c->stream));
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int check_ctx(cal_ctx* c, bool need_A) {
+    if (!c) return CAL_ERR_ARG;
+    hipSetDevice(c->device);
+    if (need_A && !c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cal_spmv(cal_ctx* c, const double* v, double* Av) {
+    CAL_TRY(check_ctx(c, true));
+    if (!v || !Av) return set_error(c, CAL_ERR_ARG, "SpMV: null vector");
+    const int64_t n = c->A.n_local, ld = c->A.ld;
+    CAL_TRY(ensure_scratch(c, 2 * ld));
+    double* x = c->d_scratch;
+    double* y = c->d_scratch + ld;
+    CAL_TRY(upload(c, x, ld, v, n, 1));
+    CAL_TRY(spmv_dev(c, x, y, 0, 0.0, 0.0, nullptr));
+    return download(c, Av, y, ld, n, 1);
+}
+
+int cal_matrix_powers_monomial(cal_ctx* c, const double* q, int s, double* V) {
+    CAL_TRY(check_ctx(c, true));
+    if (!q || !V || s < 1) return set_error(c, CAL_ERR_ARG, "matrix_powers_monomial: bad arguments");
+    const int64_t n = c->A.n_local, ld = c->A.ld;
+    CAL_TRY(ensure_scratch(c, (size_t)(s + 1) * ld));
+    double* W = c->d_scratch;
+    CAL_TRY(upload(c, W, ld, q, n, 1));
+    for (int i = 0; i < s; ++i) CAL_TRY(spmv_dev(c, W + (size_t)i * ld, W + (size_t)(i + 1) * ld, 0, 0, 0, nullptr));
+    return download(c, V, W + ld, ld, n, s);  // V excludes q (matrix_powers_monomial.m:7)
+}
+
+int cal_matrix_powers_newton(cal_ctx* c, const double* v, int s, const double* lre, const double* lim, int modifiedp,
+                             double* V) {
+    CAL_TRY(check_ctx(c, true));
+    if (!v || !V || !lre || s < 1) return set_error(c, CAL_ERR_ARG, "matrix_powers_newton: bad arguments");
+    const int64_t n = c->A.n_local, ld = c->A.ld;
+    CAL_TRY(ensure_scratch(c, (size_t)(s + 1) * ld));
+    double* W = c->d_scratch;
+    CAL_TRY(upload(c, W, ld, v, n, 1));
+    for (int k = 0; k < s; ++k) {
+        const double re = lre[k], im = lim ? lim[k] : 0.0;
+        double* x = W + (size_t)k * ld;
+        double* y = W + (size_t)(k + 1) * ld;
+        if (modifiedp == 0) {
+            if (im != 0.0)
+                return set_error(c, CAL_ERR_UNSUPPORTED, "complex shifts need modifiedp=1 (real basis)");
+            CAL_TRY(spmv_dev(c, x, y, 1, re, 0.0, nullptr));  // :28
+        } else if (im < 0.0) {
+            if (k == 0)
+                return set_error(c, CAL_ERR_NUMERIC, "k==1, but shift has a negative imaginary part");  // :36-38
+            CAL_TRY(spmv_dev(c, x, y, 2, re, im * im, W + (size_t)(k - 1) * ld));  // :40-41
+        } else {
+            CAL_TRY(spmv_dev(c, x, y, 1, re, 0.0, nullptr));  // :34, :43
+        }
+    }
+    return download(c, V, W, ld, n, s + 1);
+}
+
+int cal_tsqr(cal_ctx* c, int64_t n, int m, const double* A, double* Q, double* R) {
+    CAL_TRY(check_ctx(c, false));
+    if (!A || !Q || !R || n < 1 || m < 1 || m > 16) return set_error(c, CAL_ERR_ARG, "tsqr: need 1 <= m <= 16");
+    const int64_t ld = ld_for(n);
+    CAL_TRY(ensure_scratch(c, (size_t)2 * m * ld));
+    double* dX = c->d_scratch;
+    double* dQ = c->d_scratch + (size_t)m * ld;
+    CAL_TRY(upload(c, dX, ld, A, n, m));
+    Panel X = panel();
+    panel_add(X, dX, ld, m);
+    int rank = 0;
+    bool sh = false;
+    CAL_TRY(normalize_dev(c, n, X, panel_out(dQ, ld, m), R, 1.0e-8, &rank, &sh));
+    CAL_TRY(download(c, Q, dQ, ld, n, m));
+    return sh ? CAL_WARN_RANK_DEFICIENT : 0;
+}
+
+int cal_normalize(cal_ctx* c, int64_t n, int m, const double* X, double tol, double* Q, double* R, int* rank) {
+    CAL_TRY(check_ctx(c, false));
+    if (!X || !Q || !R || n < 1 || m < 1 || m > 16) return set_error(c, CAL_ERR_ARG, "normalize: need 1 <= m <= 16");
+    const int64_t ld = ld_for(n);
+    CAL_TRY(ensure_scratch(c, (size_t)2 * m * ld));
+    double* dX = c->d_scratch;
+    double* dQ = c->d_scratch + (size_t)m * ld;
+    CAL_TRY(upload(c, dX, ld, X, n, m));
+    Panel P = panel();
+    panel_add(P, dX, ld, m);
+    int rk = 0;
+    bool sh = false;
+    CAL_TRY(normalize_dev(c, n, P, panel_out(dQ, ld, m), R, tol > 0 ? tol : 1.0e-8, &rk, &sh));
+    if (rank) *rank = rk;
+    CAL_TRY(download(c, Q, dQ, ld, n, m));
+    return rk < m ? CAL_WARN_RANK_DEFICIENT : 0;
+}
+
+int cal_cholqr(cal_ctx* c, int64_t n, int m, const double* X, double* Q, double* R) {
+    CAL_TRY(check_ctx(c, false));
+    if (!X || !Q || !R || n < 1 || m < 1 || m > 16) return set_error(c, CAL_ERR_ARG, "cholqr: need 1 <= m <= 16");
+    const int64_t ld = ld_for(n);
+    CAL_TRY(ensure_scratch(c, (size_t)2 * m * ld));
+    double* dX = c->d_scratch;
+    double* dQ = c->d_scratch + (size_t)m * ld;
+    CAL_TRY(upload(c, dX, ld, X, n, m));
+    Panel P = panel();
+    panel_add(P, dX, ld, m);
+    std::vector<double> G((size_t)m * m), Ri((size_t)m * m);
+    CAL_TRY(gram_host(c, n, P, P, G.data()));  // cholqr.m:5
+    if (!dense::chol_upper(m, G.data(), m, R, m))  // :6
+        return set_error(c, CAL_ERR_NUMERIC, "chol: Matrix must be positive definite.");
+    dense::tri_inv_upper(m, R, m, Ri.data(), m);
+    PanelOut out = panel_out(dQ, ld, m);
+    CAL_TRY(apply_host(c, n, P, Ri.data(), m, &out, nullptr, 0, nullptr));  // :8 (Q = X/R)
+    return download(c, Q, dQ, ld, n, m);
+}
+
+// project.m:7-58 on the device (block MGS across blocks, CGS within).
+static int project_blocks(cal_ctx* c, int64_t n, int64_t ld, int nb, const std::vector<double*>& dQ,
+                          const int* widths, int m, double* dX, bool doreorth, std::vector<std::vector<double>>& R) {
+    Panel X = panel();
+    panel_add(X, dX, ld, m);
+    PanelOut Xo = panel_out(dX, ld, m);
+    auto col_norms = [&](std::vector<double>& nr) -> int {
+        std::vector<double> G((size_t)m * m);
+        CAL_TRY(gram_host(c, n, X, X, G.data()));
+        nr.resize(m);
+        for (int i = 0; i < m; ++i) nr[i] = std::sqrt(G[i + (size_t)i * m]);
+        return 0;
+    };
+    std::vector<double> before;
+    if (doreorth) CAL_TRY(col_norms(before));
+    auto one_pass = [&](bool accumulate) -> int {
+        for (int i = 0; i < nb; ++i) {
+            const int w = widths[i];
+            if (w <= 0) continue;
+            Panel Qi = panel();
+            panel_add(Qi, dQ[i], ld, w);
+            std::vector<double> Ri((size_t)w * m);
+            CAL_TRY(gram_host(c, n, Qi, X, Ri.data()));  // R{i} = Q{i}'*X
+            Panel W = panel();
+            panel_add(W, dQ[i], ld, w);
+            panel_add(W, dX, ld, m);
+            std::vector<double> M((size_t)(w + m) * m, 0.0);
+            for (int j = 0; j < m; ++j) {
+                for (int r = 0; r < w; ++r) M[r + (size_t)j * (w + m)] = -Ri[r + (size_t)j * w];
+                M[w + j + (size_t)j * (w + m)] = 1.0;
+            }
+            CAL_TRY(apply_host(c, n, W, M.data(), m, &Xo, nullptr, 0, nullptr));  // X = X - Q{i}*R{i}
+            if (accumulate)
+                for (size_t e = 0; e < Ri.size(); ++e) R[i][e] += Ri[e];
+            else
+                R[i] = Ri;
+        }
+        return 0;
+    };
+    CAL_TRY(one_pass(false));
+    if (doreorth) {  // project.m:40-57 (note the inverted test of the reference)
+        std::vector<double> after;
+        CAL_TRY(col_norms(after));
+        double mx = NAN;
+        for (int i = 0; i < m; ++i) {
+            const double d = 0.5 * before[i] - after[i];
+            if (!std::isnan(d) && (std::isnan(mx) || d > mx)) mx = d;
+        }
+        if (mx < 0) CAL_TRY(one_pass(true));
+    }
+    return 0;
+}
+
+int cal_project(cal_ctx* c, int64_t n, int nblocks, const double* const* Q, const int* widths, int m, const double* X,
+                int doreorth, double* Xout, double* const* R) {
+    CAL_TRY(check_ctx(c, false));
+    if (nblocks < 0 || (nblocks > 0 && (!Q || !widths)) || !X || !Xout || n < 1 || m < 1 || m > 16)
+        return set_error(c, CAL_ERR_ARG, "project: bad arguments");
+    const int64_t ld = ld_for(n);
+    int wtot = 0;
+    for (int i = 0; i < nblocks; ++i) {
+        if (widths[i] < 0 || widths[i] > 128) return set_error(c, CAL_ERR_ARG, "project: block width out of range");
+        wtot += widths[i];
+    }
+    CAL_TRY(ensure_scratch(c, (size_t)(wtot + m) * ld));
+    std::vector<double*> dQ(nblocks);
+    double* p = c->d_scratch;
+    for (int i = 0; i < nblocks; ++i) {
+        dQ[i] = p;
+        CAL_TRY(upload(c, p, ld, Q[i], n, widths[i]));
+        p += (size_t)widths[i] * ld;
+    }
+    double* dX = p;
+    CAL_TRY(upload(c, dX, ld, X, n, m));
+    std::vector<std::vector<double>> Rv(nblocks);
+    for (int i = 0; i < nblocks; ++i) Rv[i].assign((size_t)std::max(widths[i], 0) * m, 0.0);
+    CAL_TRY(project_blocks(c, n, ld, nblocks, dQ, widths, m, dX, doreorth != 0, Rv));
+    for (int i = 0; i < nblocks; ++i)
+        if (R && R[i] && widths[i] > 0) std::copy(Rv[i].begin(), Rv[i].end(), R[i]);
+    return download(c, Xout, dX, ld, n, m);
+}
+
+int cal_project_and_normalize(cal_ctx* c, int64_t n, int nblocks, const double* const* Q, const int* widths, int m,
+                              const double* X, int doreorth, double* QZ, double* const* RZ, int* reorth, int* rank) {
+    CAL_TRY(check_ctx(c, false));
+    if (nblocks < 0 || (nblocks > 0 && (!Q || !widths)) || !X || !QZ || n < 1 || m < 1 || m > 16)
+        return set_error(c, CAL_ERR_ARG, "projectAndNormalize: bad arguments");
+    const int64_t ld = ld_for(n);
+    int wtot = 0, nonempty = 0, only = -1;
+    for (int i = 0; i < nblocks; ++i) {
+        if (widths[i] < 0 || widths[i] > 128) return set_error(c, CAL_ERR_ARG, "block width out of range");
+        wtot += widths[i];
+        if (widths[i] > 0) {
+            nonempty++;
+            only = i;
+        }
+    }
+    CAL_TRY(ensure_scratch(c, (size_t)(wtot + 3 * m) * ld));
+    std::vector<double*> dQ(nblocks);
+    double* p = c->d_scratch;
+    for (int i = 0; i < nblocks; ++i) {
+        dQ[i] = p;
+        CAL_TRY(upload(c, p, ld, Q[i], n, widths[i]));
+        p += (size_t)widths[i] * ld;
+    }
+    double* dX = p;
+    double* dY = p + (size_t)m * ld;
+    double* dZ = p + (size_t)2 * m * ld;
+    CAL_TRY(upload(c, dX, ld, X, n, m));
+    std::vector<double> Rm((size_t)m * m);
+    int rk = m, re = 0;
+    if (nonempty == 1) {
+        // the fused device path used by the CA-Lanczos driver
+        Panel Qp = panel(), Xp = panel();
+        panel_add(Qp, dQ[only], ld, widths[only]);
+        panel_add(Xp, dX, ld, m);
+        std::vector<double> Rq((size_t)widths[only] * m);
+        PNResult res;
+        CAL_TRY(project_and_normalize_dev(c, n, Qp, Xp, doreorth != 0, panel_out(dZ, ld, m), Rq.data(), Rm.data(), &res));
+        rk = res.rank;
+        re = res.reorth ? 1 : 0;
+        for (int i = 0; i < nblocks; ++i)
+            if (RZ && RZ[i] && widths[i] > 0) std::copy(Rq.begin(), Rq.end(), RZ[i]);
+    } else {
+        // general restatement (projectAndNormalize.m:3-90) on device panels
+        std::vector<double> before(m);
+        {
+            Panel Xp = panel();
+            panel_add(Xp, dX, ld, m);
+            std::vector<double> G((size_t)m * m);
+            CAL_TRY(gram_host(c, n, Xp, Xp, G.data()));
+            for (int i = 0; i < m; ++i) before[i] = std::sqrt(G[i + (size_t)i * m]);
+        }
+        CAL_HIP(c, hipMemcpyAsync(dY, dX, (size_t)m * ld * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+        std::vector<std::vector<double>> RY(nblocks);
+        for (int i = 0; i < nblocks; ++i) RY[i].assign((size_t)std::max(widths[i], 0) * m, 0.0);
+        CAL_TRY(project_blocks(c, n, ld, nblocks, dQ, widths, m, dY, false, RY));  // :25
+        Panel Yp = panel();
+        panel_add(Yp, dY, ld, m);
+        bool sh = false;
+        CAL_TRY(normalize_dev(c, n, Yp, panel_out(dZ, ld, m), Rm.data(), 1.0e-8, &rk, &sh));  // :26
+        double mx = NAN;
+        for (int i = 0; i < m; ++i) {
+            double after = 0.0;
+            for (int r = 0; r < m; ++r) after += Rm[r + (size_t)i * m] * Rm[r + (size_t)i * m];
+            after = std::sqrt(after);
+            const double rel = std::fabs(before[i] - after) / before[i];
+            if (!std::isnan(rel) && (std::isnan(mx) || rel > mx)) mx = rel;
+        }
+        std::vector<std::vector<double>> RZv = RY;
+        if (doreorth && mx > 0.5) {  // :52-73
+            re = 1;
+            std::vector<std::vector<double>> R2(nblocks);
+            for (int i = 0; i < nblocks; ++i) R2[i].assign((size_t)std::max(widths[i], 0) * m, 0.0);
+            CAL_TRY(project_blocks(c, n, ld, nblocks, dQ, widths, m, dY, false, R2));  // Z in place of Y
+            CAL_TRY(normalize_dev(c, n, Yp, panel_out(dZ, ld, m), Rm.data(), 1.0e-8, &rk, &sh));
+            for (int i = 0; i < nblocks; ++i)
+                for (size_t e = 0; e < R2[i].size(); ++e) RZv[i][e] = R2[i][e] + RY[i][e];
+        }
+        for (int i = 0; i < nblocks; ++i)
+            if (RZ && RZ[i] && widths[i] > 0) std::copy(RZv[i].begin(), RZv[i].end(), RZ[i]);
+    }
+    if (RZ && RZ[nblocks]) std::copy(Rm.begin(), Rm.end(), RZ[nblocks]);
+    if (reorth) *reorth = re;
+    if (rank) *rank = rk;
+    CAL_TRY(download(c, QZ, dZ, ld, n, m));
+    return (re && rk < m) ? CAL_WARN_RANK_DEFICIENT : 0;
+}
+
+}  // extern "C"

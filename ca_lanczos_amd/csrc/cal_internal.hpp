@@ -1,0 +1,235 @@
+// cal_internal.hpp -- shared types of the MI355X CA-Lanczos library.
+//
+// Data layout in HBM:
+//  * A: local CSR (int32 rowptr/col, fp64 val) + "row blocks" for the
+//    LDS-staged CSR-stream SpMV (<= 256 rows and <= 2048 nonzeros each).
+//  * every n-vector (columns of V, Q, scratch) lives in a column-major buffer
+//    with leading dimension ld = roundup(n_local + nghost, 64): the ghost
+//    entries of a slab live right after its local entries, so a halo
+//    exchange writes straight into the column the SpMV gathers from.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/calanczos.h"
+
+namespace cal {
+
+constexpr int kMaxSeg = 4;
+
+// A concatenation of up to kMaxSeg column-major segments ("[Q_p | X]").
+struct Panel {
+    const double* ptr[kMaxSeg];
+    int64_t ld[kMaxSeg];
+    int ncol[kMaxSeg];
+    int nseg;
+    int total;
+};
+
+struct PanelOut {
+    double* ptr[kMaxSeg];
+    int64_t ld[kMaxSeg];
+    int ncol[kMaxSeg];
+    int nseg;
+    int total;
+};
+
+inline Panel panel() {
+    Panel p{};
+    return p;
+}
+inline Panel& panel_add(Panel& p, const double* ptr, int64_t ld, int ncol) {
+    if (ncol <= 0) return p;
+    p.ptr[p.nseg] = ptr;
+    p.ld[p.nseg] = ld;
+    p.ncol[p.nseg] = ncol;
+    p.nseg++;
+    p.total += ncol;
+    return p;
+}
+inline PanelOut panel_out(double* ptr, int64_t ld, int ncol) {
+    PanelOut p{};
+    p.ptr[0] = ptr;
+    p.ld[0] = ld;
+    p.ncol[0] = ncol;
+    p.nseg = 1;
+    p.total = ncol;
+    return p;
+}
+
+// SpMV launch description (local CSR; x/y are columns with ghost space).
+struct SpmvArgs {
+    const int* rowptr;
+    const int* col;
+    const double* val;
+    const int* blk;
+    int nblk;
+    const double* x;
+    double* y;
+    const double* xprev;  // modified Newton basis, complex shift
+    double shift;         // y = A x - shift * x
+    double im2;           //     + im2 * xprev
+    int mode;             // 0: y = A x, 1: shifted, 2: shifted + im2 term
+};
+
+struct DevMatrix {
+    int64_t n_local = 0, n_global = 0, row0 = 0, nnz = 0, nghost = 0;
+    int* rowptr = nullptr;
+    int* col = nullptr;
+    double* val = nullptr;
+    int* blk = nullptr;
+    int nblk = 0;
+    int nit = 1;     // ceil(max row-block nonzeros / 256): SpMV unroll depth
+    int64_t ld = 0;  // leading dimension of every n-vector buffer
+    // halo plan (distributed); ghost entries grouped by owning peer
+    std::vector<int> peers;              // neighbour ranks
+    std::vector<int64_t> recv_off;       // offset into ghost area per peer
+    std::vector<int64_t> recv_cnt;
+    std::vector<int64_t> send_off;       // offset into send index list
+    std::vector<int64_t> send_cnt;
+    int* send_idx = nullptr;             // device, local indices to pack
+    int64_t send_total = 0;
+    double* send_buf = nullptr;          // device pack buffer
+};
+
+struct Comm;  // comm.cpp
+struct LanczosState;  // lanczos.cpp
+
+// Launchers (kernels.hip).  All enqueue on `st` and return hipError_t.
+hipError_t launch_spmv(const SpmvArgs& a, hipStream_t st);
+// C (wa x wb, column-major ldc = 16*ceil(wa/16)) partials; see kernels.hip.
+struct GramPlan {
+    int nta;    // A tiles of 16 columns
+    int blocks;
+    int64_t entries;  // per-block partial entries
+};
+GramPlan gram_plan(int wa, int wb, int64_t n);
+hipError_t launch_gram(const Panel& A, const Panel& B, int64_t n, const GramPlan& pl, double* partial,
+                       hipStream_t st);
+struct ApplyPlan {
+    int nty;
+    int run;
+    int blocks;
+    bool gram;
+    bool gramp;
+    size_t lds_bytes;
+    int64_t entries;  // per-block partial entries (gram + gramp)
+};
+ApplyPlan apply_plan(int wp, int wy, int64_t n, bool gram, int wq);
+hipError_t launch_apply(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y, bool store,
+                        int wq, int64_t n, const ApplyPlan& pl, double* partial, hipStream_t st);
+hipError_t launch_reduce(const double* partial, int nparts, int64_t nent, double* out, hipStream_t st);
+hipError_t launch_dot(const double* x, const double* y, int64_t n, double* partial, int blocks,
+                      hipStream_t st);
+int dot_blocks(int64_t n);
+hipError_t launch_axpy_sub(double* y, const double* x, double a, int64_t n, hipStream_t st);  // y -= a*x
+hipError_t launch_div(double* y, const double* x, double b, int64_t n, hipStream_t st);      // y = x / b
+hipError_t launch_gather(double* dst, const double* src, const int* idx, int64_t cnt, hipStream_t st);
+// fused SpMV + Ritz residual partials for one Ritz pair (diagnostics)
+hipError_t launch_spmv_resid(const SpmvArgs& a, const double* xi, double lr, double li, int64_t nrows,
+                             double* partial, int blocks, hipStream_t st);
+
+}  // namespace cal
+
+// Per-launch kernel timer (HIP events on the launching stream).
+struct CalTimerRec {
+    int kind;  // 0 spmv, 1 gram, 2 apply, 3 other
+    hipEvent_t a, b;
+};
+
+struct cal_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    cal::DevMatrix A;
+    bool has_A = false;
+
+    // reduction scratch
+    double* d_partial = nullptr;
+    size_t partial_cap = 0;  // doubles
+    double* d_red = nullptr;
+    double* h_red = nullptr;  // pinned
+    size_t red_cap = 0;       // doubles
+    double* d_small = nullptr;  // small matrices (M operands)
+    double* h_small = nullptr;  // pinned staging for d_small
+    size_t small_cap = 0;
+    bool small_pending = false;  // an async copy out of h_small may be in flight
+    double* d_scratch = nullptr;  // host-pointer entry points (tier-1 calls)
+    size_t scratch_cap = 0;
+
+    // generic device workspace (n-vector columns)
+    double* d_work = nullptr;
+    int work_cols = 0;
+    int64_t work_ld = 0;
+
+    cal::LanczosState* lz = nullptr;
+    cal::Comm* comm = nullptr;
+
+    bool timing = false;
+    std::vector<CalTimerRec> timers;
+    std::vector<hipEvent_t> event_pool;
+};
+
+// ---- helpers shared by the host-side translation units -----------------
+namespace cal {
+
+int set_error(cal_ctx* c, int code, const std::string& msg);
+int hip_fail(cal_ctx* c, hipError_t e, const char* what);
+
+#define CAL_HIP(ctx, expr)                                  \
+    do {                                                    \
+        hipError_t _e = (expr);                             \
+        if (_e != hipSuccess) return cal::hip_fail((ctx), _e, #expr); \
+    } while (0)
+#define CAL_TRY(expr)             \
+    do {                          \
+        int _s = (expr);          \
+        if (_s < 0) return _s;    \
+    } while (0)
+
+int upload_matrix(cal_ctx* c, int64_t n_local, int64_t n_global, int64_t row0, int64_t nghost,
+                  const std::vector<int>& rowptr, const std::vector<int>& col, const double* val);
+int ensure_partial(cal_ctx* c, size_t doubles);
+int ensure_scratch(cal_ctx* c, size_t doubles);
+int ensure_red(cal_ctx* c, size_t doubles);
+int ensure_small(cal_ctx* c, size_t doubles);
+int ensure_work(cal_ctx* c, int cols, int64_t ld);
+double* work_col(cal_ctx* c, int j);
+
+// timer bracket: returns an index, -1 if timing is off
+int timer_begin(cal_ctx* c, int kind);
+void timer_end(cal_ctx* c, int idx);
+
+// Device block operations (blockorth.cpp).  All matrices column-major; n is
+// the number of (local) rows of the panels.
+// Gram: out (wa x wb, ld wa) = A^T B (allreduced across ranks), on host.
+int gram_host(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* out);
+// Apply: Y = P * M (M host, wp x wy col-major).  Optional gram (Y^T Y, wy x wy)
+// and gramp (Psub^T Y, wq x wy where Psub = first wq columns of P), on host.
+int apply_host(cal_ctx* c, int64_t n, const Panel& P, const double* M, int wy, const PanelOut* Y, double* gram,
+               int wq, double* gramp);
+// Reorthogonalisation helpers used by the driver and the C ABI.
+struct PNResult {
+    bool reorth = false;
+    int rank = 0;
+    bool chol_shifted = false;
+};
+// CholQR2 normalise of the n x m panel X into Qout, R (m x m) on host.
+int normalize_dev(cal_ctx* c, int64_t n, const Panel& X, const PanelOut& Qout, double* R, double tol, int* rank,
+                  bool* shifted);
+// projectAndNormalize of X (n x m) against one block Qp (n x w): QZ into Qout,
+// Rq (w x m) and R (m x m) on host.  Mirrors projectAndNormalize.m:3-90.
+int project_and_normalize_dev(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, bool doreorth,
+                              const PanelOut& Qout, double* Rq, double* R, PNResult* res);
+// Halo exchange of a column (distributed only; no-op for one rank).
+int halo_exchange(cal_ctx* c, double* x);
+// y = A x (with modes), handling the halo first.
+int spmv_dev(cal_ctx* c, const double* x, double* y, int mode, double shift, double im2,
+             const double* xprev);
+int allreduce_sum(cal_ctx* c, double* d_buf, int64_t count);
+
+}  // namespace cal

@@ -1,0 +1,264 @@
+// comm.cpp -- RCCL / host-staged communicators, halo plan, distributed matrix.
+#include "comm.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+
+namespace cal {
+
+static int nccl_fail(cal_ctx* c, ncclResult_t r, const char* what) {
+    return set_error(c, CAL_ERR_COMM, std::string("RCCL error '") + ncclGetErrorString(r) + "' in " + what);
+}
+
+#define CAL_NCCL(ctx, expr)                                        \
+    do {                                                           \
+        ncclResult_t _r = (expr);                                  \
+        if (_r != ncclSuccess) return nccl_fail((ctx), _r, #expr); \
+    } while (0)
+
+static int ensure_stage(cal_ctx* c, size_t doubles) {
+    Comm* m = c->comm;
+    if (doubles <= m->stage_cap) return 0;
+    if (m->h_stage) CAL_HIP(c, hipHostFree(m->h_stage));
+    m->h_stage = nullptr;
+    const size_t n = std::max(doubles, (size_t)65536);
+    CAL_HIP(c, hipHostMalloc((void**)&m->h_stage, n * sizeof(double), hipHostMallocDefault));
+    m->stage_cap = n;
+    return 0;
+}
+
+void comm_destroy(cal_ctx* c) {
+    if (!c->comm) return;
+    if (c->comm->nccl) ncclCommDestroy(c->comm->nccl);
+    if (c->comm->h_stage) hipHostFree(c->comm->h_stage);
+    delete c->comm;
+    c->comm = nullptr;
+}
+
+int allreduce_sum(cal_ctx* c, double* d_buf, int64_t count) {
+    Comm* m = c->comm;
+    if (!m || m->nranks <= 1 || count <= 0) return 0;
+    if (m->kind == 1) {
+        CAL_NCCL(c, ncclAllReduce(d_buf, d_buf, (size_t)count, ncclDouble, ncclSum, m->nccl, c->stream));
+        return 0;
+    }
+    CAL_TRY(ensure_stage(c, count));
+    CAL_HIP(c, hipMemcpyAsync(m->h_stage, d_buf, count * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    if (m->ar(m->user, m->h_stage, count) != 0) return set_error(c, CAL_ERR_COMM, "allreduce callback failed");
+    CAL_HIP(c, hipMemcpyAsync(d_buf, m->h_stage, count * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    return 0;
+}
+
+int halo_exchange(cal_ctx* c, double* x) {
+    Comm* m = c->comm;
+    DevMatrix& A = c->A;
+    if (!m || m->nranks <= 1 || A.peers.empty()) return 0;
+    CAL_HIP(c, launch_gather(A.send_buf, x, A.send_idx, A.send_total, c->stream));
+    double* ghost = x + A.n_local;
+    if (m->kind == 1) {
+        CAL_NCCL(c, ncclGroupStart());
+        for (size_t p = 0; p < A.peers.size(); ++p) {
+            if (A.send_cnt[p] > 0)
+                CAL_NCCL(c, ncclSend(A.send_buf + A.send_off[p], (size_t)A.send_cnt[p], ncclDouble, A.peers[p], m->nccl,
+                                     c->stream));
+            if (A.recv_cnt[p] > 0)
+                CAL_NCCL(c, ncclRecv(ghost + A.recv_off[p], (size_t)A.recv_cnt[p], ncclDouble, A.peers[p], m->nccl,
+                                     c->stream));
+        }
+        CAL_NCCL(c, ncclGroupEnd());
+        return 0;
+    }
+    const size_t need = (size_t)A.send_total + (size_t)A.nghost;
+    CAL_TRY(ensure_stage(c, need));
+    double* hs = m->h_stage;
+    double* hr = m->h_stage + A.send_total;
+    CAL_HIP(c, hipMemcpyAsync(hs, A.send_buf, A.send_total * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    for (size_t p = 0; p < A.peers.size(); ++p)
+        if (m->ex(m->user, A.peers[p], hs + A.send_off[p], A.send_cnt[p], hr + A.recv_off[p], A.recv_cnt[p]) != 0)
+            return set_error(c, CAL_ERR_COMM, "exchange callback failed");
+    CAL_HIP(c, hipMemcpyAsync(ghost, hr, A.nghost * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    return 0;
+}
+
+int comm_allreduce_host(cal_ctx* c, std::vector<double>& buf) {
+    Comm* m = c->comm;
+    if (!m || m->nranks <= 1 || buf.empty()) return 0;
+    if (m->kind == 2) {
+        if (m->ar(m->user, buf.data(), (int64_t)buf.size()) != 0)
+            return set_error(c, CAL_ERR_COMM, "allreduce callback failed");
+        return 0;
+    }
+    double* d = nullptr;
+    CAL_HIP(c, hipMalloc((void**)&d, buf.size() * sizeof(double)));
+    CAL_HIP(c, hipMemcpy(d, buf.data(), buf.size() * sizeof(double), hipMemcpyHostToDevice));
+    int s = allreduce_sum(c, d, (int64_t)buf.size());
+    if (s == 0) {
+        hipStreamSynchronize(c->stream);
+        hipMemcpy(buf.data(), d, buf.size() * sizeof(double), hipMemcpyDeviceToHost);
+    }
+    hipFree(d);
+    return s;
+}
+
+int comm_exchange_host(cal_ctx* c, int peer, const std::vector<double>& send, std::vector<double>& recv) {
+    Comm* m = c->comm;
+    if (m->kind == 2) {
+        if (m->ex(m->user, peer, send.data(), (int64_t)send.size(), recv.data(), (int64_t)recv.size()) != 0)
+            return set_error(c, CAL_ERR_COMM, "exchange callback failed");
+        return 0;
+    }
+    double *ds = nullptr, *dr = nullptr;
+    CAL_HIP(c, hipMalloc((void**)&ds, std::max<size_t>(send.size(), 1) * sizeof(double)));
+    CAL_HIP(c, hipMalloc((void**)&dr, std::max<size_t>(recv.size(), 1) * sizeof(double)));
+    if (!send.empty()) CAL_HIP(c, hipMemcpy(ds, send.data(), send.size() * sizeof(double), hipMemcpyHostToDevice));
+    CAL_NCCL(c, ncclGroupStart());
+    if (!send.empty()) CAL_NCCL(c, ncclSend(ds, send.size(), ncclDouble, peer, m->nccl, c->stream));
+    if (!recv.empty()) CAL_NCCL(c, ncclRecv(dr, recv.size(), ncclDouble, peer, m->nccl, c->stream));
+    CAL_NCCL(c, ncclGroupEnd());
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    if (!recv.empty()) CAL_HIP(c, hipMemcpy(recv.data(), dr, recv.size() * sizeof(double), hipMemcpyDeviceToHost));
+    hipFree(ds);
+    hipFree(dr);
+    return 0;
+}
+
+}  // namespace cal
+
+using namespace cal;
+
+extern "C" {
+
+int cal_comm_unique_id(void* id128) {
+    if (!id128) return CAL_ERR_ARG;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return CAL_ERR_COMM;
+    memcpy(id128, &id, sizeof(id));
+    return 0;
+}
+
+int cal_comm_init_rccl(cal_ctx* c, int nranks, int rank, const void* id128) {
+    if (!c || nranks < 1 || rank < 0 || rank >= nranks || !id128) return set_error(c, CAL_ERR_ARG, "bad comm args");
+    hipSetDevice(c->device);
+    comm_destroy(c);
+    Comm* m = new Comm();
+    m->nranks = nranks;
+    m->rank = rank;
+    m->kind = 1;
+    ncclUniqueId id;
+    memcpy(&id, id128, sizeof(id));
+    ncclResult_t r = ncclCommInitRank(&m->nccl, nranks, id, rank);
+    if (r != ncclSuccess) {
+        delete m;
+        return nccl_fail(c, r, "ncclCommInitRank");
+    }
+    c->comm = m;
+    return 0;
+}
+
+int cal_comm_init_host(cal_ctx* c, int nranks, int rank, cal_allreduce_fn allreduce, cal_exchange_fn exchange,
+                       void* user) {
+    if (!c || nranks < 1 || rank < 0 || rank >= nranks || !allreduce || !exchange)
+        return set_error(c, CAL_ERR_ARG, "bad comm args");
+    comm_destroy(c);
+    Comm* m = new Comm();
+    m->nranks = nranks;
+    m->rank = rank;
+    m->kind = 2;
+    m->ar = allreduce;
+    m->ex = exchange;
+    m->user = user;
+    c->comm = m;
+    return 0;
+}
+
+int cal_comm_info(cal_ctx* c, int* nranks, int* rank, int* kind) {
+    if (!c) return CAL_ERR_ARG;
+    if (nranks) *nranks = c->comm ? c->comm->nranks : 1;
+    if (rank) *rank = c->comm ? c->comm->rank : 0;
+    if (kind) *kind = c->comm ? c->comm->kind : 0;
+    return 0;
+}
+
+// Row slab [row0, row0+nlocal) with global column indices.  Ghost columns are
+// numbered n_local.. grouped by owning rank (ascending), ascending global id
+// inside a group, so each peer's halo lands contiguously after the local rows.
+int cal_set_matrix_csr_dist(cal_ctx* c, int64_t n_global, int64_t row0, int64_t nlocal, const int64_t* rowptr,
+                            const int64_t* colind_global, const double* val) {
+    if (!c || nlocal < 0 || row0 < 0 || row0 + nlocal > n_global || !rowptr)
+        return set_error(c, CAL_ERR_ARG, "cal_set_matrix_csr_dist: bad arguments");
+    hipSetDevice(c->device);
+    const int nranks = c->comm ? c->comm->nranks : 1;
+    const int rank = c->comm ? c->comm->rank : 0;
+    // slab starts of every rank
+    std::vector<double> starts(nranks + 1, 0.0);
+    starts[rank] = (double)row0;
+    if (rank == nranks - 1) starts[nranks] = (double)(row0 + nlocal);
+    CAL_TRY(comm_allreduce_host(c, starts));
+    std::vector<int64_t> st(nranks + 1);
+    for (int i = 0; i <= nranks; ++i) st[i] = (int64_t)starts[i];
+    if (st[nranks] != n_global) return set_error(c, CAL_ERR_ARG, "slabs do not cover the matrix");
+    auto owner = [&](int64_t j) {
+        return (int)(std::upper_bound(st.begin(), st.end() - 1, j) - st.begin()) - 1;
+    };
+    const int64_t nnz = rowptr[nlocal] - rowptr[0];
+    if (nnz >= ((int64_t)1 << 31) || nlocal >= ((int64_t)1 << 31))
+        return set_error(c, CAL_ERR_UNSUPPORTED, "n and nnz must be < 2^31 per rank");
+    // collect ghosts
+    std::map<int64_t, int64_t> ghost;  // global -> (owner-ordered) index, filled below
+    for (int64_t p = 0; p < nnz; ++p) {
+        const int64_t j = colind_global[p];
+        if (j < 0 || j >= n_global) return set_error(c, CAL_ERR_ARG, "column index out of range");
+        if (j < row0 || j >= row0 + nlocal) ghost[j] = 0;
+    }
+    // std::map iterates in ascending global id == grouped by owner ascending
+    std::vector<std::vector<int64_t>> need(nranks);
+    int64_t gi = 0;
+    for (auto& kv : ghost) {
+        kv.second = gi++;
+        need[owner(kv.first)].push_back(kv.first);
+    }
+    const int64_t nghost = gi;
+    std::vector<int> rp(nlocal + 1), col(nnz);
+    for (int64_t i = 0; i <= nlocal; ++i) rp[i] = (int)(rowptr[i] - rowptr[0]);
+    for (int64_t p = 0; p < nnz; ++p) {
+        const int64_t j = colind_global[p];
+        col[p] = (j >= row0 && j < row0 + nlocal) ? (int)(j - row0) : (int)(nlocal + ghost[j]);
+    }
+    // counts matrix: cnt[p*nranks+q] = #entries rank p needs from rank q
+    std::vector<double> cnt((size_t)nranks * nranks, 0.0);
+    for (int q = 0; q < nranks; ++q) cnt[(size_t)rank * nranks + q] = (double)need[q].size();
+    CAL_TRY(comm_allreduce_host(c, cnt));
+    CAL_TRY(upload_matrix(c, nlocal, n_global, row0, nghost, rp, col, val + rowptr[0]));
+    DevMatrix& A = c->A;
+    int64_t roff = 0, soff = 0;
+    std::vector<int> send_idx;
+    for (int q = 0; q < nranks; ++q) {
+        if (q == rank) continue;
+        const int64_t nrecv = (int64_t)cnt[(size_t)rank * nranks + q];
+        const int64_t nsend = (int64_t)cnt[(size_t)q * nranks + rank];
+        if (nrecv == 0 && nsend == 0) continue;
+        // tell q which of its rows we need; learn which of ours q needs
+        std::vector<double> want(need[q].begin(), need[q].end()), theirs(nsend);
+        CAL_TRY(comm_exchange_host(c, q, want, theirs));
+        A.peers.push_back(q);
+        A.recv_off.push_back(roff);
+        A.recv_cnt.push_back(nrecv);
+        A.send_off.push_back(soff);
+        A.send_cnt.push_back(nsend);
+        for (double g : theirs) send_idx.push_back((int)((int64_t)g - row0));
+        roff += nrecv;
+        soff += nsend;
+    }
+    A.send_total = soff;
+    if (soff > 0) {
+        CAL_HIP(c, hipMalloc((void**)&A.send_idx, soff * sizeof(int)));
+        CAL_HIP(c, hipMalloc((void**)&A.send_buf, soff * sizeof(double)));
+        CAL_HIP(c, hipMemcpy(A.send_idx, send_idx.data(), soff * sizeof(int), hipMemcpyHostToDevice));
+    }
+    return 0;
+}
+
+}  // extern "C"

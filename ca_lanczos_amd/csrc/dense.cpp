@@ -1,0 +1,569 @@
+// dense.cpp -- small dense host linear algebra (see dense.hpp).
+#include "dense.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+namespace cal {
+namespace dense {
+
+bool chol_upper(int m, const double* G, int ldg, double* R, int ldr) {
+    for (int j = 0; j < m; ++j)
+        for (int i = 0; i < m; ++i) R[i + (size_t)j * ldr] = 0.0;
+    for (int j = 0; j < m; ++j) {
+        double s = G[j + (size_t)j * ldg];
+        for (int k = 0; k < j; ++k) s -= R[k + (size_t)j * ldr] * R[k + (size_t)j * ldr];
+        if (!(s > 0.0) || !std::isfinite(s)) return false;
+        const double rjj = std::sqrt(s);
+        R[j + (size_t)j * ldr] = rjj;
+        for (int i = j + 1; i < m; ++i) {
+            double t = G[j + (size_t)i * ldg];
+            for (int k = 0; k < j; ++k) t -= R[k + (size_t)j * ldr] * R[k + (size_t)i * ldr];
+            R[j + (size_t)i * ldr] = t / rjj;
+        }
+    }
+    return true;
+}
+
+void tri_inv_upper(int m, const double* R, int ldr, double* Ri, int ldi) {
+    for (int j = 0; j < m; ++j)
+        for (int i = 0; i < m; ++i) Ri[i + (size_t)j * ldi] = 0.0;
+    // solve R * Ri(:,j) = e_j by back substitution
+    for (int j = 0; j < m; ++j) {
+        for (int i = j; i >= 0; --i) {
+            double s = (i == j) ? 1.0 : 0.0;
+            for (int k = i + 1; k <= j; ++k) s -= R[i + (size_t)k * ldr] * Ri[k + (size_t)j * ldi];
+            Ri[i + (size_t)j * ldi] = s / R[i + (size_t)i * ldr];
+        }
+    }
+}
+
+void matmul(int m, int k, int n, const double* A, int lda, const double* B, int ldb, double* C, int ldc) {
+    std::vector<double> tmp((size_t)m * n, 0.0);
+    for (int j = 0; j < n; ++j)
+        for (int i = 0; i < m; ++i) {
+            double s = 0.0;
+            for (int p = 0; p < k; ++p) s += A[i + (size_t)p * lda] * B[p + (size_t)j * ldb];
+            tmp[i + (size_t)j * m] = s;
+        }
+    for (int j = 0; j < n; ++j)
+        for (int i = 0; i < m; ++i) C[i + (size_t)j * ldc] = tmp[i + (size_t)j * m];
+}
+
+void rdiv_upper(int r, int m, double* X, int ldx, const double* R, int ldr) {
+    // Y R = X  ->  Y(:,j) = (X(:,j) - sum_{k<j} Y(:,k) R(k,j)) / R(j,j)
+    for (int j = 0; j < m; ++j) {
+        for (int i = 0; i < r; ++i) {
+            double s = X[i + (size_t)j * ldx];
+            for (int k = 0; k < j; ++k) s -= X[i + (size_t)k * ldx] * R[k + (size_t)j * ldr];
+            X[i + (size_t)j * ldx] = s / R[j + (size_t)j * ldr];
+        }
+    }
+}
+
+bool tridiag_eigvals(int n, const double* dd, const double* ee, double* w) {
+    if (n <= 0) return true;
+    std::vector<double> d(dd, dd + n), e(n, 0.0);
+    for (int i = 0; i < n - 1; ++i) e[i] = ee[i];
+    const double eps = std::ldexp(1.0, -52);
+    for (int l = 0; l < n; ++l) {
+        int iter = 0, m;
+        do {
+            for (m = l; m < n - 1; ++m) {
+                const double dd2 = std::fabs(d[m]) + std::fabs(d[m + 1]);
+                if (std::fabs(e[m]) <= eps * dd2) break;
+            }
+            if (m != l) {
+                if (iter++ == 100) return false;
+                double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
+                double r = std::hypot(g, 1.0);
+                g = d[m] - d[l] + e[l] / (g + (g >= 0 ? std::fabs(r) : -std::fabs(r)));
+                double s = 1.0, c = 1.0, p = 0.0;
+                int i;
+                bool early = false;
+                for (i = m - 1; i >= l; --i) {
+                    double f = s * e[i], b = c * e[i];
+                    e[i + 1] = (r = std::hypot(f, g));
+                    if (r == 0.0) {
+                        d[i + 1] -= p;
+                        e[m] = 0.0;
+                        early = true;
+                        break;
+                    }
+                    s = f / r;
+                    c = g / r;
+                    g = d[i + 1] - p;
+                    r = (d[i] - g) * s + 2.0 * c * b;
+                    d[i + 1] = g + (p = s * r);
+                    g = c * r - b;
+                }
+                if (early) continue;
+                d[l] -= p;
+                e[l] = g;
+                e[m] = 0.0;
+            }
+        } while (m != l);
+    }
+    std::sort(d.begin(), d.end());
+    for (int i = 0; i < n; ++i) w[i] = d[i];
+    return true;
+}
+
+void singular_values(int m, const double* A, int lda, double* sv) {
+    std::vector<double> U((size_t)m * m);
+    for (int j = 0; j < m; ++j)
+        for (int i = 0; i < m; ++i) U[i + (size_t)j * m] = A[i + (size_t)j * lda];
+    const double eps = std::ldexp(1.0, -52);
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        double off = 0.0;
+        for (int p = 0; p < m - 1; ++p)
+            for (int q = p + 1; q < m; ++q) {
+                double a = 0, b = 0, c = 0;
+                for (int i = 0; i < m; ++i) {
+                    const double up = U[i + (size_t)p * m], uq = U[i + (size_t)q * m];
+                    a += up * up;
+                    b += uq * uq;
+                    c += up * uq;
+                }
+                if (std::fabs(c) <= eps * std::sqrt(a * b) || c == 0.0) continue;
+                off = std::max(off, std::fabs(c) / std::sqrt(a * b));
+                const double zeta = (b - a) / (2.0 * c);
+                const double t = (zeta >= 0 ? 1.0 : -1.0) / (std::fabs(zeta) + std::sqrt(1.0 + zeta * zeta));
+                const double cs = 1.0 / std::sqrt(1.0 + t * t), sn = cs * t;
+                for (int i = 0; i < m; ++i) {
+                    const double up = U[i + (size_t)p * m], uq = U[i + (size_t)q * m];
+                    U[i + (size_t)p * m] = cs * up - sn * uq;
+                    U[i + (size_t)q * m] = sn * up + cs * uq;
+                }
+            }
+        if (off <= eps) break;
+    }
+    for (int j = 0; j < m; ++j) {
+        double s = 0;
+        for (int i = 0; i < m; ++i) s += U[i + (size_t)j * m] * U[i + (size_t)j * m];
+        sv[j] = std::sqrt(s);
+    }
+    std::sort(sv, sv + m, [](double x, double y) { return x > y; });
+}
+
+void eig_symmetric(int n, const double* A, int lda, double* w, double* V, int ldv) {
+    std::vector<double> a((size_t)n * n), v((size_t)n * n, 0.0);
+    for (int j = 0; j < n; ++j)
+        for (int i = 0; i < n; ++i) a[i + (size_t)j * n] = A[i + (size_t)j * lda];
+    for (int i = 0; i < n; ++i) v[i + (size_t)i * n] = 1.0;
+    const double eps = std::ldexp(1.0, -52);
+    for (int sweep = 0; sweep < 100; ++sweep) {
+        double off = 0.0, nrm = 0.0;
+        for (int j = 0; j < n; ++j)
+            for (int i = 0; i < n; ++i) {
+                nrm += a[i + (size_t)j * n] * a[i + (size_t)j * n];
+                if (i != j) off += a[i + (size_t)j * n] * a[i + (size_t)j * n];
+            }
+        if (off <= eps * eps * nrm) break;
+        for (int p = 0; p < n - 1; ++p)
+            for (int q = p + 1; q < n; ++q) {
+                const double apq = a[p + (size_t)q * n];
+                if (apq == 0.0) continue;
+                const double app = a[p + (size_t)p * n], aqq = a[q + (size_t)q * n];
+                const double theta = (aqq - app) / (2.0 * apq);
+                const double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
+                const double c = 1.0 / std::sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < n; ++k) {
+                    const double akp = a[k + (size_t)p * n], akq = a[k + (size_t)q * n];
+                    a[k + (size_t)p * n] = c * akp - s * akq;
+                    a[k + (size_t)q * n] = s * akp + c * akq;
+                }
+                for (int k = 0; k < n; ++k) {
+                    const double apk = a[p + (size_t)k * n], aqk = a[q + (size_t)k * n];
+                    a[p + (size_t)k * n] = c * apk - s * aqk;
+                    a[q + (size_t)k * n] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < n; ++k) {
+                    const double vkp = v[k + (size_t)p * n], vkq = v[k + (size_t)q * n];
+                    v[k + (size_t)p * n] = c * vkp - s * vkq;
+                    v[k + (size_t)q * n] = s * vkp + c * vkq;
+                }
+            }
+    }
+    std::vector<int> idx(n);
+    for (int i = 0; i < n; ++i) idx[i] = i;
+    std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return a[x + (size_t)x * n] < a[y + (size_t)y * n]; });
+    for (int j = 0; j < n; ++j) {
+        w[j] = a[idx[j] + (size_t)idx[j] * n];
+        for (int i = 0; i < n; ++i) V[i + (size_t)j * ldv] = v[i + (size_t)idx[j] * n];
+    }
+}
+
+// ---- general eigenproblem: orthes + hqr2 (EISPACK algorithm) -------------
+namespace {
+
+struct Mat {
+    int n;
+    std::vector<double> a;
+    explicit Mat(int n_) : n(n_), a((size_t)n_ * n_, 0.0) {}
+    double& operator()(int i, int j) { return a[i + (size_t)j * n]; }
+};
+
+inline void cdiv(double xr, double xi, double yr, double yi, double& cr, double& ci) {
+    double r, d;
+    if (std::fabs(yr) > std::fabs(yi)) {
+        r = yi / yr;
+        d = yr + r * yi;
+        cr = (xr + r * xi) / d;
+        ci = (xi - r * xr) / d;
+    } else {
+        r = yr / yi;
+        d = yi + r * yr;
+        cr = (r * xr + xi) / d;
+        ci = (r * xi - xr) / d;
+    }
+}
+
+void orthes(Mat& H, Mat& V) {
+    const int n = H.n, low = 0, high = n - 1;
+    std::vector<double> ort(n, 0.0);
+    for (int m = low + 1; m <= high - 1; ++m) {
+        double scale = 0.0;
+        for (int i = m; i <= high; ++i) scale += std::fabs(H(i, m - 1));
+        if (scale != 0.0) {
+            double h = 0.0;
+            for (int i = high; i >= m; --i) {
+                ort[i] = H(i, m - 1) / scale;
+                h += ort[i] * ort[i];
+            }
+            double g = std::sqrt(h);
+            if (ort[m] > 0) g = -g;
+            h = h - ort[m] * g;
+            ort[m] = ort[m] - g;
+            for (int j = m; j < n; ++j) {
+                double f = 0.0;
+                for (int i = high; i >= m; --i) f += ort[i] * H(i, j);
+                f = f / h;
+                for (int i = m; i <= high; ++i) H(i, j) -= f * ort[i];
+            }
+            for (int i = 0; i <= high; ++i) {
+                double f = 0.0;
+                for (int j = high; j >= m; --j) f += ort[j] * H(i, j);
+                f = f / h;
+                for (int j = m; j <= high; ++j) H(i, j) -= f * ort[j];
+            }
+            ort[m] = scale * ort[m];
+            H(m, m - 1) = scale * g;
+        }
+    }
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) V(i, j) = (i == j ? 1.0 : 0.0);
+    for (int m = high - 1; m >= low + 1; --m) {
+        if (H(m, m - 1) != 0.0) {
+            for (int i = m + 1; i <= high; ++i) ort[i] = H(i, m - 1);
+            for (int j = m; j <= high; ++j) {
+                double g = 0.0;
+                for (int i = m; i <= high; ++i) g += ort[i] * V(i, j);
+                g = (g / ort[m]) / H(m, m - 1);
+                for (int i = m; i <= high; ++i) V(i, j) += g * ort[i];
+            }
+        }
+    }
+}
+
+bool hqr2(Mat& H, Mat& V, std::vector<double>& d, std::vector<double>& e) {
+    const int nn = H.n;
+    int n = nn - 1;
+    const int low = 0, high = nn - 1;
+    const double eps = std::ldexp(1.0, -52);
+    double exshift = 0.0;
+    double p = 0, q = 0, r = 0, s = 0, z = 0, t, w, x, y;
+    double norm = 0.0;
+    for (int i = 0; i < nn; ++i)
+        for (int j = std::max(i - 1, 0); j < nn; ++j) norm += std::fabs(H(i, j));
+    int iter = 0, total_iter = 0;
+    while (n >= low) {
+        int l = n;
+        while (l > low) {
+            s = std::fabs(H(l - 1, l - 1)) + std::fabs(H(l, l));
+            if (s == 0.0) s = norm;
+            if (std::fabs(H(l, l - 1)) < eps * s) break;
+            l--;
+        }
+        if (l == n) {
+            H(n, n) = H(n, n) + exshift;
+            d[n] = H(n, n);
+            e[n] = 0.0;
+            n--;
+            iter = 0;
+        } else if (l == n - 1) {
+            w = H(n, n - 1) * H(n - 1, n);
+            p = (H(n - 1, n - 1) - H(n, n)) / 2.0;
+            q = p * p + w;
+            z = std::sqrt(std::fabs(q));
+            H(n, n) = H(n, n) + exshift;
+            H(n - 1, n - 1) = H(n - 1, n - 1) + exshift;
+            x = H(n, n);
+            if (q >= 0) {
+                z = (p >= 0) ? p + z : p - z;
+                d[n - 1] = x + z;
+                d[n] = d[n - 1];
+                if (z != 0.0) d[n] = x - w / z;
+                e[n - 1] = 0.0;
+                e[n] = 0.0;
+                x = H(n, n - 1);
+                s = std::fabs(x) + std::fabs(z);
+                p = x / s;
+                q = z / s;
+                r = std::sqrt(p * p + q * q);
+                p = p / r;
+                q = q / r;
+                for (int j = n - 1; j < nn; ++j) {
+                    z = H(n - 1, j);
+                    H(n - 1, j) = q * z + p * H(n, j);
+                    H(n, j) = q * H(n, j) - p * z;
+                }
+                for (int i = 0; i <= n; ++i) {
+                    z = H(i, n - 1);
+                    H(i, n - 1) = q * z + p * H(i, n);
+                    H(i, n) = q * H(i, n) - p * z;
+                }
+                for (int i = low; i <= high; ++i) {
+                    z = V(i, n - 1);
+                    V(i, n - 1) = q * z + p * V(i, n);
+                    V(i, n) = q * V(i, n) - p * z;
+                }
+            } else {
+                d[n - 1] = x + p;
+                d[n] = x + p;
+                e[n - 1] = z;
+                e[n] = -z;
+            }
+            n = n - 2;
+            iter = 0;
+        } else {
+            x = H(n, n);
+            y = 0.0;
+            w = 0.0;
+            if (l < n) {
+                y = H(n - 1, n - 1);
+                w = H(n, n - 1) * H(n - 1, n);
+            }
+            if (iter == 10) {
+                exshift += x;
+                for (int i = low; i <= n; ++i) H(i, i) -= x;
+                s = std::fabs(H(n, n - 1)) + std::fabs(H(n - 1, n - 2));
+                x = y = 0.75 * s;
+                w = -0.4375 * s * s;
+            }
+            if (iter == 30) {
+                s = (y - x) / 2.0;
+                s = s * s + w;
+                if (s > 0) {
+                    s = std::sqrt(s);
+                    if (y < x) s = -s;
+                    s = x - w / ((y - x) / 2.0 + s);
+                    for (int i = low; i <= n; ++i) H(i, i) -= s;
+                    exshift += s;
+                    x = y = w = 0.964;
+                }
+            }
+            iter = iter + 1;
+            if (++total_iter > 100 * nn) return false;
+            int m = n - 2;
+            while (m >= l) {
+                z = H(m, m);
+                r = x - z;
+                s = y - z;
+                p = (r * s - w) / H(m + 1, m) + H(m, m + 1);
+                q = H(m + 1, m + 1) - z - r - s;
+                r = H(m + 2, m + 1);
+                s = std::fabs(p) + std::fabs(q) + std::fabs(r);
+                p = p / s;
+                q = q / s;
+                r = r / s;
+                if (m == l) break;
+                if (std::fabs(H(m, m - 1)) * (std::fabs(q) + std::fabs(r)) <
+                    eps * (std::fabs(p) * (std::fabs(H(m - 1, m - 1)) + std::fabs(z) + std::fabs(H(m + 1, m + 1)))))
+                    break;
+                m--;
+            }
+            for (int i = m + 2; i <= n; ++i) {
+                H(i, i - 2) = 0.0;
+                if (i > m + 2) H(i, i - 3) = 0.0;
+            }
+            for (int k = m; k <= n - 1; ++k) {
+                const bool notlast = (k != n - 1);
+                if (k != m) {
+                    p = H(k, k - 1);
+                    q = H(k + 1, k - 1);
+                    r = notlast ? H(k + 2, k - 1) : 0.0;
+                    x = std::fabs(p) + std::fabs(q) + std::fabs(r);
+                    if (x == 0.0) continue;
+                    p = p / x;
+                    q = q / x;
+                    r = r / x;
+                }
+                s = std::sqrt(p * p + q * q + r * r);
+                if (p < 0) s = -s;
+                if (s != 0) {
+                    if (k != m)
+                        H(k, k - 1) = -s * x;
+                    else if (l != m)
+                        H(k, k - 1) = -H(k, k - 1);
+                    p = p + s;
+                    x = p / s;
+                    y = q / s;
+                    z = r / s;
+                    q = q / p;
+                    r = r / p;
+                    for (int j = k; j < nn; ++j) {
+                        p = H(k, j) + q * H(k + 1, j);
+                        if (notlast) {
+                            p = p + r * H(k + 2, j);
+                            H(k + 2, j) = H(k + 2, j) - p * z;
+                        }
+                        H(k, j) = H(k, j) - p * x;
+                        H(k + 1, j) = H(k + 1, j) - p * y;
+                    }
+                    for (int i = 0; i <= std::min(n, k + 3); ++i) {
+                        p = x * H(i, k) + y * H(i, k + 1);
+                        if (notlast) {
+                            p = p + z * H(i, k + 2);
+                            H(i, k + 2) = H(i, k + 2) - p * r;
+                        }
+                        H(i, k) = H(i, k) - p;
+                        H(i, k + 1) = H(i, k + 1) - p * q;
+                    }
+                    for (int i = low; i <= high; ++i) {
+                        p = x * V(i, k) + y * V(i, k + 1);
+                        if (notlast) {
+                            p = p + z * V(i, k + 2);
+                            V(i, k + 2) = V(i, k + 2) - p * r;
+                        }
+                        V(i, k) = V(i, k) - p;
+                        V(i, k + 1) = V(i, k + 1) - p * q;
+                    }
+                }
+            }
+        }
+    }
+    if (norm == 0.0) return true;
+    for (n = nn - 1; n >= 0; --n) {
+        p = d[n];
+        q = e[n];
+        if (q == 0) {
+            int l = n;
+            H(n, n) = 1.0;
+            for (int i = n - 1; i >= 0; --i) {
+                w = H(i, i) - p;
+                r = 0.0;
+                for (int j = l; j <= n; ++j) r = r + H(i, j) * H(j, n);
+                if (e[i] < 0.0) {
+                    z = w;
+                    s = r;
+                } else {
+                    l = i;
+                    if (e[i] == 0.0) {
+                        H(i, n) = (w != 0.0) ? -r / w : -r / (eps * norm);
+                    } else {
+                        x = H(i, i + 1);
+                        y = H(i + 1, i);
+                        q = (d[i] - p) * (d[i] - p) + e[i] * e[i];
+                        t = (x * s - z * r) / q;
+                        H(i, n) = t;
+                        if (std::fabs(x) > std::fabs(z))
+                            H(i + 1, n) = (-r - w * t) / x;
+                        else
+                            H(i + 1, n) = (-s - y * t) / z;
+                    }
+                    t = std::fabs(H(i, n));
+                    if ((eps * t) * t > 1)
+                        for (int j = i; j <= n; ++j) H(j, n) = H(j, n) / t;
+                }
+            }
+        } else if (q < 0) {
+            int l = n - 1;
+            double cr, ci;
+            if (std::fabs(H(n, n - 1)) > std::fabs(H(n - 1, n))) {
+                H(n - 1, n - 1) = q / H(n, n - 1);
+                H(n - 1, n) = -(H(n, n) - p) / H(n, n - 1);
+            } else {
+                cdiv(0.0, -H(n - 1, n), H(n - 1, n - 1) - p, q, cr, ci);
+                H(n - 1, n - 1) = cr;
+                H(n - 1, n) = ci;
+            }
+            H(n, n - 1) = 0.0;
+            H(n, n) = 1.0;
+            for (int i = n - 2; i >= 0; --i) {
+                double ra = 0.0, sa = 0.0, vr, vi;
+                for (int j = l; j <= n; ++j) {
+                    ra = ra + H(i, j) * H(j, n - 1);
+                    sa = sa + H(i, j) * H(j, n);
+                }
+                w = H(i, i) - p;
+                if (e[i] < 0.0) {
+                    z = w;
+                    r = ra;
+                    s = sa;
+                } else {
+                    l = i;
+                    if (e[i] == 0) {
+                        cdiv(-ra, -sa, w, q, cr, ci);
+                        H(i, n - 1) = cr;
+                        H(i, n) = ci;
+                    } else {
+                        x = H(i, i + 1);
+                        y = H(i + 1, i);
+                        vr = (d[i] - p) * (d[i] - p) + e[i] * e[i] - q * q;
+                        vi = (d[i] - p) * 2.0 * q;
+                        if (vr == 0.0 && vi == 0.0)
+                            vr = eps * norm * (std::fabs(w) + std::fabs(q) + std::fabs(x) + std::fabs(y) + std::fabs(z));
+                        cdiv(x * r - z * ra + q * sa, x * s - z * sa - q * ra, vr, vi, cr, ci);
+                        H(i, n - 1) = cr;
+                        H(i, n) = ci;
+                        if (std::fabs(x) > (std::fabs(z) + std::fabs(q))) {
+                            H(i + 1, n - 1) = (-ra - w * H(i, n - 1) + q * H(i, n)) / x;
+                            H(i + 1, n) = (-sa - w * H(i, n) - q * H(i, n - 1)) / x;
+                        } else {
+                            cdiv(-r - y * H(i, n - 1), -s - y * H(i, n), z, q, cr, ci);
+                            H(i + 1, n - 1) = cr;
+                            H(i + 1, n) = ci;
+                        }
+                    }
+                    t = std::max(std::fabs(H(i, n - 1)), std::fabs(H(i, n)));
+                    if ((eps * t) * t > 1)
+                        for (int j = i; j <= n; ++j) {
+                            H(j, n - 1) = H(j, n - 1) / t;
+                            H(j, n) = H(j, n) / t;
+                        }
+                }
+            }
+        }
+    }
+    for (int j = nn - 1; j >= low; --j)
+        for (int i = low; i <= high; ++i) {
+            z = 0.0;
+            for (int k = low; k <= std::min(j, high); ++k) z = z + V(i, k) * H(k, j);
+            V(i, j) = z;
+        }
+    return true;
+}
+
+}  // namespace
+
+bool eig_general(int n, const double* A, int lda, double* wr, double* wi, double* V, int ldv) {
+    if (n <= 0) return true;
+    Mat H(n), Vm(n);
+    for (int j = 0; j < n; ++j)
+        for (int i = 0; i < n; ++i) H(i, j) = A[i + (size_t)j * lda];
+    std::vector<double> d(n, 0.0), e(n, 0.0);
+    orthes(H, Vm);
+    const bool ok = hqr2(H, Vm, d, e);
+    for (int i = 0; i < n; ++i) {
+        wr[i] = d[i];
+        wi[i] = e[i];
+    }
+    for (int j = 0; j < n; ++j)
+        for (int i = 0; i < n; ++i) V[i + (size_t)j * ldv] = Vm(i, j);
+    return ok;
+}
+
+}  // namespace dense
+}  // namespace cal

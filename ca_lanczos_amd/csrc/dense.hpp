@@ -1,0 +1,36 @@
+// dense.hpp -- small dense host linear algebra for the s x s / (sk) x (sk)
+// matrices of the CA-Lanczos outer loop (no LAPACK dependency).
+// All matrices are column-major: A(i,j) = A[i + j*ld].
+#pragma once
+
+#include <vector>
+
+namespace cal {
+namespace dense {
+
+// Upper Cholesky G = R^T R (m x m).  Returns false if G is not positive
+// definite (a non-positive or non-finite pivot).
+bool chol_upper(int m, const double* G, int ldg, double* R, int ldr);
+// Inverse of an upper-triangular R (m x m) into Ri (upper).
+void tri_inv_upper(int m, const double* R, int ldr, double* Ri, int ldi);
+// C = A (m x k) * B (k x n)
+void matmul(int m, int k, int n, const double* A, int lda, const double* B, int ldb, double* C, int ldc);
+// X (r x m) <- X / R for upper-triangular R (MATLAB right division).
+void rdiv_upper(int r, int m, double* X, int ldx, const double* R, int ldr);
+// Eigenvalues of the symmetric tridiagonal matrix (diag d, off-diagonal e,
+// n-1 entries), ascending.  Implicit QL.
+bool tridiag_eigvals(int n, const double* d, const double* e, double* w);
+// Singular values of a small square matrix (one-sided Jacobi), descending.
+void singular_values(int m, const double* A, int lda, double* sv);
+// General real eigenproblem (Householder Hessenberg reduction + shifted QR,
+// EISPACK orthes/hqr2 algorithm).  A (n x n) is not modified.  On return
+// wr/wi hold the eigenvalues; V (n x n) holds real vectors in the column of a
+// real eigenvalue, and for a complex pair (wi[j] > 0, wi[j+1] = -wi[j])
+// columns j and j+1 hold the real and imaginary part of the eigenvector of
+// wr[j] + i wi[j].  Returns false if QR failed to converge.
+bool eig_general(int n, const double* A, int lda, double* wr, double* wi, double* V, int ldv);
+// Symmetric eigenproblem (Jacobi), ascending, orthonormal vectors.
+void eig_symmetric(int n, const double* A, int lda, double* w, double* V, int ldv);
+
+}  // namespace dense
+}  // namespace cal

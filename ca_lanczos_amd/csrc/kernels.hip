@@ -1,0 +1,607 @@
+// kernels.hip -- hand-written gfx950 (CDNA4) kernels of the CA-Lanczos hot path.
+//
+// Compiled with -ffp-contract=off: every a*b+c below rounds twice, exactly
+// like the reference's (and the oracle's) unfused sparse/dense arithmetic, so
+// the SpMV and the Newton matrix-powers recurrence are bit-identical to a
+// sequential CSR SpMV.  MFMA accumulates inside the matrix core.
+//
+// Kernels:
+//   k_spmv      CSR-stream SpMV: coalesced val/col loads of a row block,
+//               products staged in LDS, sequential per-row sums (bit-exact),
+//               fused Newton shift epilogue (matrix_powers_newton.m:31-47).
+//   k_gram      tall-skinny C = A^T B with v_mfma_f64_16x16x4_f64, per-lane
+//               row runs (16-B loads), deterministic block partials.
+//   k_apply     tall-skinny Y = P M (MFMA), optional fused Y^T Y and
+//               Psub^T Y Grams on the accumulator registers, in-place safe.
+//   k_reduce    fixed-order sum of block partials.
+//   k_dot, k_axpy_sub, k_div, k_gather, k_spmv_resid: small vector kernels.
+#include "cal_internal.hpp"
+
+namespace cal {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+constexpr int kSpmvThreads = 256;
+constexpr int kSpmvNnz = 2048;  // LDS-staged nonzeros per row block (16 KiB)
+
+__device__ __forceinline__ const double* pcol(const Panel& P, int c) {
+#pragma unroll
+    for (int s = 0; s < kMaxSeg; ++s) {
+        if (s < P.nseg) {
+            if (c < P.ncol[s]) return P.ptr[s] + (int64_t)c * P.ld[s];
+            c -= P.ncol[s];
+        }
+    }
+    return P.ptr[0];
+}
+
+__device__ __forceinline__ double* pcol_out(const PanelOut& P, int c) {
+#pragma unroll
+    for (int s = 0; s < kMaxSeg; ++s) {
+        if (s < P.nseg) {
+            if (c < P.ncol[s]) return P.ptr[s] + (int64_t)c * P.ld[s];
+            c -= P.ncol[s];
+        }
+    }
+    return P.ptr[0];
+}
+
+__device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// --------------------------------------------------------------------------
+// SpMV (SpMV.m:8) with the Newton epilogue (matrix_powers_newton.m:28-43)
+// --------------------------------------------------------------------------
+template <int MODE>
+__device__ __forceinline__ double spmv_epilogue(double sum, const SpmvArgs& a, int r) {
+    if (MODE == 0) return sum;
+    double t = a.shift * a.x[r];
+    double y = sum - t;
+    if (MODE == 2) {
+        double u = a.im2 * a.xprev[r];
+        y = y + u;
+    }
+    return y;
+}
+
+template <int MODE, int NIT>
+__global__ __launch_bounds__(kSpmvThreads) void k_spmv(SpmvArgs a) {
+    __shared__ double prod[kSpmvNnz];
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int r0 = a.blk[b], r1 = a.blk[b + 1];
+    const int p0 = a.rowptr[r0], p1 = a.rowptr[r1];
+    const int cnt = p1 - p0;
+    if (cnt <= kSpmvNnz) {
+        if (cnt > 0) {
+            // all loads first (clamped, never branched around: one vmcnt wait
+            // per phase), then the dependent x gathers, then LDS products.
+            const int pl = p1 - 1;
+            int ci[NIT];
+            double v[NIT], xv[NIT];
+#pragma unroll
+            for (int it = 0; it < NIT; ++it) {
+                int p = min(p0 + it * kSpmvThreads + tid, pl);
+                ci[it] = a.col[p];
+                v[it] = a.val[p];
+            }
+#pragma unroll
+            for (int it = 0; it < NIT; ++it) xv[it] = a.x[ci[it]];
+#pragma unroll
+            for (int it = 0; it < NIT; ++it) {
+                int q = it * kSpmvThreads + tid;
+                if (q < cnt) prod[q] = v[it] * xv[it];
+            }
+        }
+        __syncthreads();
+        const int r = r0 + tid;
+        if (r < r1) {
+            const int q0 = a.rowptr[r] - p0, q1 = a.rowptr[r + 1] - p0;
+            double sum = 0.0;
+            for (int j = q0; j < q1; ++j) sum = sum + prod[j];
+            a.y[r] = spmv_epilogue<MODE>(sum, a, r);
+        }
+    } else {
+        // one long row (> kSpmvNnz nonzeros): chunked, still summed in order
+        double sum = 0.0;
+        for (int c = p0; c < p1; c += kSpmvNnz) {
+            const int m = min(kSpmvNnz, p1 - c);
+            for (int q = tid; q < m; q += kSpmvThreads) prod[q] = a.val[c + q] * a.x[a.col[c + q]];
+            __syncthreads();
+            if (tid == 0)
+                for (int j = 0; j < m; ++j) sum = sum + prod[j];
+            __syncthreads();
+        }
+        if (tid == 0) a.y[r0] = spmv_epilogue<MODE>(sum, a, r0);
+    }
+}
+
+template <int MODE>
+static hipError_t launch_spmv_mode(const SpmvArgs& a, int nit, hipStream_t st) {
+    dim3 g(a.nblk), b(kSpmvThreads);
+    switch (nit) {
+        case 1: hipLaunchKernelGGL((k_spmv<MODE, 1>), g, b, 0, st, a); break;
+        case 2: hipLaunchKernelGGL((k_spmv<MODE, 2>), g, b, 0, st, a); break;
+        case 3: hipLaunchKernelGGL((k_spmv<MODE, 3>), g, b, 0, st, a); break;
+        case 4: hipLaunchKernelGGL((k_spmv<MODE, 4>), g, b, 0, st, a); break;
+        case 5: hipLaunchKernelGGL((k_spmv<MODE, 5>), g, b, 0, st, a); break;
+        case 6: hipLaunchKernelGGL((k_spmv<MODE, 6>), g, b, 0, st, a); break;
+        case 7: hipLaunchKernelGGL((k_spmv<MODE, 7>), g, b, 0, st, a); break;
+        default: hipLaunchKernelGGL((k_spmv<MODE, 8>), g, b, 0, st, a); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_spmv(const SpmvArgs& a, hipStream_t st) {
+    if (a.nblk <= 0) return hipSuccess;
+    // a.mode carries the per-matrix iteration count in bits 8..15
+    const int nit = (a.mode >> 8) & 0xff;
+    switch (a.mode & 0xff) {
+        case 0: return launch_spmv_mode<0>(a, nit, st);
+        case 1: return launch_spmv_mode<1>(a, nit, st);
+        default: return launch_spmv_mode<2>(a, nit, st);
+    }
+}
+
+// --------------------------------------------------------------------------
+// Gram: C = A^T B (MFMA f64 16x16x4).  A: up to 16*NTA columns, B: <= 16.
+// Lane l owns column (l&15) of every 16-column tile and rows g*RUN..g*RUN+RUN-1
+// (g = l>>4) of each 4*RUN-row wave step: MFMA k index = g, so A-operand
+// A[i][k] = A(row_k, i) and B-operand B[k][j] = B(row_k, j) are plain loads.
+// Output tile layout (f64 16x16x4): lane l, reg r -> C[(l>>4)+4r][l&15].
+// Block partial: column-major 16*NTA x 16 (ld 16*NTA).
+// --------------------------------------------------------------------------
+template <int NTA, int RUN>
+__global__ __launch_bounds__(256) void k_gram(Panel A, Panel B, int64_t n, double* __restrict__ partial) {
+    __shared__ double red[3][NTA][64][4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int c16 = lane & 15, g = lane >> 4;
+    const double* ac[NTA];
+    bool aon[NTA];
+#pragma unroll
+    for (int t = 0; t < NTA; ++t) {
+        const int c = t * 16 + c16;
+        aon[t] = c < A.total;
+        ac[t] = pcol(A, aon[t] ? c : 0);
+    }
+    const bool bon = c16 < B.total;
+    const double* bc = pcol(B, bon ? c16 : 0);
+    d4 acc[NTA];
+#pragma unroll
+    for (int t = 0; t < NTA; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+
+    const int64_t wstep = 4 * RUN;
+    const int64_t stride = (int64_t)gridDim.x * 4 * wstep;
+    for (int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * wstep; r0 < n; r0 += stride) {
+        const int64_t rb = r0 + g * RUN;
+        double av[NTA][RUN], bv[RUN];
+        if (r0 + wstep <= n) {
+            if (RUN % 2 == 0) {
+#pragma unroll
+                for (int m = 0; m < RUN; m += 2) {
+                    d2 x = *reinterpret_cast<const d2*>(bc + rb + m);
+                    bv[m] = bon ? x[0] : 0.0;
+                    bv[m + 1] = bon ? x[1] : 0.0;
+#pragma unroll
+                    for (int t = 0; t < NTA; ++t) {
+                        d2 y = *reinterpret_cast<const d2*>(ac[t] + rb + m);
+                        av[t][m] = aon[t] ? y[0] : 0.0;
+                        av[t][m + 1] = aon[t] ? y[1] : 0.0;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int m = 0; m < RUN; ++m) {
+                    bv[m] = bon ? bc[rb + m] : 0.0;
+#pragma unroll
+                    for (int t = 0; t < NTA; ++t) av[t][m] = aon[t] ? ac[t][rb + m] : 0.0;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < RUN; ++m) {
+                const bool in = rb + m < n;
+                const int64_t rr = in ? rb + m : 0;
+                double x = bc[rr];
+                bv[m] = (bon && in) ? x : 0.0;
+#pragma unroll
+                for (int t = 0; t < NTA; ++t) {
+                    double y = ac[t][rr];
+                    av[t][m] = (aon[t] && in) ? y : 0.0;
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < RUN; ++m)
+#pragma unroll
+            for (int t = 0; t < NTA; ++t) acc[t] = mfma64(av[t][m], bv[m], acc[t]);
+    }
+    // deterministic block reduction: waves 1..3 park, wave 0 adds in order
+    if (wave > 0) {
+#pragma unroll
+        for (int t = 0; t < NTA; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[wave - 1][t][lane][r] = acc[t][r];
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const int ldc = 16 * NTA;
+        double* out = partial + (int64_t)blockIdx.x * (ldc * 16);
+#pragma unroll
+        for (int t = 0; t < NTA; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                double v = acc[t][r];
+                v = v + red[0][t][lane][r];
+                v = v + red[1][t][lane][r];
+                v = v + red[2][t][lane][r];
+                const int i = t * 16 + g + 4 * r, j = c16;
+                out[j * ldc + i] = v;
+            }
+    }
+}
+
+GramPlan gram_plan(int wa, int wb, int64_t n) {
+    (void)wb;
+    GramPlan p;
+    p.nta = (wa + 15) / 16;
+    if (p.nta < 1) p.nta = 1;
+    const int run = p.nta <= 2 ? 16 : (p.nta <= 4 ? 8 : 4);
+    int64_t blocks = (n + 16 * run - 1) / (16 * run);
+    if (blocks > 2048) blocks = 2048;
+    if (blocks < 1) blocks = 1;
+    p.blocks = (int)blocks;
+    p.entries = (int64_t)16 * p.nta * 16;
+    return p;
+}
+
+hipError_t launch_gram(const Panel& A, const Panel& B, int64_t n, const GramPlan& pl, double* partial,
+                       hipStream_t st) {
+    dim3 g(pl.blocks), b(256);
+    switch (pl.nta) {
+        case 1: hipLaunchKernelGGL((k_gram<1, 16>), g, b, 0, st, A, B, n, partial); break;
+        case 2: hipLaunchKernelGGL((k_gram<2, 16>), g, b, 0, st, A, B, n, partial); break;
+        case 3: hipLaunchKernelGGL((k_gram<3, 8>), g, b, 0, st, A, B, n, partial); break;
+        case 4: hipLaunchKernelGGL((k_gram<4, 8>), g, b, 0, st, A, B, n, partial); break;
+        case 5: hipLaunchKernelGGL((k_gram<5, 4>), g, b, 0, st, A, B, n, partial); break;
+        case 6: hipLaunchKernelGGL((k_gram<6, 4>), g, b, 0, st, A, B, n, partial); break;
+        case 7: hipLaunchKernelGGL((k_gram<7, 4>), g, b, 0, st, A, B, n, partial); break;
+        case 8: hipLaunchKernelGGL((k_gram<8, 4>), g, b, 0, st, A, B, n, partial); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// --------------------------------------------------------------------------
+// Apply: Y = P M (+ optional Y^T Y and Psub^T Y).  MFMA A-operand = P rows:
+// lane l holds P(row r0 + (l&15)*RUN + t, col 4*kc + (l>>4)) for tile t; the
+// B-operand M(4*kc + (l>>4), 16*ty + (l&15)) comes from LDS.  Accumulator
+// tile (ty,t) reg r holds Y(row r0 + ((l>>4)+4r)*RUN + t, col 16*ty + (l&15)),
+// which is directly the A and B operand of the fused Gram MFMAs (k = l>>4).
+// --------------------------------------------------------------------------
+template <int NTY, int RUN, bool GRAM, bool GRAMP, bool STORE>
+__global__ __launch_bounds__(256) void k_apply(Panel P, const double* __restrict__ M, int wp, int wy,
+                                               PanelOut Y, int wq, int64_t n,
+                                               double* __restrict__ partial) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int wpp = (wp + 3) & ~3;
+    const int ldm = 16 * NTY;
+    double* Ms = smem;                      // [wpp][ldm]
+    double* red = smem + (size_t)wpp * ldm;  // [3][2][64][4]
+    for (int e = threadIdx.x; e < wpp * ldm; e += 256) {
+        const int k = e / ldm, j = e % ldm;
+        Ms[e] = (k < wp && j < wy) ? M[(int64_t)j * wp + k] : 0.0;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int c16 = lane & 15, g = lane >> 4;
+    const int nkc = wpp / 4;
+    d4 gacc = d4{0.0, 0.0, 0.0, 0.0}, gpacc = d4{0.0, 0.0, 0.0, 0.0};
+    const bool qon = c16 < wq;
+    const double* qc = pcol(P, qon ? c16 : 0);
+
+    const int64_t wstep = 16 * RUN;
+    const int64_t stride = (int64_t)gridDim.x * 4 * wstep;
+    for (int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * wstep; r0 < n; r0 += stride) {
+        const bool full = r0 + wstep <= n;
+        d4 acc[NTY][RUN];
+#pragma unroll
+        for (int ty = 0; ty < NTY; ++ty)
+#pragma unroll
+            for (int t = 0; t < RUN; ++t) acc[ty][t] = d4{0.0, 0.0, 0.0, 0.0};
+        const int64_t ra = r0 + (int64_t)c16 * RUN;  // this lane's A-operand rows
+        for (int kc = 0; kc < nkc; ++kc) {
+            const int c = kc * 4 + g;
+            const bool con = c < wp;
+            const double* pc = pcol(P, con ? c : 0);
+            double av[RUN];
+            if (full && RUN % 2 == 0) {
+#pragma unroll
+                for (int t = 0; t < RUN; t += 2) {
+                    d2 x = *reinterpret_cast<const d2*>(pc + ra + t);
+                    av[t] = con ? x[0] : 0.0;
+                    av[t + 1] = con ? x[1] : 0.0;
+                }
+            } else {
+#pragma unroll
+                for (int t = 0; t < RUN; ++t) {
+                    const bool in = ra + t < n;
+                    double x = pc[in ? ra + t : 0];
+                    av[t] = (con && in) ? x : 0.0;
+                }
+            }
+#pragma unroll
+            for (int ty = 0; ty < NTY; ++ty) {
+                const double bm = Ms[(kc * 4 + g) * ldm + ty * 16 + c16];
+#pragma unroll
+                for (int t = 0; t < RUN; ++t) acc[ty][t] = mfma64(av[t], bm, acc[ty][t]);
+            }
+        }
+        if (STORE) {
+#pragma unroll
+            for (int ty = 0; ty < NTY; ++ty) {
+                const int j = ty * 16 + c16;
+                if (j < wy) {
+                    double* yc = pcol_out(Y, j);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int64_t rr = r0 + (int64_t)(g + 4 * r) * RUN;
+                        if (full && RUN % 2 == 0) {
+#pragma unroll
+                            for (int t = 0; t < RUN; t += 2) {
+                                d2 x;
+                                x[0] = acc[ty][t][r];
+                                x[1] = acc[ty][t + 1][r];
+                                *reinterpret_cast<d2*>(yc + rr + t) = x;
+                            }
+                        } else {
+#pragma unroll
+                            for (int t = 0; t < RUN; ++t)
+                                if (rr + t < n) yc[rr + t] = acc[ty][t][r];
+                        }
+                    }
+                }
+            }
+        }
+        if (GRAM) {
+#pragma unroll
+            for (int t = 0; t < RUN; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) gacc = mfma64(acc[0][t][r], acc[0][t][r], gacc);
+        }
+        if (GRAMP) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t rr = r0 + (int64_t)(g + 4 * r) * RUN;
+#pragma unroll
+                for (int t = 0; t < RUN; ++t) {
+                    const bool in = rr + t < n;
+                    double x = qc[in ? rr + t : 0];
+                    const double qv = (qon && in) ? x : 0.0;
+                    gpacc = mfma64(qv, acc[0][t][r], gpacc);
+                }
+            }
+        }
+    }
+    if (GRAM || GRAMP) {
+        __syncthreads();
+        if (wave > 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                red[(((wave - 1) * 2 + 0) * 64 + lane) * 4 + r] = gacc[r];
+                red[(((wave - 1) * 2 + 1) * 64 + lane) * 4 + r] = gpacc[r];
+            }
+        }
+        __syncthreads();
+        if (wave == 0) {
+            const int nent = 256 * ((GRAM ? 1 : 0) + (GRAMP ? 1 : 0));
+            double* out = partial + (int64_t)blockIdx.x * nent;
+            int base = 0;
+#pragma unroll
+            for (int which = 0; which < 2; ++which) {
+                if ((which == 0 && !GRAM) || (which == 1 && !GRAMP)) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    double v = which == 0 ? gacc[r] : gpacc[r];
+                    v = v + red[((0 * 2 + which) * 64 + lane) * 4 + r];
+                    v = v + red[((1 * 2 + which) * 64 + lane) * 4 + r];
+                    v = v + red[((2 * 2 + which) * 64 + lane) * 4 + r];
+                    const int i = g + 4 * r, j = c16;
+                    out[base + j * 16 + i] = v;
+                }
+                base += 256;
+            }
+        }
+    }
+}
+
+ApplyPlan apply_plan(int wp, int wy, int64_t n, bool gram, int wq) {
+    ApplyPlan p;
+    p.nty = wy <= 16 ? 1 : (wy <= 32 ? 2 : (wy <= 64 ? 4 : 8));
+    p.run = p.nty == 1 ? 4 : (p.nty == 2 ? 2 : 1);
+    p.gram = gram && p.nty == 1;
+    p.gramp = wq > 0 && p.nty == 1;
+    int64_t blocks = (n + 64 * p.run - 1) / (64 * p.run);
+    if (blocks > 2048) blocks = 2048;
+    if (blocks < 1) blocks = 1;
+    p.blocks = (int)blocks;
+    const int wpp = (wp + 3) & ~3;
+    p.lds_bytes = sizeof(double) * ((size_t)wpp * 16 * p.nty + 3 * 2 * 64 * 4);
+    p.entries = 256 * ((p.gram ? 1 : 0) + (p.gramp ? 1 : 0));
+    return p;
+}
+
+hipError_t launch_apply(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y, bool store,
+                        int wq, int64_t n, const ApplyPlan& pl, double* partial, hipStream_t st) {
+    dim3 g(pl.blocks), b(256);
+    const size_t sh = pl.lds_bytes;
+#define CAL_APPLY(NTY, RUN, G, GP, S) \
+    hipLaunchKernelGGL((k_apply<NTY, RUN, G, GP, S>), g, b, sh, st, P, dM, wp, wy, Y, wq, n, partial)
+    if (pl.nty == 1) {
+        const int key = (pl.gram ? 4 : 0) | (pl.gramp ? 2 : 0) | (store ? 1 : 0);
+        switch (key) {
+            case 1: CAL_APPLY(1, 4, false, false, true); break;
+            case 2: CAL_APPLY(1, 4, false, true, false); break;
+            case 3: CAL_APPLY(1, 4, false, true, true); break;
+            case 4: CAL_APPLY(1, 4, true, false, false); break;
+            case 5: CAL_APPLY(1, 4, true, false, true); break;
+            case 6: CAL_APPLY(1, 4, true, true, false); break;
+            case 7: CAL_APPLY(1, 4, true, true, true); break;
+            default: return hipErrorInvalidValue;
+        }
+    } else {
+        if (!store) return hipErrorInvalidValue;
+        switch (pl.nty) {
+            case 2: CAL_APPLY(2, 2, false, false, true); break;
+            case 4: CAL_APPLY(4, 1, false, false, true); break;
+            case 8: CAL_APPLY(8, 1, false, false, true); break;
+            default: return hipErrorInvalidValue;
+        }
+    }
+#undef CAL_APPLY
+    return hipGetLastError();
+}
+
+// --------------------------------------------------------------------------
+// fixed-order partial reduction and small vector kernels
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_reduce(const double* __restrict__ part, int nparts, int64_t nent,
+                                                double* __restrict__ out) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= nent) return;
+    double s = 0.0;
+    for (int p = 0; p < nparts; ++p) s = s + part[(int64_t)p * nent + e];
+    out[e] = s;
+}
+
+hipError_t launch_reduce(const double* partial, int nparts, int64_t nent, double* out, hipStream_t st) {
+    dim3 g((unsigned)((nent + 255) / 256)), b(256);
+    hipLaunchKernelGGL(k_reduce, g, b, 0, st, partial, nparts, nent, out);
+    return hipGetLastError();
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = v + __shfl_xor(v, off, 64);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_dot(const double* __restrict__ x, const double* __restrict__ y,
+                                             int64_t n, double* __restrict__ partial) {
+    __shared__ double ws[4];
+    double s = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) s = s + x[i] * y[i];
+    s = wave_sum(s);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) ws[wave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) partial[blockIdx.x] = ((ws[0] + ws[1]) + ws[2]) + ws[3];
+}
+
+int dot_blocks(int64_t n) {
+    int64_t b = (n + 255) / 256;
+    if (b > 1024) b = 1024;
+    if (b < 1) b = 1;
+    return (int)b;
+}
+
+hipError_t launch_dot(const double* x, const double* y, int64_t n, double* partial, int blocks,
+                      hipStream_t st) {
+    hipLaunchKernelGGL(k_dot, dim3(blocks), dim3(256), 0, st, x, y, n, partial);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_axpy_sub(double* __restrict__ y, const double* __restrict__ x, double a,
+                                                  int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const double t = a * x[i];
+        y[i] = y[i] - t;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_div(double* __restrict__ y, const double* __restrict__ x, double b,
+                                             int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) y[i] = x[i] / b;
+}
+
+__global__ __launch_bounds__(256) void k_gather(double* __restrict__ dst, const double* __restrict__ src,
+                                                const int* __restrict__ idx, int64_t cnt) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < cnt) dst[i] = src[idx[i]];
+}
+
+static unsigned vec_blocks(int64_t n) {
+    int64_t b = (n + 255) / 256;
+    if (b > 4096) b = 4096;
+    if (b < 1) b = 1;
+    return (unsigned)b;
+}
+
+hipError_t launch_axpy_sub(double* y, const double* x, double a, int64_t n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_axpy_sub, dim3(vec_blocks(n)), dim3(256), 0, st, y, x, a, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_div(double* y, const double* x, double b, int64_t n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_div, dim3(vec_blocks(n)), dim3(256), 0, st, y, x, b, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather(double* dst, const double* src, const int* idx, int64_t cnt, hipStream_t st) {
+    if (cnt <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gather, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, dst, src, idx, cnt);
+    return hipGetLastError();
+}
+
+// --------------------------------------------------------------------------
+// Ritz residual (compute_ritz_rnorm, ca_lanczos.m:92-96) for one Ritz pair:
+// x = xr + i xi, l = lr + i li; partial[2b] = sum |A x - l x|^2,
+// partial[2b+1] = sum |l x|^2 over the rows of block b.
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_spmv_resid(SpmvArgs a, const double* __restrict__ xi, double lr,
+                                                    double li, int64_t nrows, double* __restrict__ partial) {
+    __shared__ double ws[2][4];
+    double s_num = 0.0, s_den = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < nrows; r += stride) {
+        double axr = 0.0, axi = 0.0;
+        for (int j = a.rowptr[r]; j < a.rowptr[r + 1]; ++j) {
+            const int c = a.col[j];
+            axr = axr + a.val[j] * a.x[c];
+            if (xi) axi = axi + a.val[j] * xi[c];
+        }
+        const double xr_ = a.x[r], xi_ = xi ? xi[r] : 0.0;
+        const double lxr = lr * xr_ - li * xi_;
+        const double lxi = lr * xi_ + li * xr_;
+        const double er = axr - lxr, ei = axi - lxi;
+        s_num = s_num + (er * er + ei * ei);
+        s_den = s_den + (lxr * lxr + lxi * lxi);
+    }
+    s_num = wave_sum(s_num);
+    s_den = wave_sum(s_den);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+        ws[0][wave] = s_num;
+        ws[1][wave] = s_den;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        partial[2 * blockIdx.x] = ((ws[0][0] + ws[0][1]) + ws[0][2]) + ws[0][3];
+        partial[2 * blockIdx.x + 1] = ((ws[1][0] + ws[1][1]) + ws[1][2]) + ws[1][3];
+    }
+}
+
+hipError_t launch_spmv_resid(const SpmvArgs& a, const double* xi, double lr, double li, int64_t nrows,
+                             double* partial, int blocks, hipStream_t st) {
+    hipLaunchKernelGGL(k_spmv_resid, dim3(blocks), dim3(256), 0, st, a, xi, lr, li, nrows, partial);
+    return hipGetLastError();
+}
+
+}  // namespace cal

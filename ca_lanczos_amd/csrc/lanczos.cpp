@@ -1,0 +1,516 @@
+// lanczos.cpp -- the device-resident CA-Lanczos outer loop (ca_lanczos.m).
+//
+//   begin():  q = r/sqrt(r'r) (ca_lanczos.m:55); change of basis Bk: monomial
+//             (:63-65) or Newton (:66-72: 2s-step Lanczos 'fro' on the GPU,
+//             eig + modified Leja + newton_basis_matrix on the host).
+//   step():   one outer iteration (:166-237): s fused SpMV+shift launches
+//             into V, block orthogonalisation (normalize at k=1,
+//             projectAndNormalize against the previous block otherwise, plus
+//             the 'fro' pass against all of Q), the host-side T extension
+//             (:200-223) and, optionally, the Ritz residuals / orthogonality
+//             error diagnostics (:228-236).
+// Only (s+1) x s, s x s and (2s+1) x s matrices cross PCIe per iteration.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <complex>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/calanczos_host.h"
+#include "cal_internal.hpp"
+#include "comm.hpp"
+#include "dense.hpp"
+#include "leja.hpp"
+
+namespace cal {
+
+struct LanczosState {
+    int s = 0, max_outer = 0, k = 0;
+    bool newton = false, full = false;
+    int64_t n = 0, ld = 0;
+    double* dQ = nullptr;  // ld x (s*max_outer + 1)
+    double* dV = nullptr;  // ld x (s+1)
+    std::vector<double> Bk;  // (s+1) x s
+    int Tld = 0;
+    std::vector<double> T;  // Tld x Tld
+    std::vector<double> b;
+    std::vector<int> reorth;
+    std::vector<std::vector<double>> rn;
+    std::vector<double> oe;
+    cal_lanczos_info info{};
+    bool breakdown = false;
+    double* col(int j) { return dQ + (size_t)j * ld; }
+};
+
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// global dot product x'y of two device n-vectors (allreduced)
+static int dot_host(cal_ctx* c, int64_t n, const double* x, const double* y, double* out) {
+    const int nb = dot_blocks(n);
+    CAL_TRY(ensure_partial(c, nb));
+    CAL_TRY(ensure_red(c, 1));
+    CAL_HIP(c, launch_dot(x, y, n, c->d_partial, nb, c->stream));
+    CAL_HIP(c, launch_reduce(c->d_partial, nb, 1, c->d_red, c->stream));
+    CAL_TRY(allreduce_sum(c, c->d_red, 1));
+    CAL_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    c->small_pending = false;
+    *out = c->h_red[0];
+    return 0;
+}
+
+// ---- Newton prologue: lanczos(A,q,2s,'full') (lanczos.m:18-134) ----------
+static int newton_prologue(cal_ctx* c, LanczosState& L) {
+    const int s = L.s, m = 2 * s;
+    const int64_t n = c->A.n_local, ld = c->A.ld;
+    CAL_TRY(ensure_work(c, m + 2, ld));
+    double* r = work_col(c, m + 1);
+    auto Qc = [&](int j) { return work_col(c, j); };
+    // q = r/norm(r) (lanczos.m:47) of the already normalised start vector
+    double nrm2 = 0.0;
+    CAL_TRY(dot_host(c, n, L.col(0), L.col(0), &nrm2));
+    CAL_HIP(c, launch_div(Qc(0), L.col(0), std::sqrt(nrm2), n, c->stream));
+    std::vector<double> alpha(m), beta(m);
+    for (int j = 0; j < m; ++j) {
+        CAL_TRY(spmv_dev(c, Qc(j), r, 0, 0.0, 0.0, nullptr));  // :103
+        if (j > 0) CAL_HIP(c, launch_axpy_sub(r, Qc(j - 1), beta[j - 1], n, c->stream));  // :105
+        CAL_TRY(dot_host(c, n, r, Qc(j), &alpha[j]));                                       // :107
+        CAL_HIP(c, launch_axpy_sub(r, Qc(j), alpha[j], n, c->stream));                      // :108
+        double rr = 0.0;
+        CAL_TRY(dot_host(c, n, r, r, &rr));
+        beta[j] = std::sqrt(rr);  // :109
+        if (!(beta[j] > 0.0) || !std::isfinite(beta[j])) {
+            L.breakdown = true;
+            return set_error(c, CAL_ERR_NUMERIC, "Lanczos breakdown (beta = 0) in the Newton prologue");
+        }
+        CAL_HIP(c, launch_div(Qc(j + 1), r, beta[j], n, c->stream));  // :110
+        // one CGS pass against Q(:,1:j) (lanczos.m:62-66)
+        Panel Qj = panel();
+        panel_add(Qj, Qc(0), ld, j + 1);
+        Panel qn = panel();
+        panel_add(qn, Qc(j + 1), ld, 1);
+        std::vector<double> Rkk(j + 1), M(j + 2);
+        CAL_TRY(gram_host(c, n, Qj, qn, Rkk.data()));
+        for (int i = 0; i <= j; ++i) M[i] = -Rkk[i];
+        M[j + 1] = 1.0;
+        Panel W = panel();
+        panel_add(W, Qc(0), ld, j + 2);  // [Q(:,1:j) | q_{j+1}] contiguous
+        PanelOut out = panel_out(Qc(j + 1), ld, 1);
+        CAL_TRY(apply_host(c, n, W, M.data(), 1, &out, nullptr, 0, nullptr));
+    }
+    // eig(T) of the 2s x 2s symmetric tridiagonal (ca_lanczos.m:69): ascending
+    std::vector<double> w(m);
+    if (!dense::tridiag_eigvals(m, alpha.data(), beta.data(), w.data()))
+        return set_error(c, CAL_ERR_NUMERIC, "tridiagonal eigensolver did not converge");
+    std::vector<std::complex<double>> x(m), y;
+    for (int i = 0; i < m; ++i) x[i] = std::complex<double>(w[i], 0.0);
+    std::vector<int> oi;
+    std::string err;
+    if (leja::real_leja(x, y, oi, err) != 0) return set_error(c, CAL_ERR_NUMERIC, "leja: " + err);  // :70
+    for (int i = 0; i < m && i < 64; ++i) {
+        L.info.shifts[i] = y[i].real();
+        L.info.shifts_im[i] = y[i].imag();
+    }
+    if (leja::newton_basis_matrix(s, y, 1, L.Bk, err) != 0)  // :71
+        return set_error(c, CAL_ERR_NUMERIC, "newton_basis_matrix: " + err);
+    return 0;
+}
+
+// ---- Ritz residuals (compute_ritz_rnorm, ca_lanczos.m:88-97) --------------
+struct RitzPair {
+    double lr, li;
+    int cr, ci;  // columns of the real / imaginary part in V (ci = -1: real)
+};
+
+static void matlab_sort_desc(std::vector<RitzPair>& v, bool cplx) {
+    std::stable_sort(v.begin(), v.end(), [&](const RitzPair& a, const RitzPair& b) {
+        if (!cplx) return a.lr > b.lr;
+        const double aa = std::hypot(a.lr, a.li), ab = std::hypot(b.lr, b.li);
+        if (aa != ab) return aa > ab;
+        return std::atan2(a.li, a.lr) > std::atan2(b.li, b.lr);
+    });
+}
+
+static int ritz_diagnostics(cal_ctx* c, LanczosState& L) {
+    const int s = L.s, k = L.k, sk = s * k;
+    const int64_t n = c->A.n_local, ld = c->A.ld;
+    // eig(T(1:sk,1:sk)) (ca_lanczos.m:229)
+    std::vector<double> Tk((size_t)sk * sk), wr(sk), wi(sk), V((size_t)sk * sk);
+    for (int j = 0; j < sk; ++j)
+        for (int i = 0; i < sk; ++i) Tk[i + (size_t)j * sk] = L.T[i + (size_t)j * L.Tld];
+    if (cal_eig(sk, Tk.data(), sk, wr.data(), wi.data(), V.data()) != 0)
+        return set_error(c, CAL_ERR_NUMERIC, "eig(T) did not converge");
+    std::vector<RitzPair> pairs;
+    bool cplx = false;
+    for (int j = 0; j < sk; ++j) {
+        if (wi[j] != 0.0) {
+            cplx = true;
+            // V(:,j) + i V(:,j+1) belongs to wr + i|wi|; the conjugate uses the
+            // conjugate vector (same residual norm)
+            const int jr = wi[j] > 0 ? j : j - 1;
+            pairs.push_back({wr[j], wi[j], jr, jr + 1});
+        } else {
+            pairs.push_back({wr[j], 0.0, j, -1});
+        }
+    }
+    matlab_sort_desc(pairs, cplx);
+    // X = Q(:,1:sk) * V on the GPU (MFMA apply), into work columns
+    CAL_TRY(ensure_work(c, sk, ld));
+    Panel Qp = panel();
+    panel_add(Qp, L.col(0), ld, sk);
+    PanelOut X = panel_out(work_col(c, 0), ld, sk);
+    CAL_TRY(apply_host(c, n, Qp, V.data(), sk, &X, nullptr, 0, nullptr));
+    // ||A x - l x|| / ||l x|| per Ritz pair: fused SpMV + residual partials
+    const int nb = 256;
+    CAL_TRY(ensure_partial(c, (size_t)nb * 2 * sk));
+    CAL_TRY(ensure_red(c, 2 * sk));
+    for (int i = 0; i < sk; ++i) {
+        const RitzPair& p = pairs[i];
+        double* xr = work_col(c, p.cr);
+        double* xi = p.ci >= 0 ? work_col(c, p.ci) : nullptr;
+        CAL_TRY(halo_exchange(c, xr));
+        if (xi) CAL_TRY(halo_exchange(c, xi));
+        SpmvArgs a{};
+        a.rowptr = c->A.rowptr;
+        a.col = c->A.col;
+        a.val = c->A.val;
+        a.x = xr;
+        const int t = timer_begin(c, 3);
+        CAL_HIP(c, launch_spmv_resid(a, xi, p.lr, p.li, n, c->d_partial + (size_t)i * nb * 2, nb, c->stream));
+        timer_end(c, t);
+        CAL_HIP(c, launch_reduce(c->d_partial + (size_t)i * nb * 2, nb, 2, c->d_red + 2 * i, c->stream));
+    }
+    CAL_TRY(allreduce_sum(c, c->d_red, 2 * sk));
+    CAL_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, 2 * sk * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    c->small_pending = false;
+    std::vector<double> rn(sk);
+    for (int i = 0; i < sk; ++i) rn[i] = std::sqrt(c->h_red[2 * i]) / std::sqrt(c->h_red[2 * i + 1]);
+    L.rn.push_back(rn);
+    // orthogonality error (compute_orth_err, ca_lanczos.m:99-107)
+    const int j = sk + 1;
+    double oe = 0.0;
+    if (j > s + 1) {
+        const int wa = j - s - 1;
+        Panel A1 = panel(), B1 = panel();
+        panel_add(A1, L.col(0), ld, wa);
+        panel_add(B1, L.col(wa), ld, s + 1);
+        std::vector<double> G((size_t)wa * (s + 1));
+        CAL_TRY(gram_host(c, n, A1, B1, G.data()));
+        for (double g : G) oe = std::max(oe, std::fabs(g));
+    } else {
+        Panel A1 = panel();
+        panel_add(A1, L.col(0), ld, s + 1);
+        std::vector<double> G((size_t)(s + 1) * (s + 1));
+        CAL_TRY(gram_host(c, n, A1, A1, G.data()));
+        for (int jj = 0; jj <= s; ++jj)
+            for (int ii = 0; ii <= s; ++ii)
+                oe = std::max(oe, std::fabs(G[ii + (size_t)jj * (s + 1)] - (ii == jj ? 1.0 : 0.0)));
+    }
+    L.oe.push_back(oe);
+    return 0;
+}
+
+// ---- T extension (ca_lanczos.m:176-223) -----------------------------------
+static int extend_T_first(cal_ctx* c, LanczosState& L, const std::vector<double>& Rk) {
+    const int s = L.s, s1 = s + 1;
+    // T = Rk*Bk/Rk(1:s,1:s)   ((s+1) x s)
+    std::vector<double> RB((size_t)s1 * s), R11((size_t)s * s);
+    dense::matmul(s1, s1, s, Rk.data(), s1, L.Bk.data(), s1, RB.data(), s1);
+    for (int j = 0; j < s; ++j)
+        for (int i = 0; i < s; ++i) R11[i + (size_t)j * s] = Rk[i + (size_t)j * s1];
+    if (R11[(s - 1) + (size_t)(s - 1) * s] == 0.0) {
+        L.breakdown = true;
+        return CAL_WARN_BREAKDOWN;
+    }
+    dense::rdiv_upper(s1, s, RB.data(), s1, R11.data(), s);
+    for (int j = 0; j < s; ++j)
+        for (int i = 0; i < s1; ++i) L.T[i + (size_t)j * L.Tld] = RB[i + (size_t)j * s1];
+    L.b.assign(1, RB[s + (size_t)(s - 1) * s1]);  // b(1) = T(s+1,s)
+    return 0;
+}
+
+static int extend_T(cal_ctx* c, LanczosState& L, const std::vector<double>& Rkk_s, const std::vector<double>& Rk_s) {
+    (void)c;
+    const int s = L.s, s1 = s + 1, k = L.k;
+    // Rk = [e1, [Rkk_s(s+1,1:s); Rk_s]]  ((s+1) x (s+1))
+    std::vector<double> Rk((size_t)s1 * s1, 0.0);
+    Rk[0] = 1.0;
+    for (int j = 1; j <= s; ++j) {
+        Rk[0 + (size_t)j * s1] = Rkk_s[s + (size_t)(j - 1) * s1];
+        for (int i = 1; i <= s; ++i) Rk[i + (size_t)j * s1] = Rk_s[(i - 1) + (size_t)(j - 1) * s];
+    }
+    std::vector<double> R11((size_t)s * s), Rkk11((size_t)s * s, 0.0);
+    for (int j = 0; j < s; ++j)
+        for (int i = 0; i < s; ++i) R11[i + (size_t)j * s] = Rk[i + (size_t)j * s1];
+    // Rkk = [zeros(s,1), Rkk_s(1:s,:)] -> Rkk(1:s,1:s) = [0, Rkk_s(1:s,1:s-1)]
+    for (int j = 1; j < s; ++j)
+        for (int i = 0; i < s; ++i) Rkk11[i + (size_t)j * s] = Rkk_s[i + (size_t)(j - 1) * s1];
+    const double rho = Rk[s + (size_t)s * s1];
+    const double rho_t = Rk[(s - 1) + (size_t)(s - 1) * s1];
+    const double bk = L.Bk[s + (size_t)(s - 1) * s1];
+    const double bprev = L.b[k - 2];
+    if (rho_t == 0.0) {
+        L.breakdown = true;
+        return CAL_WARN_BREAKDOWN;
+    }
+    // term1 = R11*Bk(1:s,:)/R11
+    std::vector<double> B11((size_t)s * s), t1((size_t)s * s), t3((size_t)s * s, 0.0);
+    for (int j = 0; j < s; ++j)
+        for (int i = 0; i < s; ++i) B11[i + (size_t)j * s] = L.Bk[i + (size_t)j * s1];
+    dense::matmul(s, s, s, R11.data(), s, B11.data(), s, t1.data(), s);
+    dense::rdiv_upper(s, s, t1.data(), s, R11.data(), s);
+    // term2 = ((bk/rho_t)*zk)*es'  (last column only)
+    const double f = bk / rho_t;
+    // term3 = (((b(k-1)*e1)*es')*Rkk(1:s,1:s))/R11  (first row only)
+    for (int j = 0; j < s; ++j) t3[0 + (size_t)j * s] = bprev * Rkk11[(s - 1) + (size_t)j * s];
+    dense::rdiv_upper(s, s, t3.data(), s, R11.data(), s);
+    const int m0 = s * (k - 1);
+    for (int j = 0; j < s; ++j)
+        for (int i = 0; i < s; ++i) {
+            double v = t1[i + (size_t)j * s];
+            if (j == s - 1) v = v + f * Rk[i + (size_t)s * s1];
+            v = v - t3[i + (size_t)j * s];
+            L.T[(m0 + i) + (size_t)(m0 + j) * L.Tld] = v;
+        }
+    const double bk_new = bk * (rho / rho_t);  // :214
+    L.b.push_back(bk_new);
+    L.T[(m0 - 1) + (size_t)m0 * L.Tld] = bprev;               // T12
+    L.T[m0 + (size_t)(m0 - 1) * L.Tld] = bprev;               // T21
+    L.T[(m0 + s) + (size_t)(m0 + s - 1) * L.Tld] = bk_new;    // T32
+    return 0;
+}
+
+int lanczos_step(cal_ctx* c, int diagnostics) {
+    LanczosState& L = *c->lz;
+    if (L.k >= L.max_outer) return set_error(c, CAL_ERR_ARG, "lanczos_step: max_outer iterations reached");
+    if (L.breakdown) return set_error(c, CAL_WARN_BREAKDOWN, "lanczos_step: breakdown already hit");
+    const double t0 = now_ms();
+    const int s = L.s;
+    const int64_t n = c->A.n_local, ld = L.ld;
+    L.k += 1;
+    const int k = L.k;
+    const double* q = L.col((k - 1) * s);  // ca_lanczos.m:171 (k=1: q itself)
+    auto Vc = [&](int j) { return L.dV + (size_t)j * ld; };
+    // matrix powers (ca_lanczos.m:110-118); V(:,1) = q is not copied: the
+    // panels below reference q's column of Q directly.
+    for (int i = 0; i < s; ++i) {
+        const double* x = (i == 0) ? q : Vc(i);
+        if (L.newton)
+            CAL_TRY(spmv_dev(c, x, Vc(i + 1), 1, L.Bk[i + (size_t)i * (s + 1)], 0.0, nullptr));
+        else
+            CAL_TRY(spmv_dev(c, x, Vc(i + 1), 0, 0.0, 0.0, nullptr));
+    }
+    int status = 0;
+    if (k == 1) {
+        Panel X = panel();
+        panel_add(X, q, ld, 1);
+        panel_add(X, Vc(1), ld, s);
+        PanelOut Qo = panel_out(L.col(0), ld, s + 1);
+        std::vector<double> Rk((size_t)(s + 1) * (s + 1));
+        int rank = 0;
+        bool sh = false;
+        CAL_TRY(normalize_dev(c, n, X, Qo, Rk.data(), 1.0e-8, &rank, &sh));
+        if (rank < s + 1) L.info.n_rank_deficient++;
+        L.reorth.push_back(0);
+        status = extend_T_first(c, L, Rk);
+    } else {
+        Panel Qp = panel(), X = panel();
+        panel_add(Qp, L.col((k - 2) * s), ld, s + 1);
+        panel_add(X, Vc(1), ld, s);
+        PanelOut Qo = panel_out(L.col((k - 1) * s + 1), ld, s);
+        std::vector<double> Rq((size_t)(s + 1) * s), R((size_t)s * s);
+        PNResult res;
+        CAL_TRY(project_and_normalize_dev(c, n, Qp, X, true, Qo, Rq.data(), R.data(), &res));
+        L.reorth.push_back(res.reorth ? 1 : 0);
+        if (res.reorth) L.info.n_reorth++;
+        if (res.reorth && res.rank < s) L.info.n_rank_deficient++;
+        if (L.full) {  // ca_lanczos.m:197
+            Panel Qall = panel(), Xn = panel();
+            panel_add(Qall, L.col(0), ld, (k - 1) * s + 1);
+            panel_add(Xn, L.col((k - 1) * s + 1), ld, s);
+            std::vector<double> Rq2((size_t)((k - 1) * s + 1) * s), R2((size_t)s * s);
+            PNResult res2;
+            CAL_TRY(project_and_normalize_dev(c, n, Qall, Xn, true, Qo, Rq2.data(), R2.data(), &res2));
+        }
+        status = extend_T(c, L, Rq, R);
+    }
+    if (status == CAL_WARN_BREAKDOWN) {
+        L.info.breakdown = 1;
+        return set_error(c, CAL_WARN_BREAKDOWN, "CA-Lanczos breakdown: rho_t = Rk(s,s) = 0");
+    }
+    const double t1 = now_ms();
+    if (diagnostics) CAL_TRY(ritz_diagnostics(c, L));
+    const double t2 = now_ms();
+    L.info.loop_ms += t2 - t0;
+    L.info.diag_ms += t2 - t1;
+    L.info.t = k;
+    return 0;
+}
+
+}  // namespace cal
+
+using namespace cal;
+
+extern "C" {
+
+void cal_lanczos_free_state(cal_ctx* c) {
+    if (!c || !c->lz) return;
+    if (c->lz->dQ) hipFree(c->lz->dQ);
+    if (c->lz->dV) hipFree(c->lz->dV);
+    delete c->lz;
+    c->lz = nullptr;
+}
+
+int cal_lanczos_begin(cal_ctx* c, const double* r, int s, int max_outer, const char* basis, const char* orth) {
+    if (!c) return CAL_ERR_ARG;
+    if (!c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
+    if (!r || s < 1 || s > 15 || max_outer < 1 || !basis)
+        return set_error(c, CAL_ERR_ARG, "cal_lanczos_begin: need r, 1 <= s <= 15, max_outer >= 1");
+    std::string o = orth ? orth : "local", b = basis;
+    for (auto& ch : o) ch = (char)tolower(ch);
+    for (auto& ch : b) ch = (char)tolower(ch);
+    if (o != "local" && o != "full" && o != "periodic" && o != "selective")
+        return set_error(c, CAL_ERR_ARG, "ca_lanczos.m: Invalid option value for orth: " + o);
+    if (o == "periodic" || o == "selective")
+        return set_error(c, CAL_ERR_UNSUPPORTED, "orth='" + o + "' is outside the built scope (SURVEY §8f1)");
+    if (b != "monomial" && b != "newton") return set_error(c, CAL_ERR_ARG, "ERROR: Unknown basis type: " + b);
+    hipSetDevice(c->device);
+    cal_lanczos_free_state(c);
+    LanczosState* L = new LanczosState();
+    c->lz = L;
+    L->s = s;
+    L->max_outer = max_outer;
+    L->newton = b == "newton";
+    L->full = o == "full";
+    L->n = c->A.n_local;
+    L->ld = c->A.ld;
+    L->info.s = s;
+    const size_t qcols = (size_t)s * max_outer + 1;
+    CAL_HIP(c, hipMalloc((void**)&L->dQ, qcols * L->ld * sizeof(double)));
+    CAL_HIP(c, hipMalloc((void**)&L->dV, (size_t)(s + 1) * L->ld * sizeof(double)));
+    CAL_HIP(c, hipMemsetAsync(L->dQ, 0, qcols * L->ld * sizeof(double), c->stream));
+    CAL_HIP(c, hipMemsetAsync(L->dV, 0, (size_t)(s + 1) * L->ld * sizeof(double), c->stream));
+    L->Tld = s * max_outer + 1;
+    L->T.assign((size_t)L->Tld * L->Tld, 0.0);
+    const double t0 = now_ms();
+    // q = r/sqrt(r'*r) (ca_lanczos.m:55)
+    CAL_HIP(c, hipMemcpyAsync(L->dV, r, L->n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    double rr = 0.0;
+    CAL_TRY(dot_host(c, L->n, L->dV, L->dV, &rr));
+    CAL_HIP(c, launch_div(L->dQ, L->dV, std::sqrt(rr), L->n, c->stream));
+    if (L->newton) {
+        CAL_TRY(newton_prologue(c, *L));
+    } else {  // Bk = I(:,2:s+1) (ca_lanczos.m:63-65)
+        L->Bk.assign((size_t)(s + 1) * s, 0.0);
+        for (int j = 0; j < s; ++j) L->Bk[(j + 1) + (size_t)j * (s + 1)] = 1.0;
+    }
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    L->info.prologue_ms = now_ms() - t0;
+    return 0;
+}
+
+int cal_lanczos_step(cal_ctx* c, int diagnostics) {
+    if (!c || !c->lz) return set_error(c, CAL_ERR_ARG, "cal_lanczos_step: no active CA-Lanczos run");
+    hipSetDevice(c->device);
+    return lanczos_step(c, diagnostics);
+}
+
+int cal_lanczos_state(cal_ctx* c, int* k, int* s, int* reorth_last) {
+    if (!c || !c->lz) return CAL_ERR_ARG;
+    if (k) *k = c->lz->k;
+    if (s) *s = c->lz->s;
+    if (reorth_last) *reorth_last = c->lz->reorth.empty() ? 0 : c->lz->reorth.back();
+    return 0;
+}
+
+int cal_lanczos_get(cal_ctx* c, double* T, int ldt, double* rn, double* oe, int* reorth_flags,
+                    cal_lanczos_info* info) {
+    if (!c || !c->lz) return CAL_ERR_ARG;
+    LanczosState& L = *c->lz;
+    const int k = L.k, sk = L.s * L.k;
+    if (T) {
+        if (ldt < sk) return set_error(c, CAL_ERR_ARG, "cal_lanczos_get: ldt < s*k");
+        for (int j = 0; j < sk; ++j)
+            for (int i = 0; i < sk; ++i) T[i + (size_t)j * ldt] = L.T[i + (size_t)j * L.Tld];
+    }
+    if (rn) {  // k x sk column-major (MATLAB rnorm(1:k,:))
+        for (int j = 0; j < sk; ++j)
+            for (int i = 0; i < k; ++i) {
+                double v = 0.0;
+                if (i < (int)L.rn.size() && j < (int)L.rn[i].size()) v = L.rn[i][j];
+                rn[i + (size_t)j * k] = v;
+            }
+    }
+    if (oe)
+        for (int i = 0; i < k; ++i) oe[i] = i < (int)L.oe.size() ? L.oe[i] : 0.0;
+    if (reorth_flags)
+        for (int i = 0; i < k; ++i) reorth_flags[i] = L.reorth[i];
+    if (info) *info = L.info;
+    return 0;
+}
+
+int cal_lanczos_get_Q(cal_ctx* c, int64_t col0, int ncols, double* Q) {
+    if (!c || !c->lz || !Q || col0 < 0 || ncols < 0) return CAL_ERR_ARG;
+    LanczosState& L = *c->lz;
+    if (col0 + ncols > (int64_t)L.s * L.max_outer + 1) return set_error(c, CAL_ERR_ARG, "Q column range");
+    CAL_HIP(c, hipMemcpy2DAsync(Q, L.n * sizeof(double), L.dQ + col0 * L.ld, L.ld * sizeof(double),
+                                L.n * sizeof(double), ncols, hipMemcpyDeviceToHost, c->stream));
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int cal_lanczos_end(cal_ctx* c) {
+    if (!c) return CAL_ERR_ARG;
+    cal_lanczos_free_state(c);
+    return 0;
+}
+
+int cal_ca_lanczos(cal_ctx* c, const double* r, int s, int iter, const char* basis, const char* orth,
+                   int diagnostics, double* T, double* Q, double* rn, double* oe, int* reorth_flags,
+                   cal_lanczos_info* info) {
+    if (!c) return CAL_ERR_ARG;
+    if (s < 1 || iter < 1) return set_error(c, CAL_ERR_ARG, "cal_ca_lanczos: need s >= 1 and iter >= 1");
+    const int t = (iter + s - 1) / s;  // ca_lanczos.m:52
+    CAL_TRY(cal_lanczos_begin(c, r, s, t, basis, orth));
+    int status = 0;
+    for (int k = 0; k < t; ++k) {
+        status = cal_lanczos_step(c, diagnostics);
+        if (status != 0) break;
+    }
+    if (status < 0) return status;
+    const int k = c->lz->k, sk = s * k;
+    CAL_TRY(cal_lanczos_get(c, T, sk, rn, oe, reorth_flags, info));
+    if (Q) CAL_TRY(cal_lanczos_get_Q(c, 0, sk, Q));
+    cal_lanczos_free_state(c);
+    return status;
+}
+
+// ---- host-only exports (calanczos_host.h) ----------------------------------
+int cal_eig(int n, const double* T, int ldt, double* wr, double* wi, double* V) {
+    if (n < 0 || !T || !wr || !wi || !V) return CAL_ERR_ARG;
+    bool sym = true;
+    for (int j = 0; j < n && sym; ++j)
+        for (int i = 0; i < j; ++i)
+            if (T[i + (size_t)j * ldt] != T[j + (size_t)i * ldt]) {
+                sym = false;
+                break;
+            }
+    if (sym) {
+        dense::eig_symmetric(n, T, ldt, wr, V, n);
+        for (int i = 0; i < n; ++i) wi[i] = 0.0;
+        return 0;
+    }
+    return dense::eig_general(n, T, ldt, wr, wi, V, n) ? 0 : CAL_ERR_NUMERIC;
+}
+
+int cal_tridiag_eigvals(int n, const double* alpha, const double* beta, double* w) {
+    if (n < 0 || !alpha || (n > 1 && !beta) || !w) return CAL_ERR_ARG;
+    return dense::tridiag_eigvals(n, alpha, beta, w) ? 0 : CAL_ERR_NUMERIC;
+}
+
+}  // extern "C"

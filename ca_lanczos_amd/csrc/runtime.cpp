@@ -1,0 +1,347 @@
+// runtime.cpp -- context lifecycle, device buffers, matrix upload, timers.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "cal_internal.hpp"
+#include "comm.hpp"
+
+namespace cal {
+
+constexpr int kRowBlockRows = 256;   // rows per CSR-stream block (= threads)
+constexpr int kRowBlockNnz = 2048;   // nonzeros staged in LDS per block
+
+int set_error(cal_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+int hip_fail(cal_ctx* c, hipError_t e, const char* what) {
+    std::string m = std::string("HIP error '") + hipGetErrorString(e) + "' in " + what;
+    return set_error(c, CAL_ERR_HIP, m);
+}
+
+static int grow(cal_ctx* c, double** p, size_t* cap, size_t need) {
+    if (need <= *cap) return 0;
+    if (*p) CAL_HIP(c, hipFree(*p));
+    *p = nullptr;
+    size_t n = std::max(need, (size_t)4096);
+    CAL_HIP(c, hipMalloc((void**)p, n * sizeof(double)));
+    *cap = n;
+    return 0;
+}
+
+int ensure_partial(cal_ctx* c, size_t doubles) { return grow(c, &c->d_partial, &c->partial_cap, doubles); }
+int ensure_scratch(cal_ctx* c, size_t doubles) { return grow(c, &c->d_scratch, &c->scratch_cap, doubles); }
+
+int ensure_small(cal_ctx* c, size_t doubles) {
+    if (doubles <= c->small_cap) return 0;
+    if (c->d_small) CAL_HIP(c, hipFree(c->d_small));
+    if (c->h_small) CAL_HIP(c, hipHostFree(c->h_small));
+    c->d_small = nullptr;
+    c->h_small = nullptr;
+    size_t n = std::max(doubles, (size_t)65536);
+    CAL_HIP(c, hipMalloc((void**)&c->d_small, n * sizeof(double)));
+    CAL_HIP(c, hipHostMalloc((void**)&c->h_small, n * sizeof(double), hipHostMallocDefault));
+    c->small_cap = n;
+    return 0;
+}
+
+int ensure_red(cal_ctx* c, size_t doubles) {
+    if (doubles <= c->red_cap) return 0;
+    if (c->d_red) CAL_HIP(c, hipFree(c->d_red));
+    if (c->h_red) CAL_HIP(c, hipHostFree(c->h_red));
+    c->d_red = nullptr;
+    c->h_red = nullptr;
+    size_t n = std::max(doubles, (size_t)65536);
+    CAL_HIP(c, hipMalloc((void**)&c->d_red, n * sizeof(double)));
+    CAL_HIP(c, hipHostMalloc((void**)&c->h_red, n * sizeof(double), hipHostMallocDefault));
+    c->red_cap = n;
+    return 0;
+}
+
+int ensure_work(cal_ctx* c, int cols, int64_t ld) {
+    if (cols <= c->work_cols && ld == c->work_ld) return 0;
+    if (c->d_work) CAL_HIP(c, hipFree(c->d_work));
+    c->d_work = nullptr;
+    c->work_cols = 0;
+    CAL_HIP(c, hipMalloc((void**)&c->d_work, (size_t)cols * ld * sizeof(double)));
+    CAL_HIP(c, hipMemsetAsync(c->d_work, 0, (size_t)cols * ld * sizeof(double), c->stream));
+    c->work_cols = cols;
+    c->work_ld = ld;
+    return 0;
+}
+
+double* work_col(cal_ctx* c, int j) { return c->d_work + (size_t)j * c->work_ld; }
+
+int timer_begin(cal_ctx* c, int kind) {
+    if (!c->timing) return -1;
+    CalTimerRec r;
+    r.kind = kind;
+    if (c->event_pool.size() >= 2) {
+        r.a = c->event_pool.back();
+        c->event_pool.pop_back();
+        r.b = c->event_pool.back();
+        c->event_pool.pop_back();
+    } else {
+        if (hipEventCreate(&r.a) != hipSuccess) return -1;
+        if (hipEventCreate(&r.b) != hipSuccess) return -1;
+    }
+    hipEventRecord(r.a, c->stream);
+    c->timers.push_back(r);
+    return (int)c->timers.size() - 1;
+}
+
+void timer_end(cal_ctx* c, int idx) {
+    if (idx < 0) return;
+    hipEventRecord(c->timers[idx].b, c->stream);
+}
+
+// Split rows into CSR-stream blocks: <= kRowBlockRows rows and <= kRowBlockNnz
+// nonzeros; a longer row gets a block of its own (long-row path).
+static void build_row_blocks(int64_t n, const std::vector<int>& rowptr, std::vector<int>& blk, int* max_nnz) {
+    blk.clear();
+    blk.push_back(0);
+    int64_t r = 0;
+    int mx = 0;
+    while (r < n) {
+        const int64_t start = r;
+        const int len0 = rowptr[r + 1] - rowptr[r];
+        if (len0 > kRowBlockNnz) {
+            r++;
+            blk.push_back((int)r);
+            continue;
+        }
+        int nz = 0;
+        while (r < n && r - start < kRowBlockRows) {
+            const int len = rowptr[r + 1] - rowptr[r];
+            if (len > kRowBlockNnz || nz + len > kRowBlockNnz) break;
+            nz += len;
+            r++;
+        }
+        mx = std::max(mx, nz);
+        blk.push_back((int)r);
+    }
+    *max_nnz = mx;
+}
+
+static void free_matrix(cal_ctx* c) {
+    DevMatrix& A = c->A;
+    if (A.rowptr) hipFree(A.rowptr);
+    if (A.col) hipFree(A.col);
+    if (A.val) hipFree(A.val);
+    if (A.blk) hipFree(A.blk);
+    if (A.send_idx) hipFree(A.send_idx);
+    if (A.send_buf) hipFree(A.send_buf);
+    A = DevMatrix();
+    if (c->d_work) hipFree(c->d_work);
+    c->d_work = nullptr;
+    c->work_cols = 0;
+    c->has_A = false;
+}
+
+// Upload a local CSR (int32 indices, columns already in local+ghost numbering).
+int upload_matrix(cal_ctx* c, int64_t n_local, int64_t n_global, int64_t row0, int64_t nghost,
+                  const std::vector<int>& rowptr, const std::vector<int>& col, const double* val) {
+    free_matrix(c);
+    DevMatrix& A = c->A;
+    A.n_local = n_local;
+    A.n_global = n_global;
+    A.row0 = row0;
+    A.nghost = nghost;
+    A.nnz = rowptr[n_local];
+    A.ld = ((n_local + nghost + 63) / 64) * 64;
+    if (A.ld == 0) A.ld = 64;
+    std::vector<int> blk;
+    int max_nnz = 0;
+    build_row_blocks(n_local, rowptr, blk, &max_nnz);
+    A.nblk = (int)blk.size() - 1;
+    int nit = (max_nnz + 255) / 256;
+    if (nit < 1) nit = 1;
+    if (nit > 8) nit = 8;
+    A.nit = nit;
+    CAL_HIP(c, hipMalloc((void**)&A.rowptr, (n_local + 1) * sizeof(int)));
+    CAL_HIP(c, hipMalloc((void**)&A.col, std::max<int64_t>(A.nnz, 1) * sizeof(int)));
+    CAL_HIP(c, hipMalloc((void**)&A.val, std::max<int64_t>(A.nnz, 1) * sizeof(double)));
+    CAL_HIP(c, hipMalloc((void**)&A.blk, blk.size() * sizeof(int)));
+    CAL_HIP(c, hipMemcpy(A.rowptr, rowptr.data(), (n_local + 1) * sizeof(int), hipMemcpyHostToDevice));
+    if (A.nnz > 0) {
+        CAL_HIP(c, hipMemcpy(A.col, col.data(), A.nnz * sizeof(int), hipMemcpyHostToDevice));
+        CAL_HIP(c, hipMemcpy(A.val, val, A.nnz * sizeof(double), hipMemcpyHostToDevice));
+    }
+    CAL_HIP(c, hipMemcpy(A.blk, blk.data(), blk.size() * sizeof(int), hipMemcpyHostToDevice));
+    c->has_A = true;
+    return 0;
+}
+
+int spmv_dev(cal_ctx* c, const double* x, double* y, int mode, double shift, double im2, const double* xprev) {
+    if (!c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
+    CAL_TRY(halo_exchange(c, const_cast<double*>(x)));
+    SpmvArgs a;
+    a.rowptr = c->A.rowptr;
+    a.col = c->A.col;
+    a.val = c->A.val;
+    a.blk = c->A.blk;
+    a.nblk = c->A.nblk;
+    a.x = x;
+    a.y = y;
+    a.xprev = xprev;
+    a.shift = shift;
+    a.im2 = im2;
+    a.mode = mode | (c->A.nit << 8);
+    const int t = timer_begin(c, 0);
+    CAL_HIP(c, launch_spmv(a, c->stream));
+    timer_end(c, t);
+    return 0;
+}
+
+}  // namespace cal
+
+using namespace cal;
+
+extern "C" {
+
+int cal_version(void) { return 1; }
+
+int cal_device_count(int* count) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    if (count) *count = n;
+    return e == hipSuccess ? 0 : CAL_ERR_HIP;
+}
+
+int cal_create(int device, cal_ctx** out) {
+    if (!out) return CAL_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return CAL_ERR_HIP;
+    if (device < 0 || device >= n) return CAL_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return CAL_ERR_HIP;
+    cal_ctx* c = new cal_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return CAL_ERR_HIP;
+    }
+    *out = c;
+    return 0;
+}
+
+void cal_lanczos_free_state(cal_ctx* c);  // lanczos.cpp
+
+void cal_destroy(cal_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    cal_lanczos_free_state(c);
+    cal::comm_destroy(c);
+    free_matrix(c);
+    if (c->d_partial) hipFree(c->d_partial);
+    if (c->d_red) hipFree(c->d_red);
+    if (c->h_red) hipHostFree(c->h_red);
+    if (c->d_small) hipFree(c->d_small);
+    if (c->h_small) hipHostFree(c->h_small);
+    if (c->d_scratch) hipFree(c->d_scratch);
+    for (auto& r : c->timers) {
+        hipEventDestroy(r.a);
+        hipEventDestroy(r.b);
+    }
+    for (auto e : c->event_pool) hipEventDestroy(e);
+    hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* cal_last_error(const cal_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int cal_synchronize(cal_ctx* c) {
+    if (!c) return CAL_ERR_ARG;
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int cal_timer_enable(cal_ctx* c, int on) {
+    if (!c) return CAL_ERR_ARG;
+    c->timing = on != 0;
+    return 0;
+}
+
+int cal_timer_reset(cal_ctx* c) {
+    if (!c) return CAL_ERR_ARG;
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    for (auto& r : c->timers) {
+        c->event_pool.push_back(r.a);
+        c->event_pool.push_back(r.b);
+    }
+    c->timers.clear();
+    return 0;
+}
+
+int cal_timer_read(cal_ctx* c, const char* kind, int64_t* count, double* total_ms) {
+    if (!c || !kind) return CAL_ERR_ARG;
+    int k = -1;
+    if (!strcmp(kind, "spmv")) k = 0;
+    else if (!strcmp(kind, "gram")) k = 1;
+    else if (!strcmp(kind, "apply")) k = 2;
+    else if (!strcmp(kind, "other")) k = 3;
+    else if (strcmp(kind, "all")) return set_error(c, CAL_ERR_ARG, "unknown timer kind");
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    int64_t cnt = 0;
+    double tot = 0.0;
+    for (auto& r : c->timers) {
+        if (k >= 0 && r.kind != k) continue;
+        float ms = 0.f;
+        CAL_HIP(c, hipEventElapsedTime(&ms, r.a, r.b));
+        cnt++;
+        tot += ms;
+    }
+    if (count) *count = cnt;
+    if (total_ms) *total_ms = tot;
+    return 0;
+}
+
+int cal_set_matrix_csr(cal_ctx* c, int64_t n, const int64_t* rowptr, const int32_t* colind, const double* val) {
+    if (!c || n < 0 || !rowptr || (n > 0 && rowptr[n] > 0 && (!colind || !val)))
+        return set_error(c, CAL_ERR_ARG, "cal_set_matrix_csr: bad arguments");
+    if (c->comm && c->comm->nranks > 1)
+        return set_error(c, CAL_ERR_ARG, "distributed context: use cal_set_matrix_csr_dist");
+    const int64_t nnz = rowptr[n];
+    if (nnz >= ((int64_t)1 << 31) || n >= ((int64_t)1 << 31))
+        return set_error(c, CAL_ERR_UNSUPPORTED, "n and nnz must be < 2^31 per rank");
+    hipSetDevice(c->device);
+    std::vector<int> rp(n + 1), col(nnz);
+    for (int64_t i = 0; i <= n; ++i) rp[i] = (int)rowptr[i];
+    for (int64_t p = 0; p < nnz; ++p) {
+        const int32_t j = colind[p];
+        if (j < 0 || j >= n) return set_error(c, CAL_ERR_ARG, "column index out of range");
+        col[p] = j;
+    }
+    for (int64_t i = 0; i < n; ++i)
+        if (rp[i + 1] < rp[i]) return set_error(c, CAL_ERR_ARG, "row pointers must be non-decreasing");
+    return upload_matrix(c, n, n, 0, 0, rp, col, val);
+}
+
+int cal_set_matrix_csc(cal_ctx* c, int64_t n, const int64_t* jc, const int64_t* ir, const double* pr) {
+    // A is symmetric (ca_lanczos.m:8), so its CSC arrays are its CSR arrays.
+    if (!c || n < 0 || !jc) return set_error(c, CAL_ERR_ARG, "cal_set_matrix_csc: bad arguments");
+    const int64_t nnz = jc[n];
+    std::vector<int32_t> col32(nnz);
+    for (int64_t p = 0; p < nnz; ++p) {
+        if (ir[p] < 0 || ir[p] >= n) return set_error(c, CAL_ERR_ARG, "row index out of range");
+        col32[p] = (int32_t)ir[p];
+    }
+    return cal_set_matrix_csr(c, n, jc, col32.data(), pr);
+}
+
+int cal_matrix_info(cal_ctx* c, int64_t* n_local, int64_t* nnz_local, int64_t* n_global, int64_t* nghost) {
+    if (!c) return CAL_ERR_ARG;
+    if (!c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
+    if (n_local) *n_local = c->A.n_local;
+    if (nnz_local) *nnz_local = c->A.nnz;
+    if (n_global) *n_global = c->A.n_global;
+    if (nghost) *nghost = c->A.nghost;
+    return 0;
+}
+
+}  // extern "C"

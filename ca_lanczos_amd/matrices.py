@@ -1,0 +1,127 @@
+"""Synthetic test matrices of BASELINE.json (CSR, sorted, int32 columns).
+
+Vectorised generators that scale to the 3-D 215^3 config (n = 9,938,375,
+nnz = 69,291,275) without building a Kronecker product.
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.sparse as sp
+
+
+def _stencil_csr(dims, diag, r0=0, r1=None, col_dtype=np.int32):
+    """Rows [r0, r1) of the Dirichlet stencil matrix on grid ``dims`` (CSR,
+    global column indices, sorted)."""
+    dims = tuple(int(d) for d in dims)
+    n_all = int(np.prod(dims))
+    r1 = n_all if r1 is None else r1
+    idx = np.arange(r0, r1, dtype=np.int64)
+    n = len(idx)
+    coords, stride, strides = [], 1, []
+    for d in dims:  # first dimension is the fastest (column-major grid)
+        coords.append((idx // stride) % d)
+        strides.append(stride)
+        stride *= d
+    offsets = []  # increasing column offset: -s_last .. -s_0, 0, +s_0 .. +s_last
+    for k in reversed(range(len(dims))):
+        offsets.append((-strides[k], coords[k] > 0))
+    offsets.append((0, None))
+    for k in range(len(dims)):
+        offsets.append((strides[k], coords[k] < dims[k] - 1))
+    counts = np.ones(n, dtype=np.int64)
+    for off, m in offsets:
+        if m is not None:
+            counts += m
+    rowptr = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(counts, out=rowptr[1:])
+    nnz = int(rowptr[-1])
+    col = np.empty(nnz, dtype=col_dtype)
+    val = np.empty(nnz, dtype=np.float64)
+    pos = rowptr[:-1].copy()
+    for off, m in offsets:
+        if m is None:
+            rows, p = idx, pos
+            col[p] = rows
+            val[p] = diag
+            pos += 1
+        else:
+            rows = idx[m]
+            p = pos[m]
+            col[p] = rows + off
+            val[p] = -1.0
+            pos[m] += 1
+    del coords, idx, pos
+    return rowptr, col, val
+
+
+WORKLOADS = {
+    # name: (grid dims, diagonal)
+    "lap2d": (2, 4.0),
+    "lap3d": (3, 6.0),
+}
+
+
+def laplacian_2d(N: int) -> sp.csr_matrix:
+    """5-point Dirichlet Laplacian on N x N (stencil 4, -1): BASELINE config 2."""
+    rowptr, col, val = _stencil_csr((N, N), 4.0)
+    return sp.csr_matrix((val, col, rowptr), shape=(N * N, N * N))
+
+
+def laplacian_3d(N: int) -> sp.csr_matrix:
+    """7-point Dirichlet Laplacian on N^3 (stencil 6, -1): BASELINE configs 3-4."""
+    rowptr, col, val = _stencil_csr((N, N, N), 6.0)
+    return sp.csr_matrix((val, col, rowptr), shape=(N ** 3, N ** 3))
+
+
+def laplacian_rows(dim: int, N: int, r0: int, r1: int):
+    """Rows [r0, r1) of the 2-D/3-D Laplacian with global int64 columns (a
+    row slab of the distributed config 4): (rowptr, col, val)."""
+    diag = 4.0 if dim == 2 else 6.0
+    return _stencil_csr((N,) * dim, diag, r0, r1, col_dtype=np.int64)
+
+
+def slab_bounds(n: int, nranks: int, plane: int = 1):
+    """Contiguous row slabs aligned to whole planes (z-slabs for 3-D)."""
+    nplanes = n // plane
+    return [(plane * (nplanes * r // nranks)) for r in range(nranks)] + [n]
+
+
+def diagonal(a) -> sp.csr_matrix:
+    """``sparse(diag(a))`` -- BASELINE config 1 and the reference's diagonal tests."""
+    a = np.asarray(a, dtype=np.float64)
+    n = len(a)
+    return sp.csr_matrix((a, np.arange(n, dtype=np.int32), np.arange(n + 1, dtype=np.int64)), shape=(n, n))
+
+
+def read_matrix_market(path: str) -> sp.csr_matrix:
+    """Coordinate MatrixMarket reader (real/integer/pattern, general/symmetric)."""
+    with open(path) as f:
+        header = f.readline().lower().split()
+        if len(header) < 5 or header[0] != "%%matrixmarket":
+            raise ValueError("not a MatrixMarket file: %s" % path)
+        field, symm = header[3], header[4]
+        line = f.readline()
+        while line.startswith("%"):
+            line = f.readline()
+        m, n, nz = (int(t) for t in line.split())
+        data = np.loadtxt(f, ndmin=2, max_rows=nz)
+    i = data[:, 0].astype(np.int64) - 1
+    j = data[:, 1].astype(np.int64) - 1
+    v = np.ones(len(i)) if field == "pattern" else data[:, 2].astype(np.float64)
+    if symm in ("symmetric", "hermitian"):
+        off = i != j
+        i, j, v = np.concatenate([i, j[off]]), np.concatenate([j, i[off]]), np.concatenate([v, v[off]])
+    A = sp.csr_matrix((v, (i, j)), shape=(m, n))
+    A.sum_duplicates()
+    A.sort_indices()
+    return A
+
+
+def to_csr(A) -> sp.csr_matrix:
+    """Canonical CSR (sorted, summed duplicates) with int32 column indices."""
+    A = sp.csr_matrix(A)
+    if not A.has_canonical_format:
+        A = A.copy()
+        A.sum_duplicates()
+    A.sort_indices()
+    return A

@@ -1,0 +1,156 @@
+/*
+ * calanczos.h -- C ABI of the MI355X-native CA-Lanczos hot path.
+ *
+ * Drop-in boundary for the MATLAB reference (magnusgrandin/ca-lanczos).  The
+ * reference resolves every hot-path function by file name, so a MEX file of
+ * the same name shadows the .m file.  Each entry point below
+ * is what such a MEX shim binds; the comment on each cites
+ * the reference interface it replaces.
+ *
+ * Conventions
+ *  - Dense matrices are column-major double (MATLAB layout).  Host-pointer
+ *    entry points take leading dimension == rows.
+ *  - A is the n x n sparse symmetric matrix.  It is handed over once per
+ *    context (cal_set_matrix_*), kept resident in HBM and reused by every
+ *    call, as the SURVEY §8b "two tiers" design prescribes.
+ *  - Every function returns an int status: 0 ok, < 0 error, > 0 warning.
+ *    cal_last_error(ctx) holds the message of the last non-zero status.
+ *  - Calls are synchronous (outputs valid on return) and a context may be
+ *    used by one host thread at a time, like mexFunction.
+ *  - Cell arrays of blocks ({Q1,Q2,...}) are passed as (nblocks, const
+ *    double* const* blocks, const int* widths); a block of width 0 is the
+ *    MATLAB empty matrix [].
+ */
+#ifndef CALANCZOS_H
+#define CALANCZOS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CAL_OK 0
+#define CAL_ERR_ARG (-1)          /* bad argument (reference: disp()+return)        */
+#define CAL_ERR_HIP (-2)          /* HIP runtime failure                            */
+#define CAL_ERR_NOMATRIX (-3)     /* no matrix set on the context                   */
+#define CAL_ERR_NUMERIC (-4)      /* NaN/Inf, Leja error() cases                    */
+#define CAL_ERR_COMM (-5)         /* collective / halo failure                      */
+#define CAL_ERR_UNSUPPORTED (-6)  /* option outside the built scope                 */
+#define CAL_WARN_RANK_DEFICIENT 1 /* reference: disp('Rank deficient'), continues   */
+#define CAL_WARN_BREAKDOWN 2      /* rho_t == 0 or beta == 0 (reference divides)    */
+
+typedef struct cal_ctx cal_ctx;
+
+/* ---- context lifecycle ------------------------------------------------- */
+int cal_version(void);
+int cal_device_count(int* count);
+/* Create a context on HIP device `device` with its own stream. */
+int cal_create(int device, cal_ctx** out);
+void cal_destroy(cal_ctx* ctx);
+const char* cal_last_error(const cal_ctx* ctx);
+int cal_synchronize(cal_ctx* ctx);
+/* Kernel-duration timer (HIP events on the context stream).  kind: "spmv",
+ * "gram", "apply", "all".  Returns the number of launches timed and their
+ * summed duration since the last reset. */
+int cal_timer_enable(cal_ctx* ctx, int on);
+int cal_timer_read(cal_ctx* ctx, const char* kind, int64_t* count, double* total_ms);
+int cal_timer_reset(cal_ctx* ctx);
+
+/* ---- the sparse matrix A ------------------------------------------------ */
+/* MATLAB mxArray sparse storage (CSC: jc colptr, ir rowidx, pr values, all
+ * mwIndex = int64).  A is symmetric, so CSC(A) == CSR(A) and the arrays are
+ * consumed as CSR.  Replaces the `A` argument of SpMV.m:6, ca_lanczos.m:24. */
+int cal_set_matrix_csc(cal_ctx* ctx, int64_t n, const int64_t* jc, const int64_t* ir, const double* pr);
+/* CSR with int64 row pointers and int32 column indices (SciPy layout). */
+int cal_set_matrix_csr(cal_ctx* ctx, int64_t n, const int64_t* rowptr, const int32_t* colind, const double* val);
+/* Row-slab of a distributed matrix: rows [row0, row0+nlocal) of the global
+ * n_global x n_global matrix, global column indices.  Requires a communicator
+ * (cal_comm_*) when nranks > 1. */
+int cal_set_matrix_csr_dist(cal_ctx* ctx, int64_t n_global, int64_t row0, int64_t nlocal,
+                            const int64_t* rowptr, const int64_t* colind_global, const double* val);
+int cal_matrix_info(cal_ctx* ctx, int64_t* n_local, int64_t* nnz_local, int64_t* n_global, int64_t* nghost);
+
+/* ---- a1-a4: SpMV and the s-step matrix-powers kernel -------------------- */
+/* Av = SpMV(A,v)                                       SpMV.m:6-8           */
+int cal_spmv(cal_ctx* ctx, const double* v, double* Av);
+/* V = matrix_powers_monomial(A,q,s); V is n x s        matrix_powers_monomial.m:6-12 */
+int cal_matrix_powers_monomial(cal_ctx* ctx, const double* q, int s, double* V);
+/* V = matrix_powers_newton(A,v,s,lambda,modifiedp); V is n x (s+1).
+ * lambda = lambda_re + i*lambda_im (lambda_im may be NULL: real shifts).
+ *                                                      matrix_powers_newton.m:15-54 */
+int cal_matrix_powers_newton(cal_ctx* ctx, const double* v, int s, const double* lambda_re,
+                             const double* lambda_im, int modifiedp, double* V);
+
+/* ---- a5-a9: tall-skinny block orthogonalisation ------------------------- */
+/* [Q,R] = tsqr(A): A n x m -> Q n x m, R m x m upper, diag(R) >= 0.   tsqr.m:7-12 */
+int cal_tsqr(cal_ctx* ctx, int64_t n, int m, const double* A, double* Q, double* R);
+/* [Q,R] = cholqr(X): G = X'X, R = chol(G), Q = X/R.                  cholqr.m:3-8 */
+int cal_cholqr(cal_ctx* ctx, int64_t n, int m, const double* X, double* Q, double* R);
+/* [X,R] = project(Q,X,doreorth); Xout may alias X; R[i] is widths[i] x m.  project.m:7-58 */
+int cal_project(cal_ctx* ctx, int64_t n, int nblocks, const double* const* Q, const int* widths,
+                int m, const double* X, int doreorth, double* Xout, double* const* R);
+/* [Q,R,rank] = normalize(X,'None',tol).                               normalize.m:3-36 */
+int cal_normalize(cal_ctx* ctx, int64_t n, int m, const double* X, double tol, double* Q, double* R,
+                  int* rank);
+/* [QZ,RZ] = projectAndNormalize(Q,X,doreorth); RZ has nblocks+1 entries:
+ * RZ[i] widths[i] x m, RZ[nblocks] m x m.  *reorth = 1 when the reference
+ * would disp('second').                                    projectAndNormalize.m:3-90 */
+int cal_project_and_normalize(cal_ctx* ctx, int64_t n, int nblocks, const double* const* Q,
+                              const int* widths, int m, const double* X, int doreorth, double* QZ,
+                              double* const* RZ, int* reorth, int* rank);
+
+/* ---- a10-a14: the CA-Lanczos driver ------------------------------------- */
+typedef struct cal_lanczos_info {
+    int t;              /* outer iterations run                                 */
+    int s;
+    int n_reorth;       /* projectAndNormalize second passes ('second')         */
+    int n_rank_deficient;
+    int breakdown;      /* 1 if rho_t == 0 / beta == 0 was hit                  */
+    double shifts[64];  /* Newton shifts (first 2s, Leja order; re part)        */
+    double shifts_im[64];
+    double prologue_ms; /* Newton prologue wall time                            */
+    double loop_ms;     /* outer loop wall time (incl. diagnostics)             */
+    double diag_ms;     /* of which diagnostics                                 */
+} cal_lanczos_info;
+
+/* [T,Q,rn,oe] = ca_lanczos(A,r,s,iter,basis,orth).           ca_lanczos.m:24-86
+ * basis in {"monomial","newton"}, orth in {"local","full"}.
+ * Outputs (any may be NULL): T (s*t x s*t), Q (n x s*t), rn (t x s*t),
+ * oe (t), reorth_flags (t).  t = ceil(iter/s).  diagnostics=0 skips the
+ * per-iteration Ritz residuals / orthogonality error (rn, oe left zero);
+ * they never feed back into T or Q (ca_lanczos.m:228-236). */
+int cal_ca_lanczos(cal_ctx* ctx, const double* r, int s, int iter, const char* basis, const char* orth,
+                   int diagnostics, double* T, double* Q, double* rn, double* oe, int* reorth_flags,
+                   cal_lanczos_info* info);
+
+/* Step-wise, device-resident form of the same loop (benchmarks, restart
+ * drivers).  begin() normalises r and runs the basis set-up (Newton
+ * prologue); step() runs one outer iteration (s SpMVs + block orth + T
+ * update); get() copies the current T (sk x sk, ldt >= sk) and flags. */
+int cal_lanczos_begin(cal_ctx* ctx, const double* r, int s, int max_outer, const char* basis,
+                      const char* orth);
+int cal_lanczos_step(cal_ctx* ctx, int diagnostics);
+int cal_lanczos_state(cal_ctx* ctx, int* k, int* s, int* reorth_last);
+int cal_lanczos_get(cal_ctx* ctx, double* T, int ldt, double* rn, double* oe, int* reorth_flags,
+                    cal_lanczos_info* info);
+int cal_lanczos_get_Q(cal_ctx* ctx, int64_t col0, int ncols, double* Q);
+int cal_lanczos_end(cal_ctx* ctx);
+
+/* ---- multi-GPU (row slabs, RCCL over xGMI) ------------------------------ */
+/* 128-byte RCCL unique id; broadcast it out of band (e.g. torch.distributed). */
+int cal_comm_unique_id(void* id128);
+int cal_comm_init_rccl(cal_ctx* ctx, int nranks, int rank, const void* id128);
+/* Host-staged communicator (tests, CPU rendezvous): device buffers are
+ * staged through pinned host memory and handed to these callbacks. */
+typedef int (*cal_allreduce_fn)(void* user, double* buf, int64_t count);
+typedef int (*cal_exchange_fn)(void* user, int peer, const double* send, int64_t nsend, double* recv,
+                               int64_t nrecv);
+int cal_comm_init_host(cal_ctx* ctx, int nranks, int rank, cal_allreduce_fn allreduce,
+                       cal_exchange_fn exchange, void* user);
+int cal_comm_info(cal_ctx* ctx, int* nranks, int* rank, int* kind);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CALANCZOS_H */

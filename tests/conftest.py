@@ -1,0 +1,26 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); run with -m gpu")
+
+
+@pytest.fixture(scope="session")
+def cal():
+    import ca_lanczos_amd
+
+    return ca_lanczos_amd
+
+
+@pytest.fixture(scope="session")
+def ref():
+    from oracle import ca_lanczos_ref
+
+    return ca_lanczos_ref

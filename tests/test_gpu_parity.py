@@ -1,0 +1,218 @@
+"""GPU parity tests: the HIP path through the C ABI vs the oracle restatement.
+
+Bars:
+  * SpMV / matrix powers: bit-identical to the oracle's sequential CSR SpMV
+    (same summation order, no FMA contraction);
+  * tsqr/normalize/cholqr/project/projectAndNormalize: same R up to
+    |dR| <= 1e-12 * ||X|| * kappa-scaled tolerance, Q orthonormal to 1e-13;
+  * CA-Lanczos: identical reorthogonalisation flags, Newton shifts within
+    1e-9 * ||A||, converged Ritz values within 1e-10 * ||A||, residual norms
+    above 1e-10 within a factor 2 of the oracle's.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _lap2d(cal, N):
+    return cal.matrices.laplacian_2d(N)
+
+
+# ---------------------------------------------------------------- a1 - a4
+@pytest.mark.parametrize("N", [1, 7, 32, 100])
+def test_spmv_bitexact_lap2d(cal, ref, N):
+    A = cal.matrices.laplacian_2d(N)
+    v = ref.matlab_rand(N * N, seed=3) - 0.5
+    assert np.array_equal(cal.SpMV(A, v), ref.SpMV(A, v))
+
+
+def test_spmv_bitexact_lap3d(cal, ref):
+    A = cal.matrices.laplacian_3d(20)
+    v = ref.matlab_rand(A.shape[0], seed=4)
+    assert np.array_equal(cal.SpMV(A, v), ref.SpMV(A, v))
+
+
+def test_spmv_irregular_and_long_rows(cal, ref):
+    import scipy.sparse as sp
+    rng = np.random.RandomState(1)
+    n = 3000
+    B = sp.random(n, n, density=0.002, random_state=rng, format="csr")
+    B = B + B.T
+    # a few dense rows/cols (> 2048 nonzeros: the long-row path) and empty rows
+    D = sp.lil_matrix((n, n))
+    for r in (5, 1500):
+        D[r, :] = rng.rand(n)
+        D[:, r] = D[r, :].T
+    A = (B + D.tocsr()).tocsr()
+    A[17, :] = 0
+    A[:, 17] = 0
+    A.eliminate_zeros()
+    A.sort_indices()
+    v = rng.randn(n)
+    assert np.array_equal(cal.SpMV(A, v), ref.SpMV(A, v))
+
+
+def test_spmv_diag_config1(cal, ref):
+    A = cal.matrices.diagonal(np.arange(1.0, 1001.0))
+    v = np.ones(1000)
+    assert np.array_equal(cal.SpMV(A, v), np.arange(1.0, 1001.0))
+
+
+def test_matrix_powers_monomial_bitexact(cal, ref):
+    A = cal.matrices.laplacian_2d(30)
+    q = ref.matlab_rand(900)
+    q = q / np.linalg.norm(q)
+    assert np.array_equal(cal.matrix_powers_monomial(A, q, 8), ref.matrix_powers_monomial(A, q, 8))
+
+
+def test_matrix_powers_newton_bitexact(cal, ref):
+    A = cal.matrices.laplacian_3d(10)
+    v = ref.matlab_rand(1000)
+    lam = np.array([11.5, 0.3, 6.1, 2.2, 9.0, 4.4, 1.1, 7.7])
+    for modifiedp in (0, 1):
+        assert np.array_equal(cal.matrix_powers_newton(A, v, 8, lam, modifiedp),
+                              ref.matrix_powers_newton(A, v, 8, lam, modifiedp))
+
+
+def test_matrix_powers_newton_complex_modified(cal, ref):
+    A = cal.matrices.laplacian_2d(12)
+    v = ref.matlab_rand(144)
+    lam = np.array([7.0, 3 + 0.5j, 3 - 0.5j, 1.0])
+    assert np.array_equal(cal.matrix_powers_newton(A, v, 4, lam, 1), ref.matrix_powers_newton(A, v, 4, lam, 1))
+
+
+# ---------------------------------------------------------------- a5 - a9
+def _rand_block(n, m, seed, cond=1e3):
+    rng = np.random.RandomState(seed)
+    U, _ = np.linalg.qr(rng.randn(n, m))
+    V, _ = np.linalg.qr(rng.randn(m, m))
+    s = np.logspace(0, -np.log10(cond), m)
+    return (U * s) @ V.T
+
+
+@pytest.mark.parametrize("n,m,cond", [(1000, 8, 1e2), (5000, 9, 1e5), (777, 1, 1.0), (20000, 16, 1e6)])
+def test_tsqr_normalize(cal, ref, n, m, cond):
+    X = _rand_block(n, m, 5, cond)
+    Q, R = cal.tsqr(X)
+    Qr, Rr = ref.tsqr(X)
+    assert np.all(np.diag(R) > 0)
+    assert np.allclose(np.triu(R), R)
+    assert np.max(np.abs(Q.T @ Q - np.eye(m))) < 1e-13
+    assert np.max(np.abs(R - Rr)) <= 1e-13 * cond * np.linalg.norm(X, 2)
+    assert np.max(np.abs(Q @ R - X)) <= 1e-13 * np.linalg.norm(X, 2)
+    Qn, Rn, rank = cal.normalize(X)
+    assert rank == ref.normalize(X)[2]
+
+
+def test_cholqr(cal, ref):
+    X = _rand_block(4000, 8, 2, 1e2)
+    Q, R = cal.cholqr(X)
+    Qr, Rr = ref.cholqr(X)
+    assert np.max(np.abs(R - Rr)) < 1e-12
+    assert np.max(np.abs(Q - Qr)) < 1e-11
+
+
+def test_project_blocks(cal, ref):
+    rng = np.random.RandomState(9)
+    n = 3000
+    Q1, _ = np.linalg.qr(rng.randn(n, 5))
+    Q2, _ = np.linalg.qr(rng.randn(n, 3))
+    X = rng.randn(n, 4)
+    for doreorth in (False, True):
+        Xg, Rg = cal.project([Q1, np.zeros((n, 0)), Q2], X, doreorth)
+        Xr, Rr = ref.project([Q1, np.zeros((n, 0)), Q2], X, doreorth)
+        assert np.max(np.abs(Xg - Xr)) < 1e-12
+        assert np.max(np.abs(Rg[0] - Rr[0])) < 1e-12 and np.max(np.abs(Rg[2] - Rr[2])) < 1e-12
+        assert Rg[1].shape == (0, 4)
+
+
+@pytest.mark.parametrize("frac", [0.9, 0.1])
+def test_project_and_normalize_one_block(cal, ref, frac):
+    """frac = share of X inside span(Qp): 0.9 triggers the second pass."""
+    rng = np.random.RandomState(11)
+    n, w, m = 6000, 9, 8
+    Qp, _ = np.linalg.qr(rng.randn(n, w))
+    X = frac * Qp @ rng.randn(w, m) + (1 - frac) * rng.randn(n, m) / np.sqrt(n) * 3
+    QZ, RZ, re, rank = cal.projectAndNormalize_ex([Qp], X)
+    QZr, RZr, info = ref.projectAndNormalize_ex([Qp], X)
+    assert re == info.reorth
+    assert np.max(np.abs(RZ[0] - RZr[0])) < 1e-12
+    assert np.max(np.abs(RZ[1] - RZr[1])) < 1e-11
+    assert np.max(np.abs(QZ - QZr)) < 1e-10
+    assert np.max(np.abs(QZ.T @ Qp)) < 1e-13
+
+
+def test_project_and_normalize_two_blocks(cal, ref):
+    rng = np.random.RandomState(12)
+    n = 2000
+    Q1, _ = np.linalg.qr(rng.randn(n, 6))
+    Q2, _ = np.linalg.qr(rng.randn(n, 6))
+    Q2 = Q2 - Q1 @ (Q1.T @ Q2)
+    Q2, _ = np.linalg.qr(Q2)
+    X = Q1 @ rng.randn(6, 4) * 5 + rng.randn(n, 4)
+    QZ, RZ, re, _ = cal.projectAndNormalize_ex([Q1, Q2], X)
+    QZr, RZr, info = ref.projectAndNormalize_ex([Q1, Q2], X)
+    assert re == info.reorth
+    for a, b in zip(RZ, RZr):
+        assert np.max(np.abs(a - b)) < 1e-11
+
+
+# ---------------------------------------------------------------- a10 - a14
+def _compare_lanczos(out, exp, normA, check_rn=True):
+    assert out.T.shape == exp.T.shape
+    assert list(out.reorth) == list(exp.reorth)
+    if len(exp.shifts):
+        assert np.max(np.abs(out.shifts - exp.shifts)) <= 1e-9 * normA
+    # first block of T (k <= 2)
+    s = exp.Bk.shape[1]
+    m = min(2 * s, exp.T.shape[0])
+    assert np.max(np.abs(out.T[:m, :m] - exp.T[:m, :m])) <= 1e-9 * normA
+    # converged Ritz values of the final T
+    w = np.sort(np.linalg.eigvals(out.T).real)
+    we = np.sort(np.linalg.eigvals(exp.T).real)
+    assert abs(w[-1] - we[-1]) <= 1e-10 * normA
+    assert abs(w[0] - we[0]) <= 1e-10 * normA
+    if check_rn:
+        # largest Ritz pair's residual history (the reference's plotted metric)
+        a, b = out.ritz_rnorm[:, 0], exp.ritz_rnorm[:, 0]
+        big = b > 1e-10
+        assert np.all(np.abs(np.log(a[big] / b[big])) < np.log(2.0))
+        assert np.all(a[~big] < 1e-9)
+        assert np.all(out.orth_err < 1e-6) == np.all(exp.orth_err < 1e-6)
+
+
+def test_ca_lanczos_config1_monomial(cal, ref):
+    A = cal.matrices.diagonal(np.arange(1.0, 1001.0))
+    r = np.ones(1000)
+    out = cal.ca_lanczos_ex(A, r, 4, 120, "monomial", "local")
+    exp = ref.ca_lanczos(A, r, 4, 120, "monomial", "local")
+    _compare_lanczos(out, exp, 1000.0)
+
+
+@pytest.mark.parametrize("N,dim,it", [(32, 2, 80), (12, 3, 80)])
+def test_ca_lanczos_newton_local(cal, ref, N, dim, it):
+    A = cal.matrices.laplacian_2d(N) if dim == 2 else cal.matrices.laplacian_3d(N)
+    r = ref.matlab_rand(A.shape[0])
+    out = cal.ca_lanczos_ex(A, r, 8, it, "newton", "local")
+    exp = ref.ca_lanczos(A, r, 8, it, "newton", "local")
+    _compare_lanczos(out, exp, 4.0 * dim)
+
+
+def test_ca_lanczos_newton_full(cal, ref):
+    A = cal.matrices.laplacian_2d(24)
+    r = ref.matlab_rand(A.shape[0])
+    out = cal.ca_lanczos_ex(A, r, 8, 64, "newton", "full")
+    exp = ref.ca_lanczos(A, r, 8, 64, "newton", "full")
+    _compare_lanczos(out, exp, 8.0)
+    assert np.max(out.orth_err) < 1e-12
+
+
+def test_ca_lanczos_bad_args(cal):
+    A = cal.matrices.laplacian_2d(8)
+    with pytest.raises(ValueError):
+        cal.ca_lanczos(A, np.ones(64), 4, 16, "newton", "bogus")
+    with pytest.raises(cal.CalError):
+        cal.ca_lanczos(A, np.ones(64), 4, 16, "chebyshev", "local")
+    with pytest.raises(cal.CalError):
+        cal.ca_lanczos(A, np.ones(64), 4, 16, "newton", "periodic")
