@@ -154,6 +154,73 @@ int apply_host(cal_ctx* c, int64_t n, const Panel& P, const double* M, int wy, c
     return 0;
 }
 
+// ---- hot-shape paths (s <= 8) ---------------------------------------------
+static int fetch_tile(cal_ctx* c, int blocks, double* G16, double* e16) {
+    const int64_t nent = 272;
+    CAL_TRY(ensure_red(c, nent));
+    CAL_HIP(c, launch_reduce(c->d_partial, blocks, nent, c->d_red, c->stream));
+    CAL_TRY(allreduce_sum(c, c->d_red, nent));
+    CAL_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, nent * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    c->small_pending = false;
+    std::copy(c->h_red, c->h_red + 256, G16);
+    std::copy(c->h_red + 256, c->h_red + 272, e16);
+    return 0;
+}
+
+// G16 = T'T (T <= 16 columns), e16 = E'T (E one column or null).
+static int tilegram_host(cal_ctx* c, int64_t n, const Panel& T, const double* E, double* G16, double* e16) {
+    // row-parallel loader (lane <-> row, LDS transpose, one MFMA tile)
+    ColList cl{};
+    const int nt = T.total;
+    for (int cc = 0; cc < 16; ++cc) cl.p[cc] = panel_slice(T, cc < nt ? cc : nt - 1, 1).ptr[0];
+    cl.p[16] = E ? E : cl.p[0];
+    int64_t blocks = (n + 255) / 256;
+    blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, 768));
+    CAL_TRY(ensure_partial(c, (size_t)blocks * 272));
+    const int t = timer_begin(c, 1);
+    CAL_HIP(c, launch_rowgram(cl, nt, E != nullptr, n, (int)blocks, c->d_partial, c->stream));
+    timer_end(c, t);
+    return fetch_tile(c, (int)blocks, G16, e16);
+}
+
+static bool rowapply_ok(int wp, int m, bool gram, int wq) {
+    const int WP = rowapply_wpmax(wp), MO = rowapply_mout(m);
+    if (!WP || !MO) return false;
+    if (WP == 17 && MO == 16 && gram) return false;
+    if (WP == 5 && MO != 4) return false;
+    if (gram && ((wq < 8 ? wq : 8) + m > 16 || wq > 9)) return false;
+    return true;
+}
+
+// Y = P*M (M wp x m col-major) with the row kernel; optional tile Gram of
+// [Qp(0:nq) | Y] (Qp = first wq columns of P).
+static int rowapply_host(cal_ctx* c, int64_t n, const Panel& P, const double* M, int m, const PanelOut& Y, bool gram,
+                         int wq, double* G16, double* e16) {
+    const int wp = P.total;
+    const int WP = rowapply_wpmax(wp), MO = rowapply_mout(m);
+    std::vector<double> Mp((size_t)WP * MO, 0.0);
+    for (int cc = 0; cc < wp; ++cc)
+        for (int j = 0; j < m; ++j) Mp[(size_t)cc * MO + j] = M[cc + (size_t)j * wp];
+    CAL_TRY(stage_small(c, Mp.data(), Mp.size()));
+    ColList cl{};
+    OutList ol{};
+    for (int cc = 0; cc < 17; ++cc) cl.p[cc] = panel_slice(P, cc < wp ? cc : wp - 1, 1).ptr[0];
+    for (int j = 0; j < 16; ++j) {
+        const PanelOut s1 = panel_out_slice(Y, j < m ? j : 0, 1);
+        ol.p[j] = s1.ptr[0];
+    }
+    int64_t blocks = (n + 255) / 256;  // without the Gram: one row per thread
+    if (gram) blocks = std::min<int64_t>(blocks, 768);
+    blocks = std::max<int64_t>(1, blocks);
+    if (gram) CAL_TRY(ensure_partial(c, (size_t)blocks * 272));
+    const int t = timer_begin(c, 2);
+    CAL_HIP(c, launch_rowapply(cl, c->d_small, wp, m, ol, gram, wq, n, (int)blocks, c->d_partial, c->stream));
+    timer_end(c, t);
+    if (!gram) return 0;
+    return fetch_tile(c, (int)blocks, G16, e16);
+}
+
 // ---- small helpers ------------------------------------------------------
 static double nan_max(const std::vector<double>& v) {
     double m = NAN;
@@ -187,42 +254,97 @@ static bool chol_or_shift(int m, const double* G, int64_t n_glob, double* R, boo
 
 static int64_t global_rows(cal_ctx* c, int64_t n) { return c->has_A ? std::max(c->A.n_global, n) : n; }
 
-// CholQR passes on the on-the-fly block Z = W * Mz (W = panel, Mz wp x m):
-// first pass from the Gram Gz of Z, later passes in place on Qout.
-static int cholqr_passes(cal_ctx* c, int64_t n, const Panel& W, const std::vector<double>& Mz, int m,
-                         const double* Gz, const PanelOut& Qout, double* R, bool* shifted) {
-    const int wp = W.total;
+// Two-pass orthonormalisation of the block Z = W*Mz (never stored) against the
+// orthonormal block Qp (the first w columns of W; w may be 0):
+//   pass A: Q1 = Z Ra^-1 stored, Ra = chol(Z'Z); fused Grams Q1'Q1, Qp'Q1;
+//   pass B: Q  = (Q1 - Qp C3) Rb^-1 in place, Rb = chol(Q1'Q1 - C3'C3),
+// i.e. CholQR2 inside the block and a second classical Gram-Schmidt pass
+// against Qp in the same two sweeps.  Then X = Qp*(RY + Ctot) + Q*R with
+// Ctot = C3*Ra and R = Rb*Ra.  A shifted Cholesky adds one more pass B.
+static int two_pass(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& W, const std::vector<double>& Mz, int m,
+                    const double* GZ, const PanelOut& Qout, double* R, std::vector<double>& Ctot, bool* shifted) {
+    const int w = Qp.total, wp = W.total;
     const int64_t ng = global_rows(c, n);
-    std::vector<double> Ra((size_t)m * m), Rai((size_t)m * m), G1((size_t)m * m), Rb((size_t)m * m),
-        Rbi((size_t)m * m), Racc((size_t)m * m);
+    std::vector<double> Ra((size_t)m * m), Rai((size_t)m * m), G1((size_t)m * m), C3((size_t)std::max(w, 1) * m, 0.0);
     bool sh = false;
-    if (!chol_or_shift(m, Gz, ng, Ra.data(), &sh))
+    if (!chol_or_shift(m, GZ, ng, Ra.data(), &sh))
         return set_error(c, CAL_ERR_NUMERIC, "block orthogonalisation: Gram matrix is not positive definite");
-    *shifted = *shifted || sh;
     dense::tri_inv_upper(m, Ra.data(), m, Rai.data(), m);
-    // first pass: Qout = (W Mz) Ra^-1, fused Gram of Qout
     std::vector<double> M1((size_t)wp * m);
     dense::matmul(wp, m, m, Mz.data(), wp, Rai.data(), m, M1.data(), wp);
-    CAL_TRY(apply_host(c, n, W, M1.data(), m, &Qout, G1.data(), 0, nullptr));
-    Racc = Ra;
-    // second pass (third if the first was shifted): in place on Qout
+    const Panel Q1 = as_panel(Qout);
+    const Panel P2 = panel_concat(Qp, Q1);
+    // fused Grams of the freshly written block: Q1'Q1 and Qp'Q1
+    const bool fast = rowapply_ok(wp, m, true, w) && rowapply_ok(w + m, m, true, w);
+    auto grams = [&](const Panel& P, const std::vector<double>& M, std::vector<double>& G,
+                     std::vector<double>& Cq, bool store_only) -> int {
+        if (fast) {
+            double G16[256], e16[16];
+            CAL_TRY(rowapply_host(c, n, P, M.data(), m, Qout, !store_only, w, G16, e16));
+            if (store_only) return 0;
+            const int nq = w < 8 ? w : 8;
+            for (int j = 0; j < m; ++j) {
+                for (int i = 0; i < m; ++i) G[i + (size_t)j * m] = G16[(nq + i) + (nq + j) * 16];
+                for (int i = 0; i < nq; ++i) Cq[i + (size_t)j * w] = G16[i + (nq + j) * 16];
+                if (w == 9) Cq[8 + (size_t)j * w] = e16[nq + j];
+            }
+            return 0;
+        }
+        if (store_only) return apply_host(c, n, P, M.data(), m, &Qout, nullptr, 0, nullptr);
+        if (w == 0) return apply_host(c, n, P, M.data(), m, &Qout, G.data(), 0, nullptr);
+        if (w <= 16) return apply_host(c, n, P, M.data(), m, &Qout, G.data(), w, Cq.data());
+        CAL_TRY(apply_host(c, n, P, M.data(), m, &Qout, nullptr, 0, nullptr));
+        std::vector<double> GG((size_t)(w + m) * m);
+        CAL_TRY(gram_host(c, n, P2, Q1, GG.data()));
+        for (int j = 0; j < m; ++j) {
+            for (int i = 0; i < w; ++i) Cq[i + (size_t)j * w] = GG[i + (size_t)j * (w + m)];
+            for (int i = 0; i < m; ++i) G[i + (size_t)j * m] = GG[w + i + (size_t)j * (w + m)];
+        }
+        return 0;
+    };
+    CAL_TRY(grams(W, M1, G1, C3, false));  // pass A
+    std::vector<double> Racc = Ra;
+    Ctot.assign((size_t)w * m, 0.0);
     const int passes = sh ? 2 : 1;
-    const Panel Qp = as_panel(Qout);
-    for (int p = 0; p < passes; ++p) {
+    for (int p = 0; p < passes; ++p) {  // pass B
+        std::vector<double> Gp = G1, Rb((size_t)m * m), Rbi((size_t)m * m);
+        for (int j = 0; j < m; ++j)
+            for (int i = 0; i < m; ++i) {
+                double s = 0.0;
+                for (int k = 0; k < w; ++k) s += C3[k + (size_t)i * w] * C3[k + (size_t)j * w];
+                Gp[i + (size_t)j * m] -= s;
+            }
         bool sh2 = false;
-        if (!chol_or_shift(m, G1.data(), ng, Rb.data(), &sh2))
+        if (!chol_or_shift(m, Gp.data(), ng, Rb.data(), &sh2))
             return set_error(c, CAL_ERR_NUMERIC, "block orthogonalisation: second Cholesky failed");
-        *shifted = *shifted || sh2;
+        sh = sh || sh2;
         dense::tri_inv_upper(m, Rb.data(), m, Rbi.data(), m);
-        const bool more = p + 1 < passes;
-        CAL_TRY(apply_host(c, n, Qp, Rbi.data(), m, &Qout, more ? G1.data() : nullptr, 0, nullptr));
-        std::vector<double> Rn((size_t)m * m);
+        std::vector<double> M2((size_t)(w + m) * m, 0.0);
+        for (int j = 0; j < m; ++j) {
+            for (int i = 0; i < w; ++i) {
+                double s = 0.0;
+                for (int k = 0; k <= j; ++k) s += C3[i + (size_t)k * w] * Rbi[k + (size_t)j * m];
+                M2[i + (size_t)j * (w + m)] = -s;
+            }
+            for (int i = 0; i < m; ++i) M2[w + i + (size_t)j * (w + m)] = Rbi[i + (size_t)j * m];
+        }
+        // Ctot += C3 * Racc ; Racc = Rb * Racc  (before C3 is overwritten)
+        for (int j = 0; j < m; ++j)
+            for (int i = 0; i < w; ++i) {
+                double s = 0.0;
+                for (int k = 0; k <= j; ++k) s += C3[i + (size_t)k * w] * Racc[k + (size_t)j * m];
+                Ctot[i + (size_t)j * w] += s;
+            }
+        std::vector<double> Rn((size_t)m * m, 0.0);
         dense::matmul(m, m, m, Rb.data(), m, Racc.data(), m, Rn.data(), m);
         for (int j = 0; j < m; ++j)
             for (int i = j + 1; i < m; ++i) Rn[i + (size_t)j * m] = 0.0;
         Racc = Rn;
+        const bool more = p + 1 < passes;
+        CAL_TRY(grams(P2, M2, G1, C3, !more));
     }
     std::copy(Racc.begin(), Racc.end(), R);
+    *shifted = *shifted || sh;
     return 0;
 }
 
@@ -230,11 +352,18 @@ int normalize_dev(cal_ctx* c, int64_t n, const Panel& X, const PanelOut& Qout, d
                   bool* shifted) {
     const int m = X.total;
     if (m < 1 || m > 16) return set_error(c, CAL_ERR_ARG, "normalize: 1..16 columns supported");
-    std::vector<double> G((size_t)m * m), Mz((size_t)m * m, 0.0);
-    CAL_TRY(gram_host(c, n, X, X, G.data()));
+    std::vector<double> G((size_t)m * m), Mz((size_t)m * m, 0.0), Ctot;
+    if (X.nseg <= kMaxSeg) {
+        double G16[256], e16[16];
+        CAL_TRY(tilegram_host(c, n, X, nullptr, G16, e16));
+        for (int j = 0; j < m; ++j)
+            for (int i = 0; i < m; ++i) G[i + (size_t)j * m] = G16[i + j * 16];
+    } else {
+        CAL_TRY(gram_host(c, n, X, X, G.data()));
+    }
     for (int i = 0; i < m; ++i) Mz[i + (size_t)i * m] = 1.0;
     bool sh = false;
-    CAL_TRY(cholqr_passes(c, n, X, Mz, m, G.data(), Qout, R, &sh));
+    CAL_TRY(two_pass(c, n, panel(), X, Mz, m, G.data(), Qout, R, Ctot, &sh));
     if (shifted) *shifted = sh;
     if (rank) *rank = rank_from_R(m, R, tol);
     return 0;
@@ -248,72 +377,60 @@ int project_and_normalize_dev(cal_ctx* c, int64_t n, const Panel& Qp, const Pane
     const Panel W = panel_concat(Qp, X);
     const int wp = w + m;
     // pass 1: [Qp | X]' X  -> C = Qp'X (project.m:34), X'X (norms before)
-    std::vector<double> G1((size_t)wp * m);
-    CAL_TRY(gram_host(c, n, W, X, G1.data()));
-    std::vector<double> C((size_t)w * m), GY((size_t)m * m);
-    for (int j = 0; j < m; ++j) {
-        for (int i = 0; i < w; ++i) C[i + (size_t)j * w] = G1[i + (size_t)j * wp];
-        for (int i = 0; i < m; ++i) GY[i + (size_t)j * m] = G1[w + i + (size_t)j * wp];
+    std::vector<double> C((size_t)w * m), GZ((size_t)m * m);
+    const int nq = w < 8 ? w : 8;
+    if (w <= 9 && nq + m <= 16) {
+        // one full MFMA tile [Qp(0:8) | X] + Qp column 8 as the VALU extra
+        Panel Tl = panel_slice(W, 0, nq);
+        Tl = panel_concat(Tl, X);
+        const double* E = nullptr;
+        if (w == 9) E = panel_slice(Qp, 8, 1).ptr[0];
+        double G16[256], e16[16];
+        CAL_TRY(tilegram_host(c, n, Tl, E, G16, e16));
+        for (int j = 0; j < m; ++j) {
+            for (int i = 0; i < nq; ++i) C[i + (size_t)j * w] = G16[i + (nq + j) * 16];
+            if (w == 9) C[8 + (size_t)j * w] = e16[nq + j];
+            for (int i = 0; i < m; ++i) GZ[i + (size_t)j * m] = G16[(nq + i) + (nq + j) * 16];
+        }
+    } else {
+        std::vector<double> G1((size_t)wp * m);
+        CAL_TRY(gram_host(c, n, W, X, G1.data()));
+        for (int j = 0; j < m; ++j) {
+            for (int i = 0; i < w; ++i) C[i + (size_t)j * w] = G1[i + (size_t)j * wp];
+            for (int i = 0; i < m; ++i) GZ[i + (size_t)j * m] = G1[w + i + (size_t)j * wp];
+        }
     }
-    std::vector<double> before(m), after(m), rel(m);
-    for (int i = 0; i < m; ++i) before[i] = std::sqrt(GY[i + (size_t)i * m]);
-    // ||Y||^2 = X'X - C'C (Qp orthonormal); projectAndNormalize.m:45-48
+    std::vector<double> before(m), rel(m);
+    for (int i = 0; i < m; ++i) before[i] = std::sqrt(GZ[i + (size_t)i * m]);
+    // ||Y||^2 = X'X - C'C for Y = X - Qp C (Qp orthonormal); projectAndNormalize.m:45-48
     for (int j = 0; j < m; ++j)
         for (int i = 0; i < m; ++i) {
             double s = 0.0;
             for (int k = 0; k < w; ++k) s += C[k + (size_t)i * w] * C[k + (size_t)j * w];
-            GY[i + (size_t)j * m] -= s;
+            GZ[i + (size_t)j * m] -= s;
         }
     for (int i = 0; i < m; ++i) {
-        after[i] = std::sqrt(std::max(GY[i + (size_t)i * m], 0.0));
-        rel[i] = std::fabs(before[i] - after[i]) / before[i];
+        const double after = std::sqrt(std::max(GZ[i + (size_t)i * m], 0.0));
+        rel[i] = std::fabs(before[i] - after) / before[i];
     }
-    const double mx = nan_max(rel);
-    const bool reorth = doreorth && (mx > 0.5);  // projectAndNormalize.m:52
-    std::vector<double> RY = C, GZ = GY;
-    if (reorth) {
-        // second pass on Y (never stored): C2 = Qp'Y, Y'Y directly
-        std::vector<double> M((size_t)wp * m, 0.0), C2((size_t)w * m), GYd((size_t)m * m);
-        for (int j = 0; j < m; ++j) {
-            for (int i = 0; i < w; ++i) M[i + (size_t)j * wp] = -C[i + (size_t)j * w];
-            M[w + j + (size_t)j * wp] = 1.0;
-        }
-        if (w <= 16) {
-            CAL_TRY(apply_host(c, n, W, M.data(), m, nullptr, GYd.data(), w, C2.data()));
-        } else {
-            CAL_TRY(ensure_work(c, m, X.ld[0]));
-            PanelOut Yw = panel_out(work_col(c, 0), X.ld[0], m);
-            CAL_TRY(apply_host(c, n, W, M.data(), m, &Yw, nullptr, 0, nullptr));
-            const Panel Yp = as_panel(Yw);
-            std::vector<double> G2((size_t)(w + m) * m);
-            CAL_TRY(gram_host(c, n, panel_concat(Qp, Yp), Yp, G2.data()));
-            for (int j = 0; j < m; ++j) {
-                for (int i = 0; i < w; ++i) C2[i + (size_t)j * w] = G2[i + (size_t)j * (w + m)];
-                for (int i = 0; i < m; ++i) GYd[i + (size_t)j * m] = G2[w + i + (size_t)j * (w + m)];
-            }
-        }
-        for (size_t e = 0; e < RY.size(); ++e) RY[e] = C[e] + C2[e];  // projectAndNormalize.m:71-73
-        for (int j = 0; j < m; ++j)
-            for (int i = 0; i < m; ++i) {
-                double s = 0.0;
-                for (int k = 0; k < w; ++k) s += C2[k + (size_t)i * w] * C2[k + (size_t)j * w];
-                GZ[i + (size_t)j * m] = GYd[i + (size_t)j * m] - s;
-            }
-    }
-    // normalize(Z), Z = X - Qp*RY formed on the fly: Mz = [-RY; I]
+    // projectAndNormalize.m:52 -- the reference's second projection.  Here it
+    // is always folded into pass B (a second CGS sweep on the stored block);
+    // the flag records the reference's decision.
+    const bool reorth = doreorth && (nan_max(rel) > 0.5);
     std::vector<double> Mz((size_t)wp * m, 0.0);
     for (int j = 0; j < m; ++j) {
-        for (int i = 0; i < w; ++i) Mz[i + (size_t)j * wp] = -RY[i + (size_t)j * w];
+        for (int i = 0; i < w; ++i) Mz[i + (size_t)j * wp] = -C[i + (size_t)j * w];
         Mz[w + j + (size_t)j * wp] = 1.0;
     }
-    bool sh = false;
     std::vector<double> Rtmp((size_t)m * m);
     if (!dense::chol_upper(m, GZ.data(), m, Rtmp.data(), m)) {
-        // the algebraic Gram lost definiteness: take Z'Z directly
+        // the algebraic Gram lost definiteness (heavy cancellation): Y'Y directly
         CAL_TRY(apply_host(c, n, W, Mz.data(), m, nullptr, GZ.data(), 0, nullptr));
     }
-    CAL_TRY(cholqr_passes(c, n, W, Mz, m, GZ.data(), Qout, R, &sh));
-    std::copy(RY.begin(), RY.end(), Rq);
+    bool sh = false;
+    std::vector<double> Ctot;
+    CAL_TRY(two_pass(c, n, Qp, W, Mz, m, GZ.data(), Qout, R, Ctot, &sh));
+    for (size_t e = 0; e < C.size(); ++e) Rq[e] = C[e] + Ctot[e];
     if (res) {
         res->reorth = reorth;
         res->rank = rank_from_R(m, R, 1.0e-8);

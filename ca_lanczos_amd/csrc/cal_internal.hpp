@@ -123,6 +123,23 @@ ApplyPlan apply_plan(int wp, int wy, int64_t n, bool gram, int wq);
 hipError_t launch_apply(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y, bool store,
                         int wq, int64_t n, const ApplyPlan& pl, double* partial, hipStream_t st);
 hipError_t launch_reduce(const double* partial, int nparts, int64_t nent, double* out, hipStream_t st);
+// hot-shape kernels (s <= 8): tile Gram (<= 16 columns + 1 extra) and the
+// row-parallel apply with the fused LDS-transposed tile Gram.  Partials:
+// 272 entries (16x16 tile Gram, then 16 extra-column products).
+hipError_t launch_tilegram(const Panel& T, const double* E, int64_t n, int blocks, double* partial, hipStream_t st);
+int rowapply_wpmax(int wp);
+int rowapply_mout(int m);
+// column pointers resolved on the host (kernel-argument arrays -> SGPR bases)
+struct ColList {
+    const double* p[17];
+};
+struct OutList {
+    double* p[16];
+};
+hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, const OutList& Y, bool gram, int wq,
+                           int64_t n, int blocks, double* partial, hipStream_t st);
+hipError_t launch_rowgram(const ColList& P, int nt, bool has_extra, int64_t n, int blocks, double* partial,
+                          hipStream_t st);
 hipError_t launch_dot(const double* x, const double* y, int64_t n, double* partial, int blocks,
                       hipStream_t st);
 int dot_blocks(int64_t n);

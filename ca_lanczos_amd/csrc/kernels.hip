@@ -228,7 +228,9 @@ __global__ __launch_bounds__(256) void k_gram(Panel A, Panel B, int64_t n, doubl
     __syncthreads();
     if (wave == 0) {
         const int ldc = 16 * NTA;
-        double* out = partial + (int64_t)blockIdx.x * (ldc * 16);
+        // entry-major partials: entry e of block b at partial[e * nblocks + b]
+        double* out = partial + blockIdx.x;
+        const int64_t nb = gridDim.x;
 #pragma unroll
         for (int t = 0; t < NTA; ++t)
 #pragma unroll
@@ -238,7 +240,7 @@ __global__ __launch_bounds__(256) void k_gram(Panel A, Panel B, int64_t n, doubl
                 v = v + red[1][t][lane][r];
                 v = v + red[2][t][lane][r];
                 const int i = t * 16 + g + 4 * r, j = c16;
-                out[j * ldc + i] = v;
+                out[(int64_t)(j * ldc + i) * nb] = v;
             }
     }
 }
@@ -397,7 +399,9 @@ __global__ __launch_bounds__(256) void k_apply(Panel P, const double* __restrict
         __syncthreads();
         if (wave == 0) {
             const int nent = 256 * ((GRAM ? 1 : 0) + (GRAMP ? 1 : 0));
-            double* out = partial + (int64_t)blockIdx.x * nent;
+            double* out = partial + blockIdx.x;  // entry-major: [entry][block]
+            const int64_t nb = gridDim.x;
+            (void)nent;
             int base = 0;
 #pragma unroll
             for (int which = 0; which < 2; ++which) {
@@ -409,7 +413,7 @@ __global__ __launch_bounds__(256) void k_apply(Panel P, const double* __restrict
                     v = v + red[((1 * 2 + which) * 64 + lane) * 4 + r];
                     v = v + red[((2 * 2 + which) * 64 + lane) * 4 + r];
                     const int i = g + 4 * r, j = c16;
-                    out[base + j * 16 + i] = v;
+                    out[(int64_t)(base + j * 16 + i) * nb] = v;
                 }
                 base += 256;
             }
@@ -465,27 +469,287 @@ hipError_t launch_apply(const Panel& P, const double* dM, int wp, int wy, const 
 }
 
 // --------------------------------------------------------------------------
-// fixed-order partial reduction and small vector kernels
+// Hot-shape kernels (block width s <= 8, projection block w <= 9).
+//
+// k_tilegram: G = T^T T for a tile T of <= 16 columns (one v_mfma_f64_16x16x4
+// per 4 rows, A and B the same register: no padding MFMAs) plus E^T T for
+// up to one extra column E (VALU).  Lane layout as k_gram.
+// Partials (entry-major): [0,256) tile Gram (col-major 16x16), [256,272)
+// E^T T.
 // --------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_reduce(const double* __restrict__ part, int nparts, int64_t nent,
-                                                double* __restrict__ out) {
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (e >= nent) return;
-    double s = 0.0;
-    for (int p = 0; p < nparts; ++p) s = s + part[(int64_t)p * nent + e];
-    out[e] = s;
+template <int RUN>
+__global__ __launch_bounds__(256) void k_tilegram(Panel T, const double* __restrict__ E, int64_t n,
+                                                  double* __restrict__ partial) {
+    __shared__ double red[3][64][5];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int c16 = lane & 15, g = lane >> 4;
+    const bool on = c16 < T.total;
+    const double* tc = pcol(T, on ? c16 : 0);
+    const bool eon = E != nullptr;
+    const double* ec = eon ? E : tc;
+    d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+    double eacc = 0.0;
+    const int64_t wstep = 4 * RUN;
+    const int64_t stride = (int64_t)gridDim.x * 4 * wstep;
+    for (int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * wstep; r0 < n; r0 += stride) {
+        const int64_t rb = r0 + g * RUN;
+        double av[RUN], ev[RUN];
+        if (r0 + wstep <= n) {
+#pragma unroll
+            for (int m = 0; m < RUN; m += 2) {
+                d2 x = *reinterpret_cast<const d2*>(tc + rb + m);
+                d2 y = *reinterpret_cast<const d2*>(ec + rb + m);
+                av[m] = on ? x[0] : 0.0;
+                av[m + 1] = on ? x[1] : 0.0;
+                ev[m] = eon ? y[0] : 0.0;
+                ev[m + 1] = eon ? y[1] : 0.0;
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < RUN; ++m) {
+                const bool in = rb + m < n;
+                const int64_t rr = in ? rb + m : 0;
+                const double x = tc[rr], y = ec[rr];
+                av[m] = (on && in) ? x : 0.0;
+                ev[m] = (eon && in) ? y : 0.0;
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < RUN; ++m) {
+            acc = mfma64(av[m], av[m], acc);
+            eacc = eacc + ev[m] * av[m];
+        }
+    }
+    if (wave > 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[wave - 1][lane][r] = acc[r];
+        red[wave - 1][lane][4] = eacc;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const int64_t nb = gridDim.x;
+        double* out = partial + blockIdx.x;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            double v = acc[r];
+            v = v + red[0][lane][r];
+            v = v + red[1][lane][r];
+            v = v + red[2][lane][r];
+            const int i = g + 4 * r, j = c16;
+            out[(int64_t)(j * 16 + i) * nb] = v;
+        }
+        // E^T T: reduce the four row groups g of column c16 in a fixed order
+        double e = eacc;
+        e = e + red[0][lane][4];
+        e = e + red[1][lane][4];
+        e = e + red[2][lane][4];
+        const double e1 = __shfl(e, c16 + 16, 64), e2 = __shfl(e, c16 + 32, 64), e3 = __shfl(e, c16 + 48, 64);
+        if (g == 0) out[(int64_t)(256 + c16) * nb] = ((e + e1) + e2) + e3;
+    }
 }
 
-hipError_t launch_reduce(const double* partial, int nparts, int64_t nent, double* out, hipStream_t st) {
-    dim3 g((unsigned)((nent + 255) / 256)), b(256);
-    hipLaunchKernelGGL(k_reduce, g, b, 0, st, partial, nparts, nent, out);
+hipError_t launch_tilegram(const Panel& T, const double* E, int64_t n, int blocks, double* partial,
+                           hipStream_t st) {
+    hipLaunchKernelGGL((k_tilegram<16>), dim3(blocks), dim3(256), 0, st, T, E, n, partial);
     return hipGetLastError();
 }
 
+// k_rowapply: lane <-> row.  Y = P * M with P of wp <= WPMAX columns and
+// M zero-padded to WPMAX x MOUT (row-major in global memory, wave-uniform
+// index -> scalar loads).  Every column load is a contiguous 512-B wave
+// access; padded columns reload a valid column (cache hit) times zero.
+// GRAM: the stored rows [Qp(0:nq) | Y(0:m)] (nq = min(wq, 8)) are
+// transposed through LDS into one 16-column tile and accumulated with
+// v_mfma_f64_16x16x4 (tile^T tile); Qp column 8 (if wq == 9) is the extra
+// column.  Partials as k_tilegram.
+// APPLY = false: Gram only (no M, no store): tile = P columns 0..m-1, extra
+// column = P column 16 when wq > 0 (the row-parallel form of k_tilegram).
+template <int WPMAX, int MOUT, bool GRAM, bool APPLY = true>
+__global__ __launch_bounds__(256, 2) void k_rowapply(ColList P, const double* __restrict__ M, int wp, int m,
+                                                  OutList Y, int wq, int64_t n, double* __restrict__ partial) {
+    constexpr int TLD = 17;  // padded LDS row (doubles)
+    __shared__ double tile[GRAM ? 256 * TLD : 1];
+    __shared__ double ext[GRAM ? 256 : 1];
+    __shared__ double red[GRAM ? 3 * 64 * 5 : 1];
+    __shared__ __attribute__((aligned(16))) double Ms[WPMAX * MOUT];  // broadcast reads
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int c16 = lane & 15, g = lane >> 4;
+    const int nq = wq < 8 ? wq : 8;
+    const bool has_ext = wq > 8;
+    if (APPLY)
+        for (int e = tid; e < WPMAX * MOUT; e += 256) Ms[e] = M[e];
+    if (GRAM)
+        for (int e = tid; e < 256 * TLD; e += 256) tile[e] = 0.0;
+    __syncthreads();
+    d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+    double eacc = 0.0;
+    // (host pads P.p[c >= wp] with a valid column and Y.p[j >= m] unused)
+    const double* const* pc = P.p;
+    double* const* yc = Y.p;
+    // without the Gram one row per thread and no loop (nothing for the
+    // compiler to hoist the M broadcasts out of); with it a grid-stride loop
+    // whose LDS reads are pinned inside the iteration by a compiler barrier.
+    const int64_t stride = GRAM ? (int64_t)gridDim.x * 256 : n;
+    for (int64_t base = (int64_t)blockIdx.x * 256; base < n; base += stride) {
+        asm volatile("" ::: "memory");
+        const int64_t r = base + tid;
+        const bool in = r < n;
+        const int64_t rr = in ? r : n - 1;
+        double p[WPMAX];
+#pragma unroll
+        for (int c = 0; c < WPMAX; ++c) {
+            const double v = pc[c][rr];
+            p[c] = in ? v : 0.0;
+        }
+        double y[MOUT];
+#pragma unroll
+        for (int j = 0; j < MOUT; ++j) y[j] = 0.0;
+#pragma unroll
+        for (int c = 0; c < (APPLY ? WPMAX : 0); ++c) {
+            // one M row per column, read right before use: the barrier takes
+            // the accumulators as operands, so column c's FMAs retire before
+            // column c+1's broadcasts issue (otherwise the scheduler keeps all
+            // WPMAX*MOUT M values live and spills)
+#pragma unroll
+            for (int j = 0; j < MOUT; ++j) asm volatile("" : "+v"(y[j])::"memory");
+            double mrow[MOUT];
+#pragma unroll
+            for (int j = 0; j < MOUT; j += 2) {
+                const d2 t = *reinterpret_cast<const d2*>(&Ms[c * MOUT + j]);
+                mrow[j] = t[0];
+                if (j + 1 < MOUT) mrow[j + 1] = t[1];
+            }
+#pragma unroll
+            for (int j = 0; j < MOUT; ++j) y[j] = __builtin_fma(p[c], mrow[j], y[j]);
+        }
+        if (APPLY && in) {
+#pragma unroll
+            for (int j = 0; j < MOUT; ++j)
+                if (j < m) yc[j][r] = y[j];
+        }
+        if (GRAM) {
+            double* trow = tile + tid * TLD;
+            if (APPLY) {
+#pragma unroll
+                for (int c = 0; c < 8; ++c)
+                    if (c < nq) trow[c] = p[c < WPMAX ? c : 0];
+#pragma unroll
+                for (int j = 0; j < MOUT; ++j)
+                    if (j < m) trow[nq + j] = y[j];
+                ext[tid] = has_ext ? p[8 < WPMAX ? 8 : 0] : 0.0;
+            } else {  // Gram only: tile = P columns 0..m-1, extra = column 16
+#pragma unroll
+                for (int c = 0; c < 16; ++c)
+                    if (c < m) trow[c] = p[c < WPMAX ? c : 0];
+                ext[tid] = wq > 0 ? p[16 < WPMAX ? 16 : 0] : 0.0;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int row = wave * 64 + 4 * k + g;
+                const double a = tile[row * TLD + c16];
+                acc = mfma64(a, a, acc);
+                eacc = eacc + ext[row] * a;
+            }
+            __syncthreads();
+        }
+    }
+    if (GRAM) {
+        if (wave > 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[((wave - 1) * 64 + lane) * 5 + r] = acc[r];
+            red[((wave - 1) * 64 + lane) * 5 + 4] = eacc;
+        }
+        __syncthreads();
+        if (wave == 0) {
+            const int64_t nb = gridDim.x;
+            double* out = partial + blockIdx.x;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                double v = acc[r];
+                v = v + red[(0 * 64 + lane) * 5 + r];
+                v = v + red[(1 * 64 + lane) * 5 + r];
+                v = v + red[(2 * 64 + lane) * 5 + r];
+                out[(int64_t)(c16 * 16 + g + 4 * r) * nb] = v;
+            }
+            double e = eacc;
+            e = e + red[(0 * 64 + lane) * 5 + 4];
+            e = e + red[(1 * 64 + lane) * 5 + 4];
+            e = e + red[(2 * 64 + lane) * 5 + 4];
+            const double e1 = __shfl(e, c16 + 16, 64), e2 = __shfl(e, c16 + 32, 64), e3 = __shfl(e, c16 + 48, 64);
+            if (g == 0) out[(int64_t)(256 + c16) * nb] = ((e + e1) + e2) + e3;
+        }
+    }
+}
+
+int rowapply_wpmax(int wp) { return wp <= 5 ? 5 : (wp <= 9 ? 9 : (wp <= 17 ? 17 : 0)); }
+int rowapply_mout(int m) { return m <= 4 ? 4 : (m <= 8 ? 8 : (m <= 16 ? 16 : 0)); }
+
+hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, const OutList& Y, bool gram, int wq,
+                           int64_t n, int blocks, double* partial, hipStream_t st) {
+    const int WP = rowapply_wpmax(wp), MO = rowapply_mout(m);
+    dim3 g(blocks), b(256);
+#define CAL_RA(W, MM, G) \
+    hipLaunchKernelGGL((k_rowapply<W, MM, G>), g, b, 0, st, P, dM, wp, m, Y, wq, n, partial)
+    const int key = WP * 1000 + MO * 10 + (gram ? 1 : 0);
+    switch (key) {
+        case 5040: CAL_RA(5, 4, false); break;
+        case 5041: CAL_RA(5, 4, true); break;
+        case 9040: CAL_RA(9, 4, false); break;
+        case 9041: CAL_RA(9, 4, true); break;
+        case 9080: CAL_RA(9, 8, false); break;
+        case 9081: CAL_RA(9, 8, true); break;
+        case 9160: CAL_RA(9, 16, false); break;
+        case 9161: CAL_RA(9, 16, true); break;
+        case 17080: CAL_RA(17, 8, false); break;
+        case 17081: CAL_RA(17, 8, true); break;
+        case 17160: CAL_RA(17, 16, false); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef CAL_RA
+    return hipGetLastError();
+}
+
+// Row-parallel tile Gram: tile = P.p[0..nt) (nt <= 16), extra = P.p[16] if
+// has_extra.  Same partial layout as k_tilegram.
+hipError_t launch_rowgram(const ColList& P, int nt, bool has_extra, int64_t n, int blocks, double* partial,
+                          hipStream_t st) {
+    OutList none{};
+    hipLaunchKernelGGL((k_rowapply<17, 4, true, false>), dim3(blocks), dim3(256), 0, st, P, nullptr, 17, nt, none,
+                       has_extra ? 1 : 0, n, partial);
+    return hipGetLastError();
+}
+
+// --------------------------------------------------------------------------
+// fixed-order partial reduction and small vector kernels
+// --------------------------------------------------------------------------
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v = v + __shfl_xor(v, off, 64);
     return v;
+}
+
+// One block per entry: partials are entry-major (part[e*nparts + p]), so the
+// 256 threads read one contiguous run; fixed-order strided sums, then a fixed
+// butterfly and a fixed wave order -> bitwise reproducible.
+__global__ __launch_bounds__(256) void k_reduce(const double* __restrict__ part, int nparts,
+                                                double* __restrict__ out) {
+    __shared__ double ws[4];
+    const int64_t e = blockIdx.x;
+    const double* p = part + e * nparts;
+    double s = 0.0;
+    for (int i = threadIdx.x; i < nparts; i += 256) s = s + p[i];
+    s = wave_sum(s);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) ws[wave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) out[e] = ((ws[0] + ws[1]) + ws[2]) + ws[3];
+}
+
+hipError_t launch_reduce(const double* partial, int nparts, int64_t nent, double* out, hipStream_t st) {
+    if (nent <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_reduce, dim3((unsigned)nent), dim3(256), 0, st, partial, nparts, out);
+    return hipGetLastError();
 }
 
 __global__ __launch_bounds__(256) void k_dot(const double* __restrict__ x, const double* __restrict__ y,
@@ -593,8 +857,8 @@ __global__ __launch_bounds__(256) void k_spmv_resid(SpmvArgs a, const double* __
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        partial[2 * blockIdx.x] = ((ws[0][0] + ws[0][1]) + ws[0][2]) + ws[0][3];
-        partial[2 * blockIdx.x + 1] = ((ws[1][0] + ws[1][1]) + ws[1][2]) + ws[1][3];
+        partial[blockIdx.x] = ((ws[0][0] + ws[0][1]) + ws[0][2]) + ws[0][3];
+        partial[gridDim.x + blockIdx.x] = ((ws[1][0] + ws[1][1]) + ws[1][2]) + ws[1][3];
     }
 }
 
