@@ -19,13 +19,17 @@ using cd = std::complex<double>;
 
 static bool is_conj_pair(cd a, cd b) { return a.real() == b.real() && a.imag() == -b.imag() && a.imag() != 0; }
 
+// |z| exactly as MATLAB/NumPy/glibc compute it (hypot); clang may lower
+// std::abs(std::complex) to an inline sqrt(re^2 + im^2) that rounds differently.
+static double cabs_h(cd z) { return std::hypot(z.real(), z.imag()); }
+
 // permutation of MATLAB [~,ix] = sort(x) (stable; complex: |x| then angle)
 static std::vector<int> sort_perm(const std::vector<cd>& x, bool cplx) {
     std::vector<int> idx(x.size());
     for (size_t i = 0; i < x.size(); ++i) idx[i] = (int)i;
     auto key_less = [&](int a, int b) {
         if (!cplx) return x[a].real() < x[b].real();
-        const double aa = std::abs(x[a]), ab = std::abs(x[b]);
+        const double aa = cabs_h(x[a]), ab = cabs_h(x[b]);
         if (aa != ab) return aa < ab;
         return std::atan2(x[a].imag(), x[a].real()) < std::atan2(x[b].imag(), x[b].real());
     };
@@ -85,7 +89,7 @@ int modified_leja(std::vector<cd> x, int n, const std::vector<double>& mults, st
         outidx.push_back(0);
     } else {  // modified_leja_start (modified_leja.m:41-78)
         std::vector<double> ax(n);
-        for (int i = 0; i < n; ++i) ax[i] = std::abs(x[i]);
+        for (int i = 0; i < n; ++i) ax[i] = cabs_h(x[i]);
         const int j = first_max(ax);
         if (x[j].imag() == 0) {
             y.push_back(x[j]);
@@ -126,7 +130,7 @@ int modified_leja(std::vector<cd> x, int n, const std::vector<double>& mults, st
             std::vector<double> terms;
             for (int t = 0; t < num_points - 1; ++t) {
                 const int o = outidx[t];
-                terms.push_back(std::pow(std::abs(y_last - x[o]), mults[o] * (1.0 / num_points)));
+                terms.push_back(std::pow(cabs_h(y_last - x[o]), mults[o] * (1.0 / num_points)));
             }
             capacity = seq_prod(terms);
             const double ratio = capacity / old_capacity;
@@ -137,7 +141,7 @@ int modified_leja(std::vector<cd> x, int n, const std::vector<double>& mults, st
         std::vector<double> zprod;
         for (int j : inidx) {
             std::vector<double> terms;
-            for (int o : outidx) terms.push_back(std::pow(std::abs(x[j] - x[o]) / capacity, mults[o]));
+            for (int o : outidx) terms.push_back(std::pow(cabs_h(x[j] - x[o]) / capacity, mults[o]));
             zprod.push_back(seq_prod(terms));
         }
         const int k = first_max(zprod);

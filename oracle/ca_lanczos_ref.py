@@ -445,8 +445,13 @@ def modified_leja(x, n, mults):
             terms = [abs(y_last - x[o]) ** (mults[o] * (1.0 / num_points))
                      for o in outidx[: num_points - 1]]
             capacity = _seq_prod(terms)
-            x = x / (capacity / old_capacity)
-            y = y / (capacity / old_capacity)
+            ratio = capacity / old_capacity
+            if cplx:  # MATLAB complex ./ real is componentwise (NumPy uses a reciprocal)
+                x = x.real / ratio + 1j * (x.imag / ratio)
+                y = y.real / ratio + 1j * (y.imag / ratio)
+            else:
+                x = x / ratio
+                y = y / ratio
         first = False
         zprod = []
         for j in inidx:                                         # :121-128

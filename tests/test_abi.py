@@ -1,0 +1,98 @@
+"""The C ABI: the library loads without a GPU, exports every symbol the
+public headers declare, and its host-only entry points match the oracle.
+CPU only (no compute call needs a GPU here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    names = set()
+    for h in ("calanczos.h", "calanczos_host.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(cal_[a-z0-9_]+)\s*\(", src))
+    names -= {"cal_allreduce_fn", "cal_exchange_fn"}
+    return names
+
+
+def test_library_exports_every_declared_symbol(cal):
+    lib = ctypes.CDLL(cal.LIB_PATH)
+    declared = _declared_symbols()
+    assert len(declared) >= 35
+    missing = [s for s in declared if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_binding_covers_header():
+    from ca_lanczos_amd import _lib
+    bound = {s[0] for s in _lib.SIGNATURES}
+    assert _declared_symbols() <= bound
+
+
+def test_version_and_no_gpu_behaviour(cal):
+    from ca_lanczos_amd._lib import lib
+    assert lib.cal_version() >= 1
+    n = ctypes.c_int(-1)
+    lib.cal_device_count(ctypes.byref(n))
+    h = ctypes.c_void_p()
+    st = lib.cal_create(0, ctypes.byref(h))
+    if n.value == 0:
+        assert st != 0 and not h.value  # fails loudly, no CPU fallback
+    else:  # pragma: no cover - a GPU is present
+        lib.cal_destroy(h)
+
+
+def test_leja_bitexact_vs_oracle(cal, ref):
+    g = np.load(os.path.join(ROOT, "tests", "golden", "leja.npz"))
+    for i in range(5):
+        y, idx = cal.leja(g["x%d" % i], "nonmodified")
+        assert np.array_equal(y, g["y%d" % i]), i
+        assert np.array_equal(idx, g["idx%d" % i]), i
+    rng = np.random.RandomState(7)
+    for _ in range(20):
+        x = np.sort(rng.uniform(-1, 13, 16))
+        assert np.array_equal(cal.leja(x, "m")[0], ref.leja(x, "m")[0])
+
+
+def test_newton_basis_matrix_vs_oracle(cal, ref):
+    for lam in (np.array([11.5, 0.3, 6.1, 2.2, 9.0, 4.4, 1.1, 7.7]), np.array([2 + 1j, 2 - 1j, 5.0, 1.0])):
+        s = len(lam)
+        for modifiedp in (1,):
+            assert np.array_equal(cal.newton_basis_matrix(lam, s, modifiedp), ref.newton_basis_matrix(lam, s, modifiedp))
+    lam = np.arange(1.0, 5.0)
+    assert np.array_equal(cal.newton_basis_matrix(lam, 4, 0), ref.newton_basis_matrix(lam, 4, 0))
+
+
+def test_eig_general_and_symmetric(cal):
+    rng = np.random.RandomState(5)
+    for n in (1, 2, 7, 40, 121):
+        T = rng.randn(n, n)
+        w, V = cal.eig(T)
+        assert np.max(np.abs(np.sort_complex(w) - np.sort_complex(np.linalg.eigvals(T)))) < 1e-10 * max(1, n)
+        assert np.max(np.abs(T @ V - V * w[None, :])) < 1e-10 * max(1, n)
+    S = rng.randn(30, 30)
+    S = S + S.T
+    w, V = cal.eig(S)
+    assert np.isrealobj(w) and np.allclose(w, np.linalg.eigvalsh(S)) and np.allclose(V.T @ V, np.eye(30))
+
+
+def test_eig_on_ca_lanczos_T(cal):
+    g = np.load(os.path.join(ROOT, "tests", "golden", "lap2d_32_s8_newton_local.npz"))
+    T = g["T"]
+    w, V = cal.eig(T)
+    assert np.max(np.abs(np.sort_complex(w) - g["ritz"])) < 1e-10
+    assert np.max(np.abs(T @ V - V * w[None, :])) < 1e-10
+
+
+def test_tridiag_eigvals(cal):
+    from ca_lanczos_amd._lib import lib, ptr
+    rng = np.random.RandomState(2)
+    a, b = rng.randn(16), rng.rand(15)
+    w = np.zeros(16)
+    assert lib.cal_tridiag_eigvals(16, ptr(a), ptr(b), ptr(w)) == 0
+    assert np.allclose(w, np.linalg.eigvalsh(np.diag(a) + np.diag(b, 1) + np.diag(b, -1)), atol=1e-13)

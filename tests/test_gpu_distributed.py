@@ -1,0 +1,97 @@
+"""The library's own distributed path (cal_set_matrix_csr_dist + halo
+exchange + allreduced Grams) on the GPU: 2 ranks share the one GPU of the
+test box and talk through the host-staged communicator (gloo callbacks);
+RCCL replaces exactly these two callbacks on a multi-GPU node."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, case, out_q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import ca_lanczos_amd as cal
+    from oracle import ca_lanczos_ref as ref
+
+    def allreduce(a):
+        t = torch.from_numpy(a)
+        dist.all_reduce(t)
+
+    def exchange(peer, send, recv):
+        reqs = []
+        if send.size:
+            reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(send)), peer))
+        rt = torch.zeros(recv.size, dtype=torch.float64)
+        if recv.size:
+            reqs.append(dist.irecv(rt, peer))
+        for r in reqs:
+            r.wait()
+        if recv.size:
+            recv[:] = rt.numpy()
+
+    dim, N, s, it, orth = case
+    A = cal.matrices.laplacian_2d(N) if dim == 2 else cal.matrices.laplacian_3d(N)
+    n = A.shape[0]
+    b = cal.matrices.slab_bounds(n, world, N ** (dim - 1))
+    r0, r1 = b[rank], b[rank + 1]
+    ctx = cal.Context(0)
+    ctx.comm_init_host(world, rank, allreduce, exchange)
+    ctx.set_matrix_slab(n, r0, A[r0:r1])
+    info = ctx.matrix_info()
+    x = ref.matlab_rand(n, seed=5)
+    from ca_lanczos_amd._lib import check, lib, ptr
+    xl = np.ascontiguousarray(x[r0:r1])
+    y = np.zeros(r1 - r0)
+    check(ctx.h, lib.cal_spmv(ctx.h, ptr(xl), ptr(y)))
+    ok_spmv = np.array_equal(y, (A @ x)[r0:r1])
+    out = cal.ca_lanczos_ex(A, ref.matlab_rand(n)[r0:r1], s, it, "newton", orth, diagnostics=True, ctx=ctx)
+    out_q.put((rank, ok_spmv, info, out.T, out.ritz_rnorm, out.orth_err, list(out.reorth)))
+    ctx.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", [(2, 32, 8, 48, "local"), (3, 10, 8, 32, "full")])
+def test_two_ranks_one_gpu_match_single(cal, ref, case):
+    world = 2
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    procs = [mpc.Process(target=_worker, args=(r, world, port, case, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    dim, N, s, it, orth = case
+    A = cal.matrices.laplacian_2d(N) if dim == 2 else cal.matrices.laplacian_3d(N)
+    r = ref.matlab_rand(A.shape[0])
+    single = cal.ca_lanczos_ex(A, r, s, it, "newton", orth, diagnostics=True)
+    normA = 4.0 * dim
+    for rank, ok_spmv, info, T, rn, oe, flags in res:
+        assert ok_spmv, rank
+        assert info["nghost"] > 0
+        assert flags == list(single.reorth)
+        assert np.max(np.abs(T - single.T)) <= 1e-9 * normA
+        big = single.ritz_rnorm[:, 0] > 1e-10
+        assert np.all(np.abs(np.log(rn[big, 0] / single.ritz_rnorm[big, 0])) < np.log(1.5))
+    assert np.array_equal(res[0][3], res[1][3])

@@ -1,0 +1,113 @@
+"""The oracle restatement, pinned against (1) the analytic known answers of
+the reference's own synthetic inputs and (2) the committed golden fixtures
+(tests/golden/make_golden.py).  CPU only."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _case(name):
+    from golden_cases import CASES  # noqa: F401
+    return CASES[name]
+
+
+@pytest.fixture(scope="module")
+def golden_mod():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLD, "make_golden.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_matlab_rand_seed_5489(ref):
+    # MATLAB: rand(5,1) in a fresh session
+    assert np.allclose(ref.matlab_rand(5), [0.8147, 0.9058, 0.1270, 0.9134, 0.6324], atol=5e-5)
+
+
+def test_matlab_linspace(ref):
+    y = ref.matlab_linspace(1.0, 100.0, 500)
+    assert y[0] == 1.0 and y[-1] == 100.0 and len(y) == 500
+    assert np.allclose(np.diff(y), 99.0 / 499.0)
+
+
+def test_sort_semantics(ref):
+    d = np.array([1 + 1j, 1 - 1j, -2.0 + 0j, 0.5 + 0j])
+    ix = ref._sort_perm(d, True)
+    assert list(ix) == [2, 0, 1, 3]  # |.| desc, then angle desc (+pi/4 before -pi/4)
+    assert ref._matlab_max([1.0, float("nan"), 3.0, 3.0]) == (3.0, 2)
+
+
+def test_tsqr_positive_diagonal(ref):
+    X = np.random.RandomState(0).randn(200, 6)
+    Q, R = ref.tsqr(X)
+    assert np.all(np.diag(R) > 0) and np.allclose(Q @ R, X) and np.allclose(Q.T @ Q, np.eye(6))
+
+
+def test_project_inverted_reorth_rule(ref):
+    # project.m:44-47 reorthogonalises when NO column lost more than half its norm
+    rng = np.random.RandomState(1)
+    Q, _ = np.linalg.qr(rng.randn(100, 3))
+    X = rng.randn(100, 2)
+    X1, R1 = ref.project([Q], X, True)
+    X0, R0 = ref.project([Q], X, False)
+    assert np.max(np.abs(Q.T @ X1)) <= np.max(np.abs(Q.T @ X0)) + 1e-15
+
+
+def test_newton_basis_matrix(ref):
+    B = ref.newton_basis_matrix(np.array([3.0, 1.0, 2.0]), 3, 1)
+    assert np.array_equal(B, np.array([[3, 0, 0], [1, 1, 0], [0, 1, 2], [0, 0, 1.0]]))
+    Bc = ref.newton_basis_matrix(np.array([2 + 1j, 2 - 1j, 5.0]), 3, 1)
+    assert Bc[0, 1] == -1.0 and Bc[1, 1] == 2.0 and Bc[0, 0] == 2.0
+
+
+@pytest.mark.parametrize("name", ["c1_diag1000_s4_monomial_local", "diag500_linspace_s4_newton_local",
+                                  "lap2d_32_s8_newton_local", "lap3d_12_s8_newton_local",
+                                  "lap2d_24_s8_newton_full", "diag5000_linspace_s4_newton_full"])
+def test_oracle_vs_golden_and_known_answers(ref, golden_mod, name):
+    spec = golden_mod.CASES[name]
+    A, exact, r, res = golden_mod.run_case(spec)
+    g = np.load(os.path.join(GOLD, name + ".npz"))
+    normA = max(abs(exact[0]), abs(exact[-1]))
+    # regression against the committed fixture
+    assert res.T.shape == g["T"].shape
+    assert np.max(np.abs(res.T - g["T"])) <= 1e-9 * normA
+    assert list(res.reorth) == list(g["reorth"])
+    if len(g["shifts"]):
+        assert np.max(np.abs(res.shifts - g["shifts"])) <= 1e-12 * normA
+    # known answer: converged extreme Ritz values are eigenvalues of A
+    w = np.sort(np.linalg.eigvals(res.T).real)
+    rn = res.ritz_rnorm[-1]
+    if rn[0] < 1e-6:  # largest Ritz pair converged (rn(:,1) is the largest, ca_lanczos.m:91)
+        assert abs(w[-1] - exact[-1]) <= 1e-6 * normA
+    assert exact[0] - 1e-8 * normA <= w[0] and w[-1] <= exact[-1] + 1e-8 * normA
+    # relative residuals are reported for every Ritz pair, sorted by value
+    assert res.ritz_rnorm.shape == (len(res.reorth), res.T.shape[0])
+    assert np.all(res.orth_err >= 0)
+
+
+def test_leja_golden(ref):
+    g = np.load(os.path.join(GOLD, "leja.npz"))
+    for i in range(5):
+        y, idx = ref.leja(g["x%d" % i], "nonmodified")
+        assert np.array_equal(y, g["y%d" % i]) and np.array_equal(idx, g["idx%d" % i])
+
+
+def test_leja_is_leja(ref):
+    # defining property of (modified) Leja points: each new point maximises
+    # the product of distances to the points already chosen
+    x = np.sort(np.random.RandomState(3).uniform(0, 12, 16))
+    y, _ = ref.leja(x, "nonmodified")
+    # (the capacity rescaling of modified_leja.m:100-114,192 moves values by ulps)
+    assert np.isclose(abs(y[0]), np.max(np.abs(x)), rtol=1e-14)
+    for k in range(1, len(y)):
+        prods = [np.prod(np.abs(c - y[:k])) for c in y[k:]]
+        assert np.isclose(prods[0], max(prods), rtol=1e-10)
+
+
+def test_fixture_files_present():
+    assert len(glob.glob(os.path.join(GOLD, "*.npz"))) >= 7
