@@ -66,6 +66,9 @@ SIGNATURES = [
      [c_void_p, c_int64, c_int64, c_int64, POINTER(c_int64), POINTER(c_int64), dp]),
     ("cal_matrix_info", c_int,
      [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64), POINTER(c_int64)]),
+    ("cal_set_spmv_format", c_int, [c_void_p, c_char_p]),
+    ("cal_spmv_format", c_int, [c_void_p, ip, ip, ip]),
+    ("cal_bench_spmv", c_int, [c_void_p, c_int, c_double, dp, dp]),
     ("cal_spmv", c_int, [c_void_p, dp, dp]),
     ("cal_matrix_powers_monomial", c_int, [c_void_p, dp, c_int, dp]),
     ("cal_matrix_powers_newton", c_int, [c_void_p, dp, c_int, dp, dp, c_int, dp]),

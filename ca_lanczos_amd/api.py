@@ -25,7 +25,7 @@ class Context:
     """A device context (``cal_ctx``): one HIP stream, the resident matrix and
     the device-resident CA-Lanczos state."""
 
-    def __init__(self, device: int | None = None):
+    def __init__(self, device: int | None = None, spmv_format: str | None = None):
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", "0"))
         h = ctypes.c_void_p()
@@ -36,6 +36,26 @@ class Context:
         self.device = device
         self.n = None
         self._keep = []
+        fmt = spmv_format or os.environ.get("CAL_SPMV_FORMAT", "auto")
+        check(self.h, lib.cal_set_spmv_format(self.h, fmt.encode()), "spmv format")
+
+    def bench_spmv(self, reps=20, shift=0.0):
+        """Mean and min SpMV kernel time (ms) on HBM-resident vectors."""
+        a, b = ctypes.c_double(), ctypes.c_double()
+        check(self.h, lib.cal_bench_spmv(self.h, reps, shift, ctypes.byref(a), ctypes.byref(b)), "bench_spmv")
+        return a.value, b.value
+
+    def spmv(self, v):
+        v = f64(v).ravel()
+        out = np.empty_like(v)
+        check(self.h, lib.cal_spmv(self.h, ptr(v), ptr(out)), "SpMV")
+        return out
+
+    def spmv_format(self):
+        """('pattern'|'csr', number of row patterns, table entries)."""
+        a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(self.h, lib.cal_spmv_format(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return ("pattern" if a.value else "csr", b.value, c.value)
 
     def close(self):
         if self.h:

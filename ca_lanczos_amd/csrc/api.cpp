@@ -52,11 +52,44 @@ int cal_spmv(cal_ctx* c, const double* v, double* Av) {
     if (!v || !Av) return set_error(c, CAL_ERR_ARG, "SpMV: null vector");
     const int64_t n = c->A.n_local, ld = c->A.ld;
     CAL_TRY(ensure_scratch(c, 2 * ld));
-    double* x = c->d_scratch;
-    double* y = c->d_scratch + ld;
+    double* x = vcol(c, c->d_scratch, 0);
+    double* y = vcol(c, c->d_scratch, 1);
     CAL_TRY(upload(c, x, ld, v, n, 1));
     CAL_TRY(spmv_dev(c, x, y, 0, 0.0, 0.0, nullptr));
     return download(c, Av, y, ld, n, 1);
+}
+
+int cal_bench_spmv(cal_ctx* c, int reps, double shift, double* mean_ms, double* min_ms) {
+    CAL_TRY(check_ctx(c, true));
+    if (reps < 1) return set_error(c, CAL_ERR_ARG, "bench_spmv: reps >= 1");
+    const int64_t n = c->A.n_local, ld = c->A.ld;
+    CAL_TRY(ensure_scratch(c, 2 * ld));
+    CAL_HIP(c, hipMemsetAsync(c->d_scratch, 0, 2 * ld * sizeof(double), c->stream));
+    double* x = vcol(c, c->d_scratch, 0);
+    double* y = vcol(c, c->d_scratch, 1);
+    std::vector<double> ones(n, 1.0);
+    CAL_TRY(upload(c, x, ld, ones.data(), n, 1));
+    const bool was = c->timing;
+    c->timing = true;
+    const size_t first = c->timers.size();
+    for (int i = 0; i < reps; ++i) CAL_TRY(spmv_dev(c, x, y, shift != 0.0 ? 1 : 0, shift, 0.0, nullptr));
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    double tot = 0.0, mn = 1e300;
+    for (size_t i = first; i < c->timers.size(); ++i) {
+        float ms = 0.f;
+        CAL_HIP(c, hipEventElapsedTime(&ms, c->timers[i].a, c->timers[i].b));
+        tot += ms;
+        mn = std::min(mn, (double)ms);
+    }
+    for (size_t i = first; i < c->timers.size(); ++i) {
+        c->event_pool.push_back(c->timers[i].a);
+        c->event_pool.push_back(c->timers[i].b);
+    }
+    c->timers.resize(first);
+    c->timing = was;
+    if (mean_ms) *mean_ms = tot / reps;
+    if (min_ms) *min_ms = mn;
+    return 0;
 }
 
 int cal_matrix_powers_monomial(cal_ctx* c, const double* q, int s, double* V) {
@@ -64,7 +97,7 @@ int cal_matrix_powers_monomial(cal_ctx* c, const double* q, int s, double* V) {
     if (!q || !V || s < 1) return set_error(c, CAL_ERR_ARG, "matrix_powers_monomial: bad arguments");
     const int64_t n = c->A.n_local, ld = c->A.ld;
     CAL_TRY(ensure_scratch(c, (size_t)(s + 1) * ld));
-    double* W = c->d_scratch;
+    double* W = vcol(c, c->d_scratch, 0);
     CAL_TRY(upload(c, W, ld, q, n, 1));
     for (int i = 0; i < s; ++i) CAL_TRY(spmv_dev(c, W + (size_t)i * ld, W + (size_t)(i + 1) * ld, 0, 0, 0, nullptr));
     return download(c, V, W + ld, ld, n, s);  // V excludes q (matrix_powers_monomial.m:7)
@@ -76,7 +109,7 @@ int cal_matrix_powers_newton(cal_ctx* c, const double* v, int s, const double* l
     if (!v || !V || !lre || s < 1) return set_error(c, CAL_ERR_ARG, "matrix_powers_newton: bad arguments");
     const int64_t n = c->A.n_local, ld = c->A.ld;
     CAL_TRY(ensure_scratch(c, (size_t)(s + 1) * ld));
-    double* W = c->d_scratch;
+    double* W = vcol(c, c->d_scratch, 0);
     CAL_TRY(upload(c, W, ld, v, n, 1));
     for (int k = 0; k < s; ++k) {
         const double re = lre[k], im = lim ? lim[k] : 0.0;

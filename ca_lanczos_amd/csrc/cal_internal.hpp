@@ -76,18 +76,45 @@ struct SpmvArgs {
     int mode;             // 0: y = A x, 1: shifted, 2: shifted + im2 term
 };
 
+// Row-pattern storage ("PSR"): row r is pattern pat[r], a sequence of
+// (col - row, value) pairs in increasing column order held in a small table.
+// Lossless and summed in CSR order, so SpMV results are bit-identical to CSR.
+struct PatArgs {
+    const uint16_t* pat;
+    const int2* pinfo;     // (start, len) per pattern; empty rows -> sentinel
+    const int* pdelta;
+    const double* pval;
+    int64_t n;
+    int nblk;              // ceil(n / 256)
+    const double* x;       // local origin (offsets may reach into the halo)
+    double* y;
+    const double* xprev;
+    double shift, im2;
+    int mode;              // as SpmvArgs
+    int maxlen;            // 1..8 exact, else 16 / 32
+    int npat, nent;        // table sizes (LDS-resident when small)
+};
+
 struct DevMatrix {
     int64_t n_local = 0, n_global = 0, row0 = 0, nnz = 0, nghost = 0;
     int* rowptr = nullptr;
-    int* col = nullptr;
+    int* col = nullptr;    // local column ids relative to the local origin
     double* val = nullptr;
     int* blk = nullptr;
     int nblk = 0;
     int nit = 1;     // ceil(max row-block nonzeros / 256): SpMV unroll depth
     int64_t ld = 0;  // leading dimension of every n-vector buffer
+    int64_t lpad = 0;  // offset of the local origin inside each vector column
+    // row-pattern format (chosen automatically when the table is small)
+    bool use_pat = false;
+    uint16_t* pat = nullptr;
+    int2* pinfo = nullptr;
+    int* pdelta = nullptr;
+    double* pval = nullptr;
+    int npat = 0, nent = 0, maxlen = 0;
     // halo plan (distributed); ghost entries grouped by owning peer
     std::vector<int> peers;              // neighbour ranks
-    std::vector<int64_t> recv_off;       // offset into ghost area per peer
+    std::vector<int64_t> recv_off;       // ghost destination per peer, relative to the local origin
     std::vector<int64_t> recv_cnt;
     std::vector<int64_t> send_off;       // offset into send index list
     std::vector<int64_t> send_cnt;
@@ -101,6 +128,7 @@ struct LanczosState;  // lanczos.cpp
 
 // Launchers (kernels.hip).  All enqueue on `st` and return hipError_t.
 hipError_t launch_spmv(const SpmvArgs& a, hipStream_t st);
+hipError_t launch_spmv_pat(const PatArgs& a, hipStream_t st);
 // C (wa x wb, column-major ldc = 16*ceil(wa/16)) partials; see kernels.hip.
 struct GramPlan {
     int nta;    // A tiles of 16 columns
@@ -189,6 +217,8 @@ struct cal_ctx {
     bool timing = false;
     std::vector<CalTimerRec> timers;
     std::vector<hipEvent_t> event_pool;
+
+    int spmv_format = 0;  // 0 auto, 1 CSR, 2 row-pattern (applies at the next set_matrix)
 };
 
 // ---- helpers shared by the host-side translation units -----------------
@@ -208,8 +238,12 @@ int hip_fail(cal_ctx* c, hipError_t e, const char* what);
         if (_s < 0) return _s;    \
     } while (0)
 
-int upload_matrix(cal_ctx* c, int64_t n_local, int64_t n_global, int64_t row0, int64_t nghost,
-                  const std::vector<int>& rowptr, const std::vector<int>& col, const double* val);
+// col: local ids relative to the local origin (negative = left halo);
+// lpad/rext: halo extent on each side of the local rows in a vector column.
+int upload_matrix(cal_ctx* c, int64_t n_local, int64_t n_global, int64_t row0, int64_t nghost, int64_t lpad,
+                  int64_t rext, const std::vector<int>& rowptr, const std::vector<int>& col, const double* val);
+// pointer to column j of a vector buffer laid out with A.ld / A.lpad
+inline double* vcol(const cal_ctx* c, double* base, int64_t j) { return base + j * c->A.ld + c->A.lpad; }
 int ensure_partial(cal_ctx* c, size_t doubles);
 int ensure_scratch(cal_ctx* c, size_t doubles);
 int ensure_red(cal_ctx* c, size_t doubles);

@@ -56,7 +56,8 @@ int halo_exchange(cal_ctx* c, double* x) {
     DevMatrix& A = c->A;
     if (!m || m->nranks <= 1 || A.peers.empty()) return 0;
     CAL_HIP(c, launch_gather(A.send_buf, x, A.send_idx, A.send_total, c->stream));
-    double* ghost = x + A.n_local;
+    // each peer's halo lands contiguously at x + recv_off[p] (origin-relative;
+    // negative for the left neighbour in the window layout)
     if (m->kind == 1) {
         CAL_NCCL(c, ncclGroupStart());
         for (size_t p = 0; p < A.peers.size(); ++p) {
@@ -64,7 +65,7 @@ int halo_exchange(cal_ctx* c, double* x) {
                 CAL_NCCL(c, ncclSend(A.send_buf + A.send_off[p], (size_t)A.send_cnt[p], ncclDouble, A.peers[p], m->nccl,
                                      c->stream));
             if (A.recv_cnt[p] > 0)
-                CAL_NCCL(c, ncclRecv(ghost + A.recv_off[p], (size_t)A.recv_cnt[p], ncclDouble, A.peers[p], m->nccl,
+                CAL_NCCL(c, ncclRecv(x + A.recv_off[p], (size_t)A.recv_cnt[p], ncclDouble, A.peers[p], m->nccl,
                                      c->stream));
         }
         CAL_NCCL(c, ncclGroupEnd());
@@ -76,10 +77,16 @@ int halo_exchange(cal_ctx* c, double* x) {
     double* hr = m->h_stage + A.send_total;
     CAL_HIP(c, hipMemcpyAsync(hs, A.send_buf, A.send_total * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     CAL_HIP(c, hipStreamSynchronize(c->stream));
-    for (size_t p = 0; p < A.peers.size(); ++p)
-        if (m->ex(m->user, A.peers[p], hs + A.send_off[p], A.send_cnt[p], hr + A.recv_off[p], A.recv_cnt[p]) != 0)
+    int64_t packed = 0;
+    for (size_t p = 0; p < A.peers.size(); ++p) {
+        if (m->ex(m->user, A.peers[p], hs + A.send_off[p], A.send_cnt[p], hr + packed, A.recv_cnt[p]) != 0)
             return set_error(c, CAL_ERR_COMM, "exchange callback failed");
-    CAL_HIP(c, hipMemcpyAsync(ghost, hr, A.nghost * sizeof(double), hipMemcpyHostToDevice, c->stream));
+        if (A.recv_cnt[p] > 0)
+            CAL_HIP(c, hipMemcpyAsync(x + A.recv_off[p], hr + packed, A.recv_cnt[p] * sizeof(double),
+                                      hipMemcpyHostToDevice, c->stream));
+        packed += A.recv_cnt[p];
+    }
+    CAL_HIP(c, hipStreamSynchronize(c->stream));  // hr is reused by the next exchange
     return 0;
 }
 
@@ -221,17 +228,37 @@ int cal_set_matrix_csr_dist(cal_ctx* c, int64_t n_global, int64_t row0, int64_t 
         need[owner(kv.first)].push_back(kv.first);
     }
     const int64_t nghost = gi;
+    // Window layout when every peer's halo is a dense run of global ids (row
+    // slabs of a stencil matrix): the vector buffer holds global rows
+    // [row0 - lext, row0 + nlocal + rext) contiguously, so col - row stays
+    // invariant across the slab boundary (row-pattern SpMV keeps working).
+    // Otherwise the compact layout [local | ghosts grouped by peer].
+    bool window = nghost > 0;
+    int64_t lext = 0, rext = 0;
+    for (int q = 0; q < nranks && window; ++q) {
+        if (need[q].empty()) continue;
+        const int64_t lo = need[q].front(), hi = need[q].back();
+        window = (hi - lo + 1) == (int64_t)need[q].size();
+        if (lo < row0) lext = std::max(lext, row0 - lo);
+        if (hi >= row0 + nlocal) rext = std::max(rext, hi - (row0 + nlocal) + 1);
+    }
+    if (window && lext + rext > 2 * nghost + 1024) window = false;
+    if (!window) {
+        lext = 0;
+        rext = nghost;
+    }
     std::vector<int> rp(nlocal + 1), col(nnz);
     for (int64_t i = 0; i <= nlocal; ++i) rp[i] = (int)(rowptr[i] - rowptr[0]);
     for (int64_t p = 0; p < nnz; ++p) {
         const int64_t j = colind_global[p];
-        col[p] = (j >= row0 && j < row0 + nlocal) ? (int)(j - row0) : (int)(nlocal + ghost[j]);
+        const bool local = j >= row0 && j < row0 + nlocal;
+        col[p] = (local || window) ? (int)(j - row0) : (int)(nlocal + ghost[j]);
     }
     // counts matrix: cnt[p*nranks+q] = #entries rank p needs from rank q
     std::vector<double> cnt((size_t)nranks * nranks, 0.0);
     for (int q = 0; q < nranks; ++q) cnt[(size_t)rank * nranks + q] = (double)need[q].size();
     CAL_TRY(comm_allreduce_host(c, cnt));
-    CAL_TRY(upload_matrix(c, nlocal, n_global, row0, nghost, rp, col, val + rowptr[0]));
+    CAL_TRY(upload_matrix(c, nlocal, n_global, row0, nghost, lext, rext, rp, col, val + rowptr[0]));
     DevMatrix& A = c->A;
     int64_t roff = 0, soff = 0;
     std::vector<int> send_idx;
@@ -244,7 +271,7 @@ int cal_set_matrix_csr_dist(cal_ctx* c, int64_t n_global, int64_t row0, int64_t 
         std::vector<double> want(need[q].begin(), need[q].end()), theirs(nsend);
         CAL_TRY(comm_exchange_host(c, q, want, theirs));
         A.peers.push_back(q);
-        A.recv_off.push_back(roff);
+        A.recv_off.push_back(window ? (nrecv ? need[q].front() - row0 : 0) : nlocal + roff);
         A.recv_cnt.push_back(nrecv);
         A.send_off.push_back(soff);
         A.send_cnt.push_back(nsend);

@@ -146,6 +146,149 @@ hipError_t launch_spmv(const SpmvArgs& a, hipStream_t st) {
 }
 
 // --------------------------------------------------------------------------
+// Row-pattern SpMV (same arithmetic as k_spmv, different storage): thread
+// <-> row; the row's pattern id (2 B) selects its (col - row, value) list in
+// a small L1/L2-resident table.  HBM traffic per row: 2 B of id + the x
+// gathers (contiguous across a wave for a stencil) + 8 B of y.
+// XCD-aware remap: the hardware deals blocks round-robin over the 8 XCDs;
+// remapping gives each XCD a contiguous run of rows, so the x lines of the
+// neighbouring planes (col - row = +-N^2) are re-read from that XCD's L2.
+// --------------------------------------------------------------------------
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+    const int q = nwg >> 3, r = nwg & 7, x = b & 7, i = b >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
+template <int MODE, int MAXLEN>
+__global__ __launch_bounds__(256) void k_spmv_pat(PatArgs a) {
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t r = (int64_t)lb * 256 + threadIdx.x;
+    if (r >= a.n) return;
+    const int pid = a.pat[r];
+    const int2 pi = a.pinfo[pid];
+    const int last = pi.y > 0 ? pi.y - 1 : 0;
+    double v[MAXLEN], xv[MAXLEN];
+#pragma unroll
+    for (int e = 0; e < MAXLEN; ++e) {  // clamped, unconditional loads
+        const int ee = pi.x + (e < pi.y ? e : last);
+        v[e] = a.pval[ee];
+        xv[e] = a.x[r + a.pdelta[ee]];
+    }
+    double sum = 0.0;
+#pragma unroll
+    for (int e = 0; e < MAXLEN; ++e) {  // CSR order, unfused: bit-identical to k_spmv
+        const double t = v[e] * xv[e];
+        if (e < pi.y) sum = sum + t;
+    }
+    double y = sum;
+    if (MODE != 0) {
+        const double t = a.shift * a.x[r];
+        y = y - t;
+        if (MODE == 2) {
+            const double u = a.im2 * a.xprev[r];
+            y = y + u;
+        }
+    }
+    a.y[r] = y;
+}
+
+// LDS-table variant: the pattern table is copied once per (persistent) block
+// into LDS, so the per-row lookups are LDS broadcasts and the vector-memory
+// path only carries the 2-B ids, the x gathers and the y stores.  Each block
+// sweeps a contiguous run of 256-row chunks; the XCD remap makes the chunks
+// of one XCD contiguous (x lines of the +-plane neighbours stay in its L2).
+template <int MODE, int MAXLEN>
+__global__ __launch_bounds__(256) void k_spmv_pat_lds(PatArgs a, int npat, int nent, int chunks_per_block) {
+    extern __shared__ __attribute__((aligned(16))) double lds_tab[];
+    int2* s_info = reinterpret_cast<int2*>(lds_tab);
+    double* s_val = lds_tab + npat;
+    int* s_delta = reinterpret_cast<int*>(s_val + nent);
+    for (int i = threadIdx.x; i < npat; i += 256) s_info[i] = a.pinfo[i];
+    for (int i = threadIdx.x; i < nent; i += 256) {
+        s_val[i] = a.pval[i];
+        s_delta[i] = a.pdelta[i];
+    }
+    __syncthreads();
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int c0 = lb * chunks_per_block;
+    const int c1 = min(c0 + chunks_per_block, a.nblk);
+    for (int ch = c0; ch < c1; ++ch) {
+        const int64_t r = (int64_t)ch * 256 + threadIdx.x;
+        if (r >= a.n) break;
+        const int2 pi = s_info[a.pat[r]];
+        const int last = pi.y > 0 ? pi.y - 1 : 0;
+        double v[MAXLEN], xv[MAXLEN];
+#pragma unroll
+        for (int e = 0; e < MAXLEN; ++e) {
+            const int ee = pi.x + (e < pi.y ? e : last);
+            v[e] = s_val[ee];
+            xv[e] = a.x[r + s_delta[ee]];
+        }
+        double sum = 0.0;
+#pragma unroll
+        for (int e = 0; e < MAXLEN; ++e) {
+            const double t = v[e] * xv[e];
+            if (e < pi.y) sum = sum + t;
+        }
+        double y = sum;
+        if (MODE != 0) {
+            const double t = a.shift * a.x[r];
+            y = y - t;
+            if (MODE == 2) {
+                const double u = a.im2 * a.xprev[r];
+                y = y + u;
+            }
+        }
+        a.y[r] = y;
+    }
+}
+
+constexpr size_t kPatLdsMax = 64 * 1024;
+
+template <int MODE>
+static hipError_t launch_pat_mode(const PatArgs& a, hipStream_t st) {
+    const size_t lds = (size_t)a.npat * 8 + (size_t)a.nent * 12 + 16;
+    if (lds <= kPatLdsMax) {
+        const int blocks = a.nblk < 2048 ? a.nblk : 2048;
+        const int cpb = (a.nblk + blocks - 1) / blocks;
+        dim3 g(blocks), b(256);
+#define CAL_PL(ML) \
+    hipLaunchKernelGGL((k_spmv_pat_lds<MODE, ML>), g, b, lds, st, a, a.npat, a.nent, cpb)
+        switch (a.maxlen) {
+            case 1: CAL_PL(1); break;
+            case 2: CAL_PL(2); break;
+            case 3: CAL_PL(3); break;
+            case 4: CAL_PL(4); break;
+            case 5: CAL_PL(5); break;
+            case 6: CAL_PL(6); break;
+            case 7: CAL_PL(7); break;
+            case 8: CAL_PL(8); break;
+            case 16: CAL_PL(16); break;
+            default: CAL_PL(32); break;
+        }
+#undef CAL_PL
+        return hipGetLastError();
+    }
+    dim3 g(a.nblk), b(256);
+    switch (a.maxlen) {
+        case 1: case 2: case 3: case 4: hipLaunchKernelGGL((k_spmv_pat<MODE, 4>), g, b, 0, st, a); break;
+        case 5: case 6: case 7: case 8: hipLaunchKernelGGL((k_spmv_pat<MODE, 8>), g, b, 0, st, a); break;
+        case 16: hipLaunchKernelGGL((k_spmv_pat<MODE, 16>), g, b, 0, st, a); break;
+        default: hipLaunchKernelGGL((k_spmv_pat<MODE, 32>), g, b, 0, st, a); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_spmv_pat(const PatArgs& a, hipStream_t st) {
+    if (a.nblk <= 0) return hipSuccess;
+    switch (a.mode) {
+        case 0: return launch_pat_mode<0>(a, st);
+        case 1: return launch_pat_mode<1>(a, st);
+        default: return launch_pat_mode<2>(a, st);
+    }
+}
+
+// --------------------------------------------------------------------------
 // Gram: C = A^T B (MFMA f64 16x16x4).  A: up to 16*NTA columns, B: <= 16.
 // Lane l owns column (l&15) of every 16-column tile and rows g*RUN..g*RUN+RUN-1
 // (g = l>>4) of each 4*RUN-row wave step: MFMA k index = g, so A-operand

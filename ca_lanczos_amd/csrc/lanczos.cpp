@@ -41,7 +41,9 @@ struct LanczosState {
     std::vector<double> oe;
     cal_lanczos_info info{};
     bool breakdown = false;
-    double* col(int j) { return dQ + (size_t)j * ld; }
+    int64_t lpad = 0;  // local origin inside each column (left halo space)
+    double* col(int j) { return dQ + (size_t)j * ld + lpad; }
+    double* vcolumn(int j) { return dV + (size_t)j * ld + lpad; }
 };
 
 static double now_ms() {
@@ -68,8 +70,8 @@ static int newton_prologue(cal_ctx* c, LanczosState& L) {
     const int s = L.s, m = 2 * s;
     const int64_t n = c->A.n_local, ld = c->A.ld;
     CAL_TRY(ensure_work(c, m + 2, ld));
-    double* r = work_col(c, m + 1);
-    auto Qc = [&](int j) { return work_col(c, j); };
+    double* r = work_col(c, m + 1) + c->A.lpad;
+    auto Qc = [&](int j) { return work_col(c, j) + c->A.lpad; };
     // q = r/norm(r) (lanczos.m:47) of the already normalised start vector
     double nrm2 = 0.0;
     CAL_TRY(dot_host(c, n, L.col(0), L.col(0), &nrm2));
@@ -162,7 +164,7 @@ static int ritz_diagnostics(cal_ctx* c, LanczosState& L) {
     CAL_TRY(ensure_work(c, sk, ld));
     Panel Qp = panel();
     panel_add(Qp, L.col(0), ld, sk);
-    PanelOut X = panel_out(work_col(c, 0), ld, sk);
+    PanelOut X = panel_out(work_col(c, 0) + c->A.lpad, ld, sk);
     CAL_TRY(apply_host(c, n, Qp, V.data(), sk, &X, nullptr, 0, nullptr));
     // ||A x - l x|| / ||l x|| per Ritz pair: fused SpMV + residual partials
     const int nb = 256;
@@ -170,8 +172,8 @@ static int ritz_diagnostics(cal_ctx* c, LanczosState& L) {
     CAL_TRY(ensure_red(c, 2 * sk));
     for (int i = 0; i < sk; ++i) {
         const RitzPair& p = pairs[i];
-        double* xr = work_col(c, p.cr);
-        double* xi = p.ci >= 0 ? work_col(c, p.ci) : nullptr;
+        double* xr = work_col(c, p.cr) + c->A.lpad;
+        double* xi = p.ci >= 0 ? work_col(c, p.ci) + c->A.lpad : nullptr;
         CAL_TRY(halo_exchange(c, xr));
         if (xi) CAL_TRY(halo_exchange(c, xi));
         SpmvArgs a{};
@@ -295,7 +297,7 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
     L.k += 1;
     const int k = L.k;
     const double* q = L.col((k - 1) * s);  // ca_lanczos.m:171 (k=1: q itself)
-    auto Vc = [&](int j) { return L.dV + (size_t)j * ld; };
+    auto Vc = [&](int j) { return L.vcolumn(j); };
     // matrix powers (ca_lanczos.m:110-118); V(:,1) = q is not copied: the
     // panels below reference q's column of Q directly.
     for (int i = 0; i < s; ++i) {
@@ -389,6 +391,7 @@ int cal_lanczos_begin(cal_ctx* c, const double* r, int s, int max_outer, const c
     L->full = o == "full";
     L->n = c->A.n_local;
     L->ld = c->A.ld;
+    L->lpad = c->A.lpad;
     L->info.s = s;
     const size_t qcols = (size_t)s * max_outer + 1;
     CAL_HIP(c, hipMalloc((void**)&L->dQ, qcols * L->ld * sizeof(double)));
@@ -399,10 +402,10 @@ int cal_lanczos_begin(cal_ctx* c, const double* r, int s, int max_outer, const c
     L->T.assign((size_t)L->Tld * L->Tld, 0.0);
     const double t0 = now_ms();
     // q = r/sqrt(r'*r) (ca_lanczos.m:55)
-    CAL_HIP(c, hipMemcpyAsync(L->dV, r, L->n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    CAL_HIP(c, hipMemcpyAsync(L->vcolumn(0), r, L->n * sizeof(double), hipMemcpyHostToDevice, c->stream));
     double rr = 0.0;
-    CAL_TRY(dot_host(c, L->n, L->dV, L->dV, &rr));
-    CAL_HIP(c, launch_div(L->dQ, L->dV, std::sqrt(rr), L->n, c->stream));
+    CAL_TRY(dot_host(c, L->n, L->vcolumn(0), L->vcolumn(0), &rr));
+    CAL_HIP(c, launch_div(L->col(0), L->vcolumn(0), std::sqrt(rr), L->n, c->stream));
     if (L->newton) {
         CAL_TRY(newton_prologue(c, *L));
     } else {  // Bk = I(:,2:s+1) (ca_lanczos.m:63-65)
@@ -458,7 +461,7 @@ int cal_lanczos_get_Q(cal_ctx* c, int64_t col0, int ncols, double* Q) {
     if (!c || !c->lz || !Q || col0 < 0 || ncols < 0) return CAL_ERR_ARG;
     LanczosState& L = *c->lz;
     if (col0 + ncols > (int64_t)L.s * L.max_outer + 1) return set_error(c, CAL_ERR_ARG, "Q column range");
-    CAL_HIP(c, hipMemcpy2DAsync(Q, L.n * sizeof(double), L.dQ + col0 * L.ld, L.ld * sizeof(double),
+    CAL_HIP(c, hipMemcpy2DAsync(Q, L.n * sizeof(double), L.col((int)col0), L.ld * sizeof(double),
                                 L.n * sizeof(double), ncols, hipMemcpyDeviceToHost, c->stream));
     CAL_HIP(c, hipStreamSynchronize(c->stream));
     return 0;

@@ -2,6 +2,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <unordered_map>
 #include <vector>
 
 #include "cal_internal.hpp"
@@ -134,6 +135,10 @@ static void free_matrix(cal_ctx* c) {
     if (A.blk) hipFree(A.blk);
     if (A.send_idx) hipFree(A.send_idx);
     if (A.send_buf) hipFree(A.send_buf);
+    if (A.pat) hipFree(A.pat);
+    if (A.pinfo) hipFree(A.pinfo);
+    if (A.pdelta) hipFree(A.pdelta);
+    if (A.pval) hipFree(A.pval);
     A = DevMatrix();
     if (c->d_work) hipFree(c->d_work);
     c->d_work = nullptr;
@@ -141,9 +146,69 @@ static void free_matrix(cal_ctx* c) {
     c->has_A = false;
 }
 
-// Upload a local CSR (int32 indices, columns already in local+ghost numbering).
-int upload_matrix(cal_ctx* c, int64_t n_local, int64_t n_global, int64_t row0, int64_t nghost,
-                  const std::vector<int>& rowptr, const std::vector<int>& col, const double* val) {
+// ---- row-pattern analysis -------------------------------------------------
+constexpr int kMaxPatterns = 65535;
+constexpr int kMaxPatternEntries = 1 << 16;
+constexpr int kMaxPatternLen = 32;
+
+// Returns false when the matrix has too many distinct rows for the format.
+static bool build_patterns(int64_t n, const std::vector<int>& rowptr, const std::vector<int>& col, const double* val,
+                           std::vector<uint16_t>& pat, std::vector<int2>& pinfo, std::vector<int>& pdelta,
+                           std::vector<double>& pval, int* maxlen) {
+    pat.assign(n, 0);
+    pinfo.clear();
+    pdelta.assign(1, 0);  // entry 0: sentinel (delta 0) for empty rows
+    pval.assign(1, 0.0);
+    std::unordered_map<uint64_t, std::vector<int>> buckets;
+    int mx = 0;
+    for (int64_t r = 0; r < n; ++r) {
+        const int p0 = rowptr[r], len = rowptr[r + 1] - p0;
+        if (len > kMaxPatternLen) return false;
+        mx = std::max(mx, len);
+        uint64_t h = 1469598103934665603ull ^ (uint64_t)len;
+        for (int j = 0; j < len; ++j) {
+            uint64_t vb;
+            std::memcpy(&vb, &val[p0 + j], 8);
+            const uint64_t d = (uint64_t)(uint32_t)(col[p0 + j] - (int)r);
+            h = (h ^ d) * 1099511628211ull;
+            h = (h ^ vb) * 1099511628211ull;
+        }
+        auto& cand = buckets[h];
+        int found = -1;
+        for (int id : cand) {
+            const int2 pi = pinfo[id];
+            if (pi.y != len) continue;
+            bool same = true;
+            for (int j = 0; j < len && same; ++j)
+                same = pdelta[pi.x + j] == col[p0 + j] - (int)r &&
+                       std::memcmp(&pval[pi.x + j], &val[p0 + j], 8) == 0;
+            if (same) {
+                found = id;
+                break;
+            }
+        }
+        if (found < 0) {
+            if ((int)pinfo.size() >= kMaxPatterns) return false;
+            if ((int)pdelta.size() + len > kMaxPatternEntries) return false;
+            found = (int)pinfo.size();
+            pinfo.push_back(make_int2(len > 0 ? (int)pdelta.size() : 0, len));
+            for (int j = 0; j < len; ++j) {
+                pdelta.push_back(col[p0 + j] - (int)r);
+                pval.push_back(val[p0 + j]);
+            }
+            cand.push_back(found);
+        }
+        pat[r] = (uint16_t)found;
+    }
+    *maxlen = mx;
+    return true;
+}
+
+// Upload a local matrix.  col: local column ids relative to the local origin
+// (negative ids address the left halo); lpad / rext: halo extent on either
+// side of the local rows in every vector column.
+int upload_matrix(cal_ctx* c, int64_t n_local, int64_t n_global, int64_t row0, int64_t nghost, int64_t lpad,
+                  int64_t rext, const std::vector<int>& rowptr, const std::vector<int>& col, const double* val) {
     free_matrix(c);
     DevMatrix& A = c->A;
     A.n_local = n_local;
@@ -151,8 +216,35 @@ int upload_matrix(cal_ctx* c, int64_t n_local, int64_t n_global, int64_t row0, i
     A.row0 = row0;
     A.nghost = nghost;
     A.nnz = rowptr[n_local];
-    A.ld = ((n_local + nghost + 63) / 64) * 64;
+    A.lpad = ((lpad + 63) / 64) * 64;
+    A.ld = ((A.lpad + n_local + rext + 63) / 64) * 64;
     if (A.ld == 0) A.ld = 64;
+    // storage format: row patterns when the table is small (auto) or forced
+    if (c->spmv_format != 1) {
+        std::vector<uint16_t> pat;
+        std::vector<int2> pinfo;
+        std::vector<int> pdelta;
+        std::vector<double> pval;
+        int mx = 0;
+        const bool ok = n_local > 0 && build_patterns(n_local, rowptr, col, val, pat, pinfo, pdelta, pval, &mx);
+        if (ok) {
+            A.use_pat = true;
+            A.npat = (int)pinfo.size();
+            A.nent = (int)pdelta.size();
+            A.maxlen = mx <= 8 ? std::max(mx, 1) : (mx <= 16 ? 16 : 32);
+            CAL_HIP(c, hipMalloc((void**)&A.pat, n_local * sizeof(uint16_t)));
+            CAL_HIP(c, hipMalloc((void**)&A.pinfo, pinfo.size() * sizeof(int2)));
+            CAL_HIP(c, hipMalloc((void**)&A.pdelta, pdelta.size() * sizeof(int)));
+            CAL_HIP(c, hipMalloc((void**)&A.pval, pval.size() * sizeof(double)));
+            CAL_HIP(c, hipMemcpy(A.pat, pat.data(), n_local * sizeof(uint16_t), hipMemcpyHostToDevice));
+            CAL_HIP(c, hipMemcpy(A.pinfo, pinfo.data(), pinfo.size() * sizeof(int2), hipMemcpyHostToDevice));
+            CAL_HIP(c, hipMemcpy(A.pdelta, pdelta.data(), pdelta.size() * sizeof(int), hipMemcpyHostToDevice));
+            CAL_HIP(c, hipMemcpy(A.pval, pval.data(), pval.size() * sizeof(double), hipMemcpyHostToDevice));
+        } else if (c->spmv_format == 2) {
+            return set_error(c, CAL_ERR_UNSUPPORTED, "row-pattern format requested but the matrix has too many "
+                                                     "distinct rows (or rows longer than 32)");
+        }
+    }
     std::vector<int> blk;
     int max_nnz = 0;
     build_row_blocks(n_local, rowptr, blk, &max_nnz);
@@ -178,6 +270,28 @@ int upload_matrix(cal_ctx* c, int64_t n_local, int64_t n_global, int64_t row0, i
 int spmv_dev(cal_ctx* c, const double* x, double* y, int mode, double shift, double im2, const double* xprev) {
     if (!c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
     CAL_TRY(halo_exchange(c, const_cast<double*>(x)));
+    if (c->A.use_pat) {
+        PatArgs p;
+        p.pat = c->A.pat;
+        p.pinfo = c->A.pinfo;
+        p.pdelta = c->A.pdelta;
+        p.pval = c->A.pval;
+        p.n = c->A.n_local;
+        p.nblk = (int)((c->A.n_local + 255) / 256);
+        p.x = x;
+        p.y = y;
+        p.xprev = xprev;
+        p.shift = shift;
+        p.im2 = im2;
+        p.mode = mode;
+        p.maxlen = c->A.maxlen;
+        p.npat = c->A.npat;
+        p.nent = c->A.nent;
+        const int t = timer_begin(c, 0);
+        CAL_HIP(c, launch_spmv_pat(p, c->stream));
+        timer_end(c, t);
+        return 0;
+    }
     SpmvArgs a;
     a.rowptr = c->A.rowptr;
     a.col = c->A.col;
@@ -319,7 +433,7 @@ int cal_set_matrix_csr(cal_ctx* c, int64_t n, const int64_t* rowptr, const int32
     }
     for (int64_t i = 0; i < n; ++i)
         if (rp[i + 1] < rp[i]) return set_error(c, CAL_ERR_ARG, "row pointers must be non-decreasing");
-    return upload_matrix(c, n, n, 0, 0, rp, col, val);
+    return upload_matrix(c, n, n, 0, 0, 0, 0, rp, col, val);
 }
 
 int cal_set_matrix_csc(cal_ctx* c, int64_t n, const int64_t* jc, const int64_t* ir, const double* pr) {
@@ -332,6 +446,24 @@ int cal_set_matrix_csc(cal_ctx* c, int64_t n, const int64_t* jc, const int64_t* 
         col32[p] = (int32_t)ir[p];
     }
     return cal_set_matrix_csr(c, n, jc, col32.data(), pr);
+}
+
+int cal_set_spmv_format(cal_ctx* c, const char* fmt) {
+    if (!c || !fmt) return CAL_ERR_ARG;
+    if (!strcmp(fmt, "auto")) c->spmv_format = 0;
+    else if (!strcmp(fmt, "csr")) c->spmv_format = 1;
+    else if (!strcmp(fmt, "pattern")) c->spmv_format = 2;
+    else return set_error(c, CAL_ERR_ARG, "spmv format must be auto, csr or pattern");
+    return 0;
+}
+
+int cal_spmv_format(cal_ctx* c, int* is_pattern, int* npatterns, int* nentries) {
+    if (!c) return CAL_ERR_ARG;
+    if (!c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
+    if (is_pattern) *is_pattern = c->A.use_pat ? 1 : 0;
+    if (npatterns) *npatterns = c->A.npat;
+    if (nentries) *nentries = c->A.nent;
+    return 0;
 }
 
 int cal_matrix_info(cal_ctx* c, int64_t* n_local, int64_t* nnz_local, int64_t* n_global, int64_t* nghost) {

@@ -70,6 +70,16 @@ int cal_set_matrix_csr(cal_ctx* ctx, int64_t n, const int64_t* rowptr, const int
 int cal_set_matrix_csr_dist(cal_ctx* ctx, int64_t n_global, int64_t row0, int64_t nlocal,
                             const int64_t* rowptr, const int64_t* colind_global, const double* val);
 int cal_matrix_info(cal_ctx* ctx, int64_t* n_local, int64_t* nnz_local, int64_t* n_global, int64_t* nghost);
+/* Device storage of A, chosen at the next cal_set_matrix_*: "auto" (default:
+ * row patterns when A has <= 65535 distinct rows of <= 32 entries, else
+ * CSR), "csr", or "pattern".  Both are lossless and give bit-identical SpMV
+ * results (same per-row summation order). */
+int cal_set_spmv_format(cal_ctx* ctx, const char* fmt);
+int cal_spmv_format(cal_ctx* ctx, int* is_pattern, int* npatterns, int* nentries);
+/* Device-resident SpMV timing: `reps` launches of y = (A - shift I) x on
+ * HBM-resident vectors (x = ones), HIP events around each launch on the
+ * context stream; returns the mean and the minimum kernel time. */
+int cal_bench_spmv(cal_ctx* ctx, int reps, double shift, double* mean_ms, double* min_ms);
 
 /* ---- a1-a4: SpMV and the s-step matrix-powers kernel -------------------- */
 /* Av = SpMV(A,v)                                       SpMV.m:6-8           */

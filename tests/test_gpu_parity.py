@@ -53,6 +53,41 @@ def test_spmv_irregular_and_long_rows(cal, ref):
     assert np.array_equal(cal.SpMV(A, v), ref.SpMV(A, v))
 
 
+@pytest.mark.parametrize("fmt", ["csr", "pattern"])
+@pytest.mark.parametrize("kind,N", [("2d", 1), ("2d", 33), ("3d", 17), ("diag", 1000)])
+def test_spmv_both_formats_bitexact(cal, ref, fmt, kind, N):
+    A = {"2d": cal.matrices.laplacian_2d, "3d": cal.matrices.laplacian_3d}.get(kind, None)
+    A = A(N) if A else cal.matrices.diagonal(np.arange(1.0, N + 1.0))
+    ctx = cal.Context(spmv_format=fmt).set_matrix(A)
+    assert ctx.spmv_format()[0] == fmt
+    v = ref.matlab_rand(A.shape[0], seed=13) - 0.25
+    assert np.array_equal(ctx.spmv(v), ref.SpMV(A, v))
+    ctx.close()
+
+
+def test_pattern_format_falls_back_to_csr(cal):
+    import scipy.sparse as sp
+    A = sp.random(500, 500, density=0.1, random_state=np.random.RandomState(0), format="csr")
+    A = (A + A.T).tocsr()  # rows of ~100 entries (> 32): no pattern table
+    ctx = cal.Context().set_matrix(A)
+    assert ctx.spmv_format()[0] == "csr"
+    with pytest.raises(cal.CalError):
+        cal.Context(spmv_format="pattern").set_matrix(A)
+
+
+def test_ca_lanczos_format_invariant(cal, ref):
+    """Bit-identical SpMV => the whole run is identical in both formats."""
+    A = cal.matrices.laplacian_3d(12)
+    r = ref.matlab_rand(A.shape[0])
+    outs = []
+    for fmt in ("csr", "pattern"):
+        ctx = cal.Context(spmv_format=fmt).set_matrix(A)
+        outs.append(cal.ca_lanczos_ex(A, r, 8, 40, "newton", "local", diagnostics=False, ctx=ctx))
+        ctx.close()
+    assert np.array_equal(outs[0].T, outs[1].T)
+    assert np.array_equal(outs[0].Q, outs[1].Q)
+
+
 def test_spmv_diag_config1(cal, ref):
     A = cal.matrices.diagonal(np.arange(1.0, 1001.0))
     v = np.ones(1000)
