@@ -181,8 +181,8 @@ def main():
     n_loc = r1 - r0
     # per-launch algorithmic bytes:
     #   SpMV CSR: 12 nnz + 20 n + 4; row-pattern: 2 n (ids) + 8 n (x) + 8 n (y)
-    #   apply passes A and B: (w + m) * 8 read + m * 8 written per row (w = s+1, m = s)
-    #   Gram pass P1: (w + m) * 8 read per row
+    #   apply (pass B, chained): (w + m) * 8 read + m * 8 written per row (w = s+1, m = s)
+    #   Gram sweeps (P1 and pass A): (w + m) * 8 read per row
     b_csr = 12 * nnz_local + 20 * n_loc + 4
     b_spmv_launch = 18 * n_loc if fmt == "pattern" else b_csr
     b_apply = (2 * s + 1 + s) * 8 * n_loc
@@ -192,8 +192,8 @@ def main():
     dominant = max(per_step, key=per_step.get)
     dom = {"spmv": (b_spmv_launch, spmv_avg_ms, "k_spmv_pat (row-pattern SpMV + Newton shift)" if fmt == "pattern"
                     else "k_spmv (CSR-stream SpMV + Newton shift)"),
-           "gram": (b_gram, gram_avg_ms, "k_rowapply<17,4,gram-only> ([Qp|X]'X MFMA tile Gram)"),
-           "apply": (b_apply, apply_avg_ms, "k_rowapply<17,8> (block orthogonalisation passes A/B)")}[dominant]
+           "gram": (b_gram, gram_avg_ms, "k_rowapply Gram sweeps ([Qp|X]'X and pass A, MFMA tile Gram, no store)"),
+           "apply": (b_apply, apply_avg_ms, "k_rowapply<17,8,chained> (block orthogonalisation pass B)")}[dominant]
     achieved = dom[0] / (dom[1] * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):

@@ -188,20 +188,30 @@ static bool rowapply_ok(int wp, int m, bool gram, int wq) {
     const int WP = rowapply_wpmax(wp), MO = rowapply_mout(m);
     if (!WP || !MO) return false;
     if (WP == 17 && MO == 16 && gram) return false;
-    if (WP == 5 && MO != 4) return false;
     if (gram && ((wq < 8 ? wq : 8) + m > 16 || wq > 9)) return false;
     return true;
 }
 
-// Y = P*M (M wp x m col-major) with the row kernel; optional tile Gram of
-// [Qp(0:nq) | Y] (Qp = first wq columns of P).
-static int rowapply_host(cal_ctx* c, int64_t n, const Panel& P, const double* M, int m, const PanelOut& Y, bool gram,
-                         int wq, double* G16, double* e16) {
+// Y = P*M (M wp x m col-major) with the row kernel.  kind (see
+// launch_rowapply): 0 store, 1 store + tile Gram of [Qp(0:nq) | Y] (Qp =
+// first wq columns of P), 2 the Gram without storing Y, 3 chained: store
+// [P(0:wq) | Y] * M2 (M2 (wq+m) x m col-major) with Y = P*M recomputed.
+static int rowapply_host(cal_ctx* c, int64_t n, const Panel& P, const double* M, int m, const PanelOut& Y, int kind,
+                         int wq, double* G16, double* e16, const double* M2 = nullptr) {
+    const bool gram = kind == 1 || kind == 2;
     const int wp = P.total;
     const int WP = rowapply_wpmax(wp), MO = rowapply_mout(m);
-    std::vector<double> Mp((size_t)WP * MO, 0.0);
+    std::vector<double> Mp((size_t)WP * MO * (kind == 3 ? 2 : 1) + (kind == 3 ? (size_t)MO * MO : 0), 0.0);
     for (int cc = 0; cc < wp; ++cc)
         for (int j = 0; j < m; ++j) Mp[(size_t)cc * MO + j] = M[cc + (size_t)j * wp];
+    if (kind == 3) {
+        double* M2p = Mp.data() + (size_t)WP * MO;
+        double* M2y = M2p + (size_t)WP * MO;
+        for (int j = 0; j < m; ++j) {
+            for (int cc = 0; cc < wq; ++cc) M2p[(size_t)cc * MO + j] = M2[cc + (size_t)j * (wq + m)];
+            for (int i = 0; i < m; ++i) M2y[(size_t)i * MO + j] = M2[wq + i + (size_t)j * (wq + m)];
+        }
+    }
     CAL_TRY(stage_small(c, Mp.data(), Mp.size()));
     ColList cl{};
     OutList ol{};
@@ -214,8 +224,8 @@ static int rowapply_host(cal_ctx* c, int64_t n, const Panel& P, const double* M,
     if (gram) blocks = std::min<int64_t>(blocks, 768);
     blocks = std::max<int64_t>(1, blocks);
     if (gram) CAL_TRY(ensure_partial(c, (size_t)blocks * 272));
-    const int t = timer_begin(c, 2);
-    CAL_HIP(c, launch_rowapply(cl, c->d_small, wp, m, ol, gram, wq, n, (int)blocks, c->d_partial, c->stream));
+    const int t = timer_begin(c, kind == 2 ? 1 : 2);  // Gram-only sweeps count as "gram"
+    CAL_HIP(c, launch_rowapply(cl, c->d_small, wp, m, ol, kind, wq, n, (int)blocks, c->d_partial, c->stream));
     timer_end(c, t);
     if (!gram) return 0;
     return fetch_tile(c, (int)blocks, G16, e16);
@@ -256,11 +266,13 @@ static int64_t global_rows(cal_ctx* c, int64_t n) { return c->has_A ? std::max(c
 
 // Two-pass orthonormalisation of the block Z = W*Mz (never stored) against the
 // orthonormal block Qp (the first w columns of W; w may be 0):
-//   pass A: Q1 = Z Ra^-1 stored, Ra = chol(Z'Z); fused Grams Q1'Q1, Qp'Q1;
-//   pass B: Q  = (Q1 - Qp C3) Rb^-1 in place, Rb = chol(Q1'Q1 - C3'C3),
+//   pass A: Q1 = Z Ra^-1, Ra = chol(Z'Z); fused Grams Q1'Q1, Qp'Q1;
+//   pass B: Q  = (Q1 - Qp C3) Rb^-1, Rb = chol(Q1'Q1 - C3'C3),
 // i.e. CholQR2 inside the block and a second classical Gram-Schmidt pass
 // against Qp in the same two sweeps.  Then X = Qp*(RY + Ctot) + Q*R with
-// Ctot = C3*Ra and R = Rb*Ra.  A shifted Cholesky adds one more pass B.
+// Ctot = C3*Ra and R = Rb*Ra.  On the row kernel Q1 is never stored: pass A
+// only accumulates its Grams and pass B recomputes it in registers (kind 3).
+// A shifted first Cholesky takes the stored path with one more pass B.
 static int two_pass(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& W, const std::vector<double>& Mz, int m,
                     const double* GZ, const PanelOut& Qout, double* R, std::vector<double>& Ctot, bool* shifted) {
     const int w = Qp.total, wp = W.total;
@@ -274,20 +286,22 @@ static int two_pass(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& W, cons
     dense::matmul(wp, m, m, Mz.data(), wp, Rai.data(), m, M1.data(), wp);
     const Panel Q1 = as_panel(Qout);
     const Panel P2 = panel_concat(Qp, Q1);
-    // fused Grams of the freshly written block: Q1'Q1 and Qp'Q1
     const bool fast = rowapply_ok(wp, m, true, w) && rowapply_ok(w + m, m, true, w);
+    auto unpack = [&](const double* G16, const double* e16, std::vector<double>& G, std::vector<double>& Cq) {
+        const int nq = w < 8 ? w : 8;
+        for (int j = 0; j < m; ++j) {
+            for (int i = 0; i < m; ++i) G[i + (size_t)j * m] = G16[(nq + i) + (nq + j) * 16];
+            for (int i = 0; i < nq; ++i) Cq[i + (size_t)j * w] = G16[i + (nq + j) * 16];
+            if (w == 9) Cq[8 + (size_t)j * w] = e16[nq + j];
+        }
+    };
+    // fused Grams of the freshly written block: Q1'Q1 and Qp'Q1
     auto grams = [&](const Panel& P, const std::vector<double>& M, std::vector<double>& G,
                      std::vector<double>& Cq, bool store_only) -> int {
         if (fast) {
             double G16[256], e16[16];
-            CAL_TRY(rowapply_host(c, n, P, M.data(), m, Qout, !store_only, w, G16, e16));
-            if (store_only) return 0;
-            const int nq = w < 8 ? w : 8;
-            for (int j = 0; j < m; ++j) {
-                for (int i = 0; i < m; ++i) G[i + (size_t)j * m] = G16[(nq + i) + (nq + j) * 16];
-                for (int i = 0; i < nq; ++i) Cq[i + (size_t)j * w] = G16[i + (nq + j) * 16];
-                if (w == 9) Cq[8 + (size_t)j * w] = e16[nq + j];
-            }
+            CAL_TRY(rowapply_host(c, n, P, M.data(), m, Qout, store_only ? 0 : 1, w, G16, e16));
+            if (!store_only) unpack(G16, e16, G, Cq);
             return 0;
         }
         if (store_only) return apply_host(c, n, P, M.data(), m, &Qout, nullptr, 0, nullptr);
@@ -302,11 +316,11 @@ static int two_pass(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& W, cons
         }
         return 0;
     };
-    CAL_TRY(grams(W, M1, G1, C3, false));  // pass A
-    std::vector<double> Racc = Ra;
+    // pass-B coefficients from the Grams of Q1: Rb, M2 = [-C3 Rb^-1 ; Rb^-1],
+    // Ctot += C3 Racc, Racc = Rb Racc.
+    std::vector<double> Racc = Ra, M2((size_t)(w + m) * m);
     Ctot.assign((size_t)w * m, 0.0);
-    const int passes = sh ? 2 : 1;
-    for (int p = 0; p < passes; ++p) {  // pass B
+    auto coeffs_b = [&](bool* sh2) -> int {
         std::vector<double> Gp = G1, Rb((size_t)m * m), Rbi((size_t)m * m);
         for (int j = 0; j < m; ++j)
             for (int i = 0; i < m; ++i) {
@@ -314,12 +328,10 @@ static int two_pass(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& W, cons
                 for (int k = 0; k < w; ++k) s += C3[k + (size_t)i * w] * C3[k + (size_t)j * w];
                 Gp[i + (size_t)j * m] -= s;
             }
-        bool sh2 = false;
-        if (!chol_or_shift(m, Gp.data(), ng, Rb.data(), &sh2))
+        if (!chol_or_shift(m, Gp.data(), ng, Rb.data(), sh2))
             return set_error(c, CAL_ERR_NUMERIC, "block orthogonalisation: second Cholesky failed");
-        sh = sh || sh2;
         dense::tri_inv_upper(m, Rb.data(), m, Rbi.data(), m);
-        std::vector<double> M2((size_t)(w + m) * m, 0.0);
+        std::fill(M2.begin(), M2.end(), 0.0);
         for (int j = 0; j < m; ++j) {
             for (int i = 0; i < w; ++i) {
                 double s = 0.0;
@@ -328,7 +340,6 @@ static int two_pass(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& W, cons
             }
             for (int i = 0; i < m; ++i) M2[w + i + (size_t)j * (w + m)] = Rbi[i + (size_t)j * m];
         }
-        // Ctot += C3 * Racc ; Racc = Rb * Racc  (before C3 is overwritten)
         for (int j = 0; j < m; ++j)
             for (int i = 0; i < w; ++i) {
                 double s = 0.0;
@@ -340,6 +351,25 @@ static int two_pass(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& W, cons
         for (int j = 0; j < m; ++j)
             for (int i = j + 1; i < m; ++i) Rn[i + (size_t)j * m] = 0.0;
         Racc = Rn;
+        return 0;
+    };
+    if (fast && !sh) {
+        double G16[256], e16[16];
+        CAL_TRY(rowapply_host(c, n, W, M1.data(), m, Qout, 2, w, G16, e16));  // pass A, Grams only
+        unpack(G16, e16, G1, C3);
+        bool sh2 = false;
+        CAL_TRY(coeffs_b(&sh2));
+        CAL_TRY(rowapply_host(c, n, W, M1.data(), m, Qout, 3, w, nullptr, nullptr, M2.data()));  // pass B
+        std::copy(Racc.begin(), Racc.end(), R);
+        *shifted = *shifted || sh2;
+        return 0;
+    }
+    CAL_TRY(grams(W, M1, G1, C3, false));  // pass A, Q1 stored
+    const int passes = sh ? 2 : 1;
+    for (int p = 0; p < passes; ++p) {  // pass B
+        bool sh2 = false;
+        CAL_TRY(coeffs_b(&sh2));
+        sh = sh || sh2;
         const bool more = p + 1 < passes;
         CAL_TRY(grams(P2, M2, G1, C3, !more));
     }

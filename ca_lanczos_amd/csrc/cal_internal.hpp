@@ -164,7 +164,8 @@ struct ColList {
 struct OutList {
     double* p[16];
 };
-hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, const OutList& Y, bool gram, int wq,
+// kind: 0 store, 1 store + Gram, 2 Gram only (pass A), 3 chained store (pass B)
+hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, const OutList& Y, int kind, int wq,
                            int64_t n, int blocks, double* partial, hipStream_t st);
 hipError_t launch_rowgram(const ColList& P, int nt, bool has_extra, int64_t n, int blocks, double* partial,
                           hipStream_t st);

@@ -192,13 +192,17 @@ __global__ __launch_bounds__(256) void k_spmv_pat(PatArgs a) {
     a.y[r] = y;
 }
 
-// LDS-table variant: the pattern table is copied once per (persistent) block
+// Row-pattern SpMV with the pattern table (npat*8 + nent*12 bytes) staged
 // into LDS, so the per-row lookups are LDS broadcasts and the vector-memory
-// path only carries the 2-B ids, the x gathers and the y stores.  Each block
-// sweeps a contiguous run of 256-row chunks; the XCD remap makes the chunks
-// of one XCD contiguous (x lines of the +-plane neighbours stay in its L2).
+// path only carries the 2-B ids, the x gathers and the y stores.  The grid is
+// persistent; each XCD owns a contiguous range of 256-row chunks and its
+// blocks sweep that range interleaved, so the XCD's rows in flight form one
+// moving window and the x lines of the +-plane neighbours stay in its L2.
+// The ids of the next chunk are loaded before this chunk's gathers and store
+// (vmcnt retires in order: an id load issued after the y store would wait
+// for that store).
 template <int MODE, int MAXLEN>
-__global__ __launch_bounds__(256) void k_spmv_pat_lds(PatArgs a, int npat, int nent, int chunks_per_block) {
+__global__ __launch_bounds__(256) void k_spmv_pat_lds(PatArgs a, int npat, int nent) {
     extern __shared__ __attribute__((aligned(16))) double lds_tab[];
     int2* s_info = reinterpret_cast<int2*>(lds_tab);
     double* s_val = lds_tab + npat;
@@ -209,26 +213,36 @@ __global__ __launch_bounds__(256) void k_spmv_pat_lds(PatArgs a, int npat, int n
         s_delta[i] = a.pdelta[i];
     }
     __syncthreads();
-    const int lb = xcd_remap(blockIdx.x, gridDim.x);
-    const int c0 = lb * chunks_per_block;
-    const int c1 = min(c0 + chunks_per_block, a.nblk);
-    for (int ch = c0; ch < c1; ++ch) {
+    const int G = gridDim.x, q = G >> 3, rm = G & 7, xcd = blockIdx.x & 7, bi = blockIdx.x >> 3;
+    const int nbx = q + (xcd < rm ? 1 : 0);
+    const int b0 = xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q;
+    const int c0 = (int)((int64_t)a.nblk * b0 / G) + bi;
+    const int c1 = (int)((int64_t)a.nblk * (b0 + nbx) / G);
+    auto row_of = [&](int ch) -> int64_t {
         const int64_t r = (int64_t)ch * 256 + threadIdx.x;
-        if (r >= a.n) break;
-        const int2 pi = s_info[a.pat[r]];
+        return ch < c1 && r < a.n ? r : -1;
+    };
+    int64_t rn = row_of(c0);
+    int pidn = a.pat[rn >= 0 ? rn : 0];
+    for (int ch = c0; ch < c1; ch += nbx) {
+        const int64_t rv = rn;
+        const int64_t r = rv >= 0 ? rv : 0;  // row 0 exists (a.n > 0): harmless reads
+        const int2 pi = s_info[pidn];
+        rn = row_of(ch + nbx);
+        pidn = a.pat[rn >= 0 ? rn : 0];
         const int last = pi.y > 0 ? pi.y - 1 : 0;
-        double v[MAXLEN], xv[MAXLEN];
+        double xv[MAXLEN];
 #pragma unroll
         for (int e = 0; e < MAXLEN; ++e) {
             const int ee = pi.x + (e < pi.y ? e : last);
-            v[e] = s_val[ee];
             xv[e] = a.x[r + s_delta[ee]];
         }
         double sum = 0.0;
 #pragma unroll
         for (int e = 0; e < MAXLEN; ++e) {
-            const double t = v[e] * xv[e];
-            if (e < pi.y) sum = sum + t;
+            const double t = s_val[pi.x + (e < pi.y ? e : 0)] * xv[e];
+            const double acc = sum + t;
+            sum = e < pi.y ? acc : sum;
         }
         double y = sum;
         if (MODE != 0) {
@@ -239,7 +253,7 @@ __global__ __launch_bounds__(256) void k_spmv_pat_lds(PatArgs a, int npat, int n
                 y = y + u;
             }
         }
-        a.y[r] = y;
+        if (rv >= 0) a.y[r] = y;
     }
 }
 
@@ -250,10 +264,8 @@ static hipError_t launch_pat_mode(const PatArgs& a, hipStream_t st) {
     const size_t lds = (size_t)a.npat * 8 + (size_t)a.nent * 12 + 16;
     if (lds <= kPatLdsMax) {
         const int blocks = a.nblk < 2048 ? a.nblk : 2048;
-        const int cpb = (a.nblk + blocks - 1) / blocks;
         dim3 g(blocks), b(256);
-#define CAL_PL(ML) \
-    hipLaunchKernelGGL((k_spmv_pat_lds<MODE, ML>), g, b, lds, st, a, a.npat, a.nent, cpb)
+#define CAL_PL(ML) hipLaunchKernelGGL((k_spmv_pat_lds<MODE, ML>), g, b, lds, st, a, a.npat, a.nent)
         switch (a.maxlen) {
             case 1: CAL_PL(1); break;
             case 2: CAL_PL(2); break;
@@ -707,20 +719,25 @@ hipError_t launch_tilegram(const Panel& T, const double* E, int64_t n, int block
 // column.  Partials as k_tilegram.
 // APPLY = false: Gram only (no M, no store): tile = P columns 0..m-1, extra
 // column = P column 16 when wq > 0 (the row-parallel form of k_tilegram).
-template <int WPMAX, int MOUT, bool GRAM, bool APPLY = true>
+// STORE = false: the Grams of Y without writing Y (pass A of two_pass).
+// CHAIN: Y2 = [P(0:wq) | Y] * M2 with Y = P * M1 recomputed bit-identically
+// in registers (pass B of two_pass without a stored intermediate block);
+// M = [M1 (WPMAX x MOUT) | M2p (WPMAX x MOUT, rows >= wq zero) | M2y (MOUT x MOUT)].
+template <int WPMAX, int MOUT, bool GRAM, bool APPLY = true, bool STORE = true, bool CHAIN = false>
 __global__ __launch_bounds__(256, 2) void k_rowapply(ColList P, const double* __restrict__ M, int wp, int m,
                                                   OutList Y, int wq, int64_t n, double* __restrict__ partial) {
     constexpr int TLD = 17;  // padded LDS row (doubles)
+    constexpr int MSZ = WPMAX * MOUT * (CHAIN ? 2 : 1) + (CHAIN ? MOUT * MOUT : 0);
     __shared__ double tile[GRAM ? 256 * TLD : 1];
     __shared__ double ext[GRAM ? 256 : 1];
     __shared__ double red[GRAM ? 3 * 64 * 5 : 1];
-    __shared__ __attribute__((aligned(16))) double Ms[WPMAX * MOUT];  // broadcast reads
+    __shared__ __attribute__((aligned(16))) double Ms[MSZ];  // broadcast reads
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int c16 = lane & 15, g = lane >> 4;
     const int nq = wq < 8 ? wq : 8;
     const bool has_ext = wq > 8;
     if (APPLY)
-        for (int e = tid; e < WPMAX * MOUT; e += 256) Ms[e] = M[e];
+        for (int e = tid; e < MSZ; e += 256) Ms[e] = M[e];
     if (GRAM)
         for (int e = tid; e < 256 * TLD; e += 256) tile[e] = 0.0;
     __syncthreads();
@@ -765,7 +782,33 @@ __global__ __launch_bounds__(256, 2) void k_rowapply(ColList P, const double* __
 #pragma unroll
             for (int j = 0; j < MOUT; ++j) y[j] = __builtin_fma(p[c], mrow[j], y[j]);
         }
-        if (APPLY && in) {
+        if (CHAIN) {
+            // y2 = P(0:wq) * M2p + y * M2y  (same pinning as above)
+            const double* M2p = Ms + WPMAX * MOUT;
+            const double* M2y = Ms + 2 * WPMAX * MOUT;
+            double y2[MOUT];
+#pragma unroll
+            for (int j = 0; j < MOUT; ++j) y2[j] = 0.0;
+#pragma unroll
+            for (int c = 0; c < WPMAX + MOUT; ++c) {
+#pragma unroll
+                for (int j = 0; j < MOUT; ++j) asm volatile("" : "+v"(y2[j])::"memory");
+                const double src = c < WPMAX ? p[c < WPMAX ? c : 0] : y[c >= WPMAX ? c - WPMAX : 0];
+                const double* row = c < WPMAX ? M2p + c * MOUT : M2y + (c - WPMAX) * MOUT;
+                double mrow[MOUT];
+#pragma unroll
+                for (int j = 0; j < MOUT; j += 2) {
+                    const d2 t = *reinterpret_cast<const d2*>(&row[j]);
+                    mrow[j] = t[0];
+                    if (j + 1 < MOUT) mrow[j + 1] = t[1];
+                }
+#pragma unroll
+                for (int j = 0; j < MOUT; ++j) y2[j] = __builtin_fma(src, mrow[j], y2[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < MOUT; ++j) y[j] = y2[j];
+        }
+        if (APPLY && STORE && in) {
 #pragma unroll
             for (int j = 0; j < MOUT; ++j)
                 if (j < m) yc[j][r] = y[j];
@@ -828,27 +871,37 @@ __global__ __launch_bounds__(256, 2) void k_rowapply(ColList P, const double* __
 int rowapply_wpmax(int wp) { return wp <= 5 ? 5 : (wp <= 9 ? 9 : (wp <= 17 ? 17 : 0)); }
 int rowapply_mout(int m) { return m <= 4 ? 4 : (m <= 8 ? 8 : (m <= 16 ? 16 : 0)); }
 
-hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, const OutList& Y, bool gram, int wq,
+// kind: 0 store only, 1 store + Gram, 2 Gram without store (pass A),
+// 3 chained store (pass B).  Instantiated for the shapes of s = 4 and s = 8.
+hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, const OutList& Y, int kind, int wq,
                            int64_t n, int blocks, double* partial, hipStream_t st) {
     const int WP = rowapply_wpmax(wp), MO = rowapply_mout(m);
     dim3 g(blocks), b(256);
-#define CAL_RA(W, MM, G) \
-    hipLaunchKernelGGL((k_rowapply<W, MM, G>), g, b, 0, st, P, dM, wp, m, Y, wq, n, partial)
-    const int key = WP * 1000 + MO * 10 + (gram ? 1 : 0);
-    switch (key) {
-        case 5040: CAL_RA(5, 4, false); break;
-        case 5041: CAL_RA(5, 4, true); break;
-        case 9040: CAL_RA(9, 4, false); break;
-        case 9041: CAL_RA(9, 4, true); break;
-        case 9080: CAL_RA(9, 8, false); break;
-        case 9081: CAL_RA(9, 8, true); break;
-        case 9160: CAL_RA(9, 16, false); break;
-        case 9161: CAL_RA(9, 16, true); break;
-        case 17080: CAL_RA(17, 8, false); break;
-        case 17081: CAL_RA(17, 8, true); break;
-        case 17160: CAL_RA(17, 16, false); break;
+#define CAL_RA(W, MM, G, S, C) \
+    hipLaunchKernelGGL((k_rowapply<W, MM, G, true, S, C>), g, b, 0, st, P, dM, wp, m, Y, wq, n, partial)
+#define CAL_RA_SHAPE(W, MM)                                  \
+    case W * 100 + MM:                                       \
+        switch (kind) {                                      \
+            case 0: CAL_RA(W, MM, false, true, false); break; \
+            case 1: CAL_RA(W, MM, true, true, false); break;  \
+            case 2: CAL_RA(W, MM, true, false, false); break; \
+            default: CAL_RA(W, MM, false, true, true); break; \
+        }                                                    \
+        break;
+    switch (WP * 100 + MO) {
+        CAL_RA_SHAPE(5, 4)
+        CAL_RA_SHAPE(5, 8)
+        CAL_RA_SHAPE(9, 4)
+        CAL_RA_SHAPE(9, 8)
+        CAL_RA_SHAPE(9, 16)
+        CAL_RA_SHAPE(17, 8)
+        case 1716:
+            if (kind != 0) return hipErrorInvalidValue;
+            CAL_RA(17, 16, false, true, false);
+            break;
         default: return hipErrorInvalidValue;
     }
+#undef CAL_RA_SHAPE
 #undef CAL_RA
     return hipGetLastError();
 }

@@ -1,0 +1,162 @@
+// Probe: what a 7-point gather SpMV can reach on this GPU (n = 215^3), to
+// bound the row-pattern SpMV.  Not part of the library.
+//   hipcc -O3 --offload-arch=gfx950 tools/stencil_probe.hip -o /tmp/probe
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
+
+__global__ void k_copy(const double* __restrict__ x, double* __restrict__ y, int64_t n) {
+    int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r < n) y[r] = x[r];
+}
+__global__ void k_copy2(const double* __restrict__ x, double* __restrict__ y, int64_t n) {
+    int64_t r = 2 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
+    if (r + 1 < n) {
+        double2 v = *reinterpret_cast<const double2*>(x + r);
+        *reinterpret_cast<double2*>(y + r) = v;
+    }
+}
+// fixed 7-point stencil on an origin-offset x (halo of N*N each side)
+template <bool IDS>
+__global__ void k_st7(const double* __restrict__ x, double* __restrict__ y, const uint16_t* __restrict__ id,
+                      int64_t n, int N) {
+    int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= n) return;
+    const int64_t P = (int64_t)N * N;
+    double s = 6.0 * x[r] - x[r - 1] - x[r + 1] - x[r - N] - x[r + N] - x[r - P] - x[r + P];
+    if (IDS) s += (double)id[r];
+    y[r] = s;
+}
+// two rows per lane, 16-B x/y accesses where aligned
+__global__ void k_st7x2(const double* __restrict__ x, double* __restrict__ y, int64_t n, int N) {
+    int64_t r = 2 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
+    if (r + 1 >= n) return;
+    const int64_t P = (int64_t)N * N;
+    double2 c = *reinterpret_cast<const double2*>(x + r);
+    double2 zm = *reinterpret_cast<const double2*>(x + r - P);
+    double2 zp = *reinterpret_cast<const double2*>(x + r + P);
+    double l = x[r - 1], rr = x[r + 2];
+    double ym0 = x[r - N], ym1 = x[r + 1 - N], yp0 = x[r + N], yp1 = x[r + 1 + N];
+    double2 o;
+    o.x = 6.0 * c.x - l - c.y - ym0 - yp0 - zm.x - zp.x;
+    o.y = 6.0 * c.y - c.x - rr - ym1 - yp1 - zm.y - zp.y;
+    *reinterpret_cast<double2*>(y + r) = o;
+}
+
+// generic gather kernel: NO offsets from `off`, optional XCD-contiguous block order
+struct Offs { int64_t d[8]; };
+template <int NO, bool XCD>
+__global__ void k_gen(const double* __restrict__ x, double* __restrict__ y, int64_t n, Offs off) {
+    int b = blockIdx.x;
+    if (XCD) {
+        const int G = gridDim.x, q = G >> 3, rm = G & 7, xi = b & 7, i = b >> 3;
+        b = (xi < rm ? xi * (q + 1) : rm * (q + 1) + (xi - rm) * q) + i;
+    }
+    int64_t r = (int64_t)b * 256 + threadIdx.x;
+    if (r >= n) return;
+    double s = 0.0;
+#pragma unroll
+    for (int e = 0; e < NO; ++e) s += x[r + off.d[e]];
+    y[r] = s;
+}
+
+// k_gen<7, XCD> plus a 2-B id per row (added), and/or a persistent grid
+// sweeping the XCD's chunk range interleaved (as k_spmv_pat_lds)
+template <bool IDS, bool PERSIST>
+__global__ void k_gen7x(const double* __restrict__ x, double* __restrict__ y, const uint16_t* __restrict__ id,
+                        int64_t n, Offs off, int nchunk) {
+    const int G = gridDim.x, q = G >> 3, rm = G & 7, xi = blockIdx.x & 7, i = blockIdx.x >> 3;
+    const int nbx = q + (xi < rm ? 1 : 0);
+    const int b0 = xi < rm ? xi * (q + 1) : rm * (q + 1) + (xi - rm) * q;
+    int c0, c1, cs;
+    if (PERSIST) {
+        c0 = (int)((int64_t)nchunk * b0 / G) + i;
+        c1 = (int)((int64_t)nchunk * (b0 + nbx) / G);
+        cs = nbx;
+    } else {
+        c0 = b0 + i;
+        c1 = c0 + 1;
+        cs = 1;
+    }
+    for (int c = c0; c < c1; c += cs) {
+        const int64_t r = (int64_t)c * 256 + threadIdx.x;
+        if (r >= n) break;
+        double s = IDS ? (double)id[r] : 0.0;
+#pragma unroll
+        for (int e = 0; e < 7; ++e) s += x[r + off.d[e]];
+        y[r] = s;
+    }
+}
+
+int main() {
+    const int N = 215;
+    const int64_t n = (int64_t)N * N * N, P = (int64_t)N * N;
+    double *xb, *y;
+    uint16_t* id;
+    CK(hipMalloc(&xb, (n + 2 * P + 64) * 8));
+    CK(hipMalloc(&y, n * 8));
+    CK(hipMalloc(&id, n * 2));
+    CK(hipMemset(xb, 0, (n + 2 * P + 64) * 8));
+    CK(hipMemset(id, 0, n * 2));
+    double* x = xb + P + 32;  // 256-B aligned origin
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    auto time = [&](const char* name, double bytes, auto launch) {
+        for (int i = 0; i < 5; ++i) launch();
+        hipEventRecord(a);
+        const int reps = 100;
+        for (int i = 0; i < reps; ++i) launch();
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        const double us = ms * 1e3 / reps;
+        printf("{\"kernel\": \"%s\", \"us\": %.2f, \"GBps\": %.0f}\n", name, us, bytes / (us * 1e-6) / 1e9);
+    };
+    const int g1 = (int)((n + 255) / 256), g2 = (int)((n / 2 + 255) / 256);
+    time("copy 8B/lane", 16.0 * n, [&] { hipLaunchKernelGGL(k_copy, dim3(g1), dim3(256), 0, 0, x, y, n); });
+    time("copy 16B/lane", 16.0 * n, [&] { hipLaunchKernelGGL(k_copy2, dim3(g2), dim3(256), 0, 0, x, y, n); });
+    time("st7 8B/lane", 16.0 * n, [&] { hipLaunchKernelGGL((k_st7<false>), dim3(g1), dim3(256), 0, 0, x, y, id, n, N); });
+    time("st7+ids 8B/lane", 18.0 * n, [&] { hipLaunchKernelGGL((k_st7<true>), dim3(g1), dim3(256), 0, 0, x, y, id, n, N); });
+    time("st7 2 rows/lane", 16.0 * n, [&] { hipLaunchKernelGGL(k_st7x2, dim3(g2), dim3(256), 0, 0, x, y, n, N); });
+    auto gen = [&](const char* name, std::vector<int64_t> o, bool xcd) {
+        Offs off{};
+        for (size_t i = 0; i < o.size(); ++i) off.d[i] = o[i];
+        const int no = (int)o.size();
+        time(name, 16.0 * n, [&] {
+            if (no == 1 && !xcd) hipLaunchKernelGGL((k_gen<1, false>), dim3(g1), dim3(256), 0, 0, x, y, n, off);
+            if (no == 3 && !xcd) hipLaunchKernelGGL((k_gen<3, false>), dim3(g1), dim3(256), 0, 0, x, y, n, off);
+            if (no == 3 && xcd) hipLaunchKernelGGL((k_gen<3, true>), dim3(g1), dim3(256), 0, 0, x, y, n, off);
+            if (no == 5 && !xcd) hipLaunchKernelGGL((k_gen<5, false>), dim3(g1), dim3(256), 0, 0, x, y, n, off);
+            if (no == 7 && !xcd) hipLaunchKernelGGL((k_gen<7, false>), dim3(g1), dim3(256), 0, 0, x, y, n, off);
+            if (no == 7 && xcd) hipLaunchKernelGGL((k_gen<7, true>), dim3(g1), dim3(256), 0, 0, x, y, n, off);
+        });
+    };
+    gen("gen c", {0}, false);
+    gen("gen c,+-1", {-1, 0, 1}, false);
+    gen("gen c,+-1 aligned-ish(0,+256,+512)", {0, 256, 512}, false);
+    gen("gen c,+-N", {-N, 0, N}, false);
+    gen("gen c,+-N xcd", {-N, 0, N}, true);
+    gen("gen c,+-P", {-P, 0, P}, false);
+    gen("gen c,+-P xcd", {-P, 0, P}, true);
+    gen("gen c,+-1,+-N", {-N, -1, 0, 1, N}, false);
+    gen("gen 7pt", {-P, -N, -1, 0, 1, N, P}, false);
+    gen("gen 7pt xcd", {-P, -N, -1, 0, 1, N, P}, true);
+    gen("gen 7 x aligned 0..6*64", {0, 64, 128, 192, 256, 320, 384}, false);
+    {
+        Offs off{};
+        const int64_t o7[7] = {-P, -N, -1, 0, 1, N, P};
+        for (int e = 0; e < 7; ++e) off.d[e] = o7[e];
+        const int nch = g1;
+        time("7pt xcd + ids", 18.0 * n, [&] { hipLaunchKernelGGL((k_gen7x<true, false>), dim3(g1), dim3(256), 0, 0, x, y, id, n, off, nch); });
+        time("7pt xcd persistent 2048", 16.0 * n, [&] { hipLaunchKernelGGL((k_gen7x<false, true>), dim3(2048), dim3(256), 0, 0, x, y, id, n, off, nch); });
+        time("7pt xcd persistent 2048 + ids", 18.0 * n, [&] { hipLaunchKernelGGL((k_gen7x<true, true>), dim3(2048), dim3(256), 0, 0, x, y, id, n, off, nch); });
+        time("7pt xcd persistent 8192 + ids", 18.0 * n, [&] { hipLaunchKernelGGL((k_gen7x<true, true>), dim3(8192), dim3(256), 0, 0, x, y, id, n, off, nch); });
+    }
+    CK(hipDeviceSynchronize());
+    return 0;
+}
