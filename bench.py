@@ -165,6 +165,7 @@ def main():
     apply_avg_ms = apply_ms / max(apply_cnt, 1)
     gram_avg_ms = gram_ms / max(gram_cnt, 1)
     csr_spmv = None
+    host_rt_ms = None
     if world == 1 and rank == 0:
         # the same SpMV in plain CSR (12 B/nonzero), device-resident, for reference
         ctx2 = cal.Context(device=local, spmv_format="csr")
@@ -174,6 +175,14 @@ def main():
         del rp2, col2, val2
         csr_spmv = ctx2.bench_spmv(20, 1.0)
         ctx2.close()
+        # tier-1 host-pointer SpMV (MATLAB-boundary semantics: PCIe in and out)
+        v = np.ones(n)
+        ctx.spmv(v)
+        t_h = time.perf_counter()
+        for _ in range(3):
+            ctx.spmv(v)
+        host_rt_ms = (time.perf_counter() - t_h) / 3 * 1e3
+        del v
     if rank != 0:
         dist.barrier()
         return
@@ -236,6 +245,8 @@ def main():
     if csr_spmv is not None:
         line["spmv_csr_kernel"] = {"avg_us": csr_spmv[0] * 1e3, "min_us": csr_spmv[1] * 1e3,
                                    "gbps": b_csr / (csr_spmv[0] * 1e-3) / 1e9, "bytes_per_launch": b_csr}
+    if host_rt_ms is not None:
+        line["spmv_host_roundtrip_ms"] = host_rt_ms
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(dim, N, s, args.cpu_iters)
     print(json.dumps(line), flush=True)
