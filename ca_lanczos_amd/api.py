@@ -25,7 +25,7 @@ class Context:
     """A device context (``cal_ctx``): one HIP stream, the resident matrix and
     the device-resident CA-Lanczos state."""
 
-    def __init__(self, device: int | None = None, spmv_format: str | None = None):
+    def __init__(self, device: int | None = None, spmv_format: str | None = None, orth_coef: str | None = None):
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", "0"))
         h = ctypes.c_void_p()
@@ -38,6 +38,14 @@ class Context:
         self._keep = []
         fmt = spmv_format or os.environ.get("CAL_SPMV_FORMAT", "auto")
         check(self.h, lib.cal_set_spmv_format(self.h, fmt.encode()), "spmv format")
+        if orth_coef:
+            self.set_orth_coef(orth_coef)
+
+    def set_orth_coef(self, where: str):
+        """Run the block-orthogonalisation s x s algebra on the "device"
+        (default) or on the "host" (same bits; for testing)."""
+        check(self.h, lib.cal_set_orth_coef(self.h, where.encode()), "orth coef")
+        return self
 
     def bench_spmv(self, reps=20, shift=0.0):
         """Mean and min SpMV kernel time (ms) on HBM-resident vectors."""

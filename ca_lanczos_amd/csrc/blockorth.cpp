@@ -378,10 +378,89 @@ static int two_pass(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& W, cons
     return 0;
 }
 
+// ---- device-coefficient path ----------------------------------------------
+// The same three sweeps as two_pass (P1 Gram, pass A Grams, chained pass B)
+// with the s x s algebra in k_orth_coef, so the whole block is enqueued
+// without a host round trip and the host waits once, for R and RY.  Bits are
+// identical to the host path.  Returns 1 (nothing usable written to the
+// outputs) when a Cholesky failed: the caller then redoes the block on the
+// host path, whose fallbacks (direct Y'Y, shifted CholQR) handle it.
+static bool orth_device_ok(cal_ctx* c, const Panel& Qp, const Panel& X) {
+    const int w = Qp.total, m = X.total, nq = w < 8 ? w : 8;
+    return c->orth_coef_device && m >= 1 && w <= 9 && nq + m <= 16 && Qp.nseg + X.nseg <= kMaxSeg &&
+           rowapply_ok(w + m, m, true, w);
+}
+
+static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, bool doreorth, const PanelOut& Qout,
+                       double* Rq, double* R, bool* reorth) {
+    const int w = Qp.total, m = X.total, nq = w < 8 ? w : 8, wp = w + m;
+    const int WP = rowapply_wpmax(wp), MO = rowapply_mout(m);
+    const Panel W = panel_concat(Qp, X);
+    CAL_TRY(ensure_red(c, 4096));
+    double* d_tile = c->d_red;
+    double* d_st = c->d_red + 1024;
+    double* d_mbuf = c->d_red + 2048;
+    double* d_out = c->d_red + 3072;
+    int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 768));
+    CAL_TRY(ensure_partial(c, (size_t)blocks * 272));
+    // P1: [Qp(0:nq) | X]' X (+ Qp column 8 as the extra column)
+    ColList ct{};
+    {
+        const Panel T = panel_concat(panel_slice(W, 0, nq), X);
+        const int nt = T.total;
+        for (int cc = 0; cc < 16; ++cc) ct.p[cc] = panel_slice(T, cc < nt ? cc : nt - 1, 1).ptr[0];
+        ct.p[16] = w == 9 ? panel_slice(Qp, 8, 1).ptr[0] : ct.p[0];
+        const int t = timer_begin(c, 1);
+        CAL_HIP(c, launch_rowgram(ct, nt, w == 9, n, (int)blocks, c->d_partial, c->stream));
+        timer_end(c, t);
+    }
+    CAL_HIP(c, launch_reduce(c->d_partial, (int)blocks, 272, d_tile, c->stream));
+    CAL_TRY(allreduce_sum(c, d_tile, 272));
+    CAL_HIP(c, launch_orth_coef(0, d_tile, d_st, d_mbuf, d_out, w, m, WP, MO, doreorth ? 1 : 0, c->stream));
+    ColList cw{};
+    OutList ol{};
+    for (int cc = 0; cc < 17; ++cc) cw.p[cc] = panel_slice(W, cc < wp ? cc : wp - 1, 1).ptr[0];
+    for (int j = 0; j < 16; ++j) ol.p[j] = panel_out_slice(Qout, j < m ? j : 0, 1).ptr[0];
+    // pass A: Grams of Q1 = W M1, nothing stored
+    {
+        const int t = timer_begin(c, 1);
+        CAL_HIP(c, launch_rowapply(cw, d_mbuf, wp, m, ol, 2, w, n, (int)blocks, c->d_partial, c->stream));
+        timer_end(c, t);
+    }
+    CAL_HIP(c, launch_reduce(c->d_partial, (int)blocks, 272, d_tile, c->stream));
+    CAL_TRY(allreduce_sum(c, d_tile, 272));
+    CAL_HIP(c, launch_orth_coef(1, d_tile, d_st, d_mbuf, d_out, w, m, WP, MO, 0, c->stream));
+    // pass B: Q = [Qp | W M1] M2, one store
+    {
+        const int t = timer_begin(c, 2);
+        CAL_HIP(c, launch_rowapply(cw, d_mbuf, wp, m, ol, 3, w, n, (int)((n + 255) / 256), c->d_partial, c->stream));
+        timer_end(c, t);
+    }
+    double* h_out = c->h_red + 3072;
+    CAL_HIP(c, hipMemcpyAsync(h_out, d_out, 516 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    c->small_pending = false;
+    if (h_out[512] != 0.0 || h_out[513] != 0.0) return 1;
+    std::copy(h_out, h_out + (size_t)m * m, R);
+    std::copy(h_out + 256, h_out + 256 + (size_t)w * m, Rq);
+    *reorth = h_out[514] != 0.0;
+    return 0;
+}
+
 int normalize_dev(cal_ctx* c, int64_t n, const Panel& X, const PanelOut& Qout, double* R, double tol, int* rank,
                   bool* shifted) {
     const int m = X.total;
     if (m < 1 || m > 16) return set_error(c, CAL_ERR_ARG, "normalize: 1..16 columns supported");
+    if (orth_device_ok(c, panel(), X)) {
+        bool ro = false;
+        const int st = orth_device(c, n, panel(), X, false, Qout, nullptr, R, &ro);
+        CAL_TRY(st);
+        if (st == 0) {
+            if (shifted) *shifted = false;
+            if (rank) *rank = rank_from_R(m, R, tol);
+            return 0;
+        }
+    }
     std::vector<double> G((size_t)m * m), Mz((size_t)m * m, 0.0), Ctot;
     if (X.nseg <= kMaxSeg) {
         double G16[256], e16[16];
@@ -404,6 +483,19 @@ int project_and_normalize_dev(cal_ctx* c, int64_t n, const Panel& Qp, const Pane
     const int w = Qp.total, m = X.total;
     if (m < 1 || m > 16) return set_error(c, CAL_ERR_ARG, "projectAndNormalize: 1..16 columns supported");
     if (Qp.nseg + X.nseg > kMaxSeg) return set_error(c, CAL_ERR_ARG, "projectAndNormalize: too many segments");
+    if (orth_device_ok(c, Qp, X)) {
+        bool ro = false;
+        const int st = orth_device(c, n, Qp, X, doreorth, Qout, Rq, R, &ro);
+        CAL_TRY(st);
+        if (st == 0) {
+            if (res) {
+                res->reorth = ro;
+                res->rank = rank_from_R(m, R, 1.0e-8);
+                res->chol_shifted = false;
+            }
+            return 0;
+        }
+    }
     const Panel W = panel_concat(Qp, X);
     const int wp = w + m;
     // pass 1: [Qp | X]' X  -> C = Qp'X (project.m:34), X'X (norms before)

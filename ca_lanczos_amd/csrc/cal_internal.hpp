@@ -167,6 +167,10 @@ struct OutList {
 // kind: 0 store, 1 store + Gram, 2 Gram only (pass A), 3 chained store (pass B)
 hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, const OutList& Y, int kind, int wq,
                            int64_t n, int blocks, double* partial, hipStream_t st);
+// s x s coefficients of the two-sweep block orthogonalisation (phase 0 after
+// the P1 Gram, phase 1 after pass A); see kernels.hip k_orth_coef.
+hipError_t launch_orth_coef(int phase, const double* tile, double* st, double* mbuf, double* out, int w, int m,
+                            int WP, int MO, int doreorth, hipStream_t stream);
 hipError_t launch_rowgram(const ColList& P, int nt, bool has_extra, int64_t n, int blocks, double* partial,
                           hipStream_t st);
 hipError_t launch_dot(const double* x, const double* y, int64_t n, double* partial, int blocks,
@@ -220,6 +224,7 @@ struct cal_ctx {
     std::vector<hipEvent_t> event_pool;
 
     int spmv_format = 0;  // 0 auto, 1 CSR, 2 row-pattern (applies at the next set_matrix)
+    bool orth_coef_device = true;  // block-orth s x s algebra on the device (blockorth.cpp)
 };
 
 // ---- helpers shared by the host-side translation units -----------------

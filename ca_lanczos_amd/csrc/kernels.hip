@@ -195,14 +195,16 @@ __global__ __launch_bounds__(256) void k_spmv_pat(PatArgs a) {
 // Row-pattern SpMV with the pattern table (npat*8 + nent*12 bytes) staged
 // into LDS, so the per-row lookups are LDS broadcasts and the vector-memory
 // path only carries the 2-B ids, the x gathers and the y stores.  The grid is
-// persistent; each XCD owns a contiguous range of 256-row chunks and its
-// blocks sweep that range interleaved, so the XCD's rows in flight form one
-// moving window and the x lines of the +-plane neighbours stay in its L2.
+// persistent: each block sweeps a contiguous run of 256-row chunks and the
+// XCD remap makes the runs of one XCD contiguous.  The blocks of an XCD move
+// in near lockstep, so the +-plane neighbour rows a block gathers are the
+// rows another block of the same XCD is reading at the same time (measured:
+// 146 MB fetched per SpMV vs 205 MB for an interleaved sweep, same time).
 // The ids of the next chunk are loaded before this chunk's gathers and store
 // (vmcnt retires in order: an id load issued after the y store would wait
 // for that store).
 template <int MODE, int MAXLEN>
-__global__ __launch_bounds__(256) void k_spmv_pat_lds(PatArgs a, int npat, int nent) {
+__global__ __launch_bounds__(256) void k_spmv_pat_lds(PatArgs a, int npat, int nent, int chunks_per_block) {
     extern __shared__ __attribute__((aligned(16))) double lds_tab[];
     int2* s_info = reinterpret_cast<int2*>(lds_tab);
     double* s_val = lds_tab + npat;
@@ -213,11 +215,10 @@ __global__ __launch_bounds__(256) void k_spmv_pat_lds(PatArgs a, int npat, int n
         s_delta[i] = a.pdelta[i];
     }
     __syncthreads();
-    const int G = gridDim.x, q = G >> 3, rm = G & 7, xcd = blockIdx.x & 7, bi = blockIdx.x >> 3;
-    const int nbx = q + (xcd < rm ? 1 : 0);
-    const int b0 = xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q;
-    const int c0 = (int)((int64_t)a.nblk * b0 / G) + bi;
-    const int c1 = (int)((int64_t)a.nblk * (b0 + nbx) / G);
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int c0 = lb * chunks_per_block;
+    const int c1 = min(c0 + chunks_per_block, a.nblk);
+    constexpr int nbx = 1;
     auto row_of = [&](int ch) -> int64_t {
         const int64_t r = (int64_t)ch * 256 + threadIdx.x;
         return ch < c1 && r < a.n ? r : -1;
@@ -264,8 +265,9 @@ static hipError_t launch_pat_mode(const PatArgs& a, hipStream_t st) {
     const size_t lds = (size_t)a.npat * 8 + (size_t)a.nent * 12 + 16;
     if (lds <= kPatLdsMax) {
         const int blocks = a.nblk < 2048 ? a.nblk : 2048;
+        const int cpb = (a.nblk + blocks - 1) / blocks;
         dim3 g(blocks), b(256);
-#define CAL_PL(ML) hipLaunchKernelGGL((k_spmv_pat_lds<MODE, ML>), g, b, lds, st, a, a.npat, a.nent)
+#define CAL_PL(ML) hipLaunchKernelGGL((k_spmv_pat_lds<MODE, ML>), g, b, lds, st, a, a.npat, a.nent, cpb)
         switch (a.maxlen) {
             case 1: CAL_PL(1); break;
             case 2: CAL_PL(2); break;
@@ -1061,6 +1063,199 @@ __global__ __launch_bounds__(256) void k_spmv_resid(SpmvArgs a, const double* __
 hipError_t launch_spmv_resid(const SpmvArgs& a, const double* xi, double lr, double li, int64_t nrows,
                              double* partial, int blocks, hipStream_t st) {
     hipLaunchKernelGGL(k_spmv_resid, dim3(blocks), dim3(256), 0, st, a, xi, lr, li, nrows, partial);
+    return hipGetLastError();
+}
+
+// --------------------------------------------------------------------------
+// Block-orthogonalisation coefficients on the device (blockorth.cpp,
+// orth_device).  The s x s algebra between the three sweeps of two_pass --
+// Cholesky, triangular inverse, the coefficient blocks M1 / M2 and R, RY --
+// runs in one 256-thread block right after the Gram reduction, so the sweeps
+// are enqueued back to back without a host round trip.  Every quantity is
+// computed with the same operation order as the host path in blockorth.cpp
+// (right-looking Cholesky updates reproduce the left-looking host sums term
+// for term; products and sums in the same sequence), so both paths give the
+// same bits.
+// --------------------------------------------------------------------------
+namespace {
+constexpr int kOcM = 16, kOcW = 9;
+
+// Upper Cholesky of the m x m matrix in G (ld kOcM, destroyed) into R;
+// returns false (block-uniform) on a non-positive or non-finite pivot.
+__device__ bool oc_chol(int m, double* G, double* R, int* flag) {
+    const int tid = threadIdx.x;
+    for (int e = tid; e < kOcM * kOcM; e += blockDim.x) R[e] = 0.0;
+    __syncthreads();
+    for (int j = 0; j < m; ++j) {
+        // G(j,j..m-1) already hold G - sum_{k<j} R(k,j) R(k,i) (host: chol_upper)
+        if (tid == 0) {
+            const double sj = G[j + j * kOcM];
+            *flag = !(sj > 0.0) || !isfinite(sj);
+            if (!*flag) R[j + j * kOcM] = sqrt(sj);
+        }
+        __syncthreads();
+        if (*flag) return false;
+        const double rjj = R[j + j * kOcM];
+        for (int i = j + 1 + tid; i < m; i += blockDim.x) R[j + i * kOcM] = G[j + i * kOcM] / rjj;
+        __syncthreads();
+        // trailing update of rows/cols > j, one (r, i) entry per thread
+        for (int e = tid; e < m * m; e += blockDim.x) {
+            const int r = e % m, i = e / m;
+            if (r > j && i >= r) {
+                const double t = R[j + r * kOcM] * R[j + i * kOcM];
+                G[r + i * kOcM] = G[r + i * kOcM] - t;
+            }
+        }
+        __syncthreads();
+    }
+    return true;
+}
+
+// Ri = R^-1 (upper), column j by thread j with the host's back substitution.
+__device__ void oc_trinv(int m, const double* R, double* Ri) {
+    const int tid = threadIdx.x;
+    for (int e = tid; e < kOcM * kOcM; e += blockDim.x) Ri[e] = 0.0;
+    __syncthreads();
+    if (tid < m) {
+        const int j = tid;
+        for (int i = j; i >= 0; --i) {
+            double s = (i == j) ? 1.0 : 0.0;
+            for (int k = i + 1; k <= j; ++k) {
+                const double t = R[i + k * kOcM] * Ri[k + j * kOcM];
+                s = s - t;
+            }
+            Ri[i + j * kOcM] = s / R[i + i * kOcM];
+        }
+    }
+    __syncthreads();
+}
+}  // namespace
+
+// PHASE 0 (after the P1 Gram of [Qp(0:nq) | X] (+ Qp column 8)):
+//   C = Qp'X, Y'Y = X'X - C'C, the reorth flag of projectAndNormalize.m:52,
+//   Ra = chol(Y'Y), M1 = [-C; I] Ra^-1 -> row-kernel layout in mbuf[0 : WP*MO).
+// PHASE 1 (after pass A's Grams of Q1):
+//   Rb = chol(Q1'Q1 - C3'C3), M2 = [-C3 Rb^-1; Rb^-1] -> mbuf chain part,
+//   R = Rb Ra, RY = C + C3 Ra -> out.
+// st: C (kOcW x kOcM, ld w) at 0, Ra at 256.  out: R (m x m) at 0, RY
+// (w x m) at 256, flags at 512: [0] phase-0 failure, [1] phase-1 failure,
+// [2] reorth.
+template <int PHASE>
+__global__ __launch_bounds__(256) void k_orth_coef(const double* __restrict__ tile, double* __restrict__ st,
+                                                   double* __restrict__ mbuf, double* __restrict__ out, int w, int m,
+                                                   int WP, int MO, int doreorth) {
+    __shared__ double G[kOcM * kOcM], R[kOcM * kOcM], Ri[kOcM * kOcM], C[kOcW * kOcM], Ra[kOcM * kOcM];
+    __shared__ double nb[kOcM];
+    __shared__ int flag;
+    const int tid = threadIdx.x, nq = w < 8 ? w : 8, wp = w + m;
+    // unpack the tile: G = block Gram (m x m), C = Qp' block (w x m)
+    for (int e = tid; e < m * m; e += blockDim.x) {
+        const int i = e % m, j = e / m;
+        G[i + j * kOcM] = tile[(nq + i) + (nq + j) * 16];
+    }
+    for (int e = tid; e < w * m; e += blockDim.x) {
+        const int i = e % w, j = e / w;
+        C[e] = i < 8 ? tile[i + (nq + j) * 16] : tile[256 + nq + j];
+    }
+    if (PHASE == 1)
+        for (int e = tid; e < m * m; e += blockDim.x) Ra[e % m + (e / m) * kOcM] = st[256 + e];
+    __syncthreads();
+    if (PHASE == 0 && tid < m) nb[tid] = sqrt(G[tid + tid * kOcM]);  // norms before (projectAndNormalize.m:17-22)
+    // G -= C'C   (host: s = sum_k C(k,i) C(k,j); G(i,j) -= s)
+    double upd[2] = {0.0, 0.0};
+    for (int e = tid, q = 0; e < m * m; e += blockDim.x, ++q) {
+        const int i = e % m, j = e / m;
+        double s = 0.0;
+        for (int k = 0; k < w; ++k) {
+            const double t = C[k + i * w] * C[k + j * w];
+            s = s + t;
+        }
+        upd[q] = G[i + j * kOcM] - s;
+    }
+    __syncthreads();
+    for (int e = tid, q = 0; e < m * m; e += blockDim.x, ++q) G[e % m + (e / m) * kOcM] = upd[q];
+    __syncthreads();
+    if (PHASE == 0 && tid == 0) {
+        // rel = |before - after| / before, reorth = max(rel) > 0.5 (NaN-ignoring max)
+        double mx = NAN;
+        for (int i = 0; i < m; ++i) {
+            const double after = sqrt(fmax(G[i + i * kOcM], 0.0));
+            const double rel = fabs(nb[i] - after) / nb[i];
+            if (!isnan(rel) && (isnan(mx) || rel > mx)) mx = rel;
+        }
+        out[512 + 2] = (doreorth && mx > 0.5) ? 1.0 : 0.0;
+    }
+    const bool ok = oc_chol(m, G, R, &flag);
+    if (tid == 0) out[512 + PHASE] = ok ? 0.0 : 1.0;
+    if (!ok) return;  // block-uniform: the host redoes the block on its own path
+    oc_trinv(m, R, Ri);
+    if (PHASE == 0) {
+        // M1 = Mz Ri, Mz = [-C; I] (wp x m); host: dense::matmul, p = 0..m-1
+        for (int e = tid; e < WP * MO; e += blockDim.x) {
+            const int cc = e / MO, j = e % MO;
+            double s = 0.0;
+            if (cc < wp && j < m) {
+                for (int p = 0; p < m; ++p) {
+                    const double mz = cc < w ? -C[cc + p * w] : (cc - w == p ? 1.0 : 0.0);
+                    const double t = mz * Ri[p + j * kOcM];
+                    s = s + t;
+                }
+            }
+            mbuf[e] = (cc < wp && j < m) ? s : 0.0;
+        }
+        for (int e = tid; e < w * m; e += blockDim.x) st[e] = C[e];
+        for (int e = tid; e < m * m; e += blockDim.x) st[256 + e] = R[e % m + (e / m) * kOcM];
+    } else {
+        double* M2p = mbuf + WP * MO;
+        double* M2y = M2p + WP * MO;
+        // M2 = [-C3 Rb^-1 ; Rb^-1]   (C3 is this phase's C)
+        for (int e = tid; e < WP * MO; e += blockDim.x) {
+            const int cc = e / MO, j = e % MO;
+            double v = 0.0;
+            if (cc < w && j < m) {
+                double s = 0.0;
+                for (int k = 0; k <= j; ++k) {
+                    const double t = C[cc + k * w] * Ri[k + j * kOcM];
+                    s = s + t;
+                }
+                v = -s;
+            }
+            M2p[e] = v;
+        }
+        for (int e = tid; e < MO * MO; e += blockDim.x) {
+            const int i = e / MO, j = e % MO;
+            M2y[e] = (i < m && j < m) ? Ri[i + j * kOcM] : 0.0;
+        }
+        // RY = C + C3 Ra (C from phase 0 in st), R = Rb Ra (upper)
+        for (int e = tid; e < w * m; e += blockDim.x) {
+            const int i = e % w, j = e / w;
+            double s = 0.0;
+            for (int k = 0; k <= j; ++k) {
+                const double t = C[i + k * w] * Ra[k + j * kOcM];
+                s = s + t;
+            }
+            const double ctot = 0.0 + s;
+            out[256 + e] = st[e] + ctot;
+        }
+        for (int e = tid; e < m * m; e += blockDim.x) {
+            const int i = e % m, j = e / m;
+            double s = 0.0;
+            for (int p = 0; p < m; ++p) {
+                const double t = R[i + p * kOcM] * Ra[p + j * kOcM];
+                s = s + t;
+            }
+            out[e] = i > j ? 0.0 : s;
+        }
+    }
+}
+
+hipError_t launch_orth_coef(int phase, const double* tile, double* st, double* mbuf, double* out, int w, int m,
+                            int WP, int MO, int doreorth, hipStream_t stream) {
+    if (m < 1 || m > kOcM || w < 0 || w > kOcW) return hipErrorInvalidValue;
+    if (phase == 0)
+        hipLaunchKernelGGL(k_orth_coef<0>, dim3(1), dim3(256), 0, stream, tile, st, mbuf, out, w, m, WP, MO, doreorth);
+    else
+        hipLaunchKernelGGL(k_orth_coef<1>, dim3(1), dim3(256), 0, stream, tile, st, mbuf, out, w, m, WP, MO, doreorth);
     return hipGetLastError();
 }
 

@@ -457,6 +457,14 @@ int cal_set_spmv_format(cal_ctx* c, const char* fmt) {
     return 0;
 }
 
+int cal_set_orth_coef(cal_ctx* c, const char* where) {
+    if (!c || !where) return CAL_ERR_ARG;
+    if (!strcmp(where, "device")) c->orth_coef_device = true;
+    else if (!strcmp(where, "host")) c->orth_coef_device = false;
+    else return set_error(c, CAL_ERR_ARG, "orth coefficients: \"device\" or \"host\"");
+    return 0;
+}
+
 int cal_spmv_format(cal_ctx* c, int* is_pattern, int* npatterns, int* nentries) {
     if (!c) return CAL_ERR_ARG;
     if (!c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");

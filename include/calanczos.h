@@ -76,6 +76,10 @@ int cal_matrix_info(cal_ctx* ctx, int64_t* n_local, int64_t* nnz_local, int64_t*
  * results (same per-row summation order). */
 int cal_set_spmv_format(cal_ctx* ctx, const char* fmt);
 int cal_spmv_format(cal_ctx* ctx, int* is_pattern, int* npatterns, int* nentries);
+/* Where the s x s algebra between the block-orthogonalisation sweeps runs:
+ * "device" (default: one kernel, no host round trip inside a block) or
+ * "host".  Both give bit-identical results; "host" exists for testing. */
+int cal_set_orth_coef(cal_ctx* ctx, const char* where);
 /* Device-resident SpMV timing: `reps` launches of y = (A - shift I) x on
  * HBM-resident vectors (x = ones), HIP events around each launch on the
  * context stream; returns the mean and the minimum kernel time. */

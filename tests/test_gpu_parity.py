@@ -251,3 +251,53 @@ def test_ca_lanczos_bad_args(cal):
         cal.ca_lanczos(A, np.ones(64), 4, 16, "chebyshev", "local")
     with pytest.raises(cal.CalError):
         cal.ca_lanczos(A, np.ones(64), 4, 16, "newton", "periodic")
+
+
+@pytest.mark.gpu
+def test_orth_coef_device_matches_host(cal, ref):
+    """The block-orth s x s algebra on the device (k_orth_coef) reproduces the
+    host path bit for bit: projectAndNormalize, normalize, a whole run."""
+    rng = np.random.default_rng(7)
+    n = 20000
+    Qp, _ = np.linalg.qr(rng.standard_normal((n, 9)))
+    X = rng.standard_normal((n, 8)) + Qp[:, :8] * 3.0
+    ctx = cal.default_context()
+    outs = []
+    for where in ("device", "host"):
+        ctx.set_orth_coef(where)
+        outs.append((cal.projectAndNormalize_ex([Qp], X, True), cal.normalize(X[:, :8])))
+    ctx.set_orth_coef("device")
+    (pa, na), (pb, nb) = outs
+    assert np.array_equal(pa[0], pb[0]) and pa[2] == pb[2]
+    for a, b in zip(pa[1], pb[1]):
+        assert np.array_equal(a, b)
+    for a, b in zip(na, nb):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    A = cal.matrices.laplacian_3d(12)
+    r = ref.matlab_rand(A.shape[0])
+    runs = []
+    for where in ("device", "host"):
+        c2 = cal.Context(orth_coef=where).set_matrix(A)
+        runs.append(cal.ca_lanczos_ex(A, r, 8, 40, "newton", "local", diagnostics=False, ctx=c2))
+        c2.close()
+    assert np.array_equal(runs[0].T, runs[1].T)
+    assert np.array_equal(runs[0].Q, runs[1].Q)
+    assert np.array_equal(runs[0].reorth, runs[1].reorth)
+
+
+@pytest.mark.gpu
+def test_orth_coef_device_fallback(cal):
+    """A block whose Gram is numerically singular makes the device Cholesky
+    fail; the block is redone on the host path (shifted CholQR)."""
+    rng = np.random.default_rng(3)
+    n = 5000
+    B = rng.standard_normal((n, 4))
+    X = np.hstack([B, B @ rng.standard_normal((4, 4)) + 1e-12 * rng.standard_normal((n, 4))])
+    ctx = cal.default_context()
+    res = []
+    for where in ("device", "host"):
+        ctx.set_orth_coef(where)
+        res.append(cal.normalize(X))
+    ctx.set_orth_coef("device")
+    assert np.array_equal(res[0][0], res[1][0]) and np.array_equal(res[0][1], res[1][1])
+    assert res[0][2] == res[1][2]

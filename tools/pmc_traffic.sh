@@ -25,6 +25,9 @@ for grp in fetch write hit; do
         write) C=(WRITE_SIZE) ;;
         hit) C=(TCC_HIT_sum TCC_MISS_sum) ;;
     esac
-    run spmv $grp "${C[@]}" -- python3 $GRAFT_REPO_ROOT/tools/spmv_sweep.py --reps 10 || exit $?
+    if [ -z "$BENCH_ONLY" ]; then
+        run spmv $grp "${C[@]}" -- python3 $GRAFT_REPO_ROOT/tools/spmv_sweep.py --reps 10 || exit $?
+    fi
     run bench $grp "${C[@]}" -- python3 $GRAFT_REPO_ROOT/bench.py --steps $STEPS --warmup 1 --no-cpu-baseline || exit $?
 done
+cd $GRAFT_REPO_ROOT && python3 tools/traffic_json.py gpurun_out/pmc --out gpurun_out/pmc/spmv_traffic.json > /dev/null
