@@ -170,6 +170,7 @@ def main():
         spmv_avg_ms = spmv_ms / max(spmv_cnt, 1)
 
     fmt, npat, nent = ctx.spmv_format()
+    npairpat, npent, nsplit = ctx.spmv_pair_info()
     apply_avg_ms = apply_ms / max(apply_cnt, 1)
     gram_avg_ms = gram_ms / max(gram_cnt, 1)
     csr_spmv = None
@@ -197,18 +198,20 @@ def main():
 
     n_loc = r1 - r0
     # per-launch algorithmic bytes:
-    #   SpMV CSR: 12 nnz + 20 n + 4; row-pattern: 2 n (ids) + 8 n (x) + 8 n (y)
+    #   SpMV CSR: 12 nnz + 20 n + 4; row-pattern: 2 n (ids) + 8 n (x) + 8 n (y);
     #   apply (pass B, chained): (w + m) * 8 read + m * 8 written per row (w = s+1, m = s)
     #   Gram sweeps (P1 and pass A): (w + m) * 8 read per row
     b_csr = 12 * nnz_local + 20 * n_loc + 4
-    b_spmv_launch = 18 * n_loc if fmt == "pattern" else b_csr
+    #   pair patterns: 1 B of id per row (one 2-B id per row pair)
+    b_spmv_launch = (17 if npairpat else 18) * n_loc if fmt == "pattern" else b_csr
     b_apply = (2 * s + 1 + s) * 8 * n_loc
     b_gram = (2 * s + 1) * 8 * n_loc
     spmv_gbps = b_spmv_launch / (spmv_avg_ms * 1e-3) / 1e9
     per_step = {"spmv": spmv_ms / KT, "gram": gram_ms / KT, "apply": apply_ms / KT}
     dominant = max(per_step, key=per_step.get)
-    dom = {"spmv": (b_spmv_launch, spmv_avg_ms, "k_spmv_pat (row-pattern SpMV + Newton shift)" if fmt == "pattern"
-                    else "k_spmv (CSR-stream SpMV + Newton shift)"),
+    dom = {"spmv": (b_spmv_launch, spmv_avg_ms, ("k_spmv_pair (row-pattern SpMV, two rows per lane, + Newton shift)"
+                                                 if npairpat else "k_spmv_pat_lds (row-pattern SpMV + Newton shift)")
+                    if fmt == "pattern" else "k_spmv (CSR-stream SpMV + Newton shift)"),
            "gram": (b_gram, gram_avg_ms, "k_rowapply Gram sweeps ([Qp|X]'X and pass A, MFMA tile Gram, no store)"),
            "apply": (b_apply, apply_avg_ms, "k_rowapply<17,8,chained> (block orthogonalisation pass B)")}[dominant]
     achieved = dom[0] / (dom[1] * 1e-3) / 1e9
@@ -239,7 +242,8 @@ def main():
         "config": {"workload": "%s: %s %dx..., n=%d, nnz=%d" % (args.workload, "7-pt 3-D" if dim == 3 else "5-pt 2-D",
                                                                 N, n, nnz_total),
                    "s": s, "basis": args.basis, "orth": args.orth, "parallelism": "row-slab x%d" % world},
-        "spmv_format": "%s (%d patterns, %d entries)" % (fmt, npat, nent) if fmt == "pattern" else fmt,
+        "spmv_format": ("%s (%d row patterns, %d entries; %d pair patterns, %d entries, %d split pairs)"
+                        % (fmt, npat, nent, npairpat, npent, nsplit)) if fmt == "pattern" else fmt,
         "spmv_gbps": spmv_gbps,
         "spmv_avg_us": spmv_avg_ms * 1e3,
         "spmv_csr_equiv_gbps": b_csr / (spmv_avg_ms * 1e-3) / 1e9,

@@ -68,6 +68,7 @@ SIGNATURES = [
      [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64), POINTER(c_int64)]),
     ("cal_set_spmv_format", c_int, [c_void_p, c_char_p]),
     ("cal_set_orth_coef", c_int, [c_void_p, c_char_p]),
+    ("cal_spmv_pair_info", c_int, [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_int64)]),
     ("cal_spmv_format", c_int, [c_void_p, ip, ip, ip]),
     ("cal_bench_spmv", c_int, [c_void_p, c_int, c_double, dp, dp]),
     ("cal_spmv", c_int, [c_void_p, dp, dp]),

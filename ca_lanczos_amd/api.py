@@ -65,6 +65,13 @@ class Context:
         check(self.h, lib.cal_spmv_format(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
         return ("pattern" if a.value else "csr", b.value, c.value)
 
+    def spmv_pair_info(self):
+        """(pair patterns, their table entries, pairs on the per-row path);
+        zeros when the two-rows-per-lane kernel is not in use."""
+        a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64()
+        check(self.h, lib.cal_spmv_pair_info(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, c.value
+
     def close(self):
         if self.h:
             lib.cal_destroy(self.h)

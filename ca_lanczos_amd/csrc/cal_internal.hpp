@@ -93,7 +93,17 @@ struct PatArgs {
     int mode;              // as SpmvArgs
     int maxlen;            // 1..8 exact, else 16 / 32
     int npat, nent;        // table sizes (LDS-resident when small)
+    // pair patterns (k_spmv_pair): rows 2t, 2t+1 share one merged pattern
+    const uint16_t* ppat;  // per pair; kPairSplit -> per-row fallback
+    const int2* ppinfo;    // (start, len) per pair pattern
+    const int* ppoff;      // (offset << 2) | used-by-row-2t | used-by-row-2t+1 << 1
+    const double2* ppval;  // (value for row 2t, value for row 2t+1)
+    int nppat, npent, pmaxlen;
+    int pcanon;            // every pair pattern has exactly pmaxlen entries (canonical slots)
+    int pslot[8];          // canonical slot offsets (the matrix's distinct col - row, ascending)
+    int64_t xlo, xhi;      // addressable range of a vector column around its origin
 };
+constexpr int kPairSplit = 0xFFFF;
 
 struct DevMatrix {
     int64_t n_local = 0, n_global = 0, row0 = 0, nnz = 0, nghost = 0;
@@ -112,6 +122,16 @@ struct DevMatrix {
     int* pdelta = nullptr;
     double* pval = nullptr;
     int npat = 0, nent = 0, maxlen = 0;
+    // pair patterns (two rows per lane, 16-B x loads; built with the row patterns)
+    bool use_pair = false;
+    uint16_t* ppat = nullptr;
+    int2* ppinfo = nullptr;
+    int* ppoff = nullptr;
+    double2* ppval = nullptr;
+    int nppat = 0, npent = 0, pmaxlen = 0;
+    int64_t npsplit = 0;
+    bool pcanon = false;
+    int pslot[8] = {};
     // halo plan (distributed); ghost entries grouped by owning peer
     std::vector<int> peers;              // neighbour ranks
     std::vector<int64_t> recv_off;       // ghost destination per peer, relative to the local origin

@@ -258,11 +258,159 @@ __global__ __launch_bounds__(256) void k_spmv_pat_lds(PatArgs a, int npat, int n
     }
 }
 
+// Two rows per lane on pair patterns (runtime.cpp build_pair_patterns):
+// rows 2t and 2t+1 share one merged table entry list, so every entry is ONE
+// 16-B load x[r+o .. r+o+1] serving both rows -- the wave issues half the
+// gather instructions and cache-line requests of a row-per-lane kernel, and
+// y leaves as one 16-B store.  Entry flags mark which row adds the entry;
+// each row adds exactly its own entries in column order (bit-identical to
+// CSR).  Pairs marked kPairSplit (rare: domain ends, odd n) take the
+// per-row path.  The XCD remap makes each XCD's chunks contiguous, so the
+// +-plane neighbour lines stay in its L2.  Requires x, y (and xprev) 16-B
+// aligned at the origin (checked at launch).
+__device__ __forceinline__ double2 ld16(const double* p) {
+    double2 v;
+    __builtin_memcpy(&v, p, 16);  // 8-B aligned for odd offsets: still one dwordx4
+    return v;
+}
+
+// The pair table (a few KB) is staged in LDS per block; the block's id
+// load is issued before the staging loads so both share one memory round
+// trip.  Split pairs (and the lone last row of an odd n) read the row
+// tables from global memory (rare).
+template <int MODE, int MAXLEN, bool CANON>
+__global__ __launch_bounds__(256) void k_spmv_pair(PatArgs a, const uint16_t* __restrict__ ppat,
+                                                  const int2* __restrict__ ppinfo, const int* __restrict__ ppoff,
+                                                  const double2* __restrict__ ppval) {
+    extern __shared__ __attribute__((aligned(16))) double lds_pair[];
+    double2* s_pv = reinterpret_cast<double2*>(lds_pair);
+    int2* s_pinfo = reinterpret_cast<int2*>(s_pv + a.npent);
+    int* s_poff = reinterpret_cast<int*>(s_pinfo + (CANON ? 0 : a.nppat));
+    const int tid = threadIdx.x;
+    const int64_t npairs = (a.n + 1) >> 1;
+    const int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 256 + tid;
+    const int id = ppat[t < npairs ? t : npairs - 1];
+    // canonical slots: slot e always loads x[r + pslot[e] .. +1] (clamped to
+    // the column; a slot no row of the pair uses is discarded), so the x
+    // loads depend on neither the id nor the table and leave first
+    double2 xc[CANON ? MAXLEN : 1];
+    double2 xs = make_double2(0.0, 0.0), xp = make_double2(0.0, 0.0);  // shift terms
+    {
+        const int64_t r0 = 2 * (t < npairs ? t : npairs - 1);
+        if (CANON) {
+#pragma unroll
+            for (int e = 0; e < MAXLEN; ++e) {
+                int64_t ad = r0 + a.pslot[e];
+                ad = ad < a.xlo ? a.xlo : (ad > a.xhi - 2 ? a.xhi - 2 : ad);
+                xc[e] = ld16(a.x + ad);
+            }
+        }
+        const int64_t rc = r0 < a.xhi - 2 ? r0 : a.xhi - 2;
+        if (MODE != 0) xs = ld16(a.x + rc);
+        if (MODE == 2) xp = ld16(a.xprev + rc);
+    }
+    for (int i = tid; i < a.npent; i += 256) {
+        s_pv[i] = ppval[i];
+        s_poff[i] = ppoff[i];
+    }
+    if (!CANON)
+        for (int i = tid; i < a.nppat; i += 256) s_pinfo[i] = ppinfo[i];
+    __syncthreads();
+    if (t >= npairs) return;
+    const int64_t r = 2 * t;
+    if (id != kPairSplit) {  // both rows exist (the lone last row is split)
+        // canonical tables: every pair pattern has MAXLEN entries in one
+        // global slot order -> entry id * MAXLEN + e, no length checks
+        const int2 pi = CANON ? make_int2(id * MAXLEN, MAXLEN) : s_pinfo[id];
+        const int last = pi.y > 0 ? pi.y - 1 : 0;
+        int code[MAXLEN];
+        double2 xv[MAXLEN];
+#pragma unroll
+        for (int e = 0; e < MAXLEN; ++e) {
+            code[e] = s_poff[pi.x + (CANON || e < pi.y ? e : last)];
+            if (!CANON) xv[e] = ld16(a.x + r + (code[e] >> 2));
+        }
+        if (CANON)  // loads issued before the id and table arrive (see above)
+#pragma unroll
+            for (int e = 0; e < MAXLEN; ++e) xv[e] = xc[e];
+        double y0 = 0.0, y1 = 0.0;
+#pragma unroll
+        for (int e = 0; e < MAXLEN; ++e) {
+            const double2 v = s_pv[pi.x + (CANON || e < pi.y ? e : last)];
+            const double t0 = v.x * xv[e].x, t1 = v.y * xv[e].y;
+            double a0 = y0 + t0, a1 = y1 + t1;
+            // both sums computed unconditionally (the selects stay v_cndmask;
+            // otherwise the compiler branches and splits the 16-B loads)
+            asm volatile("" : "+v"(a0), "+v"(a1));
+            y0 = ((CANON || e < pi.y) && (code[e] & 1)) ? a0 : y0;
+            y1 = ((CANON || e < pi.y) && (code[e] & 2)) ? a1 : y1;
+        }
+        if (MODE != 0) {
+            const double u0 = a.shift * xs.x, u1 = a.shift * xs.y;
+            y0 = y0 - u0;
+            y1 = y1 - u1;
+            if (MODE == 2) {
+                const double w0 = a.im2 * xp.x, w1 = a.im2 * xp.y;
+                y0 = y0 + w0;
+                y1 = y1 + w1;
+            }
+        }
+        double2 o;
+        o.x = y0;
+        o.y = y1;
+        *reinterpret_cast<double2*>(a.y + r) = o;
+        return;
+    }
+    // split pair: each row on its own from the row tables
+    for (int k = 0; k < 2 && r + k < a.n; ++k) {
+        const int64_t rr = r + k;
+        const int2 pi = a.pinfo[a.pat[rr]];
+        double sum = 0.0;
+        for (int e = 0; e < pi.y; ++e) {
+            const double tv = a.pval[pi.x + e] * a.x[rr + a.pdelta[pi.x + e]];
+            sum = sum + tv;
+        }
+        double y = sum;
+        if (MODE != 0) {
+            const double u = a.shift * a.x[rr];
+            y = y - u;
+            if (MODE == 2) {
+                const double w = a.im2 * a.xprev[rr];
+                y = y + w;
+            }
+        }
+        a.y[rr] = y;
+    }
+}
+
 constexpr size_t kPatLdsMax = 64 * 1024;
 
 template <int MODE>
 static hipError_t launch_pat_mode(const PatArgs& a, hipStream_t st) {
     const size_t lds = (size_t)a.npat * 8 + (size_t)a.nent * 12 + 16;
+    const bool al16 = (((uintptr_t)a.x | (uintptr_t)a.y | (uintptr_t)(MODE == 2 ? a.xprev : nullptr)) & 15) == 0;
+    const size_t lds2 = (size_t)a.npent * 20 + (size_t)a.nppat * 8 + 16;
+    if (a.ppat && al16 && a.maxlen <= 8 && lds2 <= kPatLdsMax) {
+        const int64_t npairs = (a.n + 1) / 2;
+        dim3 g((unsigned)((npairs + 255) / 256)), b(256);
+#define CAL_PR(ML)                                                                                           \
+    if (a.pcanon) hipLaunchKernelGGL((k_spmv_pair<MODE, ML, true>), g, b, lds2, st, a, a.ppat, a.ppinfo, a.ppoff, \
+                                     a.ppval);                                                                  \
+    else hipLaunchKernelGGL((k_spmv_pair<MODE, ML, false>), g, b, lds2, st, a, a.ppat, a.ppinfo, a.ppoff, a.ppval);
+        switch (a.pmaxlen) {
+            case 1: CAL_PR(1); break;
+            case 2: CAL_PR(2); break;
+            case 3: CAL_PR(3); break;
+            case 4: CAL_PR(4); break;
+            case 5: CAL_PR(5); break;
+            case 6: CAL_PR(6); break;
+            case 7: CAL_PR(7); break;
+            case 8: CAL_PR(8); break;
+            default: CAL_PR(16); break;
+        }
+#undef CAL_PR
+        return hipGetLastError();
+    }
     if (lds <= kPatLdsMax) {
         const int blocks = a.nblk < 2048 ? a.nblk : 2048;
         const int cpb = (a.nblk + blocks - 1) / blocks;

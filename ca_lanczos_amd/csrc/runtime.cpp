@@ -139,6 +139,10 @@ static void free_matrix(cal_ctx* c) {
     if (A.pinfo) hipFree(A.pinfo);
     if (A.pdelta) hipFree(A.pdelta);
     if (A.pval) hipFree(A.pval);
+    if (A.ppat) hipFree(A.ppat);
+    if (A.ppinfo) hipFree(A.ppinfo);
+    if (A.ppoff) hipFree(A.ppoff);
+    if (A.ppval) hipFree(A.ppval);
     A = DevMatrix();
     if (c->d_work) hipFree(c->d_work);
     c->d_work = nullptr;
@@ -204,6 +208,106 @@ static bool build_patterns(int64_t n, const std::vector<int>& rowptr, const std:
     return true;
 }
 
+// Pair patterns: rows 2t and 2t+1 get one merged pattern over the union O of
+// their column offsets, so one 16-B load x[r+o .. r+o+1] per entry serves
+// both rows.  Entry flags say which row uses it; each row still adds its own
+// entries in column order (bit-identical).  A merged entry loads the
+// unused half too, so that half must be a valid vector entry: a local row
+// or an index some row references (received halo).  Pairs that fail this,
+// and the lone last row of an odd n, are marked kPairSplit (per-row path).
+constexpr int kMaxPairLen = 16;
+
+static bool build_pair_patterns(int64_t n, const std::vector<uint16_t>& pat, const std::vector<int2>& pinfo,
+                                const std::vector<int>& pdelta, const std::vector<double>& pval,
+                                const std::vector<int>& col, std::vector<uint16_t>& ppat, std::vector<int2>& ppinfo,
+                                std::vector<int>& ppoff, std::vector<double>& ppval, int* pmaxlen, bool* pcanon,
+                                int* slots) {
+    int64_t cmin = 0, cmax = n - 1;
+    for (int v : col) {
+        cmin = std::min<int64_t>(cmin, v);
+        cmax = std::max<int64_t>(cmax, v);
+    }
+    std::vector<uint8_t> ref((size_t)(cmax - cmin + 1), 0);
+    for (int v : col) ref[(size_t)(v - cmin)] = 1;
+    auto valid = [&](int64_t i) { return (i >= 0 && i < n) || (i >= cmin && i <= cmax && ref[(size_t)(i - cmin)]); };
+    struct Merged {
+        int id;
+        std::vector<int> pad0, pad1;  // offsets row 2t / 2t+1 loads without using
+    };
+    // Canonical slots: when the matrix has few distinct offsets overall, every
+    // pair pattern lists all of them in one global order (unused slots load
+    // x[r..r+1], flags 0), so the lanes of a wave load the same offset in
+    // the same slot even across pattern changes (fewer cache lines per load).
+    std::vector<int> U;
+    for (size_t e = 1; e < pdelta.size(); ++e) U.push_back(pdelta[e]);
+    std::sort(U.begin(), U.end());
+    U.erase(std::unique(U.begin(), U.end()), U.end());
+    const bool canonical = !U.empty() && (int)U.size() <= 8;
+    *pcanon = canonical;
+    for (size_t k = 0; canonical && k < U.size(); ++k) slots[k] = U[k];
+    std::unordered_map<uint32_t, Merged> seen;
+    const int64_t npairs = (n + 1) / 2;
+    ppat.assign(npairs, (uint16_t)kPairSplit);
+    ppinfo.clear();
+    ppoff.clear();
+    ppval.clear();
+    int mx = 0;
+    for (int64_t t = 0; t < npairs; ++t) {
+        const int64_t r = 2 * t;
+        if (r + 1 >= n) break;  // lone last row: split
+        const int p0 = pat[r], p1 = pat[r + 1];
+        const uint32_t key = ((uint32_t)p0 << 16) | (uint32_t)p1;
+        auto it = seen.find(key);
+        if (it == seen.end()) {
+            const int2 a = pinfo[p0], b = pinfo[p1];
+            std::vector<int> O;
+            for (int e = 0; e < a.y; ++e) O.push_back(pdelta[a.x + e]);
+            for (int e = 0; e < b.y; ++e) O.push_back(pdelta[b.x + e]);
+            std::sort(O.begin(), O.end());
+            O.erase(std::unique(O.begin(), O.end()), O.end());
+            if (canonical) O = U;
+            if ((int)O.size() > kMaxPairLen || (int)ppinfo.size() >= kPairSplit) return false;
+            Merged mg;
+            mg.id = (int)ppinfo.size();
+            ppinfo.push_back(make_int2((int)ppoff.size(), (int)O.size()));
+            for (int o : O) {
+                if (o >= (1 << 28) || o <= -(1 << 28)) return false;
+                int f = 0;
+                double v0 = 0.0, v1 = 0.0;
+                for (int e = 0; e < a.y; ++e)
+                    if (pdelta[a.x + e] == o) {
+                        f |= 1;
+                        v0 = pval[a.x + e];
+                    }
+                for (int e = 0; e < b.y; ++e)
+                    if (pdelta[b.x + e] == o) {
+                        f |= 2;
+                        v1 = pval[b.x + e];
+                    }
+                if (f == 0) {  // canonical slot unused by both rows: load x[r..r+1]
+                    ppoff.push_back(0);
+                    ppval.push_back(0.0);
+                    ppval.push_back(0.0);
+                    continue;
+                }
+                if (!(f & 1)) mg.pad0.push_back(o);
+                if (!(f & 2)) mg.pad1.push_back(o);
+                ppoff.push_back(o * 4 + f);
+                ppval.push_back(v0);
+                ppval.push_back(v1);
+            }
+            mx = std::max(mx, (int)O.size());
+            it = seen.emplace(key, std::move(mg)).first;
+        }
+        bool ok = true;
+        for (int o : it->second.pad0) ok = ok && valid(r + o);
+        for (int o : it->second.pad1) ok = ok && valid(r + 1 + o);
+        if (ok) ppat[t] = (uint16_t)it->second.id;
+    }
+    *pmaxlen = mx;
+    return !ppinfo.empty();
+}
+
 // Upload a local matrix.  col: local column ids relative to the local origin
 // (negative ids address the left halo); lpad / rext: halo extent on either
 // side of the local rows in every vector column.
@@ -240,6 +344,29 @@ int upload_matrix(cal_ctx* c, int64_t n_local, int64_t n_global, int64_t row0, i
             CAL_HIP(c, hipMemcpy(A.pinfo, pinfo.data(), pinfo.size() * sizeof(int2), hipMemcpyHostToDevice));
             CAL_HIP(c, hipMemcpy(A.pdelta, pdelta.data(), pdelta.size() * sizeof(int), hipMemcpyHostToDevice));
             CAL_HIP(c, hipMemcpy(A.pval, pval.data(), pval.size() * sizeof(double), hipMemcpyHostToDevice));
+            std::vector<uint16_t> ppat;
+            std::vector<int2> ppinfo;
+            std::vector<int> ppoff;
+            std::vector<double> ppval;
+            int pmx = 0;
+            bool canon = false;
+            if (build_pair_patterns(n_local, pat, pinfo, pdelta, pval, col, ppat, ppinfo, ppoff, ppval, &pmx, &canon,
+                                    A.pslot)) {
+                A.use_pair = true;
+                A.nppat = (int)ppinfo.size();
+                A.npent = (int)ppoff.size();
+                A.pmaxlen = pmx <= 8 ? std::max(pmx, 1) : 16;
+                A.pcanon = canon && A.pmaxlen == pmx;
+                A.npsplit = std::count(ppat.begin(), ppat.end(), (uint16_t)kPairSplit);
+                CAL_HIP(c, hipMalloc((void**)&A.ppat, ppat.size() * sizeof(uint16_t)));
+                CAL_HIP(c, hipMalloc((void**)&A.ppinfo, ppinfo.size() * sizeof(int2)));
+                CAL_HIP(c, hipMalloc((void**)&A.ppoff, ppoff.size() * sizeof(int)));
+                CAL_HIP(c, hipMalloc((void**)&A.ppval, ppval.size() * sizeof(double)));
+                CAL_HIP(c, hipMemcpy(A.ppat, ppat.data(), ppat.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+                CAL_HIP(c, hipMemcpy(A.ppinfo, ppinfo.data(), ppinfo.size() * sizeof(int2), hipMemcpyHostToDevice));
+                CAL_HIP(c, hipMemcpy(A.ppoff, ppoff.data(), ppoff.size() * sizeof(int), hipMemcpyHostToDevice));
+                CAL_HIP(c, hipMemcpy(A.ppval, ppval.data(), ppval.size() * sizeof(double), hipMemcpyHostToDevice));
+            }
         } else if (c->spmv_format == 2) {
             return set_error(c, CAL_ERR_UNSUPPORTED, "row-pattern format requested but the matrix has too many "
                                                      "distinct rows (or rows longer than 32)");
@@ -287,6 +414,17 @@ int spmv_dev(cal_ctx* c, const double* x, double* y, int mode, double shift, dou
         p.maxlen = c->A.maxlen;
         p.npat = c->A.npat;
         p.nent = c->A.nent;
+        p.ppat = c->A.use_pair ? c->A.ppat : nullptr;
+        p.ppinfo = c->A.ppinfo;
+        p.ppoff = c->A.ppoff;
+        p.ppval = c->A.ppval;
+        p.nppat = c->A.nppat;
+        p.npent = c->A.npent;
+        p.pmaxlen = c->A.pmaxlen;
+        p.pcanon = c->A.pcanon ? 1 : 0;
+        for (int k = 0; k < 8; ++k) p.pslot[k] = c->A.pslot[k];
+        p.xlo = -c->A.lpad;
+        p.xhi = c->A.ld - c->A.lpad;
         const int t = timer_begin(c, 0);
         CAL_HIP(c, launch_spmv_pat(p, c->stream));
         timer_end(c, t);
@@ -462,6 +600,15 @@ int cal_set_orth_coef(cal_ctx* c, const char* where) {
     if (!strcmp(where, "device")) c->orth_coef_device = true;
     else if (!strcmp(where, "host")) c->orth_coef_device = false;
     else return set_error(c, CAL_ERR_ARG, "orth coefficients: \"device\" or \"host\"");
+    return 0;
+}
+
+int cal_spmv_pair_info(cal_ctx* c, int* npairpatterns, int* nentries, int64_t* nsplit) {
+    if (!c) return CAL_ERR_ARG;
+    if (!c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
+    if (npairpatterns) *npairpatterns = c->A.use_pair ? c->A.nppat : 0;
+    if (nentries) *nentries = c->A.use_pair ? c->A.npent : 0;
+    if (nsplit) *nsplit = c->A.use_pair ? c->A.npsplit : 0;
     return 0;
 }
 

@@ -76,6 +76,9 @@ int cal_matrix_info(cal_ctx* ctx, int64_t* n_local, int64_t* nnz_local, int64_t*
  * results (same per-row summation order). */
 int cal_set_spmv_format(cal_ctx* ctx, const char* fmt);
 int cal_spmv_format(cal_ctx* ctx, int* is_pattern, int* npatterns, int* nentries);
+/* Pair patterns of the row-pattern format (two rows per lane): number of
+ * merged pair patterns, their table entries, and pairs on the per-row path. */
+int cal_spmv_pair_info(cal_ctx* ctx, int* npairpatterns, int* nentries, int64_t* nsplit);
 /* Where the s x s algebra between the block-orthogonalisation sweeps runs:
  * "device" (default: one kernel, no host round trip inside a block) or
  * "host".  Both give bit-identical results; "host" exists for testing. */

@@ -65,6 +65,43 @@ def test_spmv_both_formats_bitexact(cal, ref, fmt, kind, N):
     ctx.close()
 
 
+@pytest.mark.parametrize("n", [401, 4000])
+def test_spmv_pattern_pairs_irregular(cal, ref, n):
+    """Row-pattern SpMV on a small-integer-valued irregular matrix (<= 8 per
+    row, empty rows, odd n): pair patterns with merged entries and split
+    pairs; non-finite values outside the rows' own entries must not leak."""
+    import scipy.sparse as sp
+    rng = np.random.RandomState(n)
+    rows, cols = [], []
+    for r in range(n):
+        k = rng.randint(0, 5)
+        for c in rng.randint(max(0, r - 40), min(n, r + 40), size=k):
+            rows += [r, c]
+            cols += [c, r]
+    vals = rng.randint(-3, 4, size=len(rows)).astype(float)
+    A = sp.csr_matrix((vals, (rows, cols)), shape=(n, n))
+    A.sum_duplicates()
+    A.data[A.data == 0] = 1.0
+    A.sort_indices()
+    if A.getnnz(axis=1).max() > 8:
+        keep = A.getnnz(axis=1) <= 8
+        A = sp.diags(keep.astype(float)) @ A @ sp.diags(keep.astype(float))
+        A = A.tocsr()
+        A.eliminate_zeros()
+        A.sort_indices()
+    ctx = cal.Context(spmv_format="pattern").set_matrix(A)
+    assert ctx.spmv_format()[0] == "pattern"
+    v = rng.randn(n)
+    assert np.array_equal(ctx.spmv(v), ref.SpMV(A, v))
+    # an inf in x only reaches the rows that reference it
+    v[7] = np.inf
+    got, exp = ctx.spmv(v), ref.SpMV(A, v)
+    assert np.array_equal(np.isnan(got), np.isnan(exp))
+    fin = np.isfinite(exp)
+    assert np.array_equal(got[fin], exp[fin])
+    ctx.close()
+
+
 def test_pattern_format_falls_back_to_csr(cal):
     import scipy.sparse as sp
     A = sp.random(500, 500, density=0.1, random_state=np.random.RandomState(0), format="csr")

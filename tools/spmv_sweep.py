@@ -36,8 +36,9 @@ def main():
     ctx.bench_spmv(a.reps, a.shift)  # warm (clocks, caches)
     mean, mn = ctx.bench_spmv(a.reps, a.shift)
     fmt = ctx.spmv_format()[0]
+    pairs = ctx.spmv_pair_info()
     b = 18 * n if fmt == "pattern" else 12 * nnz + 20 * n + 4
-    print(json.dumps({"workload": a.workload, "format": fmt, "env_rows": os.environ.get("CAL_PAT_ROWS"), "env_sweep": os.environ.get("CAL_PAT_SWEEP"),
+    print(json.dumps({"workload": a.workload, "format": fmt, "env": {k: v for k, v in os.environ.items() if k.startswith("CAL_")}, "pairs": pairs,
                       "mean_us": mean * 1e3, "min_us": mn * 1e3, "gbps_mean": b / (mean * 1e-3) / 1e9,
                       "csr_equiv_gbps": (12 * nnz + 20 * n + 4) / (mean * 1e-3) / 1e9}), flush=True)
 

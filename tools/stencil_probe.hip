@@ -91,6 +91,87 @@ __global__ void k_gen7x(const double* __restrict__ x, double* __restrict__ y, co
     }
 }
 
+// 2 rows per lane (r even), every offset one 16-B load (8-B aligned when the
+// offset is odd), XCD-contiguous block order
+template <bool XCD>
+__global__ void k_gen7_pair(const double* __restrict__ x, double* __restrict__ y, int64_t n, Offs off) {
+    int b = blockIdx.x;
+    if (XCD) {
+        const int G = gridDim.x, q = G >> 3, rm = G & 7, xi = b & 7, i = b >> 3;
+        b = (xi < rm ? xi * (q + 1) : rm * (q + 1) + (xi - rm) * q) + i;
+    }
+    const int64_t r = 2 * ((int64_t)b * 256 + threadIdx.x);
+    if (r + 1 >= n) return;
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int e = 0; e < 7; ++e) {
+        const double* p = x + r + off.d[e];
+        double2 v;
+        __builtin_memcpy(&v, p, 16);
+        s0 += v.x;
+        s1 += v.y;
+    }
+    double2 o;
+    o.x = s0;
+    o.y = s1;
+    *reinterpret_cast<double2*>(y + r) = o;
+}
+
+// pair kernel with the table machinery of k_spmv_pair: per-pair uint16 id,
+// LDS (offset code, value pair) table, MODE-1 centre load; ID: load ids,
+// TAB: offsets/values from the LDS table (else from kernel args)
+template <bool ID, bool TAB, bool CENTER, bool GFILL = false>
+__global__ __launch_bounds__(256) void k_pairtab(const double* __restrict__ x, double* __restrict__ y,
+                                                 const uint16_t* __restrict__ ids, int64_t n, Offs off,
+                                                 const int* __restrict__ gtab_off = nullptr,
+                                                 const double2* __restrict__ gtab_v = nullptr) {
+    __shared__ int s_off[256];
+    __shared__ double2 s_v[256];
+    if (GFILL) {  // stage a 256-entry table (4.6 KB) from global memory, as k_spmv_pair does
+        s_off[threadIdx.x] = gtab_off[threadIdx.x];
+        s_v[threadIdx.x] = gtab_v[threadIdx.x];
+    } else if (threadIdx.x < 7) {
+        s_off[threadIdx.x] = (int)off.d[threadIdx.x] * 4 + 3;
+        s_v[threadIdx.x] = make_double2(threadIdx.x == 3 ? 6.0 : -1.0, threadIdx.x == 3 ? 6.0 : -1.0);
+    }
+    __syncthreads();
+    const int G = gridDim.x, q = G >> 3, rm = G & 7, xi = blockIdx.x & 7, i = blockIdx.x >> 3;
+    const int b = (xi < rm ? xi * (q + 1) : rm * (q + 1) + (xi - rm) * q) + i;
+    const int64_t t = (int64_t)b * 256 + threadIdx.x;
+    const int64_t r = 2 * t;
+    if (r + 1 >= n) return;
+    int base = 0;
+    if (ID) base = ids[t];  // 0
+    double y0 = 0.0, y1 = 0.0;
+    int code[7];
+    double2 xv[7];
+#pragma unroll
+    for (int e = 0; e < 7; ++e) {
+        code[e] = TAB ? s_off[base + e] : (int)off.d[e] * 4 + 3;
+        double2 v;
+        __builtin_memcpy(&v, x + r + (code[e] >> 2), 16);
+        xv[e] = v;
+    }
+#pragma unroll
+    for (int e = 0; e < 7; ++e) {
+        const double2 v = TAB ? s_v[base + e] : make_double2(-1.0, -1.0);
+        const double t0 = v.x * xv[e].x, t1 = v.y * xv[e].y;
+        const double a0 = y0 + t0, a1 = y1 + t1;
+        y0 = (code[e] & 1) ? a0 : y0;
+        y1 = (code[e] & 2) ? a1 : y1;
+    }
+    if (CENTER) {
+        double2 c;
+        __builtin_memcpy(&c, x + r, 16);
+        y0 -= 0.5 * c.x;
+        y1 -= 0.5 * c.y;
+    }
+    double2 o;
+    o.x = y0;
+    o.y = y1;
+    *reinterpret_cast<double2*>(y + r) = o;
+}
+
 int main() {
     const int N = 215;
     const int64_t n = (int64_t)N * N * N, P = (int64_t)N * N;
@@ -152,6 +233,29 @@ int main() {
         const int64_t o7[7] = {-P, -N, -1, 0, 1, N, P};
         for (int e = 0; e < 7; ++e) off.d[e] = o7[e];
         const int nch = g1;
+        time("7pt pair 16B", 16.0 * n, [&] { hipLaunchKernelGGL((k_gen7_pair<false>), dim3(g2), dim3(256), 0, 0, x, y, n, off); });
+        time("7pt pair 16B xcd", 16.0 * n, [&] { hipLaunchKernelGGL((k_gen7_pair<true>), dim3(g2), dim3(256), 0, 0, x, y, n, off); });
+        time("pairtab none", 16.0 * n, [&] { hipLaunchKernelGGL((k_pairtab<false, false, false>), dim3(g2), dim3(256), 0, 0, x, y, id, n, off); });
+        time("pairtab center", 16.0 * n, [&] { hipLaunchKernelGGL((k_pairtab<false, false, true>), dim3(g2), dim3(256), 0, 0, x, y, id, n, off); });
+        time("pairtab ids", 17.0 * n, [&] { hipLaunchKernelGGL((k_pairtab<true, false, false>), dim3(g2), dim3(256), 0, 0, x, y, id, n, off); });
+        time("pairtab lds", 16.0 * n, [&] { hipLaunchKernelGGL((k_pairtab<false, true, false>), dim3(g2), dim3(256), 0, 0, x, y, id, n, off); });
+        time("pairtab ids+lds", 17.0 * n, [&] { hipLaunchKernelGGL((k_pairtab<true, true, false>), dim3(g2), dim3(256), 0, 0, x, y, id, n, off); });
+        time("pairtab ids+lds+center", 17.0 * n, [&] { hipLaunchKernelGGL((k_pairtab<true, true, true>), dim3(g2), dim3(256), 0, 0, x, y, id, n, off); });
+        {
+            std::vector<int> ho(256, 0);
+            std::vector<double2> hv(256, make_double2(0.0, 0.0));
+            for (int e = 0; e < 7; ++e) {
+                ho[e] = (int)o7[e] * 4 + 3;
+                hv[e] = make_double2(e == 3 ? 6.0 : -1.0, e == 3 ? 6.0 : -1.0);
+            }
+            int* go;
+            double2* gv;
+            CK(hipMalloc(&go, 256 * 4));
+            CK(hipMalloc(&gv, 256 * 16));
+            CK(hipMemcpy(go, ho.data(), 256 * 4, hipMemcpyHostToDevice));
+            CK(hipMemcpy(gv, hv.data(), 256 * 16, hipMemcpyHostToDevice));
+            time("pairtab ids+lds+center gfill", 17.0 * n, [&] { hipLaunchKernelGGL((k_pairtab<true, true, true, true>), dim3(g2), dim3(256), 0, 0, x, y, id, n, off, go, gv); });
+        }
         time("7pt xcd + ids", 18.0 * n, [&] { hipLaunchKernelGGL((k_gen7x<true, false>), dim3(g1), dim3(256), 0, 0, x, y, id, n, off, nch); });
         time("7pt xcd persistent 2048", 16.0 * n, [&] { hipLaunchKernelGGL((k_gen7x<false, true>), dim3(2048), dim3(256), 0, 0, x, y, id, n, off, nch); });
         time("7pt xcd persistent 2048 + ids", 18.0 * n, [&] { hipLaunchKernelGGL((k_gen7x<true, true>), dim3(2048), dim3(256), 0, 0, x, y, id, n, off, nch); });
