@@ -176,7 +176,7 @@ static int tilegram_host(cal_ctx* c, int64_t n, const Panel& T, const double* E,
     for (int cc = 0; cc < 16; ++cc) cl.p[cc] = panel_slice(T, cc < nt ? cc : nt - 1, 1).ptr[0];
     cl.p[16] = E ? E : cl.p[0];
     int64_t blocks = (n + 255) / 256;
-    blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, 768));
+    blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, kRowGramBlocks));
     CAL_TRY(ensure_partial(c, (size_t)blocks * 272));
     const int t = timer_begin(c, 1);
     CAL_HIP(c, launch_rowgram(cl, nt, E != nullptr, n, (int)blocks, c->d_partial, c->stream));
@@ -221,7 +221,7 @@ static int rowapply_host(cal_ctx* c, int64_t n, const Panel& P, const double* M,
         ol.p[j] = s1.ptr[0];
     }
     int64_t blocks = (n + 255) / 256;  // without the Gram: one row per thread
-    if (gram) blocks = std::min<int64_t>(blocks, 768);
+    if (gram) blocks = std::min<int64_t>(blocks, kRowGramBlocks);
     blocks = std::max<int64_t>(1, blocks);
     if (gram) CAL_TRY(ensure_partial(c, (size_t)blocks * 272));
     const int t = timer_begin(c, kind == 2 ? 1 : 2);  // Gram-only sweeps count as "gram"
@@ -401,7 +401,7 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
     double* d_st = c->d_red + 1024;
     double* d_mbuf = c->d_red + 2048;
     double* d_out = c->d_red + 3072;
-    int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 768));
+    int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, kRowGramBlocks));
     CAL_TRY(ensure_partial(c, (size_t)blocks * 272));
     // P1: [Qp(0:nq) | X]' X (+ Qp column 8 as the extra column)
     ColList ct{};

@@ -191,6 +191,9 @@ hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, co
 // the P1 Gram, phase 1 after pass A); see kernels.hip k_orth_coef.
 hipError_t launch_orth_coef(int phase, const double* tile, double* st, double* mbuf, double* out, int w, int m,
                             int WP, int MO, int doreorth, hipStream_t stream);
+// Grid of the row-parallel Gram sweeps (k_rowapply with GRAM): 4 blocks of
+// 38 KB LDS per CU on 256 CUs.
+constexpr int kRowGramBlocks = 1024;
 hipError_t launch_rowgram(const ColList& P, int nt, bool has_extra, int64_t n, int blocks, double* partial,
                           hipStream_t st);
 hipError_t launch_dot(const double* x, const double* y, int64_t n, double* partial, int blocks,

@@ -873,14 +873,24 @@ hipError_t launch_tilegram(const Panel& T, const double* E, int64_t n, int block
 // CHAIN: Y2 = [P(0:wq) | Y] * M2 with Y = P * M1 recomputed bit-identically
 // in registers (pass B of two_pass without a stored intermediate block);
 // M = [M1 (WPMAX x MOUT) | M2p (WPMAX x MOUT, rows >= wq zero) | M2y (MOUT x MOUT)].
+// LDS hand-off inside one wave: the wave's LDS operations retire in order;
+// the fences keep the compiler from moving LDS accesses across.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int WPMAX, int MOUT, bool GRAM, bool APPLY = true, bool STORE = true, bool CHAIN = false>
-__global__ __launch_bounds__(256, 2) void k_rowapply(ColList P, const double* __restrict__ M, int wp, int m,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_rowapply(ColList P, const double* __restrict__ M, int wp, int m,
                                                   OutList Y, int wq, int64_t n, double* __restrict__ partial) {
     constexpr int TLD = 17;  // padded LDS row (doubles)
     constexpr int MSZ = WPMAX * MOUT * (CHAIN ? 2 : 1) + (CHAIN ? MOUT * MOUT : 0);
+    // tile: 256 rows x 16 Gram columns, the pad column 16 holds the extra
+    // column; after the row loop the same LDS holds the cross-wave partials
+    // (38 KB per block -> 4 blocks per CU)
     __shared__ double tile[GRAM ? 256 * TLD : 1];
-    __shared__ double ext[GRAM ? 256 : 1];
-    __shared__ double red[GRAM ? 3 * 64 * 5 : 1];
+    double* const red = tile;
     __shared__ __attribute__((aligned(16))) double Ms[MSZ];  // broadcast reads
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int c16 = lane & 15, g = lane >> 4;
@@ -899,18 +909,26 @@ __global__ __launch_bounds__(256, 2) void k_rowapply(ColList P, const double* __
     // without the Gram one row per thread and no loop (nothing for the
     // compiler to hoist the M broadcasts out of); with it a grid-stride loop
     // whose LDS reads are pinned inside the iteration by a compiler barrier.
+    // Gram kinds: each wave transposes only its own 64 rows through the tile,
+    // so wave-level syncs suffice, and the next iteration's rows are loaded
+    // before this iteration's MFMA phase.
     const int64_t stride = GRAM ? (int64_t)gridDim.x * 256 : n;
+    double pn[WPMAX];
+    auto load_rows = [&](int64_t b, double* dst) {
+        const int64_t r = b + tid;
+        const int64_t rr = r < n ? r : n - 1;
+#pragma unroll
+        for (int c = 0; c < WPMAX; ++c) dst[c] = pc[c][rr];
+    };
+    load_rows((int64_t)blockIdx.x * 256, pn);
     for (int64_t base = (int64_t)blockIdx.x * 256; base < n; base += stride) {
         asm volatile("" ::: "memory");
         const int64_t r = base + tid;
         const bool in = r < n;
-        const int64_t rr = in ? r : n - 1;
         double p[WPMAX];
 #pragma unroll
-        for (int c = 0; c < WPMAX; ++c) {
-            const double v = pc[c][rr];
-            p[c] = in ? v : 0.0;
-        }
+        for (int c = 0; c < WPMAX; ++c) p[c] = in ? pn[c] : 0.0;
+        if (GRAM && base + stride < n) load_rows(base + stride, pn);
         double y[MOUT];
 #pragma unroll
         for (int j = 0; j < MOUT; ++j) y[j] = 0.0;
@@ -972,24 +990,25 @@ __global__ __launch_bounds__(256, 2) void k_rowapply(ColList P, const double* __
 #pragma unroll
                 for (int j = 0; j < MOUT; ++j)
                     if (j < m) trow[nq + j] = y[j];
-                ext[tid] = has_ext ? p[8 < WPMAX ? 8 : 0] : 0.0;
+                trow[16] = has_ext ? p[8 < WPMAX ? 8 : 0] : 0.0;
             } else {  // Gram only: tile = P columns 0..m-1, extra = column 16
 #pragma unroll
                 for (int c = 0; c < 16; ++c)
                     if (c < m) trow[c] = p[c < WPMAX ? c : 0];
-                ext[tid] = wq > 0 ? p[16 < WPMAX ? 16 : 0] : 0.0;
+                trow[16] = wq > 0 ? p[16 < WPMAX ? 16 : 0] : 0.0;
             }
-            __syncthreads();
+            wave_lds_sync();
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 const int row = wave * 64 + 4 * k + g;
                 const double a = tile[row * TLD + c16];
                 acc = mfma64(a, a, acc);
-                eacc = eacc + ext[row] * a;
+                eacc = eacc + tile[row * TLD + 16] * a;
             }
-            __syncthreads();
+            wave_lds_sync();
         }
     }
+    if (GRAM) __syncthreads();  // the partials below reuse the tile across waves
     if (GRAM) {
         if (wave > 0) {
 #pragma unroll

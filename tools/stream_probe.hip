@@ -1,0 +1,95 @@
+// Probe: streaming tall-skinny apply / Gram-read rates on this GPU
+// (n = 215^3 rows, 17 input columns, 8 output columns), 8-B vs 16-B lanes.
+// Not part of the library.  hipcc -O3 --offload-arch=gfx950 tools/stream_probe.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
+
+struct Cols { const double* p[17]; };
+struct OCols { double* p[8]; };
+__constant__ double cM[17 * 8];
+
+template <bool STORE>
+__global__ __launch_bounds__(256) void k_apply1(Cols P, OCols Y, int64_t n) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= n) return;
+    double y[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < 17; ++c) {
+        const double v = P.p[c][r];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = __builtin_fma(v, cM[c * 8 + j], y[j]);
+    }
+    if (STORE) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Y.p[j][r] = y[j];
+    } else {
+        double s = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += y[j];
+        if (s == 123.456) Y.p[0][r] = s;
+    }
+}
+template <bool STORE>
+__global__ __launch_bounds__(256) void k_apply2(Cols P, OCols Y, int64_t n) {
+    const int64_t r = 2 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
+    if (r + 1 >= n) return;
+    double y0[8] = {0, 0, 0, 0, 0, 0, 0, 0}, y1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < 17; ++c) {
+        const double2 v = *reinterpret_cast<const double2*>(P.p[c] + r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            y0[j] = __builtin_fma(v.x, cM[c * 8 + j], y0[j]);
+            y1[j] = __builtin_fma(v.y, cM[c * 8 + j], y1[j]);
+        }
+    }
+    if (STORE) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) *reinterpret_cast<double2*>(Y.p[j] + r) = make_double2(y0[j], y1[j]);
+    } else {
+        double s = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += y0[j] + y1[j];
+        if (s == 123.456) Y.p[0][r] = s;
+    }
+}
+
+int main() {
+    const int64_t n = 215LL * 215 * 215, ld = (n + 63) / 64 * 64;
+    double* buf;
+    CK(hipMalloc(&buf, 25 * ld * 8));
+    CK(hipMemset(buf, 0, 25 * ld * 8));
+    Cols P;
+    OCols Y;
+    for (int c = 0; c < 17; ++c) P.p[c] = buf + c * ld;
+    for (int j = 0; j < 8; ++j) Y.p[j] = buf + (17 + j) * ld;
+    double hM[17 * 8];
+    for (int i = 0; i < 17 * 8; ++i) hM[i] = 0.01 * i;
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(cM), hM, sizeof(hM)));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    auto time = [&](const char* name, double bytes, auto launch) {
+        for (int i = 0; i < 3; ++i) launch();
+        CK(hipEventRecord(a));
+        const int reps = 20;
+        for (int i = 0; i < reps; ++i) launch();
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        const double us = ms * 1e3 / reps;
+        printf("{\"kernel\": \"%s\", \"us\": %.1f, \"GBps\": %.0f}\n", name, us, bytes / (us * 1e-6) / 1e9);
+        return 0;
+    };
+    const int g1 = (int)((n + 255) / 256), g2 = (int)((n / 2 + 255) / 256);
+    time("apply 17->8 store, 8B/lane", 25.0 * 8 * n, [&] { hipLaunchKernelGGL(k_apply1<true>, dim3(g1), dim3(256), 0, 0, P, Y, n); });
+    time("apply 17->8 store, 16B/lane", 25.0 * 8 * n, [&] { hipLaunchKernelGGL(k_apply2<true>, dim3(g2), dim3(256), 0, 0, P, Y, n); });
+    time("read 17, 8B/lane", 17.0 * 8 * n, [&] { hipLaunchKernelGGL(k_apply1<false>, dim3(g1), dim3(256), 0, 0, P, Y, n); });
+    time("read 17, 16B/lane", 17.0 * 8 * n, [&] { hipLaunchKernelGGL(k_apply2<false>, dim3(g2), dim3(256), 0, 0, P, Y, n); });
+    CK(hipDeviceSynchronize());
+    return 0;
+}
