@@ -95,3 +95,31 @@ def test_two_ranks_one_gpu_match_single(cal, ref, case):
         big = single.ritz_rnorm[:, 0] > 1e-10
         assert np.all(np.abs(np.log(rn[big, 0] / single.ritz_rnorm[big, 0])) < np.log(1.5))
     assert np.array_equal(res[0][3], res[1][3])
+
+
+def test_rccl_single_rank_matches_local(cal, ref):
+    """The RCCL communicator itself (ncclCommInitRank, in-place ncclAllReduce
+    of the Gram tiles on the context stream, the distributed matrix setup)
+    with one rank: bit-identical to the communicator-free run.  Several ranks
+    per GPU are refused by RCCL, so this is the RCCL coverage a one-GPU box
+    allows; the multi-rank logic is covered above through the host-staged
+    communicator, which differs only in the transport."""
+    import ctypes
+    from ca_lanczos_amd._lib import lib
+    A = cal.matrices.laplacian_3d(14)
+    n = A.shape[0]
+    r = ref.matlab_rand(n, seed=8)
+    uid = ctypes.create_string_buffer(128)
+    assert lib.cal_comm_unique_id(uid) == 0
+    c1 = cal.Context(0)
+    c1.comm_init_rccl(1, 0, uid.raw)
+    c1.set_matrix_slab(n, 0, A)
+    assert c1.matrix_info()["nghost"] == 0
+    out1 = cal.ca_lanczos_ex(A, r, 8, 40, "newton", "local", diagnostics=True, ctx=c1)
+    c2 = cal.Context(0).set_matrix(A)
+    out2 = cal.ca_lanczos_ex(A, r, 8, 40, "newton", "local", diagnostics=True, ctx=c2)
+    assert np.array_equal(out1.T, out2.T)
+    assert np.array_equal(out1.Q, out2.Q)
+    assert np.array_equal(out1.ritz_rnorm, out2.ritz_rnorm)
+    c1.close()
+    c2.close()
