@@ -438,8 +438,14 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
     }
     double* h_out = c->h_red + 3072;
     CAL_HIP(c, hipMemcpyAsync(h_out, d_out, 516 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    CAL_HIP(c, hipStreamSynchronize(c->stream));
-    c->small_pending = false;
+    if (!c->orth_event) CAL_HIP(c, hipEventCreateWithFlags(&c->orth_event, hipEventDisableTiming));
+    CAL_HIP(c, hipEventRecord(c->orth_event, c->stream));
+    if (c->pre_wait) {  // e.g. the next step's matrix powers (lanczos_step)
+        auto hook = std::move(c->pre_wait);
+        c->pre_wait = nullptr;
+        CAL_TRY(hook());
+    }
+    CAL_HIP(c, hipEventSynchronize(c->orth_event));
     if (h_out[512] != 0.0 || h_out[513] != 0.0) return 1;
     std::copy(h_out, h_out + (size_t)m * m, R);
     std::copy(h_out + 256, h_out + 256 + (size_t)w * m, Rq);
@@ -460,6 +466,7 @@ int normalize_dev(cal_ctx* c, int64_t n, const Panel& X, const PanelOut& Qout, d
             if (rank) *rank = rank_from_R(m, R, tol);
             return 0;
         }
+        c->orth_redone = true;
     }
     std::vector<double> G((size_t)m * m), Mz((size_t)m * m, 0.0), Ctot;
     if (X.nseg <= kMaxSeg) {
@@ -495,6 +502,7 @@ int project_and_normalize_dev(cal_ctx* c, int64_t n, const Panel& Qp, const Pane
             }
             return 0;
         }
+        c->orth_redone = true;
     }
     const Panel W = panel_concat(Qp, X);
     const int wp = w + m;

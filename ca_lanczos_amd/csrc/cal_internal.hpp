@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -248,6 +249,11 @@ struct cal_ctx {
 
     int spmv_format = 0;  // 0 auto, 1 CSR, 2 row-pattern (applies at the next set_matrix)
     bool orth_coef_device = true;  // block-orth s x s algebra on the device (blockorth.cpp)
+    // set by lanczos_step: work to enqueue after a block orthogonalisation is
+    // enqueued and before the host waits for its R (orth_device)
+    std::function<int()> pre_wait;
+    bool orth_redone = false;  // the last block was redone on the host path
+    hipEvent_t orth_event = nullptr;
 };
 
 // ---- helpers shared by the host-side translation units -----------------

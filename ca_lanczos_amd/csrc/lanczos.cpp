@@ -31,7 +31,8 @@ struct LanczosState {
     bool newton = false, full = false;
     int64_t n = 0, ld = 0;
     double* dQ = nullptr;  // ld x (s*max_outer + 1)
-    double* dV = nullptr;  // ld x (s+1)
+    double* dV = nullptr;  // ld x 2(s+1): the basis block, double-buffered by step parity
+    bool powers_ready = false;  // matrix powers of step k+1 already enqueued (prefetch)
     std::vector<double> Bk;  // (s+1) x s
     int Tld = 0;
     std::vector<double> T;  // Tld x Tld
@@ -43,7 +44,7 @@ struct LanczosState {
     bool breakdown = false;
     int64_t lpad = 0;  // local origin inside each column (left halo space)
     double* col(int j) { return dQ + (size_t)j * ld + lpad; }
-    double* vcolumn(int j) { return dV + (size_t)j * ld + lpad; }
+    double* vcolumn(int j, int par = 0) { return dV + ((size_t)par * (s + 1) + j) * ld + lpad; }
 };
 
 static double now_ms() {
@@ -62,6 +63,22 @@ static int dot_host(cal_ctx* c, int64_t n, const double* x, const double* y, dou
     CAL_HIP(c, hipStreamSynchronize(c->stream));
     c->small_pending = false;
     *out = c->h_red[0];
+    return 0;
+}
+
+// matrix powers of step k into the V buffer of parity k & 1 (ca_lanczos.m:
+// 110-118); V(:,1) = q is not copied: the panels reference q's column of Q.
+static int enqueue_powers(cal_ctx* c, LanczosState& L, int k) {
+    const int s = L.s;
+    const double* q = L.col((k - 1) * s);
+    for (int i = 0; i < s; ++i) {
+        const double* x = (i == 0) ? q : L.vcolumn(i, k & 1);
+        double* y = L.vcolumn(i + 1, k & 1);
+        if (L.newton)
+            CAL_TRY(spmv_dev(c, x, y, 1, L.Bk[i + (size_t)i * (s + 1)], 0.0, nullptr));
+        else
+            CAL_TRY(spmv_dev(c, x, y, 0, 0.0, 0.0, nullptr));
+    }
     return 0;
 }
 
@@ -297,16 +314,25 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
     L.k += 1;
     const int k = L.k;
     const double* q = L.col((k - 1) * s);  // ca_lanczos.m:171 (k=1: q itself)
-    auto Vc = [&](int j) { return L.vcolumn(j); };
-    // matrix powers (ca_lanczos.m:110-118); V(:,1) = q is not copied: the
-    // panels below reference q's column of Q directly.
-    for (int i = 0; i < s; ++i) {
-        const double* x = (i == 0) ? q : Vc(i);
-        if (L.newton)
-            CAL_TRY(spmv_dev(c, x, Vc(i + 1), 1, L.Bk[i + (size_t)i * (s + 1)], 0.0, nullptr));
-        else
-            CAL_TRY(spmv_dev(c, x, Vc(i + 1), 0, 0.0, 0.0, nullptr));
-    }
+    auto Vc = [&](int j) { return L.vcolumn(j, k & 1); };
+    if (!L.powers_ready) CAL_TRY(enqueue_powers(c, L, k));
+    L.powers_ready = false;
+    // Prefetch: the matrix powers of step k+1 need only Q's last column
+    // (stream-ordered after this step's pass B) and the fixed shifts, so they
+    // are enqueued (into the other V buffer) before the host waits for this
+    // step's R: the GPU runs them while the host extends T and returns.
+    const bool prefetch = !diagnostics && !L.full && k + 1 <= L.max_outer;
+    c->orth_redone = false;
+    if (prefetch)
+        c->pre_wait = [c, &L, k]() {
+            const int st = enqueue_powers(c, L, k + 1);
+            if (st == 0) L.powers_ready = true;
+            return st;
+        };
+    struct ClearHook {
+        cal_ctx* c;
+        ~ClearHook() { c->pre_wait = nullptr; }
+    } clear_hook{c};
     int status = 0;
     if (k == 1) {
         Panel X = panel();
@@ -341,6 +367,8 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
         }
         status = extend_T(c, L, Rq, R);
     }
+    // a block redone on the host path rewrote q after the prefetched powers read it
+    if (c->orth_redone && L.powers_ready) CAL_TRY(enqueue_powers(c, L, k + 1));
     if (status == CAL_WARN_BREAKDOWN) {
         L.info.breakdown = 1;
         return set_error(c, CAL_WARN_BREAKDOWN, "CA-Lanczos breakdown: rho_t = Rk(s,s) = 0");
@@ -395,9 +423,9 @@ int cal_lanczos_begin(cal_ctx* c, const double* r, int s, int max_outer, const c
     L->info.s = s;
     const size_t qcols = (size_t)s * max_outer + 1;
     CAL_HIP(c, hipMalloc((void**)&L->dQ, qcols * L->ld * sizeof(double)));
-    CAL_HIP(c, hipMalloc((void**)&L->dV, (size_t)(s + 1) * L->ld * sizeof(double)));
+    CAL_HIP(c, hipMalloc((void**)&L->dV, (size_t)2 * (s + 1) * L->ld * sizeof(double)));
     CAL_HIP(c, hipMemsetAsync(L->dQ, 0, qcols * L->ld * sizeof(double), c->stream));
-    CAL_HIP(c, hipMemsetAsync(L->dV, 0, (size_t)(s + 1) * L->ld * sizeof(double), c->stream));
+    CAL_HIP(c, hipMemsetAsync(L->dV, 0, (size_t)2 * (s + 1) * L->ld * sizeof(double), c->stream));
     L->Tld = s * max_outer + 1;
     L->T.assign((size_t)L->Tld * L->Tld, 0.0);
     const double t0 = now_ms();

@@ -501,6 +501,7 @@ void cal_destroy(cal_ctx* c) {
         hipEventDestroy(r.b);
     }
     for (auto e : c->event_pool) hipEventDestroy(e);
+    if (c->orth_event) hipEventDestroy(c->orth_event);
     hipStreamDestroy(c->stream);
     delete c;
 }

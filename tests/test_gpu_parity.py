@@ -338,3 +338,17 @@ def test_orth_coef_device_fallback(cal):
     ctx.set_orth_coef("device")
     assert np.array_equal(res[0][0], res[1][0]) and np.array_equal(res[0][1], res[1][1])
     assert res[0][2] == res[1][2]
+
+
+def test_ca_lanczos_prefetch_invariant(cal, ref):
+    """Diagnostics off enables the next step's matrix-powers prefetch (double-
+    buffered V); diagnostics never feed back (ca_lanczos.m:228-236), so T and
+    Q must be bit-identical to the non-prefetching run."""
+    A = cal.matrices.laplacian_2d(40)
+    r = ref.matlab_rand(A.shape[0], seed=21)
+    ctx = cal.Context().set_matrix(A)
+    a = cal.ca_lanczos_ex(A, r, 8, 64, "newton", "local", diagnostics=False, ctx=ctx)
+    b = cal.ca_lanczos_ex(A, r, 8, 64, "newton", "local", diagnostics=True, ctx=ctx)
+    ctx.close()
+    assert np.array_equal(a.T, b.T) and np.array_equal(a.Q, b.Q)
+    assert np.array_equal(a.reorth, b.reorth)
