@@ -219,8 +219,8 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get("workload") == args.workload and tj.get("n_gpus", 1) == world and tj.get("kernel") == dominant:
-                traffic = tj.get("hbm_bytes_per_launch")
+            if tj.get("workload") == args.workload and tj.get("n_gpus", 1) == world:
+                traffic = tj.get("classes", {}).get(dominant)
         except Exception:
             traffic = None
     n_reorth = int(np.sum(flags[W:W + K]))

@@ -1077,71 +1077,8 @@ hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, co
 
 // Row-parallel tile Gram: tile = P.p[0..nt) (nt <= 16), extra = P.p[16] if
 // has_extra.  Same partial layout as k_tilegram.
-// EXPERIMENT (CAL_EXP=1): the stream probe's Gram loop structure
-__global__ __launch_bounds__(256) void k_gram_exp(ColList P, int nt, int has_extra, int64_t n,
-                                                  double* __restrict__ partial) {
-    __shared__ double tile[256 * 17];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, c16 = lane & 15, g = lane >> 4;
-    d4 acc = d4{0.0, 0.0, 0.0, 0.0};
-    double eacc = 0.0;
-    for (int64_t base = (int64_t)blockIdx.x * 256; base < n; base += (int64_t)gridDim.x * 256) {
-        const bool in = base + tid < n;
-        const int64_t r = in ? base + tid : n - 1;
-        double p[17];
-#pragma unroll
-        for (int c = 0; c < 17; ++c) p[c] = P.p[c][r];
-        double* trow = tile + tid * 17;
-#pragma unroll
-        for (int c = 0; c < 16; ++c) trow[c] = (in && c < nt) ? p[c] : 0.0;
-        trow[16] = (in && has_extra) ? p[16] : 0.0;
-        wave_lds_sync();
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int row = wave * 64 + 4 * k + g;
-            const double a = tile[row * 17 + c16];
-            acc = mfma64(a, a, acc);
-            eacc = eacc + tile[row * 17 + 16] * a;
-        }
-        wave_lds_sync();
-    }
-    __syncthreads();
-    double* red = tile;
-    if (wave > 0) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[((wave - 1) * 64 + lane) * 5 + r] = acc[r];
-        red[((wave - 1) * 64 + lane) * 5 + 4] = eacc;
-    }
-    __syncthreads();
-    if (wave == 0) {
-        const int64_t nb = gridDim.x;
-        double* out = partial + blockIdx.x;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            double v = acc[r];
-            v = v + red[(0 * 64 + lane) * 5 + r];
-            v = v + red[(1 * 64 + lane) * 5 + r];
-            v = v + red[(2 * 64 + lane) * 5 + r];
-            out[(int64_t)(c16 * 16 + g + 4 * r) * nb] = v;
-        }
-        double e = eacc;
-        e = e + red[(0 * 64 + lane) * 5 + 4];
-        e = e + red[(1 * 64 + lane) * 5 + 4];
-        e = e + red[(2 * 64 + lane) * 5 + 4];
-        const double e1 = __shfl(e, c16 + 16, 64), e2 = __shfl(e, c16 + 32, 64), e3 = __shfl(e, c16 + 48, 64);
-        if (g == 0) out[(int64_t)(256 + c16) * nb] = ((e + e1) + e2) + e3;
-    }
-}
-
 hipError_t launch_rowgram(const ColList& P, int nt, bool has_extra, int64_t n, int blocks, double* partial,
                           hipStream_t st) {
-    static const int exp_env = [] {
-        const char* e = getenv("CAL_EXP");
-        return e ? atoi(e) : 0;
-    }();
-    if (exp_env == 1) {
-        hipLaunchKernelGGL(k_gram_exp, dim3(blocks), dim3(256), 0, st, P, nt, has_extra ? 1 : 0, n, partial);
-        return hipGetLastError();
-    }
     OutList none{};
     hipLaunchKernelGGL((k_rowapply<17, 4, true, false>), dim3(blocks), dim3(256), 0, st, P, nullptr, 17, nt, none,
                        has_extra ? 1 : 0, n, partial);

@@ -14,13 +14,16 @@ import csv
 import json
 import os
 
-CLASSES = {  # kernel-name prefix -> bench.py kernel class
+CLASSES = {  # kernel-name prefix -> kernel
+    "void cal::k_spmv_pair<1": "spmv",
     "void cal::k_spmv_pat_lds<1": "spmv",
     "void cal::k_spmv<1": "spmv_csr",
     "void cal::k_rowapply<17, 4, true, false": "gram_p1",
     "void cal::k_rowapply<17, 8, true, true, false": "gram_passA",
     "void cal::k_rowapply<17, 8, false, true, true, true": "apply_passB",
 }
+# bench.py kernel classes (kernel_ms_per_step keys): per-launch average over members
+BENCH_CLASSES = {"spmv": ["spmv"], "gram": ["gram_p1", "gram_passA"], "apply": ["apply_passB"]}
 
 
 def per_kernel(path, counter):
@@ -47,8 +50,12 @@ def main():
         f = 2.0 * fetch.get(k, 0.0)
         w = write.get(k, 0.0)
         kernels[k] = {"fetch_bytes_x2": f, "write_bytes": w, "hbm_bytes_per_launch": f + w}
-    out = {"workload": a.workload, "n_gpus": 1, "kernel": "spmv",
-           "hbm_bytes_per_launch": kernels.get("spmv", {}).get("hbm_bytes_per_launch"),
+    classes = {}
+    for cls, members in BENCH_CLASSES.items():
+        vals = [kernels[m]["hbm_bytes_per_launch"] for m in members if m in kernels]
+        if vals:
+            classes[cls] = sum(vals) / len(vals)
+    out = {"workload": a.workload, "n_gpus": 1, "classes": classes,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over bench.py; "
                      "FETCH_SIZE x2 (gfx950 streaming-read correction), KiB x 1024",
            "kernels": kernels}
