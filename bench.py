@@ -15,6 +15,7 @@ blocks (strong scaling, whole-job outer-iters/s).
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -41,6 +42,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-iters", type=int, default=2, help="outer iterations of the CPU sample")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "spmv_traffic.json"))
+    p.add_argument("--comm", default="rccl", choices=["rccl", "host"],
+                   help="N > 1 transport: RCCL (default) or host-staged gloo callbacks (rehearsal of the "
+                        "distributed bench with several ranks on one GPU)")
     return p.parse_args()
 
 
@@ -100,23 +104,45 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo", init_method="env://")
 
-    ctx = cal.Context(device=local)
+    ndev = ctypes.c_int(0)
+    cal._lib.lib.cal_device_count(ctypes.byref(ndev))
+    ctx = cal.Context(device=local % max(ndev.value, 1))
     bounds = slab_bounds(n, world, plane)
     r0, r1 = bounds[rank], bounds[rank + 1]
     rowptr, col, val = build_rows(dim, N, r0, r1)
     nnz_local = int(rowptr[-1])
     r_full = np.random.RandomState(5489).random_sample(n)  # MATLAB rand(n,1), fresh session
-    if world > 1:
+    if world > 1 and args.comm == "host":
+        import torch
+
+        def allreduce(a):
+            t = torch.from_numpy(a)
+            dist.all_reduce(t)
+
+        def exchange(peer, send, recv):
+            reqs = []
+            if send.size:
+                reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(send)), peer))
+            rt = torch.zeros(recv.size, dtype=torch.float64)
+            if recv.size:
+                reqs.append(dist.irecv(rt, peer))
+            for q in reqs:
+                q.wait()
+            if recv.size:
+                recv[:] = rt.numpy()
+
+        ctx.comm_init_host(world, rank, allreduce, exchange)
+    elif world > 1:
         import torch
         uid = bytearray(128)
         if rank == 0:
-            import ctypes
             buf = ctypes.create_string_buffer(128)
             cal._lib.check(None, cal._lib.lib.cal_comm_unique_id(buf))
             uid = bytearray(buf.raw)
         t = torch.tensor(list(uid), dtype=torch.uint8)
         dist.broadcast(t, 0)
         ctx.comm_init_rccl(world, rank, bytes(t.tolist()))
+    if world > 1:
         import scipy.sparse as sp
         Aloc = sp.csr_matrix((val, col, rowptr), shape=(r1 - r0, n))
         ctx.set_matrix_slab(n, r0, Aloc)
@@ -241,7 +267,8 @@ def main():
                 "synthetic (5-pt Dirichlet Laplacian, r = MATLAB rand(n,1) seed 5489)",
         "config": {"workload": "%s: %s %dx..., n=%d, nnz=%d" % (args.workload, "7-pt 3-D" if dim == 3 else "5-pt 2-D",
                                                                 N, n, nnz_total),
-                   "s": s, "basis": args.basis, "orth": args.orth, "parallelism": "row-slab x%d" % world},
+                   "s": s, "basis": args.basis, "orth": args.orth, "parallelism": "row-slab x%d" % world,
+                   "comm": (args.comm if world > 1 else "none")},
         "spmv_format": ("%s (%d row patterns, %d entries; %d pair patterns, %d entries, %d split pairs)"
                         % (fmt, npat, nent, npairpat, npent, nsplit)) if fmt == "pattern" else fmt,
         "spmv_gbps": spmv_gbps,
