@@ -443,7 +443,8 @@ def ca_lanczos_ex(A, r, s, iter, basis, orth="local", diagnostics=True, return_Q
         ritz_rnorm=np.array(rn[:k, :sk]), orth_err=oe[:k].copy(), reorth=fl[:k].copy(), shifts=shifts,
         info=dict(t=k, n_reorth=info.n_reorth, n_rank_deficient=info.n_rank_deficient,
                   breakdown=info.breakdown, prologue_ms=info.prologue_ms, loop_ms=info.loop_ms,
-                  diag_ms=info.diag_ms, status=st))
+                  diag_ms=info.diag_ms, status=st, n_orth_breaks=info.n_orth_breaks,
+                  n_ritz_locked=info.n_ritz_locked, norm_A=info.norm_A))
 
 
 def ca_lanczos(A, r, s, iter, basis, orth="local"):

@@ -185,59 +185,6 @@ int cal_cholqr(cal_ctx* c, int64_t n, int m, const double* X, double* Q, double*
     return download(c, Q, dQ, ld, n, m);
 }
 
-// project.m:7-58 on the device (block MGS across blocks, CGS within).
-static int project_blocks(cal_ctx* c, int64_t n, int64_t ld, int nb, const std::vector<double*>& dQ,
-                          const int* widths, int m, double* dX, bool doreorth, std::vector<std::vector<double>>& R) {
-    Panel X = panel();
-    panel_add(X, dX, ld, m);
-    PanelOut Xo = panel_out(dX, ld, m);
-    auto col_norms = [&](std::vector<double>& nr) -> int {
-        std::vector<double> G((size_t)m * m);
-        CAL_TRY(gram_host(c, n, X, X, G.data()));
-        nr.resize(m);
-        for (int i = 0; i < m; ++i) nr[i] = std::sqrt(G[i + (size_t)i * m]);
-        return 0;
-    };
-    std::vector<double> before;
-    if (doreorth) CAL_TRY(col_norms(before));
-    auto one_pass = [&](bool accumulate) -> int {
-        for (int i = 0; i < nb; ++i) {
-            const int w = widths[i];
-            if (w <= 0) continue;
-            Panel Qi = panel();
-            panel_add(Qi, dQ[i], ld, w);
-            std::vector<double> Ri((size_t)w * m);
-            CAL_TRY(gram_host(c, n, Qi, X, Ri.data()));  // R{i} = Q{i}'*X
-            Panel W = panel();
-            panel_add(W, dQ[i], ld, w);
-            panel_add(W, dX, ld, m);
-            std::vector<double> M((size_t)(w + m) * m, 0.0);
-            for (int j = 0; j < m; ++j) {
-                for (int r = 0; r < w; ++r) M[r + (size_t)j * (w + m)] = -Ri[r + (size_t)j * w];
-                M[w + j + (size_t)j * (w + m)] = 1.0;
-            }
-            CAL_TRY(apply_host(c, n, W, M.data(), m, &Xo, nullptr, 0, nullptr));  // X = X - Q{i}*R{i}
-            if (accumulate)
-                for (size_t e = 0; e < Ri.size(); ++e) R[i][e] += Ri[e];
-            else
-                R[i] = Ri;
-        }
-        return 0;
-    };
-    CAL_TRY(one_pass(false));
-    if (doreorth) {  // project.m:40-57 (note the inverted test of the reference)
-        std::vector<double> after;
-        CAL_TRY(col_norms(after));
-        double mx = NAN;
-        for (int i = 0; i < m; ++i) {
-            const double d = 0.5 * before[i] - after[i];
-            if (!std::isnan(d) && (std::isnan(mx) || d > mx)) mx = d;
-        }
-        if (mx < 0) CAL_TRY(one_pass(true));
-    }
-    return 0;
-}
-
 int cal_project(cal_ctx* c, int64_t n, int nblocks, const double* const* Q, const int* widths, int m, const double* X,
                 int doreorth, double* Xout, double* const* R) {
     CAL_TRY(check_ctx(c, false));
@@ -310,40 +257,11 @@ int cal_project_and_normalize(cal_ctx* c, int64_t n, int nblocks, const double* 
             if (RZ && RZ[i] && widths[i] > 0) std::copy(Rq.begin(), Rq.end(), RZ[i]);
     } else {
         // general restatement (projectAndNormalize.m:3-90) on device panels
-        std::vector<double> before(m);
-        {
-            Panel Xp = panel();
-            panel_add(Xp, dX, ld, m);
-            std::vector<double> G((size_t)m * m);
-            CAL_TRY(gram_host(c, n, Xp, Xp, G.data()));
-            for (int i = 0; i < m; ++i) before[i] = std::sqrt(G[i + (size_t)i * m]);
-        }
-        CAL_HIP(c, hipMemcpyAsync(dY, dX, (size_t)m * ld * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
-        std::vector<std::vector<double>> RY(nblocks);
-        for (int i = 0; i < nblocks; ++i) RY[i].assign((size_t)std::max(widths[i], 0) * m, 0.0);
-        CAL_TRY(project_blocks(c, n, ld, nblocks, dQ, widths, m, dY, false, RY));  // :25
-        Panel Yp = panel();
-        panel_add(Yp, dY, ld, m);
-        bool sh = false;
-        CAL_TRY(normalize_dev(c, n, Yp, panel_out(dZ, ld, m), Rm.data(), 1.0e-8, &rk, &sh));  // :26
-        double mx = NAN;
-        for (int i = 0; i < m; ++i) {
-            double after = 0.0;
-            for (int r = 0; r < m; ++r) after += Rm[r + (size_t)i * m] * Rm[r + (size_t)i * m];
-            after = std::sqrt(after);
-            const double rel = std::fabs(before[i] - after) / before[i];
-            if (!std::isnan(rel) && (std::isnan(mx) || rel > mx)) mx = rel;
-        }
-        std::vector<std::vector<double>> RZv = RY;
-        if (doreorth && mx > 0.5) {  // :52-73
-            re = 1;
-            std::vector<std::vector<double>> R2(nblocks);
-            for (int i = 0; i < nblocks; ++i) R2[i].assign((size_t)std::max(widths[i], 0) * m, 0.0);
-            CAL_TRY(project_blocks(c, n, ld, nblocks, dQ, widths, m, dY, false, R2));  // Z in place of Y
-            CAL_TRY(normalize_dev(c, n, Yp, panel_out(dZ, ld, m), Rm.data(), 1.0e-8, &rk, &sh));
-            for (int i = 0; i < nblocks; ++i)
-                for (size_t e = 0; e < R2[i].size(); ++e) RZv[i][e] = R2[i][e] + RY[i][e];
-        }
+        std::vector<std::vector<double>> RZv;
+        bool ro = false;
+        CAL_TRY(project_and_normalize_blocks_dev(c, n, ld, nblocks, dQ, widths, m, dX, doreorth != 0, dY,
+                                                 panel_out(dZ, ld, m), RZv, Rm.data(), &ro, &rk));
+        re = ro ? 1 : 0;
         for (int i = 0; i < nblocks; ++i)
             if (RZ && RZ[i] && widths[i] > 0) std::copy(RZv[i].begin(), RZv[i].end(), RZ[i]);
     }

@@ -569,4 +569,153 @@ int project_and_normalize_dev(cal_ctx* c, int64_t n, const Panel& Qp, const Pane
     return 0;
 }
 
+// project.m:7-58 on the device (block MGS across blocks, CGS within).
+int project_blocks(cal_ctx* c, int64_t n, int64_t ld, int nb, const std::vector<double*>& dQ,
+                          const int* widths, int m, double* dX, bool doreorth, std::vector<std::vector<double>>& R) {
+    Panel X = panel();
+    panel_add(X, dX, ld, m);
+    PanelOut Xo = panel_out(dX, ld, m);
+    auto col_norms = [&](std::vector<double>& nr) -> int {
+        std::vector<double> G((size_t)m * m);
+        CAL_TRY(gram_host(c, n, X, X, G.data()));
+        nr.resize(m);
+        for (int i = 0; i < m; ++i) nr[i] = std::sqrt(G[i + (size_t)i * m]);
+        return 0;
+    };
+    std::vector<double> before;
+    if (doreorth) CAL_TRY(col_norms(before));
+    auto one_pass = [&](bool accumulate) -> int {
+        for (int i = 0; i < nb; ++i) {
+            const int w = widths[i];
+            if (w <= 0) continue;
+            Panel Qi = panel();
+            panel_add(Qi, dQ[i], ld, w);
+            std::vector<double> Ri((size_t)w * m);
+            CAL_TRY(gram_host(c, n, Qi, X, Ri.data()));  // R{i} = Q{i}'*X
+            Panel W = panel();
+            panel_add(W, dQ[i], ld, w);
+            panel_add(W, dX, ld, m);
+            std::vector<double> M((size_t)(w + m) * m, 0.0);
+            for (int j = 0; j < m; ++j) {
+                for (int r = 0; r < w; ++r) M[r + (size_t)j * (w + m)] = -Ri[r + (size_t)j * w];
+                M[w + j + (size_t)j * (w + m)] = 1.0;
+            }
+            CAL_TRY(apply_host(c, n, W, M.data(), m, &Xo, nullptr, 0, nullptr));  // X = X - Q{i}*R{i}
+            if (accumulate)
+                for (size_t e = 0; e < Ri.size(); ++e) R[i][e] += Ri[e];
+            else
+                R[i] = Ri;
+        }
+        return 0;
+    };
+    CAL_TRY(one_pass(false));
+    if (doreorth) {  // project.m:40-57 (note the inverted test of the reference)
+        std::vector<double> after;
+        CAL_TRY(col_norms(after));
+        double mx = NAN;
+        for (int i = 0; i < m; ++i) {
+            const double d = 0.5 * before[i] - after[i];
+            if (!std::isnan(d) && (std::isnan(mx) || d > mx)) mx = d;
+        }
+        if (mx < 0) CAL_TRY(one_pass(true));
+    }
+    return 0;
+}
+
+// projectAndNormalize.m:3-90 against several blocks (the general path:
+// project.m block MGS across blocks, then normalize; the second projection
+// of :52-73 when a column lost more than half its norm).  X is read from dX
+// and not modified; dY is an n x m work block; QZ goes to Qout.
+int project_and_normalize_blocks_dev(cal_ctx* c, int64_t n, int64_t ld, int nblocks, const std::vector<double*>& dQ,
+                                     const int* widths, int m, const double* dX, bool doreorth, double* dY,
+                                     const PanelOut& Qout, std::vector<std::vector<double>>& RZ, double* R,
+                                     bool* reorth, int* rank) {
+    std::vector<double> before(m);
+    {
+        Panel Xp = panel();
+        panel_add(Xp, dX, ld, m);
+        std::vector<double> G((size_t)m * m);
+        CAL_TRY(gram_host(c, n, Xp, Xp, G.data()));
+        for (int i = 0; i < m; ++i) before[i] = std::sqrt(G[i + (size_t)i * m]);   // :17-22
+    }
+    CAL_HIP(c, hipMemcpyAsync(dY, dX, (size_t)m * ld * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    std::vector<std::vector<double>> RY(nblocks);
+    for (int i = 0; i < nblocks; ++i) RY[i].assign((size_t)std::max(widths[i], 0) * m, 0.0);
+    CAL_TRY(project_blocks(c, n, ld, nblocks, dQ, widths, m, dY, false, RY));  // :25
+    Panel Yp = panel();
+    panel_add(Yp, dY, ld, m);
+    bool sh = false;
+    int rk = m;
+    CAL_TRY(normalize_dev(c, n, Yp, Qout, R, 1.0e-8, &rk, &sh));  // :26
+    double mx = NAN;
+    for (int i = 0; i < m; ++i) {  // :45-48 (after = ||R(:,i)||)
+        double after = 0.0;
+        for (int r = 0; r < m; ++r) after += R[r + (size_t)i * m] * R[r + (size_t)i * m];
+        after = std::sqrt(after);
+        const double rel = std::fabs(before[i] - after) / before[i];
+        if (!std::isnan(rel) && (std::isnan(mx) || rel > mx)) mx = rel;
+    }
+    RZ = RY;
+    bool re = false;
+    if (doreorth && mx > 0.5) {  // :52-73: project the unnormalised Y again
+        re = true;
+        std::vector<std::vector<double>> R2(nblocks);
+        for (int i = 0; i < nblocks; ++i) R2[i].assign((size_t)std::max(widths[i], 0) * m, 0.0);
+        CAL_TRY(project_blocks(c, n, ld, nblocks, dQ, widths, m, dY, false, R2));
+        CAL_TRY(normalize_dev(c, n, Yp, Qout, R, 1.0e-8, &rk, &sh));
+        for (int i = 0; i < nblocks; ++i)
+            for (size_t e = 0; e < R2[i].size(); ++e) RZ[i][e] = R2[i][e] + RY[i][e];
+    }
+    if (reorth) *reorth = re;
+    if (rank) *rank = rk;
+    return 0;
+}
+
+// Q factor of an n x m block with m > 16 (the converged Ritz vectors of the
+// selective variant, normalize(QR) at ca_lanczos.m:339): CholQR2 with the
+// shifted fallback on the generic MFMA Gram/apply kernels.  dW is an n x m
+// work block; Q goes to dQ.
+int normalize_wide_dev(cal_ctx* c, int64_t n, int64_t ld, const double* dX, int m, double* dQ, double* dW) {
+    const int64_t ng = global_rows(c, n);
+    auto gram_full = [&](const double* d, std::vector<double>& G) -> int {
+        Panel A = panel();
+        panel_add(A, d, ld, m);
+        G.assign((size_t)m * m, 0.0);
+        for (int j0 = 0; j0 < m; j0 += 16) {
+            const int nb = std::min(16, m - j0);
+            Panel B = panel();
+            panel_add(B, d + (size_t)j0 * ld, ld, nb);
+            std::vector<double> Gc((size_t)m * nb);
+            CAL_TRY(gram_host(c, n, A, B, Gc.data()));
+            for (int j = 0; j < nb; ++j)
+                for (int i = 0; i < m; ++i) G[i + (size_t)(j0 + j) * m] = Gc[i + (size_t)j * m];
+        }
+        return 0;
+    };
+    // CholQR2; a shifted first pass makes it shifted CholQR3 (Fukaya et al.)
+    const double* src = dX;
+    double* bufs[2] = {dW, dQ};
+    int total = 2, which = 0;
+    for (int pass = 0; pass < total; ++pass) {
+        std::vector<double> G, R((size_t)m * m), Ri((size_t)m * m);
+        CAL_TRY(gram_full(src, G));
+        bool sh = false;
+        if (!chol_or_shift(m, G.data(), ng, R.data(), &sh))
+            return set_error(c, CAL_ERR_NUMERIC, "normalize: Gram matrix is not positive definite");
+        if (sh && pass == 0) total = 3;
+        dense::tri_inv_upper(m, R.data(), m, Ri.data(), m);
+        Panel P = panel();
+        panel_add(P, src, ld, m);
+        double* out = bufs[which];
+        if (out == src) out = bufs[which ^= 1];
+        PanelOut Y = panel_out(out, ld, m);
+        CAL_TRY(apply_host(c, n, P, Ri.data(), m, &Y, nullptr, 0, nullptr));
+        src = out;
+        which ^= 1;
+    }
+    if (src != dQ)
+        CAL_HIP(c, hipMemcpyAsync(dQ, src, (size_t)m * ld * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    return 0;
+}
+
 }  // namespace cal

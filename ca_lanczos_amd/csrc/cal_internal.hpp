@@ -202,6 +202,7 @@ hipError_t launch_dot(const double* x, const double* y, int64_t n, double* parti
 int dot_blocks(int64_t n);
 hipError_t launch_axpy_sub(double* y, const double* x, double a, int64_t n, hipStream_t st);  // y -= a*x
 hipError_t launch_div(double* y, const double* x, double b, int64_t n, hipStream_t st);      // y = x / b
+hipError_t launch_abs_rowsum(const int* rowptr, const double* val, int64_t n, double* y, hipStream_t st);
 hipError_t launch_gather(double* dst, const double* src, const int* idx, int64_t cnt, hipStream_t st);
 // fused SpMV + Ritz residual partials for one Ritz pair (diagnostics)
 hipError_t launch_spmv_resid(const SpmvArgs& a, const double* xi, double lr, double li, int64_t nrows,
@@ -311,6 +312,16 @@ int normalize_dev(cal_ctx* c, int64_t n, const Panel& X, const PanelOut& Qout, d
 // Rq (w x m) and R (m x m) on host.  Mirrors projectAndNormalize.m:3-90.
 int project_and_normalize_dev(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, bool doreorth,
                               const PanelOut& Qout, double* Rq, double* R, PNResult* res);
+// project.m:7-58 on device blocks (block MGS across blocks, CGS within); X in place.
+int project_blocks(cal_ctx* c, int64_t n, int64_t ld, int nb, const std::vector<double*>& dQ, const int* widths,
+                   int m, double* dX, bool doreorth, std::vector<std::vector<double>>& R);
+// projectAndNormalize.m:3-90 against several blocks (general path; X kept).
+int project_and_normalize_blocks_dev(cal_ctx* c, int64_t n, int64_t ld, int nblocks, const std::vector<double*>& dQ,
+                                     const int* widths, int m, const double* dX, bool doreorth, double* dY,
+                                     const PanelOut& Qout, std::vector<std::vector<double>>& RZ, double* R,
+                                     bool* reorth, int* rank);
+// Q factor of a wide (m > 16) block by CholQR2 (+ shifted pass).
+int normalize_wide_dev(cal_ctx* c, int64_t n, int64_t ld, const double* dX, int m, double* dQ, double* dW);
 // Halo exchange of a column (distributed only; no-op for one rank).
 int halo_exchange(cal_ctx* c, double* x);
 // y = A x (with modes), handling the halo first.

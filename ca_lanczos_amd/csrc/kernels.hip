@@ -1426,4 +1426,21 @@ hipError_t launch_orth_coef(int phase, const double* tile, double* st, double* m
     return hipGetLastError();
 }
 
+// y(r) = sum_j |A(r,j)| over the local CSR rows: the start vector of
+// normest (sum(abs(S))' = row sums for a symmetric A).
+__global__ __launch_bounds__(256) void k_abs_rowsum(const int* __restrict__ rowptr, const double* __restrict__ val,
+                                                    int64_t n, double* __restrict__ y) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= n) return;
+    double s = 0.0;
+    for (int p = rowptr[r]; p < rowptr[r + 1]; ++p) s = s + fabs(val[p]);
+    y[r] = s;
+}
+
+hipError_t launch_abs_rowsum(const int* rowptr, const double* val, int64_t n, double* y, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_abs_rowsum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rowptr, val, n, y);
+    return hipGetLastError();
+}
+
 }  // namespace cal

@@ -12,6 +12,7 @@
 // Only (s+1) x s, s x s and (2s+1) x s matrices cross PCIe per iteration.
 #include <algorithm>
 #include <chrono>
+#include <limits>
 #include <cmath>
 #include <complex>
 #include <cstring>
@@ -29,6 +30,13 @@ namespace cal {
 struct LanczosState {
     int s = 0, max_outer = 0, k = 0;
     bool newton = false, full = false;
+    int mode = 0;  // orth: 0 local, 1 full, 2 periodic, 3 selective (ca_lanczos.m:74-84)
+    double norm_A = 0.0;  // normest(A) (periodic / selective)
+    std::vector<double> omega;  // periodic: (om_n x om_n), column-major
+    int om_n = 0;
+    double* dQR = nullptr;  // selective: converged Ritz vectors (orthonormal), ld x qr_cap
+    double* dQRy = nullptr;  // selective: their un-normalised form / work
+    int qr_cap = 0, nritz = 0;
     int64_t n = 0, ld = 0;
     double* dQ = nullptr;  // ld x (s*max_outer + 1)
     double* dV = nullptr;  // ld x 2(s+1): the basis block, double-buffered by step parity
@@ -80,6 +88,91 @@ static int enqueue_powers(cal_ctx* c, LanczosState& L, int k) {
             CAL_TRY(spmv_dev(c, x, y, 0, 0.0, 0.0, nullptr));
     }
     return 0;
+}
+
+// ---- normest(A) (MATLAB built-in; ca_lanczos.m:258,370) ---------------------
+// Power iteration on A'A = A^2 (A symmetric) from x = sum(abs(A))', until the
+// estimate changes by <= tol * e (tol 1e-6, at most 100 iterations).
+static int normest_dev(cal_ctx* c, double* out) {
+    const int64_t n = c->A.n_local, ld = c->A.ld;
+    CAL_TRY(ensure_work(c, 2, ld));
+    double* x = work_col(c, 0) + c->A.lpad;
+    double* y = work_col(c, 1) + c->A.lpad;
+    CAL_HIP(c, launch_abs_rowsum(c->A.rowptr, c->A.val, n, x, c->stream));
+    double xx = 0.0;
+    CAL_TRY(dot_host(c, n, x, x, &xx));
+    double e = std::sqrt(xx);
+    if (e == 0.0) {
+        *out = 0.0;
+        return 0;
+    }
+    CAL_HIP(c, launch_div(x, x, e, n, c->stream));
+    double e0 = 0.0;
+    for (int cnt = 0; std::fabs(e - e0) > 1.0e-6 * e && cnt <= 100; ++cnt) {
+        e0 = e;
+        CAL_TRY(spmv_dev(c, x, y, 0, 0.0, 0.0, nullptr));  // Sx = S*x
+        CAL_TRY(spmv_dev(c, y, x, 0, 0.0, 0.0, nullptr));  // x = S'*Sx
+        double nx = 0.0, ny = 0.0;
+        CAL_TRY(dot_host(c, n, x, x, &nx));
+        CAL_TRY(dot_host(c, n, y, y, &ny));
+        nx = std::sqrt(nx);
+        e = nx / std::sqrt(ny);
+        CAL_HIP(c, launch_div(x, x, nx, n, c->stream));
+    }
+    *out = e;
+    return 0;
+}
+
+// ---- periodic: the omega recurrence (ca_lanczos.m:464-549) -----------------
+static void update_omega(LanczosState& L, const std::vector<double>& alpha, const std::vector<double>& beta) {
+    const int s = L.s;
+    const double Tn = std::numeric_limits<double>::epsilon() * L.norm_A;
+    auto al = [&](int i) { return alpha[i - 1]; };  // 1-based as in the reference
+    auto be = [&](int i) { return beta[i - 1]; };
+    int jlo, jhi, nn;
+    std::vector<double> om;
+    if (L.om_n == 0) {
+        nn = s + 1;
+        om.assign((size_t)nn * nn, 0.0);
+        auto O = [&](int i, int j) -> double& { return om[(i - 1) + (size_t)(j - 1) * nn]; };
+        O(1, 1) = 1.0;
+        O(1, 2) = 0.0;
+        O(2, 1) = Tn / be(1);
+        O(2, 2) = 1.0;
+        jlo = 2;
+        jhi = s;
+    } else {
+        const int m = L.om_n - 1;
+        nn = (int)alpha.size() + 1;
+        om.assign((size_t)nn * nn, 0.0);
+        for (int j = 0; j < L.om_n; ++j)
+            for (int i = 0; i < L.om_n; ++i) om[i + (size_t)j * nn] = L.omega[i + (size_t)j * L.om_n];
+        jlo = m + 1;
+        jhi = m + s;
+    }
+    auto O = [&](int i, int j) -> double& { return om[(i - 1) + (size_t)(j - 1) * nn]; };
+    for (int j = jlo; j <= jhi; ++j) {
+        const double binv = 1.0 / be(j);
+        double v = be(2) * O(j, 2) + (al(1) - al(j)) * O(j, 1) - be(j) * O(j - 1, 1);
+        O(j + 1, 1) = v > 0 ? binv * (v + Tn) : binv * (v - Tn);
+        for (int k = 2; k <= j - 1; ++k) {
+            v = be(k + 1) * O(j, k + 1) + (al(k) - al(j)) * O(j, k) + be(k) * O(j, k - 1) - be(j) * O(j - 1, k);
+            O(j + 1, k) = v > 0 ? binv * (v + Tn) : binv * (v - Tn);
+        }
+        O(j + 1, j) = binv * Tn;
+        O(j + 1, j + 1) = 1.0;
+    }
+    L.omega.swap(om);
+    L.om_n = nn;
+}
+
+static void reset_omega(LanczosState& L) {
+    const int s = L.s, nn = L.om_n, m = nn - s - 1;
+    const double Tn = std::numeric_limits<double>::epsilon() * L.norm_A;
+    for (int j = m + 1; j <= m + s; ++j) {
+        for (int k = 1; k <= j; ++k) L.omega[j + (size_t)(k - 1) * nn] = Tn;  // omega(j+1,k)
+        L.omega[j + (size_t)j * nn] = 1.0;                                     // omega(j+1,j+1)
+    }
 }
 
 // ---- Newton prologue: lanczos(A,q,2s,'full') (lanczos.m:18-134) ----------
@@ -304,6 +397,89 @@ static int extend_T(cal_ctx* c, LanczosState& L, const std::vector<double>& Rkk_
     return 0;
 }
 
+// selective (ca_lanczos.m:321-340): the Ritz pairs of T(1:sk,1:sk) with
+// b(k)|Vp(sk,i)| < normest(A) sqrt(eps) (unit-norm eigenvectors, as MATLAB's
+// eig returns them); when their count grows, QR = normalize(Q(:,1:sk) Vp(:,conv)).
+// Deviation: complex pairs are not considered (they would make QR complex).
+static int selective_update(cal_ctx* c, LanczosState& L) {
+    const int s = L.s, k = L.k, sk = s * k;
+    const int64_t n = c->A.n_local, ld = c->A.ld;
+    std::vector<double> Tk((size_t)sk * sk), wr(sk), wi(sk), V((size_t)sk * sk);
+    for (int j = 0; j < sk; ++j)
+        for (int i = 0; i < sk; ++i) Tk[i + (size_t)j * sk] = L.T[i + (size_t)j * L.Tld];
+    if (cal_eig(sk, Tk.data(), sk, wr.data(), wi.data(), V.data()) != 0)
+        return set_error(c, CAL_ERR_NUMERIC, "eig(T) did not converge");
+    const double thresh = L.norm_A * std::sqrt(std::numeric_limits<double>::epsilon());
+    const double bk = L.b.back();
+    std::vector<int> conv;
+    for (int j = 0; j < sk; ++j) {
+        if (wi[j] != 0.0) continue;
+        double nv = 0.0;
+        for (int i = 0; i < sk; ++i) nv += V[i + (size_t)j * sk] * V[i + (size_t)j * sk];
+        nv = std::sqrt(nv);
+        if (bk * std::fabs(V[(sk - 1) + (size_t)j * sk] / nv) < thresh) conv.push_back(j);
+    }
+    if ((int)conv.size() <= L.nritz) return 0;
+    L.info.n_orth_breaks++;
+    const int nr = (int)conv.size();
+    if (nr > L.qr_cap) {
+        if (L.dQR) CAL_HIP(c, hipFree(L.dQR));
+        if (L.dQRy) CAL_HIP(c, hipFree(L.dQRy));
+        L.dQR = L.dQRy = nullptr;
+        L.qr_cap = std::max(nr, 2 * s);
+        CAL_HIP(c, hipMalloc((void**)&L.dQR, (size_t)L.qr_cap * ld * sizeof(double)));
+        CAL_HIP(c, hipMalloc((void**)&L.dQRy, (size_t)L.qr_cap * ld * sizeof(double)));
+    }
+    std::vector<double> M((size_t)sk * nr);
+    for (int q = 0; q < nr; ++q)
+        for (int i = 0; i < sk; ++i) M[i + (size_t)q * sk] = V[i + (size_t)conv[q] * sk];
+    Panel Qp = panel();
+    panel_add(Qp, L.col(0), ld, sk);
+    PanelOut Y = panel_out(L.dQRy + L.lpad, ld, nr);
+    CAL_TRY(apply_host(c, n, Qp, M.data(), nr, &Y, nullptr, 0, nullptr));  // y = Q(:,1:ks)*Vp(:,i)
+    // halo columns of the Ritz vectors are never read (they only enter Grams
+    // and row-local applies), so no exchange is needed
+    CAL_TRY(normalize_wide_dev(c, n, ld, L.dQRy + L.lpad, nr, L.dQR + L.lpad, L.dQRy + L.lpad));
+    L.nritz = nr;
+    L.info.n_ritz_locked = nr;
+    return 0;
+}
+
+// periodic (ca_lanczos.m:438-453): advance the omega estimate; when it
+// reaches sqrt(eps), reorthogonalise Q(:,(k-1)s+1:ks+1) against
+// Q(:,1:(k-1)s) (the new columns do not feed back into T).
+static int periodic_update(cal_ctx* c, LanczosState& L) {
+    const int s = L.s, k = L.k, sk = s * k;
+    const int64_t n = c->A.n_local, ld = c->A.ld;
+    std::vector<double> alpha(sk), beta(sk);
+    for (int i = 0; i < sk; ++i) {
+        alpha[i] = L.T[i + (size_t)i * L.Tld];        // diag(T,0)
+        beta[i] = L.T[(i + 1) + (size_t)i * L.Tld];   // diag(T,-1)
+    }
+    update_omega(L, alpha, beta);
+    double err = 0.0;
+    for (int i = 1; i <= s; ++i) {
+        const int row = (k - 1) * s + i;  // omega((k-1)s+i+1, 1:(k-1)s+i), 0-based row
+        double row_err = 0.0;
+        for (int j = 0; j < row; ++j) row_err = std::max(row_err, std::fabs(L.omega[row + (size_t)j * L.om_n]));
+        if (row_err > err) err = row_err;
+    }
+    if (!(err >= std::sqrt(std::numeric_limits<double>::epsilon()))) return 0;
+    L.info.n_orth_breaks++;
+    const int w = (k - 1) * s, m = s + 1;
+    CAL_TRY(ensure_work(c, m, ld));
+    double* dX = work_col(c, 0) + c->A.lpad;
+    CAL_HIP(c, hipMemcpyAsync(dX, L.col(w), (size_t)m * ld * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    Panel Qp = panel(), X = panel();
+    if (w > 0) panel_add(Qp, L.col(0), ld, w);
+    panel_add(X, dX, ld, m);
+    std::vector<double> Rq((size_t)std::max(w, 1) * m), R((size_t)m * m);
+    PNResult res;
+    CAL_TRY(project_and_normalize_dev(c, n, Qp, X, true, panel_out(L.col(w), ld, m), Rq.data(), R.data(), &res));
+    reset_omega(L);
+    return 0;
+}
+
 int lanczos_step(cal_ctx* c, int diagnostics) {
     LanczosState& L = *c->lz;
     if (L.k >= L.max_outer) return set_error(c, CAL_ERR_ARG, "lanczos_step: max_outer iterations reached");
@@ -321,7 +497,7 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
     // (stream-ordered after this step's pass B) and the fixed shifts, so they
     // are enqueued (into the other V buffer) before the host waits for this
     // step's R: the GPU runs them while the host extends T and returns.
-    const bool prefetch = !diagnostics && !L.full && k + 1 <= L.max_outer;
+    const bool prefetch = !diagnostics && L.mode == 0 && k + 1 <= L.max_outer;
     c->orth_redone = false;
     if (prefetch)
         c->pre_wait = [c, &L, k]() {
@@ -353,7 +529,22 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
         PanelOut Qo = panel_out(L.col((k - 1) * s + 1), ld, s);
         std::vector<double> Rq((size_t)(s + 1) * s), R((size_t)s * s);
         PNResult res;
-        CAL_TRY(project_and_normalize_dev(c, n, Qp, X, true, Qo, Rq.data(), R.data(), &res));
+        if (L.mode == 3 && L.nritz > 0) {
+            // projectAndNormalize({Q block, QR(:,1:nritz)}, V(:,2:s+1)) (ca_lanczos.m:287)
+            CAL_TRY(ensure_work(c, s, ld));
+            std::vector<double*> dQ{L.col((k - 2) * s), L.dQR + L.lpad};
+            const int widths[2] = {s + 1, L.nritz};
+            std::vector<std::vector<double>> RZ;
+            bool ro = false;
+            int rk = s;
+            CAL_TRY(project_and_normalize_blocks_dev(c, n, ld, 2, dQ, widths, s, Vc(1), true,
+                                                     work_col(c, 0) + c->A.lpad, Qo, RZ, R.data(), &ro, &rk));
+            Rq = RZ[0];
+            res.reorth = ro;
+            res.rank = rk;
+        } else {
+            CAL_TRY(project_and_normalize_dev(c, n, Qp, X, true, Qo, Rq.data(), R.data(), &res));
+        }
         L.reorth.push_back(res.reorth ? 1 : 0);
         if (res.reorth) L.info.n_reorth++;
         if (res.reorth && res.rank < s) L.info.n_rank_deficient++;
@@ -373,6 +564,8 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
         L.info.breakdown = 1;
         return set_error(c, CAL_WARN_BREAKDOWN, "CA-Lanczos breakdown: rho_t = Rk(s,s) = 0");
     }
+    if (L.mode == 2) CAL_TRY(periodic_update(c, L));
+    if (L.mode == 3) CAL_TRY(selective_update(c, L));
     const double t1 = now_ms();
     if (diagnostics) CAL_TRY(ritz_diagnostics(c, L));
     const double t2 = now_ms();
@@ -392,6 +585,8 @@ void cal_lanczos_free_state(cal_ctx* c) {
     if (!c || !c->lz) return;
     if (c->lz->dQ) hipFree(c->lz->dQ);
     if (c->lz->dV) hipFree(c->lz->dV);
+    if (c->lz->dQR) hipFree(c->lz->dQR);
+    if (c->lz->dQRy) hipFree(c->lz->dQRy);
     delete c->lz;
     c->lz = nullptr;
 }
@@ -406,8 +601,6 @@ int cal_lanczos_begin(cal_ctx* c, const double* r, int s, int max_outer, const c
     for (auto& ch : b) ch = (char)tolower(ch);
     if (o != "local" && o != "full" && o != "periodic" && o != "selective")
         return set_error(c, CAL_ERR_ARG, "ca_lanczos.m: Invalid option value for orth: " + o);
-    if (o == "periodic" || o == "selective")
-        return set_error(c, CAL_ERR_UNSUPPORTED, "orth='" + o + "' is outside the built scope (SURVEY §8f1)");
     if (b != "monomial" && b != "newton") return set_error(c, CAL_ERR_ARG, "ERROR: Unknown basis type: " + b);
     hipSetDevice(c->device);
     cal_lanczos_free_state(c);
@@ -417,6 +610,7 @@ int cal_lanczos_begin(cal_ctx* c, const double* r, int s, int max_outer, const c
     L->max_outer = max_outer;
     L->newton = b == "newton";
     L->full = o == "full";
+    L->mode = o == "local" ? 0 : (o == "full" ? 1 : (o == "periodic" ? 2 : 3));
     L->n = c->A.n_local;
     L->ld = c->A.ld;
     L->lpad = c->A.lpad;
@@ -440,6 +634,8 @@ int cal_lanczos_begin(cal_ctx* c, const double* r, int s, int max_outer, const c
         L->Bk.assign((size_t)(s + 1) * s, 0.0);
         for (int j = 0; j < s; ++j) L->Bk[(j + 1) + (size_t)j * (s + 1)] = 1.0;
     }
+    if (L->mode >= 2) CAL_TRY(normest_dev(c, &L->norm_A));  // ca_lanczos.m:258,370
+    L->info.norm_A = L->norm_A;
     CAL_HIP(c, hipStreamSynchronize(c->stream));
     L->info.prologue_ms = now_ms() - t0;
     return 0;

@@ -129,10 +129,13 @@ typedef struct cal_lanczos_info {
     double prologue_ms; /* Newton prologue wall time                            */
     double loop_ms;     /* outer loop wall time (incl. diagnostics)             */
     double diag_ms;     /* of which diagnostics                                 */
+    int n_orth_breaks;  /* periodic: full reorthogonalisations; selective: QR rebuilds */
+    int n_ritz_locked;  /* selective: converged Ritz vectors in QR               */
+    double norm_A;      /* normest(A) (periodic / selective)                    */
 } cal_lanczos_info;
 
 /* [T,Q,rn,oe] = ca_lanczos(A,r,s,iter,basis,orth).           ca_lanczos.m:24-86
- * basis in {"monomial","newton"}, orth in {"local","full"}.
+ * basis in {"monomial","newton"}, orth in {"local","full","periodic","selective"}.
  * Outputs (any may be NULL): T (s*t x s*t), Q (n x s*t), rn (t x s*t),
  * oe (t), reorth_flags (t).  t = ceil(iter/s).  diagnostics=0 skips the
  * per-iteration Ritz residuals / orthogonality error (rn, oe left zero);

@@ -598,6 +598,224 @@ class CALanczosResult:
     ritz_values: list = field(default_factory=list)
 
 
+def _extend_T(T, b, k, s, Bk, Rkk_s, Rk_s):
+    """The block update of T at k > 1 (ca_lanczos.m:201-223, repeated in
+    ca_lanczos_selective :293-318 and ca_lanczos_periodic :411-436); sets
+    b[k-1] and returns the extended T."""
+    Rkk = np.hstack([np.zeros((s, 1)), Rkk_s[:s, :]])          # :201
+    e1s1 = np.zeros((s + 1, 1))
+    e1s1[0, 0] = 1.0
+    Rk = np.hstack([e1s1, np.vstack([Rkk_s[s : s + 1, :s], Rk_s])])   # :202
+    zk = Rk[:s, s : s + 1]
+    rho = Rk[s, s]
+    rho_t = Rk[s - 1, s - 1]
+    bk = Bk[s, s - 1]
+    e1 = np.zeros((s, 1))
+    e1[0, 0] = 1.0
+    es = eyeshvec(s).reshape(s, 1)
+    R11 = Rk[:s, :s]
+    Tk = (_rdiv_upper(R11 @ Bk[:s, :], R11)                     # :209-211
+          + ((bk / rho_t) * zk) @ es.T
+          - _rdiv_upper(((b[k - 2] * e1) @ es.T) @ Rkk[:s, :s], R11))
+    b[k - 1] = bk * (rho / rho_t)                               # :214
+    m = s * (k - 1)
+    T11 = T[:m, :m]                                             # :217-223
+    T12 = b[k - 2] * np.outer(eyeshvec(m), np.eye(s, 1)[:, 0])
+    T21 = b[k - 2] * np.outer(np.eye(s, 1)[:, 0], eyeshvec(m))
+    T31 = np.zeros((1, m))
+    T32 = b[k - 1] * es.T
+    return np.block([[T11, T12], [T21, Tk], [T31, T32]])
+
+
+def normest(A, tol=1.0e-6, maxiter=100):
+    """MATLAB ``normest(S,tol)`` (built-in, not in the reference; restated from
+    its published algorithm): power iteration on S'S from x = sum(abs(S))',
+    stopping when |e - e0| <= tol*e.  Used by ca_lanczos.m:258,370."""
+    x = np.asarray(abs(A).sum(axis=0)).ravel().astype(float)
+    e = float(np.sqrt(x @ x))
+    if e == 0.0:
+        return 0.0
+    x = x / e
+    e0 = 0.0
+    cnt = 0
+    while abs(e - e0) > tol * e:
+        e0 = e
+        Sx = A @ x
+        x = A.T @ Sx
+        normx = float(np.sqrt(x @ x))
+        e = normx / float(np.sqrt(Sx @ Sx))
+        x = x / normx
+        cnt += 1
+        if cnt > maxiter:
+            break
+    return e
+
+
+def update_omega(omega_in, alpha, beta, anorm, s):
+    """ca_lanczos.m:464-536: the omega recurrence (Simon's estimate of the
+    loss of orthogonality), extended by s rows per outer iteration.  Indices
+    are MATLAB's, shifted by one."""
+    eps_ = np.finfo(float).eps
+    n = len(alpha)
+    Tn = eps_ * anorm
+    al = lambda i: alpha[i - 1]          # noqa: E731 (1-based accessors)
+    be = lambda i: beta[i - 1]           # noqa: E731
+    if omega_in is None:
+        om = np.zeros((s + 1, s + 1))
+        O = lambda i, j: om[i - 1, j - 1]    # noqa: E731
+        om[0, 0] = 1.0
+        om[0, 1] = 0.0
+        om[1, 0] = Tn / be(1)
+        om[1, 1] = 1.0
+        jr = range(2, s + 1)
+    else:
+        m = omega_in.shape[0] - 1
+        om = np.zeros((n + 1, n + 1))
+        om[: m + 1, : m + 1] = omega_in
+        O = lambda i, j: om[i - 1, j - 1]    # noqa: E731
+        jr = range(m + 1, m + s + 1)
+    for j in jr:
+        binv = 1.0 / be(j)
+        v = be(2) * O(j, 2) + (al(1) - al(j)) * O(j, 1) - be(j) * O(j - 1, 1)
+        om[j, 0] = binv * (v + Tn) if v > 0 else binv * (v - Tn)
+        for k in range(2, j):
+            v = be(k + 1) * O(j, k + 1) + (al(k) - al(j)) * O(j, k) + be(k) * O(j, k - 1) - be(j) * O(j - 1, k)
+            om[j, k - 1] = binv * (v + Tn) if v > 0 else binv * (v - Tn)
+        om[j, j - 1] = binv * Tn
+        om[j, j] = 1.0
+    return om
+
+
+def reset_omega(omega_in, anorm, s):
+    """ca_lanczos.m:538-549."""
+    Tn = np.finfo(float).eps * anorm
+    m = omega_in.shape[0] - s - 1
+    om = omega_in.copy()
+    for j in range(m + 1, m + s + 1):
+        om[j, :j] = Tn
+        om[j, j] = 1.0
+    return om
+
+
+def ca_lanczos_periodic(A, q, Bk, t, s, basis, diagnostics=True):
+    """ca_lanczos.m:362-462: local block orthogonalisation plus a full
+    reorthogonalisation of the newest s+1 columns whenever the omega
+    estimate reaches sqrt(eps) (the reorthogonalised columns do not feed
+    back into T, as in the reference)."""
+    n = len(q)
+    rnorm = np.zeros((t, t * s))
+    ortherr = np.zeros(t)
+    Q = np.zeros((n, t * s + 1))
+    Q[:, 0] = q
+    b = np.zeros(t + 1)
+    T = None
+    omega = None
+    norm_A = normest(A)                                         # :370
+    breaks, reorth, ritz = [], [], []
+    k = 0
+    while k < t:
+        k += 1
+        if k > 1:
+            q = Q[:, (k - 1) * s]
+        V = matrix_powers(A, q, s, Bk, basis)
+        if k == 1:
+            Qb, Rk, _ = normalize(V[:, : s + 1])
+            Q[:, : s + 1] = Qb
+            T = _rdiv_upper(Rk @ Bk, Rk[:s, :s])
+            b[0] = T[s, s - 1]
+            reorth.append(False)
+        else:
+            Qp = Q[:, (k - 2) * s : (k - 1) * s + 1]
+            Q_, Rk_, info = projectAndNormalize_ex([Qp], V[:, 1 : s + 1], True)   # :402
+            reorth.append(info.reorth)
+            Q[:, (k - 1) * s + 1 : k * s + 1] = Q_[:, :s]
+            T = _extend_T(T, b, k, s, Bk, Rk_[0], Rk_[1])
+        alpha = np.diag(T, 0)                                   # :439-441
+        beta = np.diag(T, -1)
+        omega = update_omega(omega, alpha, beta, norm_A, s)
+        err = 0.0
+        for i in range(1, s + 1):                               # :442-448
+            row = omega[(k - 1) * s + i, : (k - 1) * s + i]
+            row_err = float(np.max(np.abs(row)))
+            if row_err > err:
+                err = row_err
+        brk = err >= math.sqrt(np.finfo(float).eps)             # :449
+        breaks.append(brk)
+        if brk:
+            cols = slice((k - 1) * s, k * s + 1)
+            Q[:, cols], _ = projectAndNormalize([Q[:, : (k - 1) * s]], Q[:, cols], True)   # :451
+            omega = reset_omega(omega, norm_A, s)
+        if diagnostics:
+            w, Vp = matlab_eig(T[: s * k, : s * k])
+            ritz.append(w)
+            rnorm[k - 1, : s * k] = compute_ritz_rnorm(A, Q[:, : s * k], Vp, w)
+            ortherr[k - 1] = compute_orth_err(Q[:, : s * k + 1], s)
+    res = CALanczosResult(T=T[: s * k, : s * k], Q=Q[:, : s * k], ritz_rnorm=rnorm[:k], orth_err=ortherr[:k],
+                          Bk=Bk, shifts=np.zeros(0), reorth=reorth, ritz_values=ritz)
+    res.breaks = breaks
+    res.norm_A = norm_A
+    return res
+
+
+def ca_lanczos_selective(A, q, Bk, t, s, basis, diagnostics=True):
+    """ca_lanczos.m:248-359: local block orthogonalisation against the
+    previous block and the converged Ritz vectors QR; QR is rebuilt (all
+    converged Ritz vectors, in eig order, then normalize) whenever the count
+    b(k)|Vp(sk,i)| < normest(A) sqrt(eps) grows.  Deviation: only real
+    eigenpairs of T are considered (a complex pair would make the reference's
+    QR complex)."""
+    n = len(q)
+    rnorm = np.zeros((t, t * s))
+    ortherr = np.zeros(t)
+    Q = np.zeros((n, t * s + 1))
+    Q[:, 0] = q
+    b = np.zeros(t + 1)
+    T = None
+    QR = np.zeros((n, 0))
+    norm_A = normest(A)
+    norm_sqrt_eps = norm_A * math.sqrt(np.finfo(float).eps)     # :258
+    nritz = 0
+    breaks, reorth, ritz, nritz_hist = [], [], [], []
+    k = 0
+    while k < t:
+        k += 1
+        if k > 1:
+            q = Q[:, (k - 1) * s]
+        V = matrix_powers(A, q, s, Bk, basis)
+        if k == 1:
+            Qb, Rk, _ = normalize(V[:, : s + 1])
+            Q[:, : s + 1] = Qb
+            T = _rdiv_upper(Rk @ Bk, Rk[:s, :s])
+            b[0] = T[s, s - 1]
+            reorth.append(False)
+        else:
+            Qp = Q[:, (k - 2) * s : (k - 1) * s + 1]
+            Q_, Rk_, info = projectAndNormalize_ex([Qp, QR[:, :nritz]], V[:, 1 : s + 1], True)   # :287
+            reorth.append(info.reorth)
+            Q[:, (k - 1) * s + 1 : k * s + 1] = Q_[:, :s]
+            T = _extend_T(T, b, k, s, Bk, Rk_[0], Rk_[2])         # Rk_s = Rk_{3} (:291)
+        w, Vp = matlab_eig(T[: s * k, : s * k])                 # :321
+        real = np.isreal(w) if np.iscomplexobj(w) else np.ones(len(w), bool)
+        conv = [i for i in range(k * s) if real[i] and b[k - 1] * abs(np.real(Vp[s * k - 1, i])) < norm_sqrt_eps]
+        brk = len(conv) > nritz                                 # :329
+        breaks.append(brk)
+        if brk:
+            nritz = len(conv)
+            Y = Q[:, : k * s] @ np.real(Vp[:, conv])            # :334-336
+            QR, _, _ = normalize(Y)                             # :339
+        nritz_hist.append(nritz)
+        if diagnostics:
+            ritz.append(w)
+            rnorm[k - 1, : s * k] = compute_ritz_rnorm(A, Q[:, : s * k], Vp, w)
+            ortherr[k - 1] = compute_orth_err(Q[:, : s * k + 1], s)
+    res = CALanczosResult(T=T[: s * k, : s * k], Q=Q[:, : s * k], ritz_rnorm=rnorm[:k], orth_err=ortherr[:k],
+                          Bk=Bk, shifts=np.zeros(0), reorth=reorth, ritz_values=ritz)
+    res.breaks = breaks
+    res.nritz = nritz_hist
+    res.norm_A = norm_A
+    return res
+
+
 def ca_lanczos_basic(A, q, Bk, t, s, basis, orth="local", diagnostics=True):
     """ca_lanczos.m:150-245 ('local' and 'fro')."""
     n = len(q)
@@ -633,29 +851,7 @@ def ca_lanczos_basic(A, q, Bk, t, s, basis, orth="local", diagnostics=True):
                 Q[:, (k - 1) * s + 1 : k * s + 1] = Q_
                 Qf, _ = projectAndNormalize([Q[:, : (k - 1) * s + 1]], Q[:, (k - 1) * s + 1 : k * s + 1])
                 Q[:, (k - 1) * s + 1 : k * s + 1] = Qf
-            Rkk = np.hstack([np.zeros((s, 1)), Rkk_s[:s, :]])  # :201
-            e1s1 = np.zeros((s + 1, 1))
-            e1s1[0, 0] = 1.0
-            Rk = np.hstack([e1s1, np.vstack([Rkk_s[s : s + 1, :s], Rk_s])])   # :202
-            zk = Rk[:s, s : s + 1]
-            rho = Rk[s, s]
-            rho_t = Rk[s - 1, s - 1]
-            bk = Bk[s, s - 1]
-            e1 = np.zeros((s, 1))
-            e1[0, 0] = 1.0
-            es = eyeshvec(s).reshape(s, 1)
-            R11 = Rk[:s, :s]
-            Tk = (_rdiv_upper(R11 @ Bk[:s, :], R11)             # :209-211
-                  + ((bk / rho_t) * zk) @ es.T
-                  - _rdiv_upper(((b[k - 2] * e1) @ es.T) @ Rkk[:s, :s], R11))
-            b[k - 1] = bk * (rho / rho_t)                       # :214
-            m = s * (k - 1)
-            T11 = T[:m, :m]                                     # :217-223
-            T12 = b[k - 2] * np.outer(eyeshvec(m), np.eye(s, 1)[:, 0])
-            T21 = b[k - 2] * np.outer(np.eye(s, 1)[:, 0], eyeshvec(m))
-            T31 = np.zeros((1, m))
-            T32 = b[k - 1] * es.T
-            T = np.block([[T11, T12], [T21, Tk], [T31, T32]])
+            T = _extend_T(T, b, k, s, Bk, Rkk_s, Rk_s)             # :201-223
         if diagnostics:                                         # :228-236
             Tk_ = T[: s * k, : s * k]
             w, Vp = matlab_eig(Tk_)
@@ -677,8 +873,6 @@ def ca_lanczos(A, r, s, iter, basis, orth="local", diagnostics=True):
     o = orth.lower() if isinstance(orth, str) else str(orth)
     if o not in ("local", "full", "selective", "periodic"):
         raise ValueError("ca_lanczos.m: Invalid option value for orth: %s" % orth)   # :33-38
-    if o in ("selective", "periodic"):
-        raise NotImplementedError("orth=%s is a 'next' row (SURVEY §8f1)" % orth)
     t = int(math.ceil(iter / s))                                # :52
     q = r / math.sqrt(r @ r)                                    # :55
     b = basis.lower()
@@ -689,7 +883,12 @@ def ca_lanczos(A, r, s, iter, basis, orth="local", diagnostics=True):
         Bk, shifts, _ = newton_change_of_basis(A, q, s)
     else:
         raise ValueError("ERROR: Unknown basis type: " + basis)  # :57-59
-    res = ca_lanczos_basic(A, q, Bk, t, s, b, "local" if o == "local" else "fro", diagnostics)
+    if o == "periodic":                                         # :80-83
+        res = ca_lanczos_periodic(A, q, Bk, t, s, b, diagnostics)
+    elif o == "selective":
+        res = ca_lanczos_selective(A, q, Bk, t, s, b, diagnostics)
+    else:
+        res = ca_lanczos_basic(A, q, Bk, t, s, b, "local" if o == "local" else "fro", diagnostics)
     res.shifts = shifts
     return res
 

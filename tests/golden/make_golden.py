@@ -31,6 +31,12 @@ CASES = {
     "lap2d_32_s8_newton_local": dict(mat=("lap2d", 32), r="rand", s=8, iter=80, basis="newton", orth="local"),
     "lap3d_12_s8_newton_local": dict(mat=("lap3d", 12), r="rand", s=8, iter=80, basis="newton", orth="local"),
     "lap2d_24_s8_newton_full": dict(mat=("lap2d", 24), r="rand", s=8, iter=64, basis="newton", orth="full"),
+    # test_convergence_diagonal_matrices.m:9-21 with its own orth ('periodic'), and the
+    # 'selective' option of test_convergence_general_matrices.m:18, on the same matrix
+    "diag500_linspace_s8_newton_periodic": dict(mat=("diag_linspace", 1.0, 100.0, 500), r="ones", s=8, iter=240,
+                                                basis="newton", orth="periodic"),
+    "diag500_linspace_s8_newton_selective": dict(mat=("diag_linspace", 1.0, 100.0, 500), r="ones", s=8,
+                                                 iter=240, basis="newton", orth="selective"),
 }
 
 
@@ -71,6 +77,9 @@ def main():
             T=res.T, ritz_rnorm=res.ritz_rnorm, orth_err=res.orth_err, reorth=np.array(res.reorth, dtype=np.int8),
             shifts=res.shifts, Bk=res.Bk, ritz=np.sort_complex(w), exact_extremes=np.array([exact[0], exact[-1]]),
             Q_colsums=res.Q.sum(axis=0), Q_first_rows=res.Q[:4, :],
+            breaks=np.array(getattr(res, "breaks", []), dtype=np.int8),
+            nritz=np.array(getattr(res, "nritz", []), dtype=np.int32),
+            norm_A=np.array(getattr(res, "norm_A", 0.0)),
         )
         print("%-36s T %s  reorth %d/%d  largest Ritz %.12f (exact %.12f)  rn[-1,0] %.2e"
               % (name, res.T.shape, sum(res.reorth), len(res.reorth), np.max(w.real), exact[-1],

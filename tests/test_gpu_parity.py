@@ -286,8 +286,8 @@ def test_ca_lanczos_bad_args(cal):
         cal.ca_lanczos(A, np.ones(64), 4, 16, "newton", "bogus")
     with pytest.raises(cal.CalError):
         cal.ca_lanczos(A, np.ones(64), 4, 16, "chebyshev", "local")
-    with pytest.raises(cal.CalError):
-        cal.ca_lanczos(A, np.ones(64), 4, 16, "newton", "periodic")
+    with pytest.raises(cal.CalError):  # s > 15: s + 1 exceeds the 16-column block kernels
+        cal.ca_lanczos(A, np.ones(64), 17, 34, "newton", "local")
 
 
 @pytest.mark.gpu
@@ -352,3 +352,30 @@ def test_ca_lanczos_prefetch_invariant(cal, ref):
     ctx.close()
     assert np.array_equal(a.T, b.T) and np.array_equal(a.Q, b.Q)
     assert np.array_equal(a.reorth, b.reorth)
+
+
+@pytest.mark.parametrize("orth", ["periodic", "selective"])
+def test_ca_lanczos_periodic_selective(cal, ref, orth):
+    """the periodic (omega recurrence + full reorthogonalisation)
+    and selective (converged Ritz vectors locked into the projection)
+    variants on the reference's own test input (test_convergence_diagonal_
+    matrices.m:9-21: diag(linspace(1,100,500)), r = ones, newton), s = 8,
+    240 iterations.  Bars: the same break decisions and locked-vector counts
+    as the oracle, normest within 1e-10 relative, T within 1e-8 ||A||,
+    the extreme Ritz values within 1e-10 ||A||, orthogonality kept."""
+    import scipy.sparse as sp
+    a = ref.matlab_linspace(1.0, 100.0, 500)
+    A = sp.csr_matrix(sp.diags(a))
+    r = np.ones(500)
+    exp = ref.ca_lanczos(A, r, 8, 240, "newton", orth, diagnostics=True)
+    out = cal.ca_lanczos_ex(A, r, 8, 240, "newton", orth, diagnostics=True)
+    normA = 100.0
+    assert abs(out.info["norm_A"] - exp.norm_A) <= 1e-10 * exp.norm_A
+    assert out.info["n_orth_breaks"] == sum(exp.breaks)
+    if orth == "selective":
+        assert out.info["n_ritz_locked"] == exp.nritz[-1]
+    assert list(out.reorth) == list(exp.reorth)
+    assert np.max(np.abs(out.T - exp.T)) <= 1e-8 * normA
+    w, we = np.sort(np.linalg.eigvals(out.T).real), np.sort(np.linalg.eigvals(exp.T).real)
+    assert abs(w[-1] - we[-1]) <= 1e-10 * normA and abs(w[0] - we[0]) <= 1e-10 * normA
+    assert np.max(out.orth_err) < 1e-6 and np.max(exp.orth_err) < 1e-6

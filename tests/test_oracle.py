@@ -67,7 +67,8 @@ def test_newton_basis_matrix(ref):
 
 @pytest.mark.parametrize("name", ["c1_diag1000_s4_monomial_local", "diag500_linspace_s4_newton_local",
                                   "lap2d_32_s8_newton_local", "lap3d_12_s8_newton_local",
-                                  "lap2d_24_s8_newton_full", "diag5000_linspace_s4_newton_full"])
+                                  "lap2d_24_s8_newton_full", "diag5000_linspace_s4_newton_full",
+                                  "diag500_linspace_s8_newton_periodic", "diag500_linspace_s8_newton_selective"])
 def test_oracle_vs_golden_and_known_answers(ref, golden_mod, name):
     spec = golden_mod.CASES[name]
     A, exact, r, res = golden_mod.run_case(spec)
@@ -77,6 +78,11 @@ def test_oracle_vs_golden_and_known_answers(ref, golden_mod, name):
     assert res.T.shape == g["T"].shape
     assert np.max(np.abs(res.T - g["T"])) <= 1e-9 * normA
     assert list(res.reorth) == list(g["reorth"])
+    if "breaks" in g and len(g["breaks"]):  # periodic / selective decisions
+        assert list(res.breaks) == list(g["breaks"])
+        if len(g["nritz"]):
+            assert list(res.nritz) == list(g["nritz"])
+        assert abs(res.norm_A - float(g["norm_A"])) <= 1e-12 * normA
     if len(g["shifts"]):
         assert np.max(np.abs(res.shifts - g["shifts"])) <= 1e-12 * normA
     # known answer: converged extreme Ritz values are eigenvalues of A
