@@ -46,6 +46,13 @@ class LanczosInfo(ctypes.Structure):
     ]
 
 
+class RestartInfo(ctypes.Structure):
+    _fields_ = [
+        ("num_restarts", c_int), ("nconv", c_int), ("converged", c_int),
+        ("norm_A", c_double), ("max_ritz_norm", c_double), ("ms", c_double),
+    ]
+
+
 ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, dp, c_int64)
 EXCHANGE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_int, dp, c_int64, dp, c_int64)
 
@@ -89,6 +96,9 @@ SIGNATURES = [
     ("cal_lanczos_get", c_int, [c_void_p, dp, c_int, dp, dp, ip, POINTER(LanczosInfo)]),
     ("cal_lanczos_get_Q", c_int, [c_void_p, c_int64, c_int, dp]),
     ("cal_lanczos_end", c_int, [c_void_p]),
+    ("cal_restarted_ca_lanczos", c_int,
+     [c_void_p, dp, c_int, c_int, c_int, c_char_p, c_char_p, c_double, c_int, dp, dp, dp, dp,
+      POINTER(RestartInfo)]),
     ("cal_comm_unique_id", c_int, [c_void_p]),
     ("cal_comm_init_rccl", c_int, [c_void_p, c_int, c_int, c_void_p]),
     ("cal_comm_init_host", c_int, [c_void_p, c_int, c_int, ALLREDUCE_FN, EXCHANGE_FN, c_void_p]),

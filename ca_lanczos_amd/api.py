@@ -451,3 +451,34 @@ def ca_lanczos(A, r, s, iter, basis, orth="local"):
     """``[T,Q,ritz_rnorm,orth_err] = ca_lanczos(A,r,s,iter,basis,orth)`` -- ca_lanczos.m:24-86."""
     out = ca_lanczos_ex(A, r, s, iter, basis, orth, diagnostics=True, return_Q=True)
     return out.T, out.Q, out.ritz_rnorm, out.orth_err
+
+
+# ---------------------------------------------------------------------------
+# f2: explicit restart
+# ---------------------------------------------------------------------------
+MAX_RESTARTS = 200  # restarted_ca_lanczos.m:6
+
+
+def restarted_ca_lanczos(A, r, max_lanczos, n_wanted_eigs=10, s=6, basis="newton", orth="local", tol=1.0e-8,
+                         diagnostics=True, ctx=None):
+    """``[E,V,nres,rnorms,orth_err] = restarted_ca_lanczos(A,r,max_lanczos,
+    n_wanted_eigs,s,basis,orth,tol)`` -- restarted_ca_lanczos.m:4-198.
+
+    Returns a dict: conv_eigs (descending), Q_conv (n x nconv), num_restarts,
+    rnorms (num_restarts x n_wanted_eigs), orth_err (num_restarts),
+    converged, norm_A."""
+    ctx = ctx or context_for(A)
+    r = f64(r).ravel()
+    n = len(r)
+    E = np.zeros(n_wanted_eigs)
+    V = np.zeros((n, n_wanted_eigs), order="F")
+    rn = np.zeros((MAX_RESTARTS, n_wanted_eigs), order="F")
+    oe = np.zeros(MAX_RESTARTS)
+    info = _lib.RestartInfo()
+    st = lib.cal_restarted_ca_lanczos(ctx.h, ptr(r), int(max_lanczos), int(n_wanted_eigs), int(s), basis.encode(),
+                                      orth.encode(), float(tol), 1 if diagnostics else 0, ptr(E), ptr(V), ptr(rn),
+                                      ptr(oe), ctypes.byref(info))
+    check(ctx.h, st, "restarted_ca_lanczos")
+    k, nr = info.nconv, info.num_restarts
+    return dict(conv_eigs=E[:k].copy(), Q_conv=V[:, :k].copy(), num_restarts=nr, rnorms=rn[:nr].copy(),
+                orth_err=oe[:nr].copy(), converged=bool(info.converged), norm_A=info.norm_A, ms=info.ms)

@@ -37,6 +37,11 @@ struct LanczosState {
     double* dQR = nullptr;  // selective: converged Ritz vectors (orthonormal), ld x qr_cap
     double* dQRy = nullptr;  // selective: their un-normalised form / work
     int qr_cap = 0, nritz = 0;
+    // explicit restart (restarted_ca_lanczos.m): the converged vectors Q_conv
+    // every new block is also projected against
+    bool restart_inner = false;
+    double* dExt = nullptr;  // Q_conv columns (not owned), lpad origin
+    int next = 0;
     int64_t n = 0, ld = 0;
     double* dQ = nullptr;  // ld x (s*max_outer + 1)
     double* dV = nullptr;  // ld x 2(s+1): the basis block, double-buffered by step parity
@@ -176,7 +181,7 @@ static void reset_omega(LanczosState& L) {
 }
 
 // ---- Newton prologue: lanczos(A,q,2s,'full') (lanczos.m:18-134) ----------
-static int newton_prologue(cal_ctx* c, LanczosState& L) {
+static int newton_prologue(cal_ctx* c, LanczosState& L, bool cgs = true) {
     const int s = L.s, m = 2 * s;
     const int64_t n = c->A.n_local, ld = c->A.ld;
     CAL_TRY(ensure_work(c, m + 2, ld));
@@ -200,6 +205,7 @@ static int newton_prologue(cal_ctx* c, LanczosState& L) {
             return set_error(c, CAL_ERR_NUMERIC, "Lanczos breakdown (beta = 0) in the Newton prologue");
         }
         CAL_HIP(c, launch_div(Qc(j + 1), r, beta[j], n, c->stream));  // :110
+        if (!cgs) continue;  // lanczos(...,'local') (restarted_ca_lanczos.m:65)
         // one CGS pass against Q(:,1:j) (lanczos.m:62-66)
         Panel Qj = panel();
         panel_add(Qj, Qc(0), ld, j + 1);
@@ -497,7 +503,7 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
     // (stream-ordered after this step's pass B) and the fixed shifts, so they
     // are enqueued (into the other V buffer) before the host waits for this
     // step's R: the GPU runs them while the host extends T and returns.
-    const bool prefetch = !diagnostics && L.mode == 0 && k + 1 <= L.max_outer;
+    const bool prefetch = !diagnostics && L.mode == 0 && !L.restart_inner && k + 1 <= L.max_outer;
     c->orth_redone = false;
     if (prefetch)
         c->pre_wait = [c, &L, k]() {
@@ -520,6 +526,19 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
         bool sh = false;
         CAL_TRY(normalize_dev(c, n, X, Qo, Rk.data(), 1.0e-8, &rank, &sh));
         if (rank < s + 1) L.info.n_rank_deficient++;
+        if (L.restart_inner) {
+            // [Q(:,1:s+1),R_] = projectAndNormalize({Q_conv},Q_,true) (restarted_ca_lanczos.m:291)
+            CAL_TRY(ensure_work(c, s + 1, ld));
+            double* dW = work_col(c, 0) + c->A.lpad;
+            CAL_HIP(c, hipMemcpyAsync(dW, L.col(0), (size_t)(s + 1) * ld * sizeof(double), hipMemcpyDeviceToDevice,
+                                      c->stream));
+            Panel Qc = panel(), Xw = panel();
+            if (L.next > 0) panel_add(Qc, L.dExt, ld, L.next);
+            panel_add(Xw, dW, ld, s + 1);
+            std::vector<double> Rq((size_t)std::max(L.next, 1) * (s + 1)), R_((size_t)(s + 1) * (s + 1));
+            PNResult r_;
+            CAL_TRY(project_and_normalize_dev(c, n, Qc, Xw, true, Qo, Rq.data(), R_.data(), &r_));
+        }
         L.reorth.push_back(0);
         status = extend_T_first(c, L, Rk);
     } else {
@@ -529,11 +548,13 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
         PanelOut Qo = panel_out(L.col((k - 1) * s + 1), ld, s);
         std::vector<double> Rq((size_t)(s + 1) * s), R((size_t)s * s);
         PNResult res;
-        if (L.mode == 3 && L.nritz > 0) {
-            // projectAndNormalize({Q block, QR(:,1:nritz)}, V(:,2:s+1)) (ca_lanczos.m:287)
+        const bool ext_local = L.restart_inner && L.mode == 0 && L.next > 0;
+        if ((L.mode == 3 && L.nritz > 0) || ext_local) {
+            // projectAndNormalize({Q block, QR(:,1:nritz)}, V(:,2:s+1)) (ca_lanczos.m:287), or
+            // against {Q block, Q_conv} (restarted_ca_lanczos.m:301)
             CAL_TRY(ensure_work(c, s, ld));
-            std::vector<double*> dQ{L.col((k - 2) * s), L.dQR + L.lpad};
-            const int widths[2] = {s + 1, L.nritz};
+            std::vector<double*> dQ{L.col((k - 2) * s), ext_local ? L.dExt : L.dQR + L.lpad};
+            const int widths[2] = {s + 1, ext_local ? L.next : L.nritz};
             std::vector<std::vector<double>> RZ;
             bool ro = false;
             int rk = s;
@@ -548,7 +569,23 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
         L.reorth.push_back(res.reorth ? 1 : 0);
         if (res.reorth) L.info.n_reorth++;
         if (res.reorth && res.rank < s) L.info.n_rank_deficient++;
-        if (L.full) {  // ca_lanczos.m:197
+        if (L.full && L.restart_inner) {
+            // Q(:,(k-1)s+2:ks+1) = projectAndNormalize({Q_conv,Q(:,1:(k-2)*s)},Q_,true)
+            // (restarted_ca_lanczos.m:309)
+            CAL_TRY(ensure_work(c, 2 * s, ld));
+            double* dW = work_col(c, 0) + c->A.lpad;
+            double* dY = work_col(c, s) + c->A.lpad;
+            CAL_HIP(c, hipMemcpyAsync(dW, L.col((k - 1) * s + 1), (size_t)s * ld * sizeof(double),
+                                      hipMemcpyDeviceToDevice, c->stream));
+            std::vector<double*> dQ{L.dExt ? L.dExt : L.col(0), L.col(0)};
+            const int widths[2] = {L.next, (k - 2) * s};
+            std::vector<std::vector<double>> RZ;
+            std::vector<double> R2((size_t)s * s);
+            bool ro = false;
+            int rk = s;
+            CAL_TRY(project_and_normalize_blocks_dev(c, n, ld, 2, dQ, widths, s, dW, true, dY, Qo, RZ, R2.data(),
+                                                     &ro, &rk));
+        } else if (L.full) {  // ca_lanczos.m:197
             Panel Qall = panel(), Xn = panel();
             panel_add(Qall, L.col(0), ld, (k - 1) * s + 1);
             panel_add(Xn, L.col((k - 1) * s + 1), ld, s);
@@ -715,6 +752,257 @@ int cal_ca_lanczos(cal_ctx* c, const double* r, int s, int iter, const char* bas
     if (Q) CAL_TRY(cal_lanczos_get_Q(c, 0, sk, Q));
     cal_lanczos_free_state(c);
     return status;
+}
+
+// ---- f2: explicit restart (restarted_ca_lanczos.m) ------------------------
+}  // extern "C"
+
+namespace {
+// ||A x - l x|| / ||l x|| of one device vector (ld layout, lpad origin)
+int rel_residual(cal_ctx* c, double* x, double l, double* out) {
+    const int64_t n = c->A.n_local;
+    const int nb = 256;
+    CAL_TRY(ensure_partial(c, (size_t)nb * 2));
+    CAL_TRY(ensure_red(c, 2));
+    CAL_TRY(halo_exchange(c, x));
+    SpmvArgs a{};
+    a.rowptr = c->A.rowptr;
+    a.col = c->A.col;
+    a.val = c->A.val;
+    a.x = x;
+    CAL_HIP(c, launch_spmv_resid(a, nullptr, l, 0.0, n, c->d_partial, nb, c->stream));
+    CAL_HIP(c, launch_reduce(c->d_partial, nb, 2, c->d_red, c->stream));
+    CAL_TRY(allreduce_sum(c, c->d_red, 2));
+    CAL_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    c->small_pending = false;
+    *out = std::sqrt(c->h_red[0]) / std::sqrt(c->h_red[1]);
+    return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int cal_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, int n_wanted, int s, const char* basis,
+                             const char* orth, double tol, int diagnostics, double* conv_eigs, double* Q_conv,
+                             double* rnorms, double* orth_err, cal_restart_info* info) {
+    constexpr int kMaxRestarts = 200;  // restarted_ca_lanczos.m:6
+    if (!c || !r || n_wanted < 1 || s < 1 || s > 15 || !basis || !orth || !conv_eigs)
+        return set_error(c, CAL_ERR_ARG, "restarted_ca_lanczos: bad arguments");
+    if (!c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
+    std::string o(orth), b(basis);
+    for (auto& ch : o) ch = (char)std::tolower(ch);
+    for (auto& ch : b) ch = (char)std::tolower(ch);
+    if (o != "local" && o != "full" && o != "periodic" && o != "selective")
+        return set_error(c, CAL_ERR_ARG, "lanczos.m: Invalid option value for orth: " + o);
+    if (o == "periodic" || o == "selective")  // lanczos_periodic / lanczos_selective are not defined there
+        return set_error(c, CAL_ERR_UNSUPPORTED, "restarted_ca_lanczos.m defines no lanczos_" + o);
+    if (b != "monomial" && b != "newton") return set_error(c, CAL_ERR_ARG, "ERROR: Unknown basis type: " + b);
+    const int iters = max_lanczos / s;  // :86
+    if (iters < 1) return set_error(c, CAL_ERR_ARG, "restarted_ca_lanczos: max_lanczos < s");
+    hipSetDevice(c->device);
+    const double t_start = now_ms();
+    const int64_t n = c->A.n_local, ld = c->A.ld;
+    cal_lanczos_free_state(c);
+    LanczosState* L = new LanczosState();
+    c->lz = L;
+    L->s = s;
+    L->max_outer = iters + 1;  // the inner loop runs iters+1 blocks (:277)
+    L->newton = b == "newton";
+    L->full = o == "full";
+    L->mode = L->full ? 1 : 0;
+    L->restart_inner = true;
+    L->n = n;
+    L->ld = ld;
+    L->lpad = c->A.lpad;
+    L->info.s = s;
+    const size_t qcols = (size_t)s * L->max_outer + 1;
+    CAL_HIP(c, hipMalloc((void**)&L->dQ, qcols * ld * sizeof(double)));
+    CAL_HIP(c, hipMalloc((void**)&L->dV, (size_t)2 * (s + 1) * ld * sizeof(double)));
+    CAL_HIP(c, hipMemsetAsync(L->dQ, 0, qcols * ld * sizeof(double), c->stream));
+    CAL_HIP(c, hipMemsetAsync(L->dV, 0, (size_t)2 * (s + 1) * ld * sizeof(double), c->stream));
+    L->Tld = s * L->max_outer + 1;
+    // converged vectors Q(:,1:nconv) (the reference's Q buffer, :74)
+    int qc_cap = n_wanted + s * iters;
+    double* dQc = nullptr;
+    CAL_HIP(c, hipMalloc((void**)&dQc, (size_t)qc_cap * ld * sizeof(double)));
+    struct FreeQc {
+        double*& p;
+        ~FreeQc() {
+            if (p) hipFree(p);
+        }
+    } free_qc{dQc};
+    double norm_A = 0.0;
+    CAL_TRY(normest_dev(c, &norm_A));  // :35
+    tol = tol * norm_A;                // :39
+    // q = r/norm(r) (:56)
+    CAL_HIP(c, hipMemcpyAsync(L->vcolumn(0), r, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    double rr = 0.0;
+    CAL_TRY(dot_host(c, n, L->vcolumn(0), L->vcolumn(0), &rr));
+    CAL_HIP(c, launch_div(L->col(0), L->vcolumn(0), std::sqrt(rr), n, c->stream));
+    if (L->newton) {
+        CAL_TRY(newton_prologue(c, *L, false));  // lanczos(A,q,2*s,'local') (:65)
+    } else {
+        L->Bk.assign((size_t)(s + 1) * s, 0.0);
+        for (int j = 0; j < s; ++j) L->Bk[(j + 1) + (size_t)j * (s + 1)] = 1.0;
+    }
+    std::vector<double> ceigs, crn, rn_hist, oe_hist;
+    std::vector<double> rn_row(n_wanted, 0.0);
+    int nconv = 0, num_restarts = 0;
+    bool restart = true;
+    const int m = s * iters;
+    while (restart && num_restarts < kMaxRestarts) {
+        num_restarts++;
+        // fresh inner run from q = Q(:,1)
+        L->k = 0;
+        L->T.assign((size_t)L->Tld * L->Tld, 0.0);
+        L->b.clear();
+        L->reorth.clear();
+        L->breakdown = false;
+        L->powers_ready = false;
+        L->dExt = dQc + c->A.lpad;
+        L->next = nconv;
+        for (int it = 0; it <= iters; ++it) {
+            const int st = lanczos_step(c, 0);
+            if (st < 0) return st;
+            if (st == CAL_WARN_BREAKDOWN) return set_error(c, CAL_WARN_BREAKDOWN, "restart: inner CA-Lanczos breakdown");
+        }
+        // eig(T(1:m,1:m)), beta = T(m+1,m) (:105-107); unit-norm eigenvectors
+        std::vector<double> Tm((size_t)m * m), wr(m), wi(m), V((size_t)m * m);
+        for (int j = 0; j < m; ++j)
+            for (int i = 0; i < m; ++i) Tm[i + (size_t)j * m] = L->T[i + (size_t)j * L->Tld];
+        if (cal_eig(m, Tm.data(), m, wr.data(), wi.data(), V.data()) != 0)
+            return set_error(c, CAL_ERR_NUMERIC, "eig(T) did not converge");
+        const double beta = L->T[m + (size_t)(m - 1) * L->Tld];
+        std::vector<double> rnz(m);
+        for (int j = 0; j < m; ++j) {
+            double nv = 0.0;
+            for (int i = 0; i < m; ++i) nv += V[i + (size_t)j * m] * V[i + (size_t)j * m];
+            nv = std::sqrt(nv);
+            for (int i = 0; i < m; ++i) V[i + (size_t)j * m] /= nv;
+            // complex pairs never count as converged (deviation: the reference would
+            // carry complex Ritz vectors)
+            rnz[j] = wi[j] != 0.0 ? HUGE_VAL : beta * std::fabs(V[(m - 1) + (size_t)j * m]);
+        }
+        // push converged pairs to the front (:114-126)
+        int k = 0;
+        for (int i = 0; i < m; ++i)
+            if (rnz[i] < tol) {
+                std::swap(wr[i], wr[k]);
+                std::swap(wi[i], wi[k]);
+                std::swap(rnz[i], rnz[k]);
+                for (int q = 0; q < m; ++q) std::swap(V[q + (size_t)i * m], V[q + (size_t)k * m]);
+                ++k;
+            }
+        // Q(:,nconv+i) = Q_new*Vp(:,i) (:129-133)
+        if (nconv + k > qc_cap) {
+            const int cap2 = std::max(nconv + k, 2 * qc_cap);
+            double* p2 = nullptr;
+            CAL_HIP(c, hipMalloc((void**)&p2, (size_t)cap2 * ld * sizeof(double)));
+            CAL_HIP(c, hipMemcpyAsync(p2, dQc, (size_t)nconv * ld * sizeof(double), hipMemcpyDeviceToDevice,
+                                      c->stream));
+            CAL_HIP(c, hipStreamSynchronize(c->stream));
+            hipFree(dQc);
+            dQc = p2;
+            qc_cap = cap2;
+        }
+        Panel Qn = panel();
+        panel_add(Qn, L->col(0), ld, m);
+        if (k > 0) {
+            PanelOut Y = panel_out(dQc + c->A.lpad + (size_t)nconv * ld, ld, k);
+            CAL_TRY(apply_host(c, n, Qn, V.data(), k, &Y, nullptr, 0, nullptr));
+        }
+        for (int i = 0; i < k; ++i) {
+            ceigs.push_back(wr[i]);
+            crn.push_back(rnz[i]);
+        }
+        if (diagnostics) {  // :140-165
+            std::vector<double> row(n_wanted, 0.0);
+            for (int i = 0; i < std::min(nconv, n_wanted); ++i) row[i] = rn_row[i];
+            for (int i = 0; i < k && nconv + i < n_wanted; ++i)
+                CAL_TRY(rel_residual(c, dQc + c->A.lpad + (size_t)(nconv + i) * ld, ceigs[nconv + i],
+                                     &row[nconv + i]));
+            std::vector<int> ix;
+            for (int j = k; j < m; ++j) ix.push_back(j);
+            std::stable_sort(ix.begin(), ix.end(), [&](int a, int b2) { return wr[a] > wr[b2]; });
+            const int extra = n_wanted - nconv - k;
+            if (extra > 0) {
+                CAL_TRY(ensure_work(c, 1, ld));
+                double* x = work_col(c, 0) + c->A.lpad;
+                for (int i = 0; i < extra && i < (int)ix.size(); ++i) {
+                    PanelOut X1 = panel_out(x, ld, 1);
+                    CAL_TRY(apply_host(c, n, Qn, V.data() + (size_t)ix[i] * m, 1, &X1, nullptr, 0, nullptr));
+                    CAL_TRY(rel_residual(c, x, wr[ix[i]], &row[nconv + k + i]));
+                }
+            }
+            rn_row = row;
+            rn_hist.insert(rn_hist.end(), row.begin(), row.end());
+            // ||I - Q_'Q_||_F, Q_ = [Q_conv Q_new] (:162-165)
+            const int wq = nconv + m;
+            Panel Aall = panel();
+            if (nconv > 0) panel_add(Aall, dQc + c->A.lpad, ld, nconv);
+            panel_add(Aall, L->col(0), ld, m);
+            double fro = 0.0;
+            for (int j0 = 0, nbb = 0; j0 < wq; j0 += nbb) {
+                // chunks of <= 16 columns that do not straddle the two blocks
+                nbb = std::min(16, (j0 < nconv ? nconv : wq) - j0);
+                Panel B2 = panel();
+                const double* bp = j0 < nconv ? dQc + c->A.lpad + (size_t)j0 * ld : L->col(j0 - nconv);
+                panel_add(B2, bp, ld, nbb);
+                std::vector<double> G((size_t)wq * nbb);
+                CAL_TRY(gram_host(c, n, Aall, B2, G.data()));
+                for (int jj = 0; jj < nbb; ++jj)
+                    for (int ii = 0; ii < wq; ++ii) {
+                        const double d = (ii == j0 + jj ? 1.0 : 0.0) - G[ii + (size_t)jj * wq];
+                        fro += d * d;
+                    }
+            }
+            oe_hist.push_back(std::sqrt(fro));
+        }
+        nconv += k;
+        restart = (int)ceigs.size() < n_wanted;  // check_wanted_eigs (:236-253)
+        if (restart) {
+            // generateStartVector 'largest' (:200-214): MATLAB '>' compares real parts
+            int l = std::min(k, m - 1);
+            for (int j = k; j < m; ++j)
+                if (wr[j] > wr[l]) l = j;
+            CAL_TRY(ensure_work(c, 1, ld));
+            double* x = work_col(c, 0) + c->A.lpad;
+            PanelOut X1 = panel_out(x, ld, 1);
+            CAL_TRY(apply_host(c, n, Qn, V.data() + (size_t)l * m, 1, &X1, nullptr, 0, nullptr));
+            double xx = 0.0;
+            CAL_TRY(dot_host(c, n, x, x, &xx));
+            CAL_HIP(c, launch_div(L->col(0), x, std::sqrt(xx), n, c->stream));
+        }
+    }
+    // sort descending, keep n_wanted (or all, if not converged) (:180-196)
+    std::vector<int> ix(ceigs.size());
+    for (size_t i = 0; i < ix.size(); ++i) ix[i] = (int)i;
+    std::stable_sort(ix.begin(), ix.end(), [&](int a, int b2) { return ceigs[a] > ceigs[b2]; });
+    const int keep = restart ? nconv : n_wanted;
+    for (int i = 0; i < keep; ++i) conv_eigs[i] = ceigs[ix[i]];
+    if (Q_conv)
+        for (int i = 0; i < keep; ++i)
+            CAL_HIP(c, hipMemcpy(Q_conv + (size_t)i * n, dQc + c->A.lpad + (size_t)ix[i] * ld, n * sizeof(double),
+                                 hipMemcpyDeviceToHost));
+    if (rnorms)
+        for (int rI = 0; rI < (int)rn_hist.size() / std::max(n_wanted, 1); ++rI)
+            for (int j = 0; j < n_wanted; ++j)
+                rnorms[rI + (size_t)j * kMaxRestarts] = rn_hist[(size_t)rI * n_wanted + j];
+    if (orth_err)
+        for (size_t i = 0; i < oe_hist.size(); ++i) orth_err[i] = oe_hist[i];
+    if (info) {
+        info->num_restarts = num_restarts;
+        info->nconv = keep;
+        info->converged = restart ? 0 : 1;
+        info->norm_A = norm_A;
+        double mx = 0.0;
+        for (int i = 0; i < keep; ++i) mx = std::max(mx, crn[ix[i]]);
+        info->max_ritz_norm = mx;
+        info->ms = now_ms() - t_start;
+    }
+    cal_lanczos_free_state(c);
+    return 0;
 }
 
 // ---- host-only exports (calanczos_host.h) ----------------------------------

@@ -157,6 +157,27 @@ int cal_lanczos_get(cal_ctx* ctx, double* T, int ldt, double* rn, double* oe, in
 int cal_lanczos_get_Q(cal_ctx* ctx, int64_t col0, int ncols, double* Q);
 int cal_lanczos_end(cal_ctx* ctx);
 
+/* ---- f2: explicit restart ------------------------------------------------ */
+typedef struct cal_restart_info {
+    int num_restarts;      /* restarts run (<= 200)                                */
+    int nconv;             /* eigenpairs returned                                  */
+    int converged;         /* 1 if n_wanted eigenpairs converged                   */
+    double norm_A;         /* normest(A)                                           */
+    double max_ritz_norm;  /* largest beta|y_m| estimate among the returned pairs  */
+    double ms;             /* wall time                                            */
+} cal_restart_info;
+
+/* [E,V,nres,rnorms,orth_err] = restarted_ca_lanczos(A,r,max_lanczos,
+ * n_wanted_eigs,s,basis,orth,tol)  (restarted_ca_lanczos.m:4-198, restart
+ * strategy 'largest').  orth in {"local","full"} (the reference defines no
+ * periodic/selective inner solver).  Outputs: conv_eigs (n_wanted, descending;
+ * info->nconv valid), Q_conv (n x n_wanted, may be NULL), rnorms (200 x
+ * n_wanted column-major, rows 1..num_restarts, may be NULL; needs
+ * diagnostics), orth_err (200, may be NULL; needs diagnostics). */
+int cal_restarted_ca_lanczos(cal_ctx* ctx, const double* r, int max_lanczos, int n_wanted, int s, const char* basis,
+                             const char* orth, double tol, int diagnostics, double* conv_eigs, double* Q_conv,
+                             double* rnorms, double* orth_err, cal_restart_info* info);
+
 /* ---- multi-GPU (row slabs, RCCL over xGMI) ------------------------------ */
 /* 128-byte RCCL unique id; broadcast it out of band (e.g. torch.distributed). */
 int cal_comm_unique_id(void* id128);

@@ -551,9 +551,10 @@ def newton_basis_matrix(lam, s, modifiedp=0):
     return B
 
 
-def newton_change_of_basis(A, q, s):
-    """ca_lanczos.m:66-72: 2s-step Lanczos ('full'), eig, Leja order, B matrix."""
-    _, T, _, _ = lanczos(A, q, 2 * s, "full")
+def newton_change_of_basis(A, q, s, orth="full"):
+    """ca_lanczos.m:66-72: 2s-step Lanczos ('full'), eig, Leja order, B matrix
+    (restarted_ca_lanczos.m:63-68 uses orth 'local')."""
+    _, T, _, _ = lanczos(A, q, 2 * s, orth)
     basis_eigs = matlab_eig(T)[0]
     shifts, _ = leja(basis_eigs, "nonmodified")
     Bk = newton_basis_matrix(shifts, s, 1)
@@ -925,3 +926,124 @@ def laplacian_2d_eigs(N: int) -> np.ndarray:
 def laplacian_3d_eigs(N: int) -> np.ndarray:
     c = 2.0 - 2.0 * np.cos(np.arange(1, N + 1) * np.pi / (N + 1))
     return np.sort((c[:, None, None] + c[None, :, None] + c[None, None, :]).ravel())
+
+
+# --------------------------------------------------------------------------
+# f2: the explicit restart driver (restarted_ca_lanczos.m)
+# --------------------------------------------------------------------------
+
+def _restart_lanczos_basic(A, Q_conv, q, Bk, maxiter, s, basis, orth):
+    """restarted_ca_lanczos.m:261-367 (``lanczos_basic`` of that file): CA-
+    Lanczos kept orthogonal to the converged vectors Q_conv.  Quirk kept: the
+    loop runs maxiter+1 outer iterations (``while k <= maxiter``) and the
+    output is trimmed to s*maxiter columns (:364-366)."""
+    n = len(q)
+    Q = np.zeros((n, (maxiter + 1) * s + 1))
+    Q[:, 0] = q
+    b = np.zeros(maxiter + 2)
+    T = None
+    k = 0
+    while k <= maxiter:                                         # :277
+        k += 1
+        if k > 1:
+            q = Q[:, (k - 1) * s]
+        V = matrix_powers(A, q, s, Bk, basis)
+        if k == 1:
+            Q_, Rk, _ = normalize(V[:, : s + 1])                # :289
+            Qn, _ = projectAndNormalize([Q_conv], Q_, True)     # :291
+            Q[:, : s + 1] = Qn
+            T = _rdiv_upper(Rk @ Bk, Rk[:s, :s])                # :293
+            b[0] = T[s, s - 1]
+        else:
+            Qp = Q[:, (k - 2) * s : (k - 1) * s + 1]
+            if orth == "local":                                 # :300-304
+                Q_, Rk_ = projectAndNormalize([Qp, Q_conv], V[:, 1 : s + 1], True)
+                Q[:, (k - 1) * s + 1 : k * s + 1] = Q_[:, :s]
+                Rkk_s, Rk_s = Rk_[0], Rk_[2]
+            else:                                               # 'fro' :305-310
+                Q_, Rk_ = projectAndNormalize([Qp], V[:, 1 : s + 1], True)
+                Rkk_s, Rk_s = Rk_[0], Rk_[1]
+                Qf, _ = projectAndNormalize([Q_conv, Q[:, : (k - 2) * s]], Q_, True)
+                Q[:, (k - 1) * s + 1 : k * s + 1] = Qf
+            T = _extend_T(T, b, k, s, Bk, Rkk_s, Rk_s)
+    return Q[:, : s * (k - 1)], T[: s * (k - 1) + 1, : s * (k - 1)]   # :364-366
+
+
+def restarted_ca_lanczos(A, r, max_lanczos, n_wanted_eigs=10, s=6, basis="newton", orth="local", tol=1.0e-8,
+                         max_restarts=200, diagnostics=True):
+    """``[E,V,nres,rnorms,orth_err] = restarted_ca_lanczos(A,r,max_lanczos,
+    n_wanted_eigs,s,basis,orth,tol)`` -- restarted_ca_lanczos.m:4-198 with
+    restart_strategy 'largest'.  Only 'local' and 'full' exist in the
+    reference (its lanczos_periodic / lanczos_selective are not defined).
+    Returns (conv_eigs, Q_conv, num_restarts, rnorms, orth_err, converged)."""
+    o = orth.lower()
+    if o not in ("local", "full"):
+        raise NotImplementedError("restarted_ca_lanczos.m defines no lanczos_%s" % o)
+    norm_A = normest(A)                                         # :35
+    tol = tol * norm_A                                          # :39
+    n = len(r)
+    q = r / math.sqrt(r @ r)                                    # :56
+    if basis.lower() == "monomial":
+        Bk = np.eye(s + 1)[:, 1 : s + 1]
+    else:
+        Bk, _, _ = newton_change_of_basis(A, q, s, "local")     # :63-68
+    Qc = np.zeros((n, 0))
+    conv_eigs, conv_rnorms = [], []
+    rnorms = np.zeros((max_restarts, n_wanted_eigs))
+    orth_err = []
+    num_restarts, nconv, restart = 0, 0, True
+    while restart and num_restarts < max_restarts:              # :81
+        num_restarts += 1
+        iters = max_lanczos // s                                # :86
+        if iters == 0:
+            break
+        Q_new, T = _restart_lanczos_basic(A, Qc[:, :nconv], q, Bk, iters, s, basis.lower(),
+                                          "local" if o == "local" else "fro")
+        m = s * iters
+        w, Vp = matlab_eig(T[:m, :m])                           # :106
+        w = np.real(w)
+        Vp = np.real(Vp) / np.linalg.norm(np.real(Vp), axis=0)
+        beta = T[m, m - 1]                                      # :107
+        ritz_norms = beta * np.abs(Vp[m - 1, :])                # :108-111
+        k = 0
+        for i in range(m):                                      # :114-126
+            if ritz_norms[i] < tol:
+                k += 1
+                w[[i, k - 1]] = w[[k - 1, i]]
+                Vp[:, [i, k - 1]] = Vp[:, [k - 1, i]]
+                ritz_norms[[i, k - 1]] = ritz_norms[[k - 1, i]]
+        newQ = Q_new @ Vp[:, :k]                                # :129-133
+        Qc = np.hstack([Qc[:, :nconv], newQ])
+        conv_eigs += list(w[:k])
+        conv_rnorms += list(ritz_norms[:k])
+        if diagnostics:                                         # :140-159
+            if num_restarts > 1:
+                rnorms[num_restarts - 1, :nconv] = rnorms[num_restarts - 2, :nconv]
+            for i in range(k):
+                if nconv + i < n_wanted_eigs:
+                    lv, x = conv_eigs[nconv + i], Qc[:, nconv + i]
+                    rnorms[num_restarts - 1, nconv + i] = np.linalg.norm(A @ x - lv * x) / np.linalg.norm(lv * x)
+            rest = w[k:]
+            ix = _sort_perm(rest, True)
+            for i in range(n_wanted_eigs - nconv - k):
+                lv = rest[ix[i]]
+                x = Q_new @ Vp[:, k + ix[i]]
+                rnorms[num_restarts - 1, nconv + i + k] = np.linalg.norm(A @ x - lv * x) / np.linalg.norm(lv * x)
+            Q_ = np.hstack([Qc[:, :nconv], Q_new])              # :162-165
+            orth_err.append(np.linalg.norm(np.eye(Q_.shape[1]) - Q_.T @ Q_, "fro"))
+        nconv += k
+        restart = len(conv_eigs) < n_wanted_eigs                # check_wanted_eigs :236-253
+        if restart:                                             # generateStartVector 'largest' :200-214
+            l = k
+            for j in range(k, m):
+                if w[j] > w[l]:
+                    l = j
+            q = Q_new @ Vp[:, l]
+            q = q / math.sqrt(q @ q)
+    ce = np.array(conv_eigs)
+    ix = _sort_perm(ce, True)                                   # :180-196
+    keep = n_wanted_eigs if not restart else nconv
+    ix = ix[:keep]
+    return dict(conv_eigs=ce[ix], conv_rnorms=np.array(conv_rnorms)[ix], Q_conv=Qc[:, ix],
+                num_restarts=num_restarts, rnorms=rnorms[:num_restarts], orth_err=np.array(orth_err),
+                converged=not restart, norm_A=norm_A)

@@ -379,3 +379,49 @@ def test_ca_lanczos_periodic_selective(cal, ref, orth):
     w, we = np.sort(np.linalg.eigvals(out.T).real), np.sort(np.linalg.eigvals(exp.T).real)
     assert abs(w[-1] - we[-1]) <= 1e-10 * normA and abs(w[0] - we[0]) <= 1e-10 * normA
     assert np.max(out.orth_err) < 1e-6 and np.max(exp.orth_err) < 1e-6
+
+
+def test_restarted_ca_lanczos(cal, ref):
+    """the explicit restart driver on the reference's own input
+    (test_restart_diagonal_matrices.m:8-28: diag(linspace(1,1e4,5000)),
+    r = ones, max_lanczos 60, 10 wanted, s = 4, newton, 'full', tol 1e-8).
+    Known answer: the 10 largest diagonal entries; the oracle's restart count
+    and eigenvalues; the converged vectors orthonormal eigenvectors."""
+    import scipy.sparse as sp
+    a = ref.matlab_linspace(1.0, 1.0e4, 5000)
+    A = sp.csr_matrix(sp.diags(a))
+    r = np.ones(5000)
+    exp = ref.restarted_ca_lanczos(A, r, 60, 10, 4, "newton", "full", 1.0e-8)
+    out = cal.restarted_ca_lanczos(A, r, 60, 10, 4, "newton", "full", 1.0e-8)
+    assert out["converged"] and exp["converged"]
+    assert out["num_restarts"] == exp["num_restarts"]
+    eref = a[::-1][:10]
+    assert np.max(np.abs(out["conv_eigs"] - eref)) <= 1e-8 * 1.0e4
+    assert np.max(np.abs(out["conv_eigs"] - exp["conv_eigs"])) <= 1e-9 * 1.0e4
+    V = out["Q_conv"]
+    assert np.max(np.abs(V.T @ V - np.eye(10))) < 1e-8
+    res = np.linalg.norm(A @ V - V * out["conv_eigs"], axis=0) / np.abs(out["conv_eigs"])
+    assert np.max(res) < 1e-6
+    assert np.max(out["orth_err"]) < 1e-10
+
+
+def test_restarted_ca_lanczos_local_lap2d(cal, ref):
+    """'local' restart on a 2-D Laplacian: the 4 largest eigenvalues (closed form)."""
+    A = cal.matrices.laplacian_2d(30)
+    r = ref.matlab_rand(900, seed=2)
+    exp = ref.restarted_ca_lanczos(A, r, 48, 4, 8, "newton", "local", 1.0e-8)
+    out = cal.restarted_ca_lanczos(A, r, 48, 4, 8, "newton", "local", 1.0e-8)
+    eref = ref.laplacian_2d_eigs(30)[::-1]
+    assert out["converged"] == exp["converged"]
+    if out["converged"]:
+        assert np.max(np.abs(out["conv_eigs"] - eref[:4])) <= 1e-7 * 8.0
+    # 'local' keeps no global orthogonality and lap2d has a double eigenvalue,
+    # so the restart count is a chaotic function of rounding: a 1e-15 relative
+    # perturbation of r moves the oracle itself between 9 and 10 restarts.
+    # Parity is the oracle's spread over ulp-perturbed start vectors.
+    rng = np.random.default_rng(0)
+    counts = {exp["num_restarts"]}
+    for _ in range(5):
+        rp = r * (1.0 + 1.0e-15 * rng.standard_normal(r.shape[0]))
+        counts.add(ref.restarted_ca_lanczos(A, rp, 48, 4, 8, "newton", "local", 1.0e-8)["num_restarts"])
+    assert min(counts) <= out["num_restarts"] <= max(counts), (out["num_restarts"], counts)

@@ -117,3 +117,43 @@ def test_leja_is_leja(ref):
 
 def test_fixture_files_present():
     assert len(glob.glob(os.path.join(GOLD, "*.npz"))) >= 7
+
+
+def test_restarted_oracle_diagonal_known_answer(ref):
+    """restarted_ca_lanczos on test_restart_diagonal_matrices.m:8-28's input:
+    diag(linspace(1,1e4,5000)), r = ones, 60 vectors, 10 wanted, s = 4,
+    newton, 'full', tol 1e-8.  Known answer: the 10 largest diagonal entries,
+    orthonormal eigenvectors, residual history below tol at the end."""
+    import scipy.sparse as sp
+    a = ref.matlab_linspace(1.0, 1.0e4, 5000)
+    A = sp.csr_matrix(sp.diags(a))
+    out = ref.restarted_ca_lanczos(A, np.ones(5000), 60, 10, 4, "newton", "full", 1.0e-8)
+    assert out["converged"]
+    assert np.max(np.abs(out["conv_eigs"] - a[::-1][:10])) <= 1e-8 * 1.0e4
+    V = out["Q_conv"]
+    assert np.max(np.abs(V.T @ V - np.eye(10))) < 1e-8
+    assert np.all(np.diff(out["conv_eigs"]) <= 0)                # descending (:180-196)
+    assert out["rnorms"].shape == (out["num_restarts"], 10)
+    assert np.max(out["rnorms"][-1]) < 1e-6
+    assert np.max(out["orth_err"]) < 1e-10
+    # normest (power iteration, stops at 1e-6 relative change) under-estimates
+    # ||A|| = 1e4 on this clustered top spectrum
+    assert 0.99e4 <= out["norm_A"] <= 1.0e4 * (1 + 1e-12)
+
+
+def test_restarted_oracle_local_lap2d(ref):
+    """'local' restart on lap2d(30): the 4 largest eigenvalues in closed form,
+    including the double eigenvalue 2(2 - cos(pi/31) - cos(2 pi/31))."""
+    A = ref.laplacian_2d(30)
+    out = ref.restarted_ca_lanczos(A, ref.matlab_rand(900, seed=2), 48, 4, 8, "newton", "local", 1.0e-8)
+    assert out["converged"]
+    eref = ref.laplacian_2d_eigs(30)[::-1][:4]
+    assert np.max(np.abs(out["conv_eigs"] - eref)) <= 8e-7
+
+
+def test_restarted_oracle_rejects_undefined_orth(ref):
+    # restarted_ca_lanczos.m dispatches to lanczos_periodic/_selective, which
+    # the reference never defines (SURVEY §8f2)
+    import scipy.sparse as sp
+    with pytest.raises(NotImplementedError):
+        ref.restarted_ca_lanczos(sp.eye(50, format="csr"), np.ones(50), 12, 2, 4, "newton", "periodic")
