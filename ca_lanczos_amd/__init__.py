@@ -2,7 +2,8 @@
 
 Drop-in for the reference's hot-path functions (SpMV.m,
 matrix_powers_{monomial,newton}.m, tsqr.m, cholqr.m, project.m,
-normalize.m, projectAndNormalize.m, ca_lanczos.m, restarted_ca_lanczos.m) behind the C ABI of
+normalize.m, projectAndNormalize.m, ca_lanczos.m, restarted_ca_lanczos.m,
+impl_restarted_ca_lanczos.m) behind the C ABI of
 include/calanczos.h; see DESIGN.md and INTEGRATION.md.
 """
 from ._lib import CalError, LIB_PATH  # noqa: F401  (raises ImportError if the .so is missing)
@@ -25,6 +26,7 @@ from .api import (  # noqa: F401
     projectAndNormalize,
     projectAndNormalize_ex,
     restarted_ca_lanczos,
+    impl_restarted_ca_lanczos,
     tsqr,
 )
 from . import matrices  # noqa: F401

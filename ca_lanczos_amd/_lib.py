@@ -99,6 +99,8 @@ SIGNATURES = [
     ("cal_restarted_ca_lanczos", c_int,
      [c_void_p, dp, c_int, c_int, c_int, c_char_p, c_char_p, c_double, c_int, dp, dp, dp, dp,
       POINTER(RestartInfo)]),
+    ("cal_impl_restarted_ca_lanczos", c_int,
+     [c_void_p, dp, c_int, c_int, c_int, c_char_p, c_char_p, c_double, dp, dp, dp, POINTER(RestartInfo)]),
     ("cal_comm_unique_id", c_int, [c_void_p]),
     ("cal_comm_init_rccl", c_int, [c_void_p, c_int, c_int, c_void_p]),
     ("cal_comm_init_host", c_int, [c_void_p, c_int, c_int, ALLREDUCE_FN, EXCHANGE_FN, c_void_p]),

@@ -352,9 +352,11 @@ static int extend_T_first(cal_ctx* c, LanczosState& L, const std::vector<double>
     return 0;
 }
 
-static int extend_T(cal_ctx* c, LanczosState& L, const std::vector<double>& Rkk_s, const std::vector<double>& Rk_s) {
-    (void)c;
-    const int s = L.s, s1 = s + 1, k = L.k;
+// Tk (s x s) and the next beta of one block (ca_lanczos.m:200-214) from the
+// block's projection coefficients Rkk_s ((s+1) x s) and R factor Rk_s (s x s).
+static int block_T(const std::vector<double>& Bk, int s, double bprev, const std::vector<double>& Rkk_s,
+                   const std::vector<double>& Rk_s, std::vector<double>& Tk, double* bnew) {
+    const int s1 = s + 1;
     // Rk = [e1, [Rkk_s(s+1,1:s); Rk_s]]  ((s+1) x (s+1))
     std::vector<double> Rk((size_t)s1 * s1, 0.0);
     Rk[0] = 1.0;
@@ -370,16 +372,12 @@ static int extend_T(cal_ctx* c, LanczosState& L, const std::vector<double>& Rkk_
         for (int i = 0; i < s; ++i) Rkk11[i + (size_t)j * s] = Rkk_s[i + (size_t)(j - 1) * s1];
     const double rho = Rk[s + (size_t)s * s1];
     const double rho_t = Rk[(s - 1) + (size_t)(s - 1) * s1];
-    const double bk = L.Bk[s + (size_t)(s - 1) * s1];
-    const double bprev = L.b[k - 2];
-    if (rho_t == 0.0) {
-        L.breakdown = true;
-        return CAL_WARN_BREAKDOWN;
-    }
+    const double bk = Bk[s + (size_t)(s - 1) * s1];
+    if (rho_t == 0.0) return CAL_WARN_BREAKDOWN;
     // term1 = R11*Bk(1:s,:)/R11
     std::vector<double> B11((size_t)s * s), t1((size_t)s * s), t3((size_t)s * s, 0.0);
     for (int j = 0; j < s; ++j)
-        for (int i = 0; i < s; ++i) B11[i + (size_t)j * s] = L.Bk[i + (size_t)j * s1];
+        for (int i = 0; i < s; ++i) B11[i + (size_t)j * s] = Bk[i + (size_t)j * s1];
     dense::matmul(s, s, s, R11.data(), s, B11.data(), s, t1.data(), s);
     dense::rdiv_upper(s, s, t1.data(), s, R11.data(), s);
     // term2 = ((bk/rho_t)*zk)*es'  (last column only)
@@ -387,19 +385,40 @@ static int extend_T(cal_ctx* c, LanczosState& L, const std::vector<double>& Rkk_
     // term3 = (((b(k-1)*e1)*es')*Rkk(1:s,1:s))/R11  (first row only)
     for (int j = 0; j < s; ++j) t3[0 + (size_t)j * s] = bprev * Rkk11[(s - 1) + (size_t)j * s];
     dense::rdiv_upper(s, s, t3.data(), s, R11.data(), s);
-    const int m0 = s * (k - 1);
+    Tk.assign((size_t)s * s, 0.0);
     for (int j = 0; j < s; ++j)
         for (int i = 0; i < s; ++i) {
             double v = t1[i + (size_t)j * s];
             if (j == s - 1) v = v + f * Rk[i + (size_t)s * s1];
             v = v - t3[i + (size_t)j * s];
-            L.T[(m0 + i) + (size_t)(m0 + j) * L.Tld] = v;
+            Tk[i + (size_t)j * s] = v;
         }
-    const double bk_new = bk * (rho / rho_t);  // :214
-    L.b.push_back(bk_new);
-    L.T[(m0 - 1) + (size_t)m0 * L.Tld] = bprev;               // T12
-    L.T[m0 + (size_t)(m0 - 1) * L.Tld] = bprev;               // T21
-    L.T[(m0 + s) + (size_t)(m0 + s - 1) * L.Tld] = bk_new;    // T32
+    *bnew = bk * (rho / rho_t);  // :214
+    return 0;
+}
+
+// place block Tk at column m0 of T with the couplings b(k-1) and b(k) (:217-223)
+static void place_T(LanczosState& L, int m0, const std::vector<double>& Tk, double bprev, double bnew) {
+    const int s = L.s;
+    for (int j = 0; j < s; ++j)
+        for (int i = 0; i < s; ++i) L.T[(m0 + i) + (size_t)(m0 + j) * L.Tld] = Tk[i + (size_t)j * s];
+    L.T[(m0 - 1) + (size_t)m0 * L.Tld] = bprev;            // T12
+    L.T[m0 + (size_t)(m0 - 1) * L.Tld] = bprev;            // T21
+    L.T[(m0 + s) + (size_t)(m0 + s - 1) * L.Tld] = bnew;   // T32
+}
+
+static int extend_T(cal_ctx* c, LanczosState& L, const std::vector<double>& Rkk_s, const std::vector<double>& Rk_s) {
+    (void)c;
+    const int k = L.k;
+    std::vector<double> Tk;
+    double bnew = 0.0;
+    const double bprev = L.b[k - 2];
+    if (block_T(L.Bk, L.s, bprev, Rkk_s, Rk_s, Tk, &bnew) != 0) {
+        L.breakdown = true;
+        return CAL_WARN_BREAKDOWN;
+    }
+    L.b.push_back(bnew);
+    place_T(L, L.s * (k - 1), Tk, bprev, bnew);
     return 0;
 }
 
@@ -998,6 +1017,248 @@ int cal_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, int n
         info->norm_A = norm_A;
         double mx = 0.0;
         for (int i = 0; i < keep; ++i) mx = std::max(mx, crn[ix[i]]);
+        info->max_ritz_norm = mx;
+        info->ms = now_ms() - t_start;
+    }
+    cal_lanczos_free_state(c);
+    return 0;
+}
+
+// ---- f3: implicit restart (impl_restarted_ca_lanczos.m, the intended IRL) --
+}  // extern "C"
+
+namespace {
+// One CA block of lanczos_basic (impl_restarted_ca_lanczos.m:366-424) starting
+// at column nvecs: s matrix powers from Q(:,nvecs+1); at nvecs == 0 the
+// first block is normalised (:371-380), otherwise V(:,2:s+1) is projected
+// against {Q(:,1:nvecs-s), Q(:,nvecs-s+1:nvecs+1)} ('full', :387-392; doreorth
+// true, see oracle/ca_lanczos_ref.irl_lanczos_basic) and T is extended.
+int irl_block(cal_ctx* c, LanczosState& L, int nvecs, double* bprev) {
+    const int s = L.s;
+    const int64_t n = c->A.n_local, ld = L.ld;
+    const double* q = L.col(nvecs);
+    for (int i = 0; i < s; ++i) {
+        const double* x = (i == 0) ? q : L.vcolumn(i);
+        if (L.newton)
+            CAL_TRY(spmv_dev(c, x, L.vcolumn(i + 1), 1, L.Bk[i + (size_t)i * (s + 1)], 0.0, nullptr));
+        else
+            CAL_TRY(spmv_dev(c, x, L.vcolumn(i + 1), 0, 0.0, 0.0, nullptr));
+    }
+    if (nvecs == 0) {
+        Panel X = panel();
+        panel_add(X, q, ld, 1);
+        panel_add(X, L.vcolumn(1), ld, s);
+        std::vector<double> Rk((size_t)(s + 1) * (s + 1));
+        int rank = 0;
+        bool sh = false;
+        CAL_TRY(normalize_dev(c, n, X, panel_out(L.col(0), ld, s + 1), Rk.data(), 1.0e-8, &rank, &sh));
+        if (rank < s + 1) L.info.n_rank_deficient++;
+        if (extend_T_first(c, L, Rk) != 0) return set_error(c, CAL_WARN_BREAKDOWN, "IRL: breakdown in the first block");
+        *bprev = L.b[0];
+        return 0;
+    }
+    CAL_TRY(ensure_work(c, s, ld));
+    std::vector<double*> dQ;
+    std::vector<int> widths;
+    if (nvecs - s > 0) {
+        dQ.push_back(L.col(0));
+        widths.push_back(nvecs - s);
+    }
+    dQ.push_back(L.col(nvecs - s));
+    widths.push_back(s + 1);
+    std::vector<std::vector<double>> RZ;
+    std::vector<double> R((size_t)s * s);
+    bool ro = false;
+    int rk = s;
+    CAL_TRY(project_and_normalize_blocks_dev(c, n, ld, (int)dQ.size(), dQ, widths.data(), s, L.vcolumn(1), true,
+                                             work_col(c, 0) + c->A.lpad, panel_out(L.col(nvecs + 1), ld, s), RZ,
+                                             R.data(), &ro, &rk));
+    if (ro) L.info.n_reorth++;
+    if (ro && rk < s) L.info.n_rank_deficient++;
+    std::vector<double> Tk;
+    double bnew = 0.0;
+    if (block_T(L.Bk, s, *bprev, RZ.back(), R, Tk, &bnew) != 0)
+        return set_error(c, CAL_WARN_BREAKDOWN, "IRL: CA-Lanczos breakdown (rho_t = 0)");
+    place_T(L, nvecs, Tk, *bprev, bnew);
+    *bprev = bnew;
+    return 0;
+}
+
+// eigen-decomposition of the symmetric part of the leading m x m of T
+// (ascending, orthonormal vectors) -- the IRL's Ritz data
+void irl_sym_eig(const std::vector<double>& T, int ldt, int m, std::vector<double>& w, std::vector<double>& Y) {
+    std::vector<double> S((size_t)m * m);
+    for (int j = 0; j < m; ++j)
+        for (int i = 0; i < m; ++i) S[i + (size_t)j * m] = 0.5 * (T[i + (size_t)j * ldt] + T[j + (size_t)i * ldt]);
+    w.resize(m);
+    Y.resize((size_t)m * m);
+    dense::eig_symmetric(m, S.data(), m, w.data(), Y.data(), m);
+}
+
+// selectShifts 'largest' (impl_restarted_ca_lanczos.m:236-243): by modulus, descending (stable)
+std::vector<int> irl_order(const std::vector<double>& w) {
+    std::vector<int> ix(w.size());
+    for (size_t i = 0; i < ix.size(); ++i) ix[i] = (int)i;
+    std::stable_sort(ix.begin(), ix.end(), [&](int a, int b) { return std::fabs(w[a]) > std::fabs(w[b]); });
+    return ix;
+}
+
+// qrstep (impl_restarted_ca_lanczos.m:623-678) with a real shift on the
+// whole m x m H (k1 = 1, k2 = m): H <- Q'HQ, W <- WQ, noise below the first
+// subdiagonal zeroed.
+void irl_qrstep(int m, std::vector<double>& H, std::vector<double>& W, double mu) {
+    std::vector<double> B(H), Q((size_t)m * m), tmp((size_t)m * m);
+    for (int i = 0; i < m; ++i) B[i + (size_t)i * m] -= mu;
+    dense::qr_householder(m, B.data(), m, Q.data(), m);
+    std::vector<double> Qt((size_t)m * m);
+    for (int j = 0; j < m; ++j)
+        for (int i = 0; i < m; ++i) Qt[i + (size_t)j * m] = Q[j + (size_t)i * m];
+    dense::matmul(m, m, m, Qt.data(), m, H.data(), m, tmp.data(), m);  // H(kr,:) = Q'*H(kr,:)
+    dense::matmul(m, m, m, tmp.data(), m, Q.data(), m, H.data(), m);   // H(:,kr) = H(:,kr)*Q
+    dense::matmul(m, m, m, W.data(), m, Q.data(), m, tmp.data(), m);   // V(:,kr) = V(:,kr)*Q
+    W.swap(tmp);
+    for (int j = 0; j < m; ++j)
+        for (int i = j + 2; i < m; ++i) H[i + (size_t)j * m] = 0.0;
+}
+}  // namespace
+
+extern "C" {
+
+int cal_impl_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, int n_wanted, int s,
+                                  const char* basis, const char* orth, double tol, double* conv_eigs, double* Q_conv,
+                                  double* ritz_est, cal_restart_info* info) {
+    constexpr int kMaxRestarts = 40;  // impl_restarted_ca_lanczos.m:7
+    if (!c) return CAL_ERR_ARG;
+    if (!r || n_wanted < 1 || s < 1 || s > 15 || !basis || !orth || !conv_eigs)
+        return set_error(c, CAL_ERR_ARG, "impl_restarted_ca_lanczos: bad arguments");
+    if (!c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
+    std::string o(orth), b(basis);
+    for (auto& ch : o) ch = (char)std::tolower(ch);
+    for (auto& ch : b) ch = (char)std::tolower(ch);
+    if (o != "local" && o != "full" && o != "periodic" && o != "selective")  // :24-33
+        return set_error(c, CAL_ERR_ARG, "lanczos.m: Invalid option value for orth: " + o);
+    if (o != "full")
+        return set_error(c, CAL_ERR_UNSUPPORTED, "impl_restarted_ca_lanczos: only orth 'full' is defined (:381-392)");
+    if (b != "monomial" && b != "newton") return set_error(c, CAL_ERR_ARG, "ERROR: Unknown basis type: " + b);
+    // k kept, p shifts, m = k + p (:72-74; k >= s)
+    const int k = std::max(n_wanted + 4, s);
+    const int p = s * ((max_lanczos - k) / s);
+    const int m = k + p;
+    if (p < s) return set_error(c, CAL_ERR_ARG, "impl_restarted_ca_lanczos: max_lanczos < n_wanted+4+s");
+    const int nblk = (m + s - 1) / s;
+    hipSetDevice(c->device);
+    const double t_start = now_ms();
+    const int64_t n = c->A.n_local, ld = c->A.ld;
+    cal_lanczos_free_state(c);
+    LanczosState* L = new LanczosState();
+    c->lz = L;
+    L->s = s;
+    L->max_outer = nblk;
+    L->newton = b == "newton";
+    L->full = true;
+    L->mode = 1;
+    L->n = n;
+    L->ld = ld;
+    L->lpad = c->A.lpad;
+    L->info.s = s;
+    const size_t qcols = (size_t)s * nblk + 1;
+    CAL_HIP(c, hipMalloc((void**)&L->dQ, qcols * ld * sizeof(double)));
+    CAL_HIP(c, hipMalloc((void**)&L->dV, (size_t)2 * (s + 1) * ld * sizeof(double)));
+    CAL_HIP(c, hipMemsetAsync(L->dQ, 0, qcols * ld * sizeof(double), c->stream));
+    CAL_HIP(c, hipMemsetAsync(L->dV, 0, (size_t)2 * (s + 1) * ld * sizeof(double), c->stream));
+    L->Tld = (int)qcols;
+    L->T.assign((size_t)L->Tld * L->Tld, 0.0);
+    double norm_A = 0.0;
+    CAL_TRY(normest_dev(c, &norm_A));  // :37-40
+    tol = tol * norm_A;
+    CAL_HIP(c, hipMemcpyAsync(L->vcolumn(0), r, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    double rr = 0.0;
+    CAL_TRY(dot_host(c, n, L->vcolumn(0), L->vcolumn(0), &rr));
+    CAL_HIP(c, launch_div(L->col(0), L->vcolumn(0), std::sqrt(rr), n, c->stream));  // :53
+    if (L->newton) {
+        CAL_TRY(newton_prologue(c, *L, true));  // lanczos(A,q,2*s,'full') (:229-234)
+    } else {
+        L->Bk.assign((size_t)(s + 1) * s, 0.0);
+        for (int j = 0; j < s; ++j) L->Bk[(j + 1) + (size_t)j * (s + 1)] = 1.0;
+    }
+    int it = 0;
+    bool converged = false;
+    std::vector<double> wk, Yk, est(n_wanted, 0.0);
+    std::vector<int> wanted;
+    CAL_TRY(ensure_work(c, k + 1, ld));
+    while (!converged && it < kMaxRestarts) {
+        ++it;
+        // extend to m vectors (:85-94)
+        double bprev = it == 1 ? 0.0 : L->T[k + (size_t)(k - 1) * L->Tld];
+        for (int nv = it == 1 ? 0 : k; nv < m; nv += s) CAL_TRY(irl_block(c, *L, nv, &bprev));
+        const double beta_m = L->T[m + (size_t)(m - 1) * L->Tld];
+        // exact shifts: the p smallest-modulus Ritz values of T_m (:96-107)
+        std::vector<double> H((size_t)m * m), W((size_t)m * m, 0.0), w, Ym;
+        for (int j = 0; j < m; ++j)
+            for (int i = 0; i < m; ++i) H[i + (size_t)j * m] = L->T[i + (size_t)j * L->Tld];
+        irl_sym_eig(L->T, L->Tld, m, w, Ym);
+        const std::vector<int> u = irl_order(w);
+        for (int i = 0; i < m; ++i) W[i + (size_t)i * m] = 1.0;
+        for (int j = m; j > k; --j) irl_qrstep(m, H, W, w[u[j - 1]]);
+        // [V_k | r] = [V_m | v_{m+1}] M with r = V_m W(:,k+1) H(k+1,k) + f_m W(m,k)
+        std::vector<double> M((size_t)(m + 1) * (k + 1), 0.0);
+        for (int j = 0; j < k; ++j)
+            for (int i = 0; i < m; ++i) M[i + (size_t)j * (m + 1)] = W[i + (size_t)j * m];
+        const double hk = H[k + (size_t)(k - 1) * m];
+        for (int i = 0; i < m; ++i) M[i + (size_t)k * (m + 1)] = W[i + (size_t)k * m] * hk;
+        M[m + (size_t)k * (m + 1)] = beta_m * W[(m - 1) + (size_t)(k - 1) * m];
+        Panel P = panel();
+        panel_add(P, L->col(0), ld, m + 1);
+        double* dW = work_col(c, 0);
+        PanelOut Y = panel_out(dW + c->A.lpad, ld, k + 1);
+        CAL_TRY(apply_host(c, n, P, M.data(), k + 1, &Y, nullptr, 0, nullptr));
+        CAL_HIP(c, hipMemcpyAsync(L->dQ, dW, (size_t)(k + 1) * ld * sizeof(double), hipMemcpyDeviceToDevice,
+                                  c->stream));
+        double rk2 = 0.0;
+        CAL_TRY(dot_host(c, n, L->col(k), L->col(k), &rk2));
+        const double bk = std::sqrt(rk2);
+        if (!(bk > 0.0) || !std::isfinite(bk)) return set_error(c, CAL_ERR_NUMERIC, "IRL: zero restart residual");
+        CAL_HIP(c, launch_div(L->col(k), L->col(k), bk, n, c->stream));
+        std::fill(L->T.begin(), L->T.end(), 0.0);
+        for (int j = 0; j < k; ++j)
+            for (int i = 0; i < k; ++i) L->T[i + (size_t)j * L->Tld] = H[i + (size_t)j * m];
+        L->T[k + (size_t)(k - 1) * L->Tld] = bk;
+        // convergence of the n_wanted largest-modulus Ritz pairs of T_k (:127-143)
+        irl_sym_eig(L->T, L->Tld, k, wk, Yk);
+        const std::vector<int> ord = irl_order(wk);
+        wanted.assign(ord.begin(), ord.begin() + std::min(n_wanted, k));
+        converged = true;
+        for (int i = 0; i < (int)wanted.size(); ++i) {
+            est[i] = bk * std::fabs(Yk[(k - 1) + (size_t)wanted[i] * k]);
+            if (!(est[i] < tol)) converged = false;
+            if (ritz_est) ritz_est[(it - 1) + (size_t)i * kMaxRestarts] = est[i];
+        }
+    }
+    // wanted pairs, descending (:218-222)
+    std::vector<int> sel(wanted);
+    std::stable_sort(sel.begin(), sel.end(), [&](int a, int b2) { return wk[a] > wk[b2]; });
+    const int nw = (int)sel.size();
+    for (int i = 0; i < nw; ++i) conv_eigs[i] = wk[sel[i]];
+    if (Q_conv) {
+        std::vector<double> Ms((size_t)k * nw);
+        for (int j = 0; j < nw; ++j)
+            for (int i = 0; i < k; ++i) Ms[i + (size_t)j * k] = Yk[i + (size_t)sel[j] * k];
+        CAL_TRY(ensure_work(c, nw, ld));
+        Panel P = panel();
+        panel_add(P, L->col(0), ld, k);
+        PanelOut Y = panel_out(work_col(c, 0) + c->A.lpad, ld, nw);
+        CAL_TRY(apply_host(c, n, P, Ms.data(), nw, &Y, nullptr, 0, nullptr));
+        CAL_HIP(c, hipMemcpy2DAsync(Q_conv, n * sizeof(double), work_col(c, 0) + c->A.lpad, ld * sizeof(double),
+                                    n * sizeof(double), nw, hipMemcpyDeviceToHost, c->stream));
+        CAL_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    if (info) {
+        info->num_restarts = it;
+        info->nconv = nw;
+        info->converged = converged ? 1 : 0;
+        info->norm_A = norm_A;
+        double mx = 0.0;
+        for (int i = 0; i < nw; ++i) mx = std::max(mx, est[i]);
         info->max_ritz_norm = mx;
         info->ms = now_ms() - t_start;
     }

@@ -93,6 +93,42 @@ def diagonal(a) -> sp.csr_matrix:
     return sp.csr_matrix((a, np.arange(n, dtype=np.int32), np.arange(n + 1, dtype=np.int64)), shape=(n, n))
 
 
+def circuit_like(n_side: int, seed: int = 0, keep: float = 0.8, long_frac: float = 0.3, span: int = 4
+                 ) -> sp.csr_matrix:
+    """Synthetic stand-in for SuiteSparse G3_circuit (BASELINE config 5; the
+    .mtx is not in this container): the conductance matrix of a random
+    resistor network, SPD and irregular.  An n_side^2 grid keeps each
+    nearest-neighbour edge with probability ``keep``, adds ``long_frac * n``
+    local long-range edges (offsets up to ``span`` grid rows), conductances
+    U(0.1, 1), and grounds every node with U(1e-3, 1e-2).  At n_side = 1259
+    (n = 1,585,081) it has ~4.8 nonzeros per row like G3_circuit (n =
+    1,585,478, nnz = 7,660,826)."""
+    N = int(n_side)
+    n = N * N
+    rng = np.random.default_rng(seed)
+    idx = np.arange(n, dtype=np.int64).reshape(N, N)
+    ei = np.concatenate([idx[:, :-1].ravel(), idx[:-1, :].ravel()])
+    ej = np.concatenate([idx[:, 1:].ravel(), idx[1:, :].ravel()])
+    m = rng.random(len(ei)) < keep
+    ei, ej = ei[m], ej[m]
+    nl = int(long_frac * n)
+    li = rng.integers(0, n, nl)
+    lj = li + rng.integers(1, span * N, nl)
+    ok = lj < n
+    ei = np.concatenate([ei, li[ok]])
+    ej = np.concatenate([ej, lj[ok]])
+    g = rng.uniform(0.1, 1.0, len(ei))
+    deg = np.bincount(ei, g, n) + np.bincount(ej, g, n)
+    ground = rng.uniform(1.0e-3, 1.0e-2, n)
+    d = np.arange(n, dtype=np.int64)
+    A = sp.csr_matrix((np.concatenate([-g, -g, deg + ground]),
+                       (np.concatenate([ei, ej, d]), np.concatenate([ej, ei, d]))), shape=(n, n))
+    A.sum_duplicates()
+    A.sort_indices()
+    A.indices = A.indices.astype(np.int32)
+    return A
+
+
 def read_matrix_market(path: str) -> sp.csr_matrix:
     """Coordinate MatrixMarket reader (real/integer/pattern, general/symmetric)."""
     with open(path) as f:

@@ -178,6 +178,24 @@ int cal_restarted_ca_lanczos(cal_ctx* ctx, const double* r, int max_lanczos, int
                              const char* orth, double tol, int diagnostics, double* conv_eigs, double* Q_conv,
                              double* rnorms, double* orth_err, cal_restart_info* info);
 
+/* ---- f3: implicit restart ------------------------------------------------ */
+/* [conv_eigs,Q_conv,num_restarts] = impl_restarted_ca_lanczos(A,r,max_lanczos,
+ * n_wanted_eigs,s,basis,orth,tol)  (impl_restarted_ca_lanczos.m:4-226).  The
+ * reference file does not run; this is the implicit restart it
+ * sets out to implement: k = max(n_wanted+4, s) kept vectors, p = s*floor(
+ * (max_lanczos-k)/s) exact shifts by qrstep (:623-678) per restart, CA blocks
+ * of lanczos_basic (:333-426) with orth 'full' (the only branch that is
+ * defined: others return CAL_ERR_UNSUPPORTED), at most 40 restarts (:7).
+ * Converged when the n_wanted largest-modulus Ritz pairs of T_k all have
+ * ||r_k|||e_k'y| < tol*normest(A).  Outputs: conv_eigs (n_wanted,
+ * descending), Q_conv (n x n_wanted, may be NULL), ritz_est (40 x n_wanted
+ * column-major: the estimates after each restart, may be NULL).
+ * Parity unpinned (no runnable reference): checked against analytic spectra
+ * and scipy eigsh. */
+int cal_impl_restarted_ca_lanczos(cal_ctx* ctx, const double* r, int max_lanczos, int n_wanted, int s,
+                                  const char* basis, const char* orth, double tol, double* conv_eigs,
+                                  double* Q_conv, double* ritz_est, cal_restart_info* info);
+
 /* ---- multi-GPU (row slabs, RCCL over xGMI) ------------------------------ */
 /* 128-byte RCCL unique id; broadcast it out of band (e.g. torch.distributed). */
 int cal_comm_unique_id(void* id128);

@@ -425,3 +425,73 @@ def test_restarted_ca_lanczos_local_lap2d(cal, ref):
         rp = r * (1.0 + 1.0e-15 * rng.standard_normal(r.shape[0]))
         counts.add(ref.restarted_ca_lanczos(A, rp, 48, 4, 8, "newton", "local", 1.0e-8)["num_restarts"])
     assert min(counts) <= out["num_restarts"] <= max(counts), (out["num_restarts"], counts)
+
+
+# ---- implicit restart (parity unpinned: vs the oracle's IRL,
+# analytic spectra and eigsh) ----------------------------------------------
+
+def _irl_check(cal, ref, A, r, ml, nw, s, basis, eref, rel, same_restarts=True):
+    exp = ref.impl_restarted_ca_lanczos(A, r, ml, nw, s, basis, "full", 1.0e-8)
+    out = cal.impl_restarted_ca_lanczos(A, r, ml, nw, s, basis, "full", 1.0e-8)
+    assert out["converged"] and exp["converged"]
+    if same_restarts:   # the estimates clear tol by >= 2x either side (oracle)
+        assert out["num_restarts"] == exp["num_restarts"]
+    scale = abs(eref[0])
+    assert np.max(np.abs(out["conv_eigs"] - eref[:nw])) <= rel * scale
+    assert np.max(np.abs(out["conv_eigs"] - exp["conv_eigs"])) <= rel * scale
+    V = out["Q_conv"]
+    assert np.max(np.abs(V.T @ V - np.eye(nw))) < 1e-9
+    res = np.linalg.norm(A @ V - V * out["conv_eigs"], axis=0) / np.abs(out["conv_eigs"])
+    assert np.max(res) < 1e-7
+    assert np.max(out["ritz_est"][-1]) < 1.0e-8 * out["norm_A"]
+    return out, exp
+
+
+def test_impl_restarted_diagonal(cal, ref):
+    """diag(linspace(1,1e4,5000)), r = ones (test_restart_diagonal_matrices.m
+    input), 60 vectors, 8 wanted, s = 4 Newton: the top 8 diagonal entries,
+    the oracle's restart count (14)."""
+    import scipy.sparse as sp
+    a = ref.matlab_linspace(1.0, 1.0e4, 5000)
+    A = sp.csr_matrix(sp.diags(a))
+    out, exp = _irl_check(cal, ref, A, np.ones(5000), 60, 8, 4, "newton", a[::-1], 1e-12)
+    assert out["num_restarts"] == 14
+
+
+def test_impl_restarted_truncated_monomial(cal, ref):
+    """m = 60 with s = 8 (first pass truncated from 64 vectors), monomial basis."""
+    import scipy.sparse as sp
+    a = ref.matlab_linspace(1.0, 1.0e4, 5000)
+    A = sp.csr_matrix(sp.diags(a))
+    _irl_check(cal, ref, A, np.ones(5000), 60, 8, 8, "monomial", a[::-1], 1e-10)
+
+
+def test_impl_restarted_lap2d_multiplicity(cal, ref):
+    """lap2d(40): the top 8 eigenvalues with multiplicity (closed form); which
+    restart picks up the second copy of a double eigenvalue is a rounding
+    event, so the restart count is not compared."""
+    A = cal.matrices.laplacian_2d(40)
+    _irl_check(cal, ref, A, ref.matlab_rand(1600), 48, 8, 8, "newton", ref.laplacian_2d_eigs(40)[::-1], 1e-11,
+               same_restarts=False)
+
+
+def test_impl_restarted_circuit_vs_eigsh(cal, ref):
+    """Irregular SPD resistor network (the G3_circuit stand-in of BASELINE
+    config 5) against scipy eigsh."""
+    from scipy.sparse.linalg import eigsh
+    A = cal.matrices.circuit_like(60)
+    ev = np.sort(eigsh(A, k=8, which="LA", tol=1e-13)[0])[::-1]
+    _irl_check(cal, ref, A, np.ones(A.shape[0]), 64, 8, 8, "newton", ev, 1e-11)
+
+
+def test_impl_restarted_rejects(cal, ref):
+    A = cal.matrices.laplacian_2d(20)
+    r = np.ones(400)
+    for o in ("local", "periodic", "selective"):
+        with pytest.raises(cal.CalError) as ei:
+            cal.impl_restarted_ca_lanczos(A, r, 40, 4, 4, "newton", o)
+        assert ei.value.status == cal._lib.CAL_ERR_UNSUPPORTED
+    with pytest.raises(cal.CalError):
+        cal.impl_restarted_ca_lanczos(A, r, 40, 4, 4, "newton", "bogus")
+    with pytest.raises(cal.CalError):
+        cal.impl_restarted_ca_lanczos(A, r, 12, 8, 4, "newton", "full")
