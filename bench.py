@@ -7,10 +7,16 @@ previous block (projectAndNormalize), and the host T extension; diagnostics
 resident in HBM before the timed region.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload lap3d_215]
+  python bench.py --workload circuit_1259 --driver irl      # BASELINE config 5
+  python bench.py --matrix G3_circuit.mtx --driver irl      # a SuiteSparse file
 
-N > 1 runs one rank per GPU (torch.distributed.run): contiguous z-slabs of
-the same matrix, RCCL halo exchange per SpMV and RCCL allreduce of the Gram
-blocks (strong scaling, whole-job outer-iters/s).
+Workloads: lap2d_N / lap3d_N (Dirichlet Laplacians), circuit_N (the
+G3_circuit stand-in, matrices.circuit_like) or --matrix FILE (.mtx/.mat).
+N > 1 runs one rank per GPU (torch.distributed.run): contiguous row slabs
+(z-slabs for the Laplacians) of the same matrix, RCCL halo exchange per SpMV
+and RCCL allreduce of the Gram blocks (strong scaling, whole-job rate).
+--driver irl times whole impl_restarted_ca_lanczos solves instead of
+ca_lanczos outer iterations (a secondary line; the default is the headline).
 """
 from __future__ import annotations
 
@@ -35,7 +41,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     p.add_argument("--steps", type=int, default=15)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", default="lap3d_215")
+    p.add_argument("--workload", default="lap3d_215", help="lap2d_N | lap3d_N | circuit_N")
+    p.add_argument("--matrix", default=None, help="matrix file (.mtx[.gz] or SuiteSparse .mat); overrides --workload")
+    p.add_argument("--driver", default="lanczos", choices=["lanczos", "irl"])
+    p.add_argument("--irl", default="64,8", help="impl_restarted_ca_lanczos max_lanczos,n_wanted_eigs")
+    p.add_argument("--irl-tol", type=float, default=1.0e-8)
     p.add_argument("--s", type=int, default=8)
     p.add_argument("--basis", default="newton")
     p.add_argument("--orth", default="local")
@@ -48,53 +58,127 @@ def parse():
     return p.parse_args()
 
 
-def workload_dims(name):
-    kind, N = name.split("_")
-    dim = {"lap2d": 2, "lap3d": 3}[kind]
-    return dim, int(N)
+class Workload:
+    """The benchmark matrix: rows(r0, r1) -> local CSR slab (global int32
+    columns), full() -> the whole matrix (CPU baseline, CSR comparison)."""
+
+    def __init__(self, name, path=None):
+        self.name = name
+        self._A = None
+        if path:
+            from ca_lanczos_amd.matrices import load_matrix
+            self._A = load_matrix(path)
+            self.name = "file:" + os.path.basename(path)
+            self.kind, self.dim, self.N = "file", 0, 0
+            self.n = self._A.shape[0]
+            self.plane = 1
+            self.desc = "%s, n=%%d, nnz=%%d" % self.name
+            self.data = "file %s (symmetric sparse, r = MATLAB rand(n,1) seed 5489)" % os.path.basename(path)
+            return
+        kind, N = name.split("_")
+        self.kind, self.N = kind, int(N)
+        if kind in ("lap2d", "lap3d"):
+            self.dim = 2 if kind == "lap2d" else 3
+            self.n = self.N ** self.dim
+            self.plane = self.N ** (self.dim - 1)
+            st = "7-pt 3-D" if self.dim == 3 else "5-pt 2-D"
+            self.desc = "%s: %s %dx..., n=%%d, nnz=%%d" % (name, st, self.N)
+            self.data = "synthetic (%s Dirichlet Laplacian, r = MATLAB rand(n,1) seed 5489)" % st[:4]
+        elif kind == "circuit":
+            from ca_lanczos_amd.matrices import circuit_like
+            self.dim = 0
+            self._A = circuit_like(self.N)
+            self.n = self._A.shape[0]
+            self.plane = 1
+            self.desc = ("%s: G3_circuit stand-in (random SPD resistor network on a %dx%d grid), n=%%d, nnz=%%d"
+                         % (name, self.N, self.N))
+            self.data = "synthetic (matrices.circuit_like seed 0; G3_circuit itself is not in the image)"
+        else:
+            raise ValueError("unknown workload %s" % name)
+
+    def rows(self, r0, r1):
+        if self._A is None:
+            from ca_lanczos_amd.matrices import laplacian_rows
+            return laplacian_rows(self.dim, self.N, r0, r1)
+        A = self._A
+        rp = A.indptr[r0:r1 + 1].astype(np.int64)
+        lo, hi = int(rp[0]), int(rp[-1])
+        return rp - lo, A.indices[lo:hi].astype(np.int32), A.data[lo:hi]
+
+    def full(self):
+        import scipy.sparse as sp
+        if self._A is not None:
+            return self._A
+        rowptr, col, val = self.rows(0, self.n)
+        return sp.csr_matrix((val, col.astype(np.int32), rowptr), shape=(self.n, self.n))
 
 
-def build_rows(dim, N, r0, r1):
-    from ca_lanczos_amd.matrices import laplacian_rows
-    return laplacian_rows(dim, N, r0, r1)
+def _blas_threads():
+    try:
+        from threadpoolctl import threadpool_info
+        return max([d.get("num_threads", 1) for d in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        return 1
 
 
-def cpu_baseline(dim, N, s, iters):
+def cpu_baseline(wl, s, iters, basis="newton"):
     """The oracle restatement (NumPy/SciPy) timed on this host: Newton
     prologue excluded, `iters` outer iterations of ca_lanczos_basic with
     diagnostics off, on the same matrix and start vector."""
-    import scipy.sparse as sp
     from oracle import ca_lanczos_ref as ref
-    try:
-        from threadpoolctl import threadpool_info
-        blas_threads = max([d.get("num_threads", 1) for d in threadpool_info()] or [1])
-    except Exception:  # pragma: no cover
-        blas_threads = 1
-    n = N ** dim
-    rowptr, col, val = build_rows(dim, N, 0, n)
-    A = sp.csr_matrix((val, col.astype(np.int32), rowptr), shape=(n, n))
-    r = ref.matlab_rand(n)
+    blas_threads = _blas_threads()
+    A = wl.full()
+    r = ref.matlab_rand(wl.n)
     q = r / math.sqrt(r @ r)
     Bk, _, _ = ref.newton_change_of_basis(A, q, s)
     t0 = time.perf_counter()
-    ref.ca_lanczos_basic(A, q, Bk, iters, s, "newton", "local", diagnostics=False)
+    ref.ca_lanczos_basic(A, q, Bk, iters, s, basis, "local", diagnostics=False)
     dt = time.perf_counter() - t0
     return {"value": iters / dt, "unit": "outer-iters/s", "cores": int(blas_threads), "kind": "port",
             "sample": "oracle/ca_lanczos_ref.py ca_lanczos_basic, %d outer iterations (k=1..%d, s=%d, "
                       "Newton, 'local', diagnostics off) on the same %s matrix; SciPy CSR SpMV is "
                       "single-threaded, LAPACK QR uses %d threads; %.1f s"
-                      % (iters, iters, s, "x".join([str(N)] * dim), blas_threads, dt)}
+                      % (iters, iters, s, wl.name, blas_threads, dt)}
 
 
-def main():
-    args = parse()
+def cpu_baseline_irl(wl, s, max_lanczos, nw):
+    """The oracle's implicit restart, first pass only (ceil(m/s) CA blocks to
+    m vectors plus one compression; a whole solve is ~50 s at G3 size):
+    CA blocks/s, the unit of the GPU line's blocks_per_s."""
+    from oracle import ca_lanczos_ref as ref
+    A = wl.full()
+    n = wl.n
+    k, p, m = ref.irl_sizes(max_lanczos, nw, s)
+    ncols = s * (-(-m // s)) + 1
+    Q = np.zeros((n, ncols))
+    T = np.zeros((ncols, ncols - 1))
+    r = ref.matlab_rand(n)
+    Q[:, 0] = r / math.sqrt(r @ r)
+    Bk, _, _ = ref.newton_change_of_basis(A, Q[:, 0].copy(), s, "full")
+    t0 = time.perf_counter()
+    nb = -(-m // s)
+    ref.irl_lanczos_basic(A, Q, T, Bk, m, 0, s, "newton", "full", 0.0)
+    H = T[:m, :m].copy()
+    w = ref._sym_eig(H)[0]
+    u = [w[i] for i in ref._wanted_order(w)]
+    W = np.eye(m)
+    for j in range(m, k, -1):
+        W, H = ref.qrstep(W, H, u[j - 1], 0, m - 1)
+    Q[:, : k + 1] = Q[:, : m + 1] @ np.vstack([W[:, : k + 1], np.zeros((1, k + 1))])
+    dt = time.perf_counter() - t0
+    return {"value": nb / dt, "unit": "CA blocks/s", "cores": int(_blas_threads()), "kind": "port",
+            "sample": "oracle/ca_lanczos_ref.py implicit restart, first pass (%d CA blocks of s=%d, Newton, "
+                      "'full', to m=%d vectors) + qrstep shifts + compression on the same %s matrix; %.1f s"
+                      % (nb, s, m, wl.name, dt)}
+
+
+def setup(args):
+    """Ranks, context, communicator and the resident matrix slab."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dim, N = workload_dims(args.workload)
-    n = N ** dim
-    s = args.s
-    plane = N ** (dim - 1)
+    wl = Workload(args.workload, args.matrix)
+    n = wl.n
 
     import ca_lanczos_amd as cal
     from ca_lanczos_amd.matrices import slab_bounds
@@ -107,11 +191,10 @@ def main():
     ndev = ctypes.c_int(0)
     cal._lib.lib.cal_device_count(ctypes.byref(ndev))
     ctx = cal.Context(device=local % max(ndev.value, 1))
-    bounds = slab_bounds(n, world, plane)
+    bounds = slab_bounds(n, world, wl.plane)
     r0, r1 = bounds[rank], bounds[rank + 1]
-    rowptr, col, val = build_rows(dim, N, r0, r1)
+    rowptr, col, val = wl.rows(r0, r1)
     nnz_local = int(rowptr[-1])
-    r_full = np.random.RandomState(5489).random_sample(n)  # MATLAB rand(n,1), fresh session
     if world > 1 and args.comm == "host":
         import torch
 
@@ -142,12 +225,11 @@ def main():
         t = torch.tensor(list(uid), dtype=torch.uint8)
         dist.broadcast(t, 0)
         ctx.comm_init_rccl(world, rank, bytes(t.tolist()))
+    import scipy.sparse as sp
     if world > 1:
-        import scipy.sparse as sp
         Aloc = sp.csr_matrix((val, col, rowptr), shape=(r1 - r0, n))
         ctx.set_matrix_slab(n, r0, Aloc)
     else:
-        import scipy.sparse as sp
         ctx.set_matrix(sp.csr_matrix((val, col.astype(np.int32), rowptr), shape=(n, n)))
     del rowptr, col, val
     nnz_total = nnz_local
@@ -156,6 +238,41 @@ def main():
         tt = torch.tensor([float(nnz_local)], dtype=torch.float64)
         dist.all_reduce(tt)
         nnz_total = int(tt.item())
+    return dict(world=world, rank=rank, local=local, wl=wl, cal=cal, dist=dist, ctx=ctx, r0=r0, r1=r1,
+                nnz_local=nnz_local, nnz_total=nnz_total)
+
+
+def max_over_ranks(dist, vals):
+    if dist is None:
+        return vals
+    import torch
+    tt = torch.tensor(vals, dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return [float(x) for x in tt]
+
+
+def traffic_for(args, wl, world, cls):
+    if not os.path.exists(args.traffic_json):
+        return None
+    try:
+        tj = json.load(open(args.traffic_json))
+        if tj.get("workload") == wl.name and tj.get("n_gpus", 1) == world:
+            return tj.get("classes", {}).get(cls)
+    except Exception:
+        return None
+    return None
+
+
+def main():
+    args = parse()
+    if args.driver == "irl":
+        return main_irl(args)
+    E = setup(args)
+    world, rank, local, wl, cal, dist, ctx = (E[k] for k in ("world", "rank", "local", "wl", "cal", "dist", "ctx"))
+    r0, r1, nnz_local, nnz_total = E["r0"], E["r1"], E["nnz_local"], E["nnz_total"]
+    n = wl.n
+    s = args.s
+    r_full = np.random.RandomState(5489).random_sample(n)  # MATLAB rand(n,1), fresh session
 
     K, W = args.steps, args.warmup
     # K timed steps run without per-kernel events (an event pair around each
@@ -187,13 +304,7 @@ def main():
     apply_cnt, apply_ms = ctx.timer_read("apply")
     ctx.timer_enable(False)
     T, _, _, flags, info = ctx.lanczos_get()
-    if dist is not None:
-        import torch
-        tt = torch.tensor([elapsed, spmv_ms / max(spmv_cnt, 1)], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, spmv_avg_ms = float(tt[0]), float(tt[1])
-    else:
-        spmv_avg_ms = spmv_ms / max(spmv_cnt, 1)
+    elapsed, spmv_avg_ms = max_over_ranks(dist, [elapsed, spmv_ms / max(spmv_cnt, 1)])
 
     fmt, npat, nent = ctx.spmv_format()
     npairpat, npent, nsplit = ctx.spmv_pair_info()
@@ -204,10 +315,7 @@ def main():
     if world == 1 and rank == 0:
         # the same SpMV in plain CSR (12 B/nonzero), device-resident, for reference
         ctx2 = cal.Context(device=local, spmv_format="csr")
-        import scipy.sparse as sp
-        rp2, col2, val2 = build_rows(dim, N, 0, n)
-        ctx2.set_matrix(sp.csr_matrix((val2, col2.astype(np.int32), rp2), shape=(n, n)))
-        del rp2, col2, val2
+        ctx2.set_matrix(wl.full())
         csr_spmv = ctx2.bench_spmv(20, 1.0)
         ctx2.close()
         # tier-1 host-pointer SpMV (MATLAB-boundary semantics: PCIe in and out)
@@ -241,14 +349,7 @@ def main():
            "gram": (b_gram, gram_avg_ms, "k_rowapply Gram sweeps ([Qp|X]'X and pass A, MFMA tile Gram, no store)"),
            "apply": (b_apply, apply_avg_ms, "k_rowapply<17,8,chained> (block orthogonalisation pass B)")}[dominant]
     achieved = dom[0] / (dom[1] * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            if tj.get("workload") == args.workload and tj.get("n_gpus", 1) == world:
-                traffic = tj.get("classes", {}).get(dominant)
-        except Exception:
-            traffic = None
+    traffic = traffic_for(args, wl, world, dominant)
     n_reorth = int(np.sum(flags[W:W + K]))
     b_outer = s * (12 * nnz_total + 20 * n + 4) + 8 * n * (5 * s + 2)
     line = {
@@ -263,10 +364,8 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (7-pt Dirichlet Laplacian, r = MATLAB rand(n,1) seed 5489)" if dim == 3 else
-                "synthetic (5-pt Dirichlet Laplacian, r = MATLAB rand(n,1) seed 5489)",
-        "config": {"workload": "%s: %s %dx..., n=%d, nnz=%d" % (args.workload, "7-pt 3-D" if dim == 3 else "5-pt 2-D",
-                                                                N, n, nnz_total),
+        "data": wl.data,
+        "config": {"workload": wl.desc % (n, nnz_total),
                    "s": s, "basis": args.basis, "orth": args.orth, "parallelism": "row-slab x%d" % world,
                    "comm": (args.comm if world > 1 else "none")},
         "spmv_format": ("%s (%d row patterns, %d entries; %d pair patterns, %d entries, %d split pairs)"
@@ -287,7 +386,92 @@ def main():
     if host_rt_ms is not None:
         line["spmv_host_roundtrip_ms"] = host_rt_ms
     if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(dim, N, s, args.cpu_iters)
+        line["cpu_baseline"] = cpu_baseline(wl, s, args.cpu_iters, args.basis)
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+
+
+def main_irl(args):
+    """BASELINE config 5: whole impl_restarted_ca_lanczos solves (normest,
+    Newton prologue, CA blocks, shifts, compression) on resident A."""
+    E = setup(args)
+    world, rank, wl, cal, dist, ctx = (E[k] for k in ("world", "rank", "wl", "cal", "dist", "ctx"))
+    r0, r1, nnz_local, nnz_total = E["r0"], E["r1"], E["nnz_local"], E["nnz_total"]
+    n = wl.n
+    s = args.s
+    ml, nw = (int(x) for x in args.irl.split(","))
+    # k kept, p shifts, m = k + p (impl_restarted_ca_lanczos.m:72-74, k >= s; include/calanczos.h)
+    k = max(nw + 4, s)
+    p = s * ((ml - k) // s)
+    m = k + p
+    r_full = np.random.RandomState(5489).random_sample(n)
+    r_loc = r_full[r0:r1]
+    K, W = max(1, min(args.steps, 5)), max(0, min(args.warmup, 1))
+
+    def solve():
+        return cal.impl_restarted_ca_lanczos(None, r_loc, ml, nw, s, args.basis, "full", args.irl_tol, ctx=ctx)
+
+    for _ in range(W):
+        solve()
+    ctx.synchronize()
+    if dist is not None:
+        dist.barrier()
+    blocks = 0
+    t0 = time.perf_counter()
+    for _ in range(K):
+        out = solve()
+        blocks += -(-m // s) + (out["num_restarts"] - 1) * (p // s)
+    ctx.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+    ctx.timer_enable(True)
+    ctx.timer_reset()
+    out = solve()
+    spmv_cnt, spmv_ms = ctx.timer_read("spmv")
+    gram_cnt, gram_ms = ctx.timer_read("gram")
+    apply_cnt, apply_ms = ctx.timer_read("apply")
+    ctx.timer_enable(False)
+    elapsed, spmv_avg_ms = max_over_ranks(dist, [elapsed, spmv_ms / max(spmv_cnt, 1)])
+    if rank != 0:
+        dist.barrier()
+        return
+    fmt, _, _ = ctx.spmv_format()
+    n_loc = r1 - r0
+    b_spmv = (12 * nnz_local + 20 * n_loc + 4) if fmt == "csr" else 18 * n_loc
+    achieved = b_spmv / (spmv_avg_ms * 1e-3) / 1e9
+    line = {
+        "metric": "impl_restarted_ca_lanczos solves/sec (BASELINE config 5)",
+        "value": K / elapsed,
+        "unit": "solves/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": 1e3 * elapsed / K,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": wl.data,
+        "config": {"workload": wl.desc % (n, nnz_total), "driver": "impl_restarted_ca_lanczos",
+                   "max_lanczos": ml, "n_wanted_eigs": nw, "k": k, "m": m, "s": s, "basis": args.basis,
+                   "orth": "full", "tol": args.irl_tol, "parallelism": "row-slab x%d" % world,
+                   "comm": (args.comm if world > 1 else "none")},
+        "num_restarts": out["num_restarts"],
+        "converged": out["converged"],
+        "top_eigs": [float(x) for x in out["conv_eigs"][:3]],
+        "blocks_per_s": blocks / elapsed,
+        "spmv_format": fmt,
+        "kernel_ms_per_solve": {"spmv": spmv_ms, "gram": gram_ms, "apply": apply_ms},
+        "kernel_launches_per_solve": {"spmv": spmv_cnt, "gram": gram_cnt, "apply": apply_cnt},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_for(args, wl, world, "spmv"),
+                     "kernel": "SpMV (%s) inside the IRL" % fmt, "bytes_per_launch": b_spmv,
+                     "avg_launch_us": spmv_avg_ms * 1e3},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_irl(wl, s, ml, nw)
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()

@@ -110,6 +110,7 @@ SIGNATURES = [
     ("cal_newton_basis_matrix", c_int, [c_int, dp, dp, c_int, dp]),
     ("cal_eig", c_int, [c_int, dp, c_int, dp, dp, dp]),
     ("cal_tridiag_eigvals", c_int, [c_int, dp, dp, dp]),
+    ("cal_qrstep", c_int, [c_int, dp, c_int, dp, c_int, c_double]),
 ]
 
 for _name, _res, _args in SIGNATURES:

@@ -565,46 +565,47 @@ bool eig_general(int n, const double* A, int lda, double* wr, double* wi, double
     return ok;
 }
 
-// Householder QR of a square matrix with LAPACK's conventions (dgeqr2's
-// dlarfg reflectors: beta = -sign(alpha) ||x||, tau = (beta - alpha)/beta,
-// v(1) = 1; dorg2r accumulation), i.e. MATLAB's [Q,R] = qr(A) up to rounding.
-void qr_householder(int m, const double* A, int lda, double* Q, int ldq) {
-    std::vector<double> a((size_t)m * m), tau(m, 0.0);
-    for (int j = 0; j < m; ++j)
-        for (int i = 0; i < m; ++i) a[i + (size_t)j * m] = A[i + (size_t)j * lda];
-    auto at = [&](int i, int j) -> double& { return a[i + (size_t)j * m]; };
-    for (int j = 0; j + 1 < m; ++j) {
-        double xn = 0.0;
-        for (int i = j + 1; i < m; ++i) xn += at(i, j) * at(i, j);
-        xn = std::sqrt(xn);
-        if (xn == 0.0) continue;  // H = I
-        const double alpha = at(j, j);
-        const double beta = -std::copysign(std::hypot(alpha, xn), alpha);
-        tau[j] = (beta - alpha) / beta;
-        const double sc = 1.0 / (alpha - beta);
-        for (int i = j + 1; i < m; ++i) at(i, j) *= sc;
-        at(j, j) = beta;
-        for (int c = j + 1; c < m; ++c) {  // A(j:m,c) -= tau v (v' A(j:m,c))
-            double d = at(j, c);
-            for (int i = j + 1; i < m; ++i) d += at(i, j) * at(i, c);
-            d *= tau[j];
-            at(j, c) -= d;
-            for (int i = j + 1; i < m; ++i) at(i, c) -= d * at(i, j);
+// One explicit shifted QR step on an upper-Hessenberg H (m x m): H - mu I =
+// QR, H <- RQ + mu I = Q'HQ, W (m x m) <- WQ, with Q the product of m-1
+// Givens rotations (O(m^2); the reference's qrstep forms the same Q, up to
+// column signs, by a dense Householder QR and two m^3 products).
+void hess_qrstep(int m, double* H, int ldh, double* W, int ldw, double mu) {
+    auto h = [&](int i, int j) -> double& { return H[i + (size_t)j * ldh]; };
+    std::vector<double> cs(m, 1.0), sn(m, 0.0);
+    for (int i = 0; i < m; ++i) h(i, i) -= mu;
+    for (int j = 0; j + 1 < m; ++j) {  // R = G'_{m-2} ... G'_0 (H - mu I)
+        const double a = h(j, j), b = h(j + 1, j);
+        double c = 1.0, s = 0.0;
+        if (b != 0.0) {
+            const double r = std::hypot(a, b);
+            c = a / r;
+            s = b / r;
+        }
+        cs[j] = c;
+        sn[j] = s;
+        for (int col = j; col < m; ++col) {
+            const double x = h(j, col), y = h(j + 1, col);
+            h(j, col) = c * x + s * y;
+            h(j + 1, col) = c * y - s * x;
+        }
+        h(j + 1, j) = 0.0;
+    }
+    for (int j = 0; j + 1 < m; ++j) {  // RQ and WQ, Q = G_0 ... G_{m-2}
+        const double c = cs[j], s = sn[j];
+        for (int row = 0; row < std::min(j + 2, m); ++row) {
+            const double x = h(row, j), y = h(row, j + 1);
+            h(row, j) = c * x + s * y;
+            h(row, j + 1) = c * y - s * x;
+        }
+        double* wj = W + (size_t)j * ldw;
+        double* wj1 = W + (size_t)(j + 1) * ldw;
+        for (int row = 0; row < m; ++row) {
+            const double x = wj[row], y = wj1[row];
+            wj[row] = c * x + s * y;
+            wj1[row] = c * y - s * x;
         }
     }
-    // Q = H(0) H(1) ... H(m-2) applied to I, last reflector first
-    for (int j = 0; j < m; ++j)
-        for (int i = 0; i < m; ++i) Q[i + (size_t)j * ldq] = i == j ? 1.0 : 0.0;
-    for (int j = m - 2; j >= 0; --j) {
-        if (tau[j] == 0.0) continue;
-        for (int c = j; c < m; ++c) {
-            double d = Q[j + (size_t)c * ldq];
-            for (int i = j + 1; i < m; ++i) d += at(i, j) * Q[i + (size_t)c * ldq];
-            d *= tau[j];
-            Q[j + (size_t)c * ldq] -= d;
-            for (int i = j + 1; i < m; ++i) Q[i + (size_t)c * ldq] -= d * at(i, j);
-        }
-    }
+    for (int i = 0; i < m; ++i) h(i, i) += mu;
 }
 
 }  // namespace dense

@@ -31,9 +31,9 @@ void singular_values(int m, const double* A, int lda, double* sv);
 bool eig_general(int n, const double* A, int lda, double* wr, double* wi, double* V, int ldv);
 // Symmetric eigenproblem (Jacobi), ascending, orthonormal vectors.
 void eig_symmetric(int n, const double* A, int lda, double* w, double* V, int ldv);
-// Q (m x m) of the Householder QR of a square A (LAPACK dgeqr2/dorg2r
-// conventions = MATLAB qr(A)); used by qrstep of the implicit restart.
-void qr_householder(int m, const double* A, int lda, double* Q, int ldq);
+// One explicit shifted QR step on an upper-Hessenberg H: H <- Q'HQ,
+// W <- WQ with H - mu I = QR (Givens rotations; qrstep of the implicit restart).
+void hess_qrstep(int m, double* H, int ldh, double* W, int ldw, double mu);
 
 }  // namespace dense
 }  // namespace cal

@@ -1103,23 +1103,6 @@ std::vector<int> irl_order(const std::vector<double>& w) {
     return ix;
 }
 
-// qrstep (impl_restarted_ca_lanczos.m:623-678) with a real shift on the
-// whole m x m H (k1 = 1, k2 = m): H <- Q'HQ, W <- WQ, noise below the first
-// subdiagonal zeroed.
-void irl_qrstep(int m, std::vector<double>& H, std::vector<double>& W, double mu) {
-    std::vector<double> B(H), Q((size_t)m * m), tmp((size_t)m * m);
-    for (int i = 0; i < m; ++i) B[i + (size_t)i * m] -= mu;
-    dense::qr_householder(m, B.data(), m, Q.data(), m);
-    std::vector<double> Qt((size_t)m * m);
-    for (int j = 0; j < m; ++j)
-        for (int i = 0; i < m; ++i) Qt[i + (size_t)j * m] = Q[j + (size_t)i * m];
-    dense::matmul(m, m, m, Qt.data(), m, H.data(), m, tmp.data(), m);  // H(kr,:) = Q'*H(kr,:)
-    dense::matmul(m, m, m, tmp.data(), m, Q.data(), m, H.data(), m);   // H(:,kr) = H(:,kr)*Q
-    dense::matmul(m, m, m, W.data(), m, Q.data(), m, tmp.data(), m);   // V(:,kr) = V(:,kr)*Q
-    W.swap(tmp);
-    for (int j = 0; j < m; ++j)
-        for (int i = j + 2; i < m; ++i) H[i + (size_t)j * m] = 0.0;
-}
 }  // namespace
 
 extern "C" {
@@ -1198,8 +1181,12 @@ int cal_impl_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, 
             for (int i = 0; i < m; ++i) H[i + (size_t)j * m] = L->T[i + (size_t)j * L->Tld];
         irl_sym_eig(L->T, L->Tld, m, w, Ym);
         const std::vector<int> u = irl_order(w);
+        // T_m is tridiagonal up to rounding: drop the sub-subdiagonal noise the
+        // reference's first qrstep clean-up removes (:670-672)
+        for (int j = 0; j < m; ++j)
+            for (int i = j + 2; i < m; ++i) H[i + (size_t)j * m] = 0.0;
         for (int i = 0; i < m; ++i) W[i + (size_t)i * m] = 1.0;
-        for (int j = m; j > k; --j) irl_qrstep(m, H, W, w[u[j - 1]]);
+        for (int j = m; j > k; --j) dense::hess_qrstep(m, H.data(), m, W.data(), m, w[u[j - 1]]);
         // [V_k | r] = [V_m | v_{m+1}] M with r = V_m W(:,k+1) H(k+1,k) + f_m W(m,k)
         std::vector<double> M((size_t)(m + 1) * (k + 1), 0.0);
         for (int j = 0; j < k; ++j)
@@ -1282,6 +1269,12 @@ int cal_eig(int n, const double* T, int ldt, double* wr, double* wi, double* V) 
         return 0;
     }
     return dense::eig_general(n, T, ldt, wr, wi, V, n) ? 0 : CAL_ERR_NUMERIC;
+}
+
+int cal_qrstep(int m, double* H, int ldh, double* W, int ldw, double mu) {
+    if (m < 1 || !H || !W || ldh < m || ldw < m) return CAL_ERR_ARG;
+    dense::hess_qrstep(m, H, ldh, W, ldw, mu);
+    return 0;
 }
 
 int cal_tridiag_eigvals(int n, const double* alpha, const double* beta, double* w) {

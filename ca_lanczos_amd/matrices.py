@@ -129,27 +129,89 @@ def circuit_like(n_side: int, seed: int = 0, keep: float = 0.8, long_frac: float
     return A
 
 
+def _open_text(path: str):
+    if path.endswith(".gz"):
+        import gzip
+        return gzip.open(path, "rt")
+    return open(path)
+
+
 def read_matrix_market(path: str) -> sp.csr_matrix:
-    """Coordinate MatrixMarket reader (real/integer/pattern, general/symmetric)."""
-    with open(path) as f:
+    """Coordinate MatrixMarket reader (real/integer/pattern, general/symmetric;
+    ``.mtx`` or ``.mtx.gz``).  The entries go through pandas' C parser
+    (G3_circuit's 4.6M lines in a few seconds), or numpy.loadtxt without it."""
+    with _open_text(path) as f:
         header = f.readline().lower().split()
         if len(header) < 5 or header[0] != "%%matrixmarket":
             raise ValueError("not a MatrixMarket file: %s" % path)
+        if header[2] != "coordinate":
+            raise ValueError("only coordinate MatrixMarket files are supported: %s" % path)
         field, symm = header[3], header[4]
+        if field == "complex":
+            raise ValueError("complex MatrixMarket matrices are not supported: %s" % path)
         line = f.readline()
-        while line.startswith("%"):
+        while line.startswith("%") or not line.strip():
             line = f.readline()
-        m, n, nz = (int(t) for t in line.split())
-        data = np.loadtxt(f, ndmin=2, max_rows=nz)
+        m, n, nz = (int(t) for t in line.split()[:3])
+        ncols = 2 if field == "pattern" else 3
+        try:
+            import pandas as pd
+            data = pd.read_csv(f, sep=r"\s+", header=None, nrows=nz, usecols=range(ncols), comment="%",
+                               dtype=np.float64, engine="c", float_precision="round_trip").to_numpy()
+        except ImportError:  # pragma: no cover
+            data = np.loadtxt(f, ndmin=2, max_rows=nz, usecols=range(ncols))
+    if data.shape[0] != nz:
+        raise ValueError("MatrixMarket %s: expected %d entries, read %d" % (path, nz, data.shape[0]))
     i = data[:, 0].astype(np.int64) - 1
     j = data[:, 1].astype(np.int64) - 1
     v = np.ones(len(i)) if field == "pattern" else data[:, 2].astype(np.float64)
-    if symm in ("symmetric", "hermitian"):
+    if symm in ("symmetric", "hermitian", "skew-symmetric"):
         off = i != j
-        i, j, v = np.concatenate([i, j[off]]), np.concatenate([j, i[off]]), np.concatenate([v, v[off]])
+        vt = -v[off] if symm == "skew-symmetric" else v[off]
+        i, j, v = np.concatenate([i, j[off]]), np.concatenate([j, i[off]]), np.concatenate([v, vt])
     A = sp.csr_matrix((v, (i, j)), shape=(m, n))
     A.sum_duplicates()
     A.sort_indices()
+    return A
+
+
+def read_suitesparse_mat(path: str) -> sp.csr_matrix:
+    """``load(path); A = Problem.A`` (test_restarted_ca_lanczos_all_matrices.m:
+    25-26, test_restart_general_matrices.m:10-12): the SuiteSparse MATLAB
+    format.  scipy.io.loadmat reads MAT v4/v5/v7 without executing anything
+    from the file; v7.3 (HDF5) files need h5py, which this image lacks -- use
+    the collection's MatrixMarket download for those."""
+    import scipy.io
+    try:
+        d = scipy.io.loadmat(path, squeeze_me=True, struct_as_record=False)
+    except NotImplementedError as e:  # MAT v7.3
+        raise ValueError("%s is a MAT v7.3 (HDF5) file; h5py is not available -- use the .mtx form" % path) from e
+    if "Problem" in d:
+        A = getattr(d["Problem"], "A", None)
+    else:
+        A = d.get("A")
+    if A is None or not sp.issparse(A):
+        raise ValueError("%s holds no sparse Problem.A" % path)
+    A = sp.csr_matrix(A, dtype=np.float64)
+    A.sum_duplicates()
+    A.sort_indices()
+    return A
+
+
+def load_matrix(path: str) -> sp.csr_matrix:
+    """A matrix file of the reference's test suite as canonical CSR with int32
+    columns: SuiteSparse ``.mat`` or MatrixMarket ``.mtx[.gz]``."""
+    low = path.lower()
+    if low.endswith(".mat"):
+        A = read_suitesparse_mat(path)
+    elif low.endswith(".mtx") or low.endswith(".mtx.gz") or low.endswith(".mm"):
+        A = read_matrix_market(path)
+    else:
+        raise ValueError("unknown matrix file type: %s (expected .mat, .mtx or .mtx.gz)" % path)
+    if A.shape[0] != A.shape[1]:
+        raise ValueError("ERROR: Matrix %s is not square." % path)  # get_matrix_info.m:21
+    A = to_csr(A)
+    A.indices = A.indices.astype(np.int32)
     return A
 
 

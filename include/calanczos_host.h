@@ -35,6 +35,12 @@ int cal_eig(int n, const double* T, int ldt, double* wr, double* wi, double* V);
  * ascending (the Newton prologue's eig(T), ca_lanczos.m:69). */
 int cal_tridiag_eigvals(int n, const double* alpha, const double* beta, double* w);
 
+/* [V,H] = qrstep(V,H,mu,1,m) for a real shift on an upper-Hessenberg H
+ * (impl_restarted_ca_lanczos.m:623-678): H <- Q'HQ, W <- WQ with H - mu I =
+ * QR.  Q is built from Givens rotations (the reference's Householder Q up to
+ * column signs).  H (ldh >= m) and W (ldw >= m) column-major, in place. */
+int cal_qrstep(int m, double* H, int ldh, double* W, int ldw, double mu);
+
 #ifdef __cplusplus
 }
 #endif

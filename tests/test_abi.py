@@ -96,3 +96,30 @@ def test_tridiag_eigvals(cal):
     w = np.zeros(16)
     assert lib.cal_tridiag_eigvals(16, ptr(a), ptr(b), ptr(w)) == 0
     assert np.allclose(w, np.linalg.eigvalsh(np.diag(a) + np.diag(b, 1) + np.diag(b, -1)), atol=1e-13)
+
+
+def test_qrstep_matches_oracle_up_to_signs(cal, ref):
+    """cal_qrstep (Givens) vs the oracle's qrstep (Householder, the
+    reference's impl_restarted_ca_lanczos.m:623-678): the same orthogonal
+    similarity up to the signs of Q's columns, on a tridiagonal and on an
+    upper-Hessenberg H, with a Ritz-value shift and an arbitrary one."""
+    from ca_lanczos_amd._lib import lib, ptr
+    rng = np.random.RandomState(4)
+    m = 20
+    d, e = rng.randn(m), rng.rand(m - 1) + 0.1
+    tri = np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
+    hess = np.triu(rng.randn(m, m), -1)
+    for H0 in (tri, hess):
+        for mu in (np.linalg.eigvals(H0).real.min(), 0.37):
+            Hr, Wr = H0.copy(), np.eye(m)
+            Wr, Hr = ref.qrstep(Wr, Hr, mu, 0, m - 1)
+            H = np.asfortranarray(H0.copy())
+            W = np.asfortranarray(np.eye(m))
+            assert lib.cal_qrstep(m, ptr(H), m, ptr(W), m, float(mu)) == 0
+            sg = np.sign(np.sum(W * Wr, axis=0))
+            assert np.all(np.abs(sg) == 1)
+            # an exact shift makes H - mu I singular: the last rotation acts on
+            # rounding-level numbers, so that column agrees to ~1e-10 only
+            assert np.max(np.abs(W * sg - Wr)) < 1e-9
+            assert np.max(np.abs(H * np.outer(sg, sg) - Hr)) < 1e-9 * np.abs(H0).max()
+            assert np.max(np.abs(np.tril(H, -2))) == 0.0

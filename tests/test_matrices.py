@@ -48,3 +48,42 @@ def test_matrix_market_roundtrip(cal, tmp_path):
 def test_diagonal_config1(cal):
     A = cal.matrices.diagonal(np.arange(1.0, 1001.0))
     assert A.nnz == 1000 and A[999, 999] == 1000.0
+
+
+def test_matrix_market_general_gz_pattern(cal, tmp_path):
+    import gzip
+    p = os.path.join(tmp_path, "g.mtx.gz")
+    with gzip.open(p, "wt") as f:
+        f.write("%%MatrixMarket matrix coordinate pattern general\n% comment\n3 3 4\n1 1\n2 3\n3 2\n3 3\n")
+    B = cal.matrices.load_matrix(p)
+    assert B.indices.dtype == np.int32
+    assert np.array_equal(B.toarray(), [[1, 0, 0], [0, 0, 1], [0, 1, 1]])
+
+
+def test_suitesparse_mat_problem_struct(cal, tmp_path):
+    """load(...); A = Problem.A (test_restarted_ca_lanczos_all_matrices.m:25-26)."""
+    import scipy.io
+    import scipy.sparse as sp
+    A = cal.matrices.laplacian_2d(7).tocsc()
+    p = os.path.join(tmp_path, "lap.mat")
+    scipy.io.savemat(p, {"Problem": {"A": A, "name": "lap7", "kind": "2D/3D problem"}})
+    B = cal.matrices.load_matrix(p)
+    assert (sp.csr_matrix(A) != B).nnz == 0 and B.has_sorted_indices
+    with pytest.raises(ValueError):
+        scipy.io.savemat(os.path.join(tmp_path, "x.mat"), {"B": np.eye(3)})
+        cal.matrices.load_matrix(os.path.join(tmp_path, "x.mat"))
+    with pytest.raises(ValueError):
+        cal.matrices.load_matrix(os.path.join(tmp_path, "x.txt"))
+
+
+def test_matrix_market_values_roundtrip_exactly(cal, tmp_path):
+    import scipy.sparse as sp
+    A = cal.matrices.circuit_like(12, seed=5)
+    L = sp.tril(A).tocoo()
+    p = os.path.join(tmp_path, "c.mtx")
+    with open(p, "w") as f:
+        f.write("%%%%MatrixMarket matrix coordinate real symmetric\n%d %d %d\n" % (A.shape[0], A.shape[1], L.nnz))
+        np.savetxt(f, np.column_stack([L.row + 1, L.col + 1, L.data]), fmt="%d %d %.17g")
+    B = cal.matrices.load_matrix(p)
+    assert np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices)
+    assert np.array_equal(A.data, B.data)
