@@ -25,7 +25,8 @@ class Context:
     """A device context (``cal_ctx``): one HIP stream, the resident matrix and
     the device-resident CA-Lanczos state."""
 
-    def __init__(self, device: int | None = None, spmv_format: str | None = None, orth_coef: str | None = None):
+    def __init__(self, device: int | None = None, spmv_format: str | None = None, orth_coef: str | None = None,
+                 mpk_depth: int | None = None):
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", "0"))
         h = ctypes.c_void_p()
@@ -40,6 +41,20 @@ class Context:
         check(self.h, lib.cal_set_spmv_format(self.h, fmt.encode()), "spmv format")
         if orth_coef:
             self.set_orth_coef(orth_coef)
+        if mpk_depth is not None:
+            self.set_mpk_depth(mpk_depth)
+
+    def set_mpk_depth(self, depth: int):
+        """Ghost depth of the distributed CA matrix-powers kernel (next
+        set_matrix_slab; 1 = one halo exchange per SpMV)."""
+        check(self.h, lib.cal_set_mpk_depth(self.h, int(depth)), "mpk depth")
+        return self
+
+    def mpk_info(self):
+        """{'depth': active depth (1 = off), 'band_l', 'band_r', 'n_rows' (stored rows)}."""
+        d, bl, br, nr = ctypes.c_int(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        check(self.h, lib.cal_mpk_info(self.h, ctypes.byref(d), ctypes.byref(bl), ctypes.byref(br), ctypes.byref(nr)))
+        return dict(depth=d.value, band_l=bl.value, band_r=br.value, n_rows=nr.value)
 
     def set_orth_coef(self, where: str):
         """Run the block-orthogonalisation s x s algebra on the "device"
@@ -236,18 +251,18 @@ def SpMV(A, v):
     return out
 
 
-def matrix_powers_monomial(A, q, s):
+def matrix_powers_monomial(A, q, s, ctx=None):
     """``V = matrix_powers_monomial(A,q,s)`` (n x s) -- matrix_powers_monomial.m:6-12."""
-    ctx = context_for(A)
+    ctx = ctx or context_for(A)
     q = f64(q).ravel()
     V = np.zeros((len(q), s), order="F")
     check(ctx.h, lib.cal_matrix_powers_monomial(ctx.h, ptr(q), s, ptr(V)), "matrix_powers_monomial")
     return V
 
 
-def matrix_powers_newton(A, v, s, lam, modifiedp=0):
+def matrix_powers_newton(A, v, s, lam, modifiedp=0, ctx=None):
     """``V = matrix_powers_newton(A,v,s,lambda,modifiedp)`` (n x (s+1)) -- matrix_powers_newton.m:15-54."""
-    ctx = context_for(A)
+    ctx = ctx or context_for(A)
     v = f64(v).ravel()
     lam = np.asarray(lam)
     lre = f64(np.real(lam)).ravel()

@@ -99,7 +99,9 @@ int cal_matrix_powers_monomial(cal_ctx* c, const double* q, int s, double* V) {
     CAL_TRY(ensure_scratch(c, (size_t)(s + 1) * ld));
     double* W = vcol(c, c->d_scratch, 0);
     CAL_TRY(upload(c, W, ld, q, n, 1));
-    for (int i = 0; i < s; ++i) CAL_TRY(spmv_dev(c, W + (size_t)i * ld, W + (size_t)(i + 1) * ld, 0, 0, 0, nullptr));
+    std::vector<double*> Y(s);
+    for (int i = 0; i < s; ++i) Y[i] = W + (size_t)(i + 1) * ld;
+    CAL_TRY(powers_dev(c, s, W, Y.data(), nullptr, nullptr, nullptr));
     return download(c, V, W + ld, ld, n, s);  // V excludes q (matrix_powers_monomial.m:7)
 }
 
@@ -111,22 +113,25 @@ int cal_matrix_powers_newton(cal_ctx* c, const double* v, int s, const double* l
     CAL_TRY(ensure_scratch(c, (size_t)(s + 1) * ld));
     double* W = vcol(c, c->d_scratch, 0);
     CAL_TRY(upload(c, W, ld, v, n, 1));
+    // V(:,k+1) = A V(:,k) - Re(l_k) V(:,k) [+ Im(l_k)^2 V(:,k-1) when Im(l_k) < 0]
+    std::vector<double*> Y(s);
+    std::vector<double> sh(s), im2(s, 0.0);
+    std::vector<const double*> xp(s, nullptr);
     for (int k = 0; k < s; ++k) {
         const double re = lre[k], im = lim ? lim[k] : 0.0;
-        double* x = W + (size_t)k * ld;
-        double* y = W + (size_t)(k + 1) * ld;
+        Y[k] = W + (size_t)(k + 1) * ld;
+        sh[k] = re;
         if (modifiedp == 0) {
             if (im != 0.0)
-                return set_error(c, CAL_ERR_UNSUPPORTED, "complex shifts need modifiedp=1 (real basis)");
-            CAL_TRY(spmv_dev(c, x, y, 1, re, 0.0, nullptr));  // :28
+                return set_error(c, CAL_ERR_UNSUPPORTED, "complex shifts need modifiedp=1 (real basis)");  // :28
         } else if (im < 0.0) {
             if (k == 0)
                 return set_error(c, CAL_ERR_NUMERIC, "k==1, but shift has a negative imaginary part");  // :36-38
-            CAL_TRY(spmv_dev(c, x, y, 2, re, im * im, W + (size_t)(k - 1) * ld));  // :40-41
-        } else {
-            CAL_TRY(spmv_dev(c, x, y, 1, re, 0.0, nullptr));  // :34, :43
-        }
+            im2[k] = im * im;  // :40-41
+            xp[k] = W + (size_t)(k - 1) * ld;
+        }  // else :34, :43
     }
+    CAL_TRY(powers_dev(c, s, W, Y.data(), sh.data(), im2.data(), xp.data()));
     return download(c, V, W, ld, n, s + 1);
 }
 

@@ -108,6 +108,20 @@ constexpr int kPairSplit = 0xFFFF;
 
 struct DevMatrix {
     int64_t n_local = 0, n_global = 0, row0 = 0, nnz = 0, nghost = 0;
+    // Stored rows: n_rows = ext_off + n_local + right ghost rows.  With the
+    // CA matrix-powers kernel (mpk) a slab also stores the rows of its
+    // (depth-1)-deep ghost zone, fetched from the owners at setup, so the s
+    // powers of one outer iteration need one deep halo exchange instead of s
+    // (DESIGN.md §4).  ext_off (even, for the pair kernel) counts the stored
+    // rows before the first local row, including one empty dummy row when
+    // the ghost count is odd; columns stay relative to the local origin.
+    int64_t n_rows = 0, ext_off = 0, nnz_loc = 0;
+    bool mpk = false;
+    int mpk_depth = 1;                   // stored ghost depth D (powers per exchange)
+    int64_t band_l = 0, band_r = 0;      // global max (row - min col), (max col - row)
+    int64_t ext_lo = 0, ext_hi = 0;      // global rows of the first / one past the last real stored row
+    int ext_dummy = 0;                   // stored row 0 is an empty dummy row
+    std::vector<int64_t> slabs;          // slab starts of every rank (+ n_global)
     int* rowptr = nullptr;
     int* col = nullptr;    // local column ids relative to the local origin
     double* val = nullptr;
@@ -249,6 +263,7 @@ struct cal_ctx {
     std::vector<hipEvent_t> event_pool;
 
     int spmv_format = 0;  // 0 auto, 1 CSR, 2 row-pattern (applies at the next set_matrix)
+    int mpk_depth_req = 8;  // ghost depth of the distributed matrix-powers kernel (next set_matrix; 1 = off)
     bool orth_coef_device = true;  // block-orth s x s algebra on the device (blockorth.cpp)
     // set by lanczos_step: work to enqueue after a block orthogonalisation is
     // enqueued and before the host waits for its R (orth_device)
@@ -274,10 +289,23 @@ int hip_fail(cal_ctx* c, hipError_t e, const char* what);
         if (_s < 0) return _s;    \
     } while (0)
 
-// col: local ids relative to the local origin (negative = left halo);
+// rowptr/col/val: n_rows stored rows, the local ones starting at stored row
+// ext_off; col: ids relative to the local origin (negative = left halo);
 // lpad/rext: halo extent on each side of the local rows in a vector column.
-int upload_matrix(cal_ctx* c, int64_t n_local, int64_t n_global, int64_t row0, int64_t nghost, int64_t lpad,
-                  int64_t rext, const std::vector<int>& rowptr, const std::vector<int>& col, const double* val);
+int upload_matrix(cal_ctx* c, int64_t n_rows, int64_t ext_off, int64_t n_local, int64_t n_global, int64_t row0,
+                  int64_t nghost, int64_t lpad, int64_t rext, const std::vector<int>& rowptr,
+                  const std::vector<int>& col, const double* val);
+// Row-pattern SpMV over stored rows [o, o+len) (o even); x, y at the local origin.
+int spmv_range(cal_ctx* c, int64_t o, int64_t len, const double* x, double* y, int mode, double shift, double im2,
+               const double* xprev);
+// The s matrix powers Y[j] = (A - shift_j I) x_j (+ im2_j xprev_j), x_0 = q,
+// x_j = Y[j-1] (matrix_powers_{monomial,newton}.m): with the CA
+// matrix-powers kernel when the matrix has one (one deep halo exchange),
+// otherwise one halo exchange per SpMV.  shift/im2/xprev may be null.
+int powers_dev(cal_ctx* c, int s, const double* q, double* const* Y, const double* shift, const double* im2,
+               const double* const* xprev);
+// Halo exchange of the d-deep ghost zone of x (contiguous row ranges; mpk only).
+int halo_exchange_deep(cal_ctx* c, double* x, int d);
 // pointer to column j of a vector buffer laid out with A.ld / A.lpad
 inline double* vcol(const cal_ctx* c, double* base, int64_t j) { return base + j * c->A.ld + c->A.lpad; }
 int ensure_partial(cal_ctx* c, size_t doubles);

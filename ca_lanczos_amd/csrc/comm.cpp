@@ -90,6 +90,78 @@ int halo_exchange(cal_ctx* c, double* x) {
     return 0;
 }
 
+// The d-deep ghost zone of x for the CA matrix powers (window layout): from
+// each rank q < me the rows [max(st[q], row0 - d bl), min(st[q+1], row0)),
+// from each q > me [max(st[q], row1), min(st[q+1], row1 + d br)); every piece
+// is a contiguous run of the column on both sides, so RCCL sends and
+// receives in place (no pack kernel).  Peers ascending on every rank.
+int halo_exchange_deep(cal_ctx* c, double* x, int d) {
+    Comm* m = c->comm;
+    DevMatrix& A = c->A;
+    if (!m || m->nranks <= 1) return 0;
+    const std::vector<int64_t>& st = A.slabs;
+    const int64_t row0 = A.row0, row1 = A.row0 + A.n_local;
+    const int64_t dl = (int64_t)d * A.band_l, dr = (int64_t)d * A.band_r;
+    struct Piece {
+        int peer;
+        int64_t s_off, s_cnt, r_off, r_cnt;  // relative to the local origin
+    };
+    std::vector<Piece> pieces;
+    int64_t stot = 0, rtot = 0;
+    for (int q = 0; q < m->nranks; ++q) {
+        if (q == m->rank) continue;
+        int64_t rlo, rhi, slo, shi;
+        if (q < m->rank) {
+            rlo = std::max(st[q], row0 - dl);
+            rhi = std::min(st[q + 1], row0);
+            slo = row0;
+            shi = std::min(row1, st[q + 1] + dr);
+        } else {
+            rlo = std::max(st[q], row1);
+            rhi = std::min(st[q + 1], row1 + dr);
+            slo = std::max(row0, st[q] - dl);
+            shi = row1;
+        }
+        const int64_t rc = std::max<int64_t>(0, rhi - rlo), sc = std::max<int64_t>(0, shi - slo);
+        if (rc == 0 && sc == 0) continue;
+        pieces.push_back({q, slo - row0, sc, rlo - row0, rc});
+        stot += sc;
+        rtot += rc;
+    }
+    if (pieces.empty()) return 0;
+    if (m->kind == 1) {
+        CAL_NCCL(c, ncclGroupStart());
+        for (const Piece& p : pieces) {
+            if (p.s_cnt > 0) CAL_NCCL(c, ncclSend(x + p.s_off, (size_t)p.s_cnt, ncclDouble, p.peer, m->nccl, c->stream));
+            if (p.r_cnt > 0) CAL_NCCL(c, ncclRecv(x + p.r_off, (size_t)p.r_cnt, ncclDouble, p.peer, m->nccl, c->stream));
+        }
+        CAL_NCCL(c, ncclGroupEnd());
+        return 0;
+    }
+    CAL_TRY(ensure_stage(c, (size_t)(stot + rtot)));
+    double* hs = m->h_stage;
+    double* hr = m->h_stage + stot;
+    int64_t so = 0;
+    for (const Piece& p : pieces) {
+        if (p.s_cnt > 0)
+            CAL_HIP(c, hipMemcpyAsync(hs + so, x + p.s_off, p.s_cnt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        so += p.s_cnt;
+    }
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    so = 0;
+    int64_t ro = 0;
+    for (const Piece& p : pieces) {
+        if (m->ex(m->user, p.peer, hs + so, p.s_cnt, hr + ro, p.r_cnt) != 0)
+            return set_error(c, CAL_ERR_COMM, "exchange callback failed");
+        if (p.r_cnt > 0)
+            CAL_HIP(c, hipMemcpyAsync(x + p.r_off, hr + ro, p.r_cnt * sizeof(double), hipMemcpyHostToDevice, c->stream));
+        so += p.s_cnt;
+        ro += p.r_cnt;
+    }
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
 int comm_allreduce_host(cal_ctx* c, std::vector<double>& buf) {
     Comm* m = c->comm;
     if (!m || m->nranks <= 1 || buf.empty()) return 0;
@@ -254,11 +326,132 @@ int cal_set_matrix_csr_dist(cal_ctx* c, int64_t n_global, int64_t row0, int64_t 
         const bool local = j >= row0 && j < row0 + nlocal;
         col[p] = (local || window) ? (int)(j - row0) : (int)(nlocal + ghost[j]);
     }
+    // ---- CA matrix-powers ghost zone -----------------------
+    // Agreed by all ranks: the global band (bl, br) and whether every slab
+    // has the window layout; the kernel runs when they do, depth D > 1 and
+    // the row-pattern format is not excluded.
+    const int D = c->mpk_depth_req;
+    int64_t bl = 0, br = 0;
+    bool all_window = window;
+    {
+        int64_t lbl = 0, lbr = 0;
+        for (int64_t i = 0; i < nlocal; ++i)
+            for (int64_t p = rowptr[i] - rowptr[0]; p < rowptr[i + 1] - rowptr[0]; ++p) {
+                const int64_t d = colind_global[p] - (row0 + i);
+                lbl = std::max(lbl, -d);
+                lbr = std::max(lbr, d);
+            }
+        std::vector<double> bb((size_t)3 * nranks, 0.0);
+        bb[(size_t)3 * rank] = (double)lbl;
+        bb[(size_t)3 * rank + 1] = (double)lbr;
+        bb[(size_t)3 * rank + 2] = window ? 0.0 : 1.0;
+        CAL_TRY(comm_allreduce_host(c, bb));
+        for (int q = 0; q < nranks; ++q) {
+            bl = std::max(bl, (int64_t)bb[(size_t)3 * q]);
+            br = std::max(br, (int64_t)bb[(size_t)3 * q + 1]);
+            if (bb[(size_t)3 * q + 2] != 0.0) all_window = false;
+        }
+    }
+    const bool mpk = all_window && nranks > 1 && D > 1 && c->spmv_format != 1 && (bl > 0 || br > 0);
+    auto ext_of = [&](int q, int64_t* lo, int64_t* hi) {
+        *lo = std::max<int64_t>(0, st[q] - (int64_t)(D - 1) * bl);
+        *hi = std::min<int64_t>(n_global, st[q + 1] + (int64_t)(D - 1) * br);
+    };
+    std::vector<int> xrp, xcol;
+    std::vector<double> xval;
+    int64_t elo = row0, ehi = row0 + nlocal, ext_off = 0;
+    int dummy = 0;
+    if (mpk) {
+        ext_of(rank, &elo, &ehi);
+        // rows of the ghost zone, fetched from their owners (ascending peers,
+        // counts then rows: lengths, global columns, values)
+        std::map<int64_t, std::pair<std::vector<int64_t>, std::vector<double>>> ghost_rows;
+        for (int q = 0; q < nranks; ++q) {
+            if (q == rank) continue;
+            const int64_t nlo = std::max(st[q], elo), nhi = std::min(st[q + 1], ehi);
+            int64_t qlo, qhi;
+            ext_of(q, &qlo, &qhi);
+            const int64_t glo = std::max(row0, qlo), ghi = std::min(row0 + nlocal, qhi);
+            const bool get = nhi > nlo, give = ghi > glo;
+            if (!get && !give) continue;
+            std::vector<double> s1, r1(get ? 1 : 0);
+            if (give) s1.push_back((double)(rowptr[ghi - row0] - rowptr[glo - row0]));
+            CAL_TRY(comm_exchange_host(c, q, s1, r1));
+            std::vector<double> s2, r2;
+            if (give) {
+                const int64_t p0 = rowptr[glo - row0] - rowptr[0], p1 = rowptr[ghi - row0] - rowptr[0];
+                for (int64_t i = glo; i < ghi; ++i) s2.push_back((double)(rowptr[i - row0 + 1] - rowptr[i - row0]));
+                for (int64_t p = p0; p < p1; ++p) s2.push_back((double)colind_global[p]);
+                for (int64_t p = p0; p < p1; ++p) s2.push_back(val[rowptr[0] + p]);
+            }
+            if (get) r2.resize((size_t)(nhi - nlo) + 2 * (size_t)r1[0]);
+            CAL_TRY(comm_exchange_host(c, q, s2, r2));
+            if (get) {
+                const int64_t nr = nhi - nlo, nz = (int64_t)r1[0];
+                int64_t pc = nr, pv = nr + nz;
+                for (int64_t i = 0; i < nr; ++i) {
+                    const int64_t len = (int64_t)r2[(size_t)i];
+                    auto& row = ghost_rows[nlo + i];
+                    for (int64_t e = 0; e < len; ++e) {
+                        row.first.push_back((int64_t)r2[(size_t)(pc++)]);
+                        row.second.push_back(r2[(size_t)(pv++)]);
+                    }
+                }
+            }
+        }
+        // stored rows: [dummy] [elo, row0) [local] [row1, ehi); ext_off even
+        dummy = ((row0 - elo) & 1) ? 1 : 0;
+        ext_off = (row0 - elo) + dummy;
+        const int64_t n_rows = dummy + (ehi - elo);
+        xrp.assign(1, 0);
+        if (dummy) xrp.push_back(0);
+        auto push_ghost = [&](int64_t g) -> bool {
+            auto it = ghost_rows.find(g);
+            if (it == ghost_rows.end()) return false;
+            for (size_t e = 0; e < it->second.first.size(); ++e) {
+                xcol.push_back((int)(it->second.first[e] - row0));
+                xval.push_back(it->second.second[e]);
+            }
+            xrp.push_back((int)xcol.size());
+            return true;
+        };
+        bool okrows = true;
+        for (int64_t g = elo; g < row0 && okrows; ++g) okrows = push_ghost(g);
+        for (int64_t i = 0; i < nlocal && okrows; ++i) {
+            for (int64_t p = rowptr[i] - rowptr[0]; p < rowptr[i + 1] - rowptr[0]; ++p) {
+                xcol.push_back((int)(colind_global[p] - row0));
+                xval.push_back(val[rowptr[0] + p]);
+            }
+            xrp.push_back((int)xcol.size());
+        }
+        for (int64_t g = row0 + nlocal; g < ehi && okrows; ++g) okrows = push_ghost(g);
+        if (!okrows || (int64_t)xrp.size() != n_rows + 1 || xcol.size() >= ((size_t)1 << 31))
+            return set_error(c, CAL_ERR_COMM, "mpk: ghost-zone rows incomplete");
+        // vector window: D bands each side (deep exchange) + the edge rows'
+        // reads one band beyond the stored rows
+        const int64_t lw = std::max(lext, (int64_t)D * bl + 2), rw = std::max(rext, (int64_t)D * br + 2);
+        CAL_TRY(upload_matrix(c, n_rows, ext_off, nlocal, n_global, row0, nghost, lw, rw, xrp, xcol, xval.data()));
+        if (!c->A.use_pat) {  // no row-pattern format: plain slab, one exchange per SpMV
+            CAL_TRY(upload_matrix(c, nlocal, 0, nlocal, n_global, row0, nghost, lext, rext, rp, col,
+                                  val + rowptr[0]));
+        } else {
+            DevMatrix& A = c->A;
+            A.mpk = true;
+            A.mpk_depth = D;
+            A.ext_lo = elo;
+            A.ext_hi = ehi;
+            A.ext_dummy = dummy;
+        }
+    } else {
+        CAL_TRY(upload_matrix(c, nlocal, 0, nlocal, n_global, row0, nghost, lext, rext, rp, col, val + rowptr[0]));
+    }
+    c->A.band_l = bl;
+    c->A.band_r = br;
+    c->A.slabs = st;
     // counts matrix: cnt[p*nranks+q] = #entries rank p needs from rank q
     std::vector<double> cnt((size_t)nranks * nranks, 0.0);
     for (int q = 0; q < nranks; ++q) cnt[(size_t)rank * nranks + q] = (double)need[q].size();
     CAL_TRY(comm_allreduce_host(c, cnt));
-    CAL_TRY(upload_matrix(c, nlocal, n_global, row0, nghost, lext, rext, rp, col, val + rowptr[0]));
     DevMatrix& A = c->A;
     int64_t roff = 0, soff = 0;
     std::vector<int> send_idx;

@@ -81,18 +81,19 @@ static int dot_host(cal_ctx* c, int64_t n, const double* x, const double* y, dou
 
 // matrix powers of step k into the V buffer of parity k & 1 (ca_lanczos.m:
 // 110-118); V(:,1) = q is not copied: the panels reference q's column of Q.
-static int enqueue_powers(cal_ctx* c, LanczosState& L, int k) {
+static int lanczos_powers(cal_ctx* c, LanczosState& L, const double* q, int par) {
     const int s = L.s;
-    const double* q = L.col((k - 1) * s);
+    std::vector<double*> Y(s);
+    std::vector<double> sh(s);
     for (int i = 0; i < s; ++i) {
-        const double* x = (i == 0) ? q : L.vcolumn(i, k & 1);
-        double* y = L.vcolumn(i + 1, k & 1);
-        if (L.newton)
-            CAL_TRY(spmv_dev(c, x, y, 1, L.Bk[i + (size_t)i * (s + 1)], 0.0, nullptr));
-        else
-            CAL_TRY(spmv_dev(c, x, y, 0, 0.0, 0.0, nullptr));
+        Y[i] = L.vcolumn(i + 1, par);
+        sh[i] = L.newton ? L.Bk[i + (size_t)i * (s + 1)] : 0.0;
     }
-    return 0;
+    return powers_dev(c, s, q, Y.data(), L.newton ? sh.data() : nullptr, nullptr, nullptr);
+}
+
+static int enqueue_powers(cal_ctx* c, LanczosState& L, int k) {
+    return lanczos_powers(c, L, L.col((k - 1) * L.s), k & 1);
 }
 
 // ---- normest(A) (MATLAB built-in; ca_lanczos.m:258,370) ---------------------
@@ -103,7 +104,7 @@ static int normest_dev(cal_ctx* c, double* out) {
     CAL_TRY(ensure_work(c, 2, ld));
     double* x = work_col(c, 0) + c->A.lpad;
     double* y = work_col(c, 1) + c->A.lpad;
-    CAL_HIP(c, launch_abs_rowsum(c->A.rowptr, c->A.val, n, x, c->stream));
+    CAL_HIP(c, launch_abs_rowsum(c->A.rowptr + c->A.ext_off, c->A.val, n, x, c->stream));
     double xx = 0.0;
     CAL_TRY(dot_host(c, n, x, x, &xx));
     double e = std::sqrt(xx);
@@ -293,7 +294,7 @@ static int ritz_diagnostics(cal_ctx* c, LanczosState& L) {
         CAL_TRY(halo_exchange(c, xr));
         if (xi) CAL_TRY(halo_exchange(c, xi));
         SpmvArgs a{};
-        a.rowptr = c->A.rowptr;
+        a.rowptr = c->A.rowptr + c->A.ext_off;  // local rows of a stored slab
         a.col = c->A.col;
         a.val = c->A.val;
         a.x = xr;
@@ -785,7 +786,7 @@ int rel_residual(cal_ctx* c, double* x, double l, double* out) {
     CAL_TRY(ensure_red(c, 2));
     CAL_TRY(halo_exchange(c, x));
     SpmvArgs a{};
-    a.rowptr = c->A.rowptr;
+    a.rowptr = c->A.rowptr + c->A.ext_off;  // local rows of a stored slab
     a.col = c->A.col;
     a.val = c->A.val;
     a.x = x;
@@ -1037,13 +1038,7 @@ int irl_block(cal_ctx* c, LanczosState& L, int nvecs, double* bprev) {
     const int s = L.s;
     const int64_t n = c->A.n_local, ld = L.ld;
     const double* q = L.col(nvecs);
-    for (int i = 0; i < s; ++i) {
-        const double* x = (i == 0) ? q : L.vcolumn(i);
-        if (L.newton)
-            CAL_TRY(spmv_dev(c, x, L.vcolumn(i + 1), 1, L.Bk[i + (size_t)i * (s + 1)], 0.0, nullptr));
-        else
-            CAL_TRY(spmv_dev(c, x, L.vcolumn(i + 1), 0, 0.0, 0.0, nullptr));
-    }
+    CAL_TRY(lanczos_powers(c, L, q, 0));
     if (nvecs == 0) {
         Panel X = panel();
         panel_add(X, q, ld, 1);

@@ -156,9 +156,10 @@ constexpr int kMaxPatternEntries = 1 << 16;
 constexpr int kMaxPatternLen = 32;
 
 // Returns false when the matrix has too many distinct rows for the format.
-static bool build_patterns(int64_t n, const std::vector<int>& rowptr, const std::vector<int>& col, const double* val,
-                           std::vector<uint16_t>& pat, std::vector<int2>& pinfo, std::vector<int>& pdelta,
-                           std::vector<double>& pval, int* maxlen) {
+// n stored rows; stored row r is local row r - org (col is local-origin relative).
+static bool build_patterns(int64_t n, int64_t org, const std::vector<int>& rowptr, const std::vector<int>& col,
+                           const double* val, std::vector<uint16_t>& pat, std::vector<int2>& pinfo,
+                           std::vector<int>& pdelta, std::vector<double>& pval, int* maxlen) {
     pat.assign(n, 0);
     pinfo.clear();
     pdelta.assign(1, 0);  // entry 0: sentinel (delta 0) for empty rows
@@ -173,7 +174,7 @@ static bool build_patterns(int64_t n, const std::vector<int>& rowptr, const std:
         for (int j = 0; j < len; ++j) {
             uint64_t vb;
             std::memcpy(&vb, &val[p0 + j], 8);
-            const uint64_t d = (uint64_t)(uint32_t)(col[p0 + j] - (int)r);
+            const uint64_t d = (uint64_t)(uint32_t)(col[p0 + j] - (int)(r - org));
             h = (h ^ d) * 1099511628211ull;
             h = (h ^ vb) * 1099511628211ull;
         }
@@ -184,7 +185,7 @@ static bool build_patterns(int64_t n, const std::vector<int>& rowptr, const std:
             if (pi.y != len) continue;
             bool same = true;
             for (int j = 0; j < len && same; ++j)
-                same = pdelta[pi.x + j] == col[p0 + j] - (int)r &&
+                same = pdelta[pi.x + j] == col[p0 + j] - (int)(r - org) &&
                        std::memcmp(&pval[pi.x + j], &val[p0 + j], 8) == 0;
             if (same) {
                 found = id;
@@ -197,7 +198,7 @@ static bool build_patterns(int64_t n, const std::vector<int>& rowptr, const std:
             found = (int)pinfo.size();
             pinfo.push_back(make_int2(len > 0 ? (int)pdelta.size() : 0, len));
             for (int j = 0; j < len; ++j) {
-                pdelta.push_back(col[p0 + j] - (int)r);
+                pdelta.push_back(col[p0 + j] - (int)(r - org));
                 pval.push_back(val[p0 + j]);
             }
             cand.push_back(found);
@@ -217,19 +218,22 @@ static bool build_patterns(int64_t n, const std::vector<int>& rowptr, const std:
 // and the lone last row of an odd n, are marked kPairSplit (per-row path).
 constexpr int kMaxPairLen = 16;
 
-static bool build_pair_patterns(int64_t n, const std::vector<uint16_t>& pat, const std::vector<int2>& pinfo,
+static bool build_pair_patterns(int64_t n, int64_t org, const std::vector<uint16_t>& pat,
+                                const std::vector<int2>& pinfo,
                                 const std::vector<int>& pdelta, const std::vector<double>& pval,
                                 const std::vector<int>& col, std::vector<uint16_t>& ppat, std::vector<int2>& ppinfo,
                                 std::vector<int>& ppoff, std::vector<double>& ppval, int* pmaxlen, bool* pcanon,
                                 int* slots) {
-    int64_t cmin = 0, cmax = n - 1;
+    int64_t cmin = -org, cmax = n - 1 - org;  // local coordinates
     for (int v : col) {
         cmin = std::min<int64_t>(cmin, v);
         cmax = std::max<int64_t>(cmax, v);
     }
     std::vector<uint8_t> ref((size_t)(cmax - cmin + 1), 0);
     for (int v : col) ref[(size_t)(v - cmin)] = 1;
-    auto valid = [&](int64_t i) { return (i >= 0 && i < n) || (i >= cmin && i <= cmax && ref[(size_t)(i - cmin)]); };
+    auto valid = [&](int64_t i) {  // i: local coordinate
+        return (i >= -org && i < n - org) || (i >= cmin && i <= cmax && ref[(size_t)(i - cmin)]);
+    };
     struct Merged {
         int id;
         std::vector<int> pad0, pad1;  // offsets row 2t / 2t+1 loads without using
@@ -300,26 +304,31 @@ static bool build_pair_patterns(int64_t n, const std::vector<uint16_t>& pat, con
             it = seen.emplace(key, std::move(mg)).first;
         }
         bool ok = true;
-        for (int o : it->second.pad0) ok = ok && valid(r + o);
-        for (int o : it->second.pad1) ok = ok && valid(r + 1 + o);
+        for (int o : it->second.pad0) ok = ok && valid(r - org + o);
+        for (int o : it->second.pad1) ok = ok && valid(r - org + 1 + o);
         if (ok) ppat[t] = (uint16_t)it->second.id;
     }
     *pmaxlen = mx;
     return !ppinfo.empty();
 }
 
-// Upload a local matrix.  col: local column ids relative to the local origin
+// Upload a local matrix: n_rows stored rows, the n_local local ones from
+// stored row ext_off.  col: local column ids relative to the local origin
 // (negative ids address the left halo); lpad / rext: halo extent on either
 // side of the local rows in every vector column.
-int upload_matrix(cal_ctx* c, int64_t n_local, int64_t n_global, int64_t row0, int64_t nghost, int64_t lpad,
-                  int64_t rext, const std::vector<int>& rowptr, const std::vector<int>& col, const double* val) {
+int upload_matrix(cal_ctx* c, int64_t n_rows, int64_t ext_off, int64_t n_local, int64_t n_global, int64_t row0,
+                  int64_t nghost, int64_t lpad, int64_t rext, const std::vector<int>& rowptr,
+                  const std::vector<int>& col, const double* val) {
     free_matrix(c);
     DevMatrix& A = c->A;
     A.n_local = n_local;
+    A.n_rows = n_rows;
+    A.ext_off = ext_off;
     A.n_global = n_global;
     A.row0 = row0;
     A.nghost = nghost;
-    A.nnz = rowptr[n_local];
+    A.nnz = rowptr[n_rows];
+    A.nnz_loc = rowptr[ext_off + n_local] - rowptr[ext_off];
     A.lpad = ((lpad + 63) / 64) * 64;
     A.ld = ((A.lpad + n_local + rext + 63) / 64) * 64;
     if (A.ld == 0) A.ld = 64;
@@ -330,17 +339,17 @@ int upload_matrix(cal_ctx* c, int64_t n_local, int64_t n_global, int64_t row0, i
         std::vector<int> pdelta;
         std::vector<double> pval;
         int mx = 0;
-        const bool ok = n_local > 0 && build_patterns(n_local, rowptr, col, val, pat, pinfo, pdelta, pval, &mx);
+        const bool ok = n_rows > 0 && build_patterns(n_rows, ext_off, rowptr, col, val, pat, pinfo, pdelta, pval, &mx);
         if (ok) {
             A.use_pat = true;
             A.npat = (int)pinfo.size();
             A.nent = (int)pdelta.size();
             A.maxlen = mx <= 8 ? std::max(mx, 1) : (mx <= 16 ? 16 : 32);
-            CAL_HIP(c, hipMalloc((void**)&A.pat, n_local * sizeof(uint16_t)));
+            CAL_HIP(c, hipMalloc((void**)&A.pat, n_rows * sizeof(uint16_t)));
             CAL_HIP(c, hipMalloc((void**)&A.pinfo, pinfo.size() * sizeof(int2)));
             CAL_HIP(c, hipMalloc((void**)&A.pdelta, pdelta.size() * sizeof(int)));
             CAL_HIP(c, hipMalloc((void**)&A.pval, pval.size() * sizeof(double)));
-            CAL_HIP(c, hipMemcpy(A.pat, pat.data(), n_local * sizeof(uint16_t), hipMemcpyHostToDevice));
+            CAL_HIP(c, hipMemcpy(A.pat, pat.data(), n_rows * sizeof(uint16_t), hipMemcpyHostToDevice));
             CAL_HIP(c, hipMemcpy(A.pinfo, pinfo.data(), pinfo.size() * sizeof(int2), hipMemcpyHostToDevice));
             CAL_HIP(c, hipMemcpy(A.pdelta, pdelta.data(), pdelta.size() * sizeof(int), hipMemcpyHostToDevice));
             CAL_HIP(c, hipMemcpy(A.pval, pval.data(), pval.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -350,8 +359,8 @@ int upload_matrix(cal_ctx* c, int64_t n_local, int64_t n_global, int64_t row0, i
             std::vector<double> ppval;
             int pmx = 0;
             bool canon = false;
-            if (build_pair_patterns(n_local, pat, pinfo, pdelta, pval, col, ppat, ppinfo, ppoff, ppval, &pmx, &canon,
-                                    A.pslot)) {
+            if (build_pair_patterns(n_rows, ext_off, pat, pinfo, pdelta, pval, col, ppat, ppinfo, ppoff, ppval, &pmx,
+                                    &canon, A.pslot)) {
                 A.use_pair = true;
                 A.nppat = (int)ppinfo.size();
                 A.npent = (int)ppoff.size();
@@ -372,19 +381,22 @@ int upload_matrix(cal_ctx* c, int64_t n_local, int64_t n_global, int64_t row0, i
                                                      "distinct rows (or rows longer than 32)");
         }
     }
+    // CSR-stream row blocks over the local rows (the CSR path never runs on
+    // an extended matrix: the mpk requires the row-pattern format)
     std::vector<int> blk;
     int max_nnz = 0;
-    build_row_blocks(n_local, rowptr, blk, &max_nnz);
+    std::vector<int> rp_loc(rowptr.begin() + ext_off, rowptr.begin() + ext_off + n_local + 1);
+    build_row_blocks(n_local, rp_loc, blk, &max_nnz);
     A.nblk = (int)blk.size() - 1;
     int nit = (max_nnz + 255) / 256;
     if (nit < 1) nit = 1;
     if (nit > 8) nit = 8;
     A.nit = nit;
-    CAL_HIP(c, hipMalloc((void**)&A.rowptr, (n_local + 1) * sizeof(int)));
+    CAL_HIP(c, hipMalloc((void**)&A.rowptr, (n_rows + 1) * sizeof(int)));
     CAL_HIP(c, hipMalloc((void**)&A.col, std::max<int64_t>(A.nnz, 1) * sizeof(int)));
     CAL_HIP(c, hipMalloc((void**)&A.val, std::max<int64_t>(A.nnz, 1) * sizeof(double)));
     CAL_HIP(c, hipMalloc((void**)&A.blk, blk.size() * sizeof(int)));
-    CAL_HIP(c, hipMemcpy(A.rowptr, rowptr.data(), (n_local + 1) * sizeof(int), hipMemcpyHostToDevice));
+    CAL_HIP(c, hipMemcpy(A.rowptr, rowptr.data(), (n_rows + 1) * sizeof(int), hipMemcpyHostToDevice));
     if (A.nnz > 0) {
         CAL_HIP(c, hipMemcpy(A.col, col.data(), A.nnz * sizeof(int), hipMemcpyHostToDevice));
         CAL_HIP(c, hipMemcpy(A.val, val, A.nnz * sizeof(double), hipMemcpyHostToDevice));
@@ -394,42 +406,49 @@ int upload_matrix(cal_ctx* c, int64_t n_local, int64_t n_global, int64_t row0, i
     return 0;
 }
 
+int spmv_range(cal_ctx* c, int64_t o, int64_t len, const double* x, double* y, int mode, double shift, double im2,
+               const double* xprev) {
+    const DevMatrix& A = c->A;
+    if (o < 0 || (o & 1) || len < 0 || o + len > A.n_rows)
+        return set_error(c, CAL_ERR_ARG, "spmv_range: bad stored-row range");
+    const int64_t d = o - A.ext_off;  // launch origin relative to the local origin
+    PatArgs p;
+    p.pat = A.pat + o;
+    p.pinfo = A.pinfo;
+    p.pdelta = A.pdelta;
+    p.pval = A.pval;
+    p.n = len;
+    p.nblk = (int)((len + 255) / 256);
+    p.x = x + d;
+    p.y = y + d;
+    p.xprev = xprev ? xprev + d : nullptr;
+    p.shift = shift;
+    p.im2 = im2;
+    p.mode = mode;
+    p.maxlen = A.maxlen;
+    p.npat = A.npat;
+    p.nent = A.nent;
+    p.ppat = A.use_pair ? A.ppat + o / 2 : nullptr;
+    p.ppinfo = A.ppinfo;
+    p.ppoff = A.ppoff;
+    p.ppval = A.ppval;
+    p.nppat = A.nppat;
+    p.npent = A.npent;
+    p.pmaxlen = A.pmaxlen;
+    p.pcanon = A.pcanon ? 1 : 0;
+    for (int k = 0; k < 8; ++k) p.pslot[k] = A.pslot[k];
+    p.xlo = -(A.lpad + d);
+    p.xhi = A.ld - (A.lpad + d);
+    const int t = timer_begin(c, 0);
+    CAL_HIP(c, launch_spmv_pat(p, c->stream));
+    timer_end(c, t);
+    return 0;
+}
+
 int spmv_dev(cal_ctx* c, const double* x, double* y, int mode, double shift, double im2, const double* xprev) {
     if (!c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
     CAL_TRY(halo_exchange(c, const_cast<double*>(x)));
-    if (c->A.use_pat) {
-        PatArgs p;
-        p.pat = c->A.pat;
-        p.pinfo = c->A.pinfo;
-        p.pdelta = c->A.pdelta;
-        p.pval = c->A.pval;
-        p.n = c->A.n_local;
-        p.nblk = (int)((c->A.n_local + 255) / 256);
-        p.x = x;
-        p.y = y;
-        p.xprev = xprev;
-        p.shift = shift;
-        p.im2 = im2;
-        p.mode = mode;
-        p.maxlen = c->A.maxlen;
-        p.npat = c->A.npat;
-        p.nent = c->A.nent;
-        p.ppat = c->A.use_pair ? c->A.ppat : nullptr;
-        p.ppinfo = c->A.ppinfo;
-        p.ppoff = c->A.ppoff;
-        p.ppval = c->A.ppval;
-        p.nppat = c->A.nppat;
-        p.npent = c->A.npent;
-        p.pmaxlen = c->A.pmaxlen;
-        p.pcanon = c->A.pcanon ? 1 : 0;
-        for (int k = 0; k < 8; ++k) p.pslot[k] = c->A.pslot[k];
-        p.xlo = -c->A.lpad;
-        p.xhi = c->A.ld - c->A.lpad;
-        const int t = timer_begin(c, 0);
-        CAL_HIP(c, launch_spmv_pat(p, c->stream));
-        timer_end(c, t);
-        return 0;
-    }
+    if (c->A.use_pat) return spmv_range(c, c->A.ext_off, c->A.n_local, x, y, mode, shift, im2, xprev);
     SpmvArgs a;
     a.rowptr = c->A.rowptr;
     a.col = c->A.col;
@@ -445,6 +464,40 @@ int spmv_dev(cal_ctx* c, const double* x, double* y, int mode, double shift, dou
     const int t = timer_begin(c, 0);
     CAL_HIP(c, launch_spmv(a, c->stream));
     timer_end(c, t);
+    return 0;
+}
+
+// CA matrix powers: after one halo exchange of q's s-deep
+// ghost zone, power j (1-based) is valid on global rows [row0 - (s-j) bl,
+// row1 + (s-j) br) -- it reads power j-1 one band further out -- so power s
+// is the local slab.  Each range is launched as a sub-range of the stored
+// rows, its start rounded down to even (the pair kernel's alignment) and its
+// length up to even: the extra edge rows are computed from stale halo data
+// and never read by a valid row of the next power (they lie one row outside
+// its reach), and masked loads keep them from leaking into their pair rows.
+int powers_dev(cal_ctx* c, int s, const double* q, double* const* Y, const double* shift, const double* im2,
+               const double* const* xprev) {
+    const DevMatrix& A = c->A;
+    auto mode_of = [&](int j) { return shift ? ((im2 && im2[j] != 0.0) ? 2 : 1) : 0; };
+    if (!(A.mpk && A.use_pat && s <= A.mpk_depth && s > 1)) {
+        for (int j = 0; j < s; ++j)
+            CAL_TRY(spmv_dev(c, j == 0 ? q : Y[j - 1], Y[j], mode_of(j), shift ? shift[j] : 0.0,
+                             im2 ? im2[j] : 0.0, xprev ? xprev[j] : nullptr));
+        return 0;
+    }
+    CAL_TRY(halo_exchange_deep(c, const_cast<double*>(q), s));
+    const int64_t row1 = A.row0 + A.n_local;
+    for (int j = 1; j <= s; ++j) {
+        const int64_t glo = std::max(A.ext_lo, A.row0 - (int64_t)(s - j) * A.band_l);
+        const int64_t ghi = std::min(A.ext_hi, row1 + (int64_t)(s - j) * A.band_r);
+        int64_t o = glo - A.ext_lo + A.ext_dummy;  // stored index
+        const int64_t e = ghi - A.ext_lo + A.ext_dummy;
+        o &= ~(int64_t)1;
+        int64_t len = e - o;
+        if ((len & 1) && o + len < A.n_rows) ++len;
+        CAL_TRY(spmv_range(c, o, len, j == 1 ? q : Y[j - 2], Y[j - 1], mode_of(j - 1), shift ? shift[j - 1] : 0.0,
+                           im2 ? im2[j - 1] : 0.0, xprev ? xprev[j - 1] : nullptr));
+    }
     return 0;
 }
 
@@ -572,7 +625,7 @@ int cal_set_matrix_csr(cal_ctx* c, int64_t n, const int64_t* rowptr, const int32
     }
     for (int64_t i = 0; i < n; ++i)
         if (rp[i + 1] < rp[i]) return set_error(c, CAL_ERR_ARG, "row pointers must be non-decreasing");
-    return upload_matrix(c, n, n, 0, 0, 0, 0, rp, col, val);
+    return upload_matrix(c, n, 0, n, n, 0, 0, 0, 0, rp, col, val);
 }
 
 int cal_set_matrix_csc(cal_ctx* c, int64_t n, const int64_t* jc, const int64_t* ir, const double* pr) {
@@ -622,11 +675,27 @@ int cal_spmv_format(cal_ctx* c, int* is_pattern, int* npatterns, int* nentries) 
     return 0;
 }
 
+int cal_set_mpk_depth(cal_ctx* c, int depth) {
+    if (!c || depth < 1 || depth > 64) return set_error(c, CAL_ERR_ARG, "mpk depth must be in 1..64");
+    c->mpk_depth_req = depth;
+    return 0;
+}
+
+int cal_mpk_info(cal_ctx* c, int* depth, int64_t* band_l, int64_t* band_r, int64_t* n_rows) {
+    if (!c) return CAL_ERR_ARG;
+    if (!c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
+    if (depth) *depth = c->A.mpk ? c->A.mpk_depth : 1;
+    if (band_l) *band_l = c->A.band_l;
+    if (band_r) *band_r = c->A.band_r;
+    if (n_rows) *n_rows = c->A.n_rows;
+    return 0;
+}
+
 int cal_matrix_info(cal_ctx* c, int64_t* n_local, int64_t* nnz_local, int64_t* n_global, int64_t* nghost) {
     if (!c) return CAL_ERR_ARG;
     if (!c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
     if (n_local) *n_local = c->A.n_local;
-    if (nnz_local) *nnz_local = c->A.nnz;
+    if (nnz_local) *nnz_local = c->A.nnz_loc;
     if (n_global) *n_global = c->A.n_global;
     if (nghost) *nghost = c->A.nghost;
     return 0;

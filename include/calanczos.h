@@ -70,6 +70,16 @@ int cal_set_matrix_csr(cal_ctx* ctx, int64_t n, const int64_t* rowptr, const int
 int cal_set_matrix_csr_dist(cal_ctx* ctx, int64_t n_global, int64_t row0, int64_t nlocal,
                             const int64_t* rowptr, const int64_t* colind_global, const double* val);
 int cal_matrix_info(cal_ctx* ctx, int64_t* n_local, int64_t* nnz_local, int64_t* n_global, int64_t* nghost);
+/* CA matrix-powers kernel of a distributed banded matrix (window halo layout,
+ * row-pattern format): each slab also stores the rows of its (depth-1)-band
+ * deep ghost zone, so the s <= depth powers of matrix_powers_* / one
+ * CA-Lanczos outer iteration need ONE halo exchange of q's s-band deep ghost
+ * zone instead of s (the reference's SpMV.m / matrix_powers_*.m
+ * are serial, the powers are bit-identical either way).  Applies at the next
+ * cal_set_matrix_csr_dist; depth 1 turns it off; default 8.  mpk_info reports
+ * the active depth (1 = off), the global band and the stored row count. */
+int cal_set_mpk_depth(cal_ctx* ctx, int depth);
+int cal_mpk_info(cal_ctx* ctx, int* depth, int64_t* band_l, int64_t* band_r, int64_t* n_rows);
 /* Device storage of A, chosen at the next cal_set_matrix_*: "auto" (default:
  * row patterns when A has <= 65535 distinct rows of <= 32 entries, else
  * CSR), "csr", or "pattern".  Both are lossless and give bit-identical SpMV

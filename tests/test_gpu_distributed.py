@@ -123,3 +123,88 @@ def test_rccl_single_rank_matches_local(cal, ref):
     assert np.array_equal(out1.ritz_rnorm, out2.ritz_rnorm)
     c1.close()
     c2.close()
+
+
+def _mpk_worker(rank, world, port, case, out_q):
+    """One rank: the CA matrix-powers kernel (deep ghost zone, one exchange
+    per s powers) against the one-exchange-per-SpMV distributed path."""
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import ca_lanczos_amd as cal
+    from oracle import ca_lanczos_ref as ref
+
+    def allreduce(a):
+        t = torch.from_numpy(a)
+        dist.all_reduce(t)
+
+    def exchange(peer, send, recv):
+        reqs = []
+        if send.size:
+            reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(send)), peer))
+        rt = torch.zeros(recv.size, dtype=torch.float64)
+        if recv.size:
+            reqs.append(dist.irecv(rt, peer))
+        for r in reqs:
+            r.wait()
+        if recv.size:
+            recv[:] = rt.numpy()
+
+    dim, N, s, it, orth = case
+    A = cal.matrices.laplacian_2d(N) if dim == 2 else cal.matrices.laplacian_3d(N)
+    n = A.shape[0]
+    b = cal.matrices.slab_bounds(n, world, N ** (dim - 1))
+    r0, r1 = b[rank], b[rank + 1]
+    res = {}
+    for depth in (8, 1):
+        ctx = cal.Context(0, mpk_depth=depth)
+        ctx.comm_init_host(world, rank, allreduce, exchange)
+        ctx.set_matrix_slab(n, r0, A[r0:r1])
+        v = ref.matlab_rand(n, seed=7)[r0:r1]
+        lam = np.array([7.5, 0.5, 3.0, 11.0, 1.5, 5.0, 9.0, 2.5])[:s]
+        Vn = cal.matrix_powers_newton(None, v, s, lam, 1, ctx=ctx)
+        Vm = cal.matrix_powers_monomial(None, v / np.linalg.norm(v), s, ctx=ctx)
+        out = cal.ca_lanczos_ex(A, ref.matlab_rand(n)[r0:r1], s, it, "newton", orth, diagnostics=False, ctx=ctx)
+        res[depth] = (ctx.mpk_info(), Vn, Vm, out.T, list(out.reorth))
+        ctx.close()
+    out_q.put((rank, r0, r1, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,case", [(2, (3, 12, 8, 40, "local")), (3, (3, 10, 8, 32, "local")),
+                                        (3, (2, 30, 6, 36, "full"))])
+def test_mpk_deep_ghost_zone(cal, ref, world, case):
+    """Distributed matrix powers with one s-deep halo exchange (the stored
+    ghost-zone rows are recomputed redundantly) are bit-identical to the
+    single-GPU powers on every rank's rows, and the whole CA-Lanczos run is
+    bit-identical to the one-exchange-per-SpMV distributed run.  World 3 on
+    10 or 30 planes: the 8-plane ghost zone spans two ranks and is clipped at
+    the domain ends."""
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    procs = [mpc.Process(target=_mpk_worker, args=(r, world, port, case, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    dim, N, s, it, orth = case
+    A = cal.matrices.laplacian_2d(N) if dim == 2 else cal.matrices.laplacian_3d(N)
+    n = A.shape[0]
+    v = ref.matlab_rand(n, seed=7)
+    lam = np.array([7.5, 0.5, 3.0, 11.0, 1.5, 5.0, 9.0, 2.5])[:s]
+    Vn = ref.matrix_powers_newton(A, v, s, lam, 1)
+    for rank, r0, r1, rr in res:
+        info8, info1 = rr[8][0], rr[1][0]
+        assert info8["depth"] == 8 and info1["depth"] == 1
+        assert info8["band_l"] == N ** (dim - 1) and info8["n_rows"] > r1 - r0
+        assert np.array_equal(rr[8][1], Vn[r0:r1]), rank            # newton powers, oracle bits
+        assert np.array_equal(rr[8][1], rr[1][1]) and np.array_equal(rr[8][2], rr[1][2])
+        assert np.array_equal(rr[8][3], rr[1][3]) and rr[8][4] == rr[1][4]   # whole run
+    assert all(np.array_equal(res[0][3][8][3], x[3][8][3]) for x in res)
