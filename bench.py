@@ -52,6 +52,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-iters", type=int, default=2, help="outer iterations of the CPU sample")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "spmv_traffic.json"))
+    p.add_argument("--mpk-depth", type=int, default=8,
+                   help="N > 1: ghost depth of the CA matrix-powers kernel (1 = one halo exchange per SpMV)")
     p.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                    help="N > 1 transport: RCCL (default) or host-staged gloo callbacks (rehearsal of the "
                         "distributed bench with several ranks on one GPU)")
@@ -190,7 +192,7 @@ def setup(args):
 
     ndev = ctypes.c_int(0)
     cal._lib.lib.cal_device_count(ctypes.byref(ndev))
-    ctx = cal.Context(device=local % max(ndev.value, 1))
+    ctx = cal.Context(device=local % max(ndev.value, 1), mpk_depth=args.mpk_depth)
     bounds = slab_bounds(n, world, wl.plane)
     r0, r1 = bounds[rank], bounds[rank + 1]
     rowptr, col, val = wl.rows(r0, r1)
@@ -308,6 +310,7 @@ def main():
 
     fmt, npat, nent = ctx.spmv_format()
     npairpat, npent, nsplit = ctx.spmv_pair_info()
+    mpk = ctx.mpk_info()
     apply_avg_ms = apply_ms / max(apply_cnt, 1)
     gram_avg_ms = gram_ms / max(gram_cnt, 1)
     csr_spmv = None
@@ -367,7 +370,10 @@ def main():
         "data": wl.data,
         "config": {"workload": wl.desc % (n, nnz_total),
                    "s": s, "basis": args.basis, "orth": args.orth, "parallelism": "row-slab x%d" % world,
-                   "comm": (args.comm if world > 1 else "none")},
+                   "comm": (args.comm if world > 1 else "none"),
+                   "halo": ("CA matrix powers: one %d-band deep exchange per outer iteration (band %d rows)"
+                            % (s, mpk["band_l"]) if mpk["depth"] > 1 and s <= mpk["depth"]
+                            else "one exchange per SpMV") if world > 1 else "none"},
         "spmv_format": ("%s (%d row patterns, %d entries; %d pair patterns, %d entries, %d split pairs)"
                         % (fmt, npat, nent, npairpat, npent, nsplit)) if fmt == "pattern" else fmt,
         "spmv_gbps": spmv_gbps,
