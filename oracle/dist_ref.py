@@ -188,3 +188,114 @@ def ca_lanczos_dist(slab: Slab, r_local, s, iter, basis="newton"):
         T[m0, m0 - 1] = b[k - 2]
         T[m0 + s, m0 + s - 1] = b[k - 1]
     return T[: s * t, : s * t]
+
+
+# --------------------------------------------------------------------------
+# CA matrix powers with an s-deep ghost zone (comm.cpp cal_set_matrix_csr_dist
+# + halo_exchange_deep, runtime.cpp powers_dev): every slab stores the rows of
+# its (D-1)-band ghost zone, fetched once from their owners; the s powers of
+# an outer iteration need one exchange of q's s-band ghost zone.
+# --------------------------------------------------------------------------
+
+class MPKSlab:
+    """Rows [r0, r1) plus the ghost-zone rows [elo, ehi) of depth D."""
+
+    def __init__(self, A_rows: sp.csr_matrix, bounds, rank, depth):
+        self.rank, self.nranks, self.bounds = rank, len(bounds) - 1, bounds
+        self.r0, self.r1 = bounds[rank], bounds[rank + 1]
+        self.n = bounds[-1]
+        self.D = depth
+        rows = A_rows.tocsr()  # only this slab's rows (global columns)
+        # global band (all-reduced max of row - col and col - row)
+        ri = np.repeat(np.arange(self.r0, self.r1), np.diff(rows.indptr))
+        d = rows.indices.astype(np.int64) - ri
+        bb = torch.zeros(2 * self.nranks, dtype=torch.float64)
+        bb[2 * rank] = float(max(0, -d.min())) if d.size else 0.0
+        bb[2 * rank + 1] = float(max(0, d.max())) if d.size else 0.0
+        dist.all_reduce(bb)
+        self.bl = int(bb[0::2].max())
+        self.br = int(bb[1::2].max())
+        self.elo, self.ehi = self._ext(rank)
+        # fetch the ghost-zone rows from their owners (counts, then rows)
+        got = {}
+        for q in range(self.nranks):
+            if q == rank:
+                continue
+            nlo, nhi = max(bounds[q], self.elo), min(bounds[q + 1], self.ehi)
+            qlo, qhi = self._ext(q)
+            glo, ghi = max(self.r0, qlo), min(self.r1, qhi)
+            get, give = nhi > nlo, ghi > glo
+            if not (get or give):
+                continue
+            s1 = torch.tensor([float(rows.indptr[ghi - self.r0] - rows.indptr[glo - self.r0])] if give else [],
+                              dtype=torch.float64)
+            r1 = torch.zeros(1 if get else 0, dtype=torch.float64)
+            Slab._exchange(q, s1, r1)
+            if give:
+                sub = rows[glo - self.r0:ghi - self.r0]
+                s2 = torch.from_numpy(np.concatenate([np.diff(sub.indptr).astype(np.float64),
+                                                      sub.indices.astype(np.float64), sub.data]))
+            else:
+                s2 = torch.zeros(0, dtype=torch.float64)
+            r2 = torch.zeros((nhi - nlo) + 2 * int(r1[0]) if get else 0, dtype=torch.float64)
+            Slab._exchange(q, s2, r2)
+            if get:
+                nr, nz = nhi - nlo, int(r1[0])
+                lens = r2[:nr].numpy().astype(np.int64)
+                ip = np.concatenate([[0], np.cumsum(lens)])
+                got[(nlo, nhi)] = sp.csr_matrix((r2[nr + nz:].numpy(), r2[nr:nr + nz].numpy().astype(np.int64), ip),
+                                                shape=(nr, self.n))
+        pieces = [got[k] for k in sorted(got) if k[0] < self.r0] + [rows] + \
+                 [got[k] for k in sorted(got) if k[0] >= self.r1]
+        ext = sp.vstack(pieces).tocsr()
+        assert ext.shape[0] == self.ehi - self.elo
+        # window: global rows [wlo, whi) of every vector
+        self.wlo = max(0, self.r0 - self.D * self.bl)
+        self.whi = min(self.n, self.r1 + self.D * self.br)
+        self.ext = sp.csr_matrix((ext.data, ext.indices - self.wlo, ext.indptr),
+                                 shape=(ext.shape[0], self.whi - self.wlo))
+
+    def _ext(self, q):
+        b = self.bounds
+        return max(0, b[q] - (self.D - 1) * self.bl), min(self.n, b[q + 1] + (self.D - 1) * self.br)
+
+    def deep_halo(self, x_local, d):
+        """Window vector with q's d-band ghost zone received (halo_exchange_deep)."""
+        w = np.zeros(self.whi - self.wlo)
+        w[self.r0 - self.wlo:self.r1 - self.wlo] = x_local
+        b = self.bounds
+        for q in range(self.nranks):
+            if q == self.rank:
+                continue
+            if q < self.rank:
+                rlo, rhi = max(b[q], self.r0 - d * self.bl), min(b[q + 1], self.r0)
+                slo, shi = self.r0, min(self.r1, b[q + 1] + d * self.br)
+            else:
+                rlo, rhi = max(b[q], self.r1), min(b[q + 1], self.r1 + d * self.br)
+                slo, shi = max(self.r0, b[q] - d * self.bl), self.r1
+            rc, sc = max(0, rhi - rlo), max(0, shi - slo)
+            if rc == 0 and sc == 0:
+                continue
+            recv = torch.zeros(rc, dtype=torch.float64)
+            send = torch.from_numpy(np.ascontiguousarray(x_local[slo - self.r0:slo - self.r0 + sc]))
+            Slab._exchange(q, send, recv)
+            w[rlo - self.wlo:rlo - self.wlo + rc] = recv.numpy()
+        return w
+
+    def powers(self, q_local, s, shifts=None):
+        """V (local rows x (s+1)) = [q, (A - l_1)q, ...] from one deep exchange:
+        power j on rows [r0 - (s-j) bl, r1 + (s-j) br) of the stored ghost zone."""
+        assert s <= self.D
+        x = self.deep_halo(q_local, s)
+        V = [x]
+        for j in range(1, s + 1):
+            lo = max(self.elo, self.r0 - (s - j) * self.bl)
+            hi = min(self.ehi, self.r1 + (s - j) * self.br)
+            y = np.zeros_like(x)
+            sub = self.ext[lo - self.elo:hi - self.elo]
+            y[lo - self.wlo:hi - self.wlo] = sub @ x
+            if shifts is not None:
+                y[lo - self.wlo:hi - self.wlo] -= shifts[j - 1] * x[lo - self.wlo:hi - self.wlo]
+            V.append(y)
+            x = y
+        return np.stack([v[self.r0 - self.wlo:self.r1 - self.wlo] for v in V], axis=1)

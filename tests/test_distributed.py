@@ -71,3 +71,55 @@ def test_row_slab_ca_lanczos_matches_single_process(ref, world, case):
     # every rank holds the same (replicated) T
     for _, _, T, _, _ in res[1:]:
         assert np.array_equal(T, res[0][2])
+
+
+def _mpk_worker(rank, world, port, case, out_q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import ca_lanczos_ref as ref
+    from oracle import dist_ref as dr
+    dim, N, s, D = case
+    A = ref.laplacian_2d(N) if dim == 2 else ref.laplacian_3d(N)
+    n = A.shape[0]
+    bounds = dr.slab_bounds(n, world, N ** (dim - 1))
+    r0, r1 = bounds[rank], bounds[rank + 1]
+    m = dr.MPKSlab(A[r0:r1], bounds, rank, D)
+    q = ref.matlab_rand(n, seed=3)
+    lam = np.linspace(0.5, 4.0 * dim - 0.5, s)
+    out_q.put((rank, r0, r1, m.bl, m.elo, m.ehi, m.powers(q[r0:r1], s, lam), m.powers(q[r0:r1], s)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,case", [(2, (3, 9, 8, 8)), (3, (3, 8, 6, 8)), (4, (2, 24, 8, 8)),
+                                        (3, (2, 20, 4, 6))])
+def test_mpk_deep_ghost_zone_restatement(ref, world, case):
+    """The CA matrix-powers scheme of comm.cpp / runtime.cpp (ghost rows
+    fetched from owners, one s-band exchange, shrinking ranges) on gloo:
+    the powers equal the global Newton / monomial powers bit for bit on
+    every slab, including ghost zones that span several ranks (3-4 ranks on
+    8-9 planes with an 8-plane zone) and clip at the domain ends."""
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mpk_worker, args=(r, world, port, case, qq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [qq.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    dim, N, s, D = case
+    A = ref.laplacian_2d(N) if dim == 2 else ref.laplacian_3d(N)
+    q = ref.matlab_rand(A.shape[0], seed=3)
+    lam = np.linspace(0.5, 4.0 * dim - 0.5, s)
+    Vn = ref.matrix_powers_newton(A, q, s, lam, 1)
+    Vm = np.hstack([q[:, None], ref.matrix_powers_monomial(A, q, s)])
+    for rank, r0, r1, bl, elo, ehi, Pn, Pm in res:
+        assert bl == N ** (dim - 1)
+        assert elo == max(0, r0 - (D - 1) * bl) and ehi == min(A.shape[0], r1 + (D - 1) * bl)
+        assert np.array_equal(Pn, Vn[r0:r1]), rank
+        assert np.array_equal(Pm, Vm[r0:r1]), rank
