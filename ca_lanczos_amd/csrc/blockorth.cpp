@@ -638,7 +638,7 @@ int project_and_normalize_blocks_dev(cal_ctx* c, int64_t n, int64_t ld, int nblo
         CAL_TRY(gram_host(c, n, Xp, Xp, G.data()));
         for (int i = 0; i < m; ++i) before[i] = std::sqrt(G[i + (size_t)i * m]);   // :17-22
     }
-    CAL_HIP(c, hipMemcpyAsync(dY, dX, (size_t)m * ld * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    CAL_HIP(c, copy_cols(c, dY, dX, ld, n, m));
     std::vector<std::vector<double>> RY(nblocks);
     for (int i = 0; i < nblocks; ++i) RY[i].assign((size_t)std::max(widths[i], 0) * m, 0.0);
     CAL_TRY(project_blocks(c, n, ld, nblocks, dQ, widths, m, dY, false, RY));  // :25
@@ -714,7 +714,7 @@ int normalize_wide_dev(cal_ctx* c, int64_t n, int64_t ld, const double* dX, int 
         which ^= 1;
     }
     if (src != dQ)
-        CAL_HIP(c, hipMemcpyAsync(dQ, src, (size_t)m * ld * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+        CAL_HIP(c, copy_cols(c, dQ, src, ld, n, m));
     return 0;
 }
 

@@ -306,6 +306,14 @@ int powers_dev(cal_ctx* c, int s, const double* q, double* const* Y, const doubl
                const double* const* xprev);
 // Halo exchange of the d-deep ghost zone of x (contiguous row ranges; mpk only).
 int halo_exchange_deep(cal_ctx* c, double* x, int d);
+// copy the n local rows of m columns (leading dimension ld) on the context
+// stream; src/dst are local-origin pointers (a whole-column copy from there
+// would run lpad entries past the last column)
+inline hipError_t copy_cols(cal_ctx* c, double* dst, const double* src, int64_t ld, int64_t n, int m) {
+    if (n <= 0 || m <= 0) return hipSuccess;
+    return hipMemcpy2DAsync(dst, ld * sizeof(double), src, ld * sizeof(double), n * sizeof(double), m,
+                            hipMemcpyDeviceToDevice, c->stream);
+}
 // pointer to column j of a vector buffer laid out with A.ld / A.lpad
 inline double* vcol(const cal_ctx* c, double* base, int64_t j) { return base + j * c->A.ld + c->A.lpad; }
 int ensure_partial(cal_ctx* c, size_t doubles);

@@ -495,7 +495,7 @@ static int periodic_update(cal_ctx* c, LanczosState& L) {
     const int w = (k - 1) * s, m = s + 1;
     CAL_TRY(ensure_work(c, m, ld));
     double* dX = work_col(c, 0) + c->A.lpad;
-    CAL_HIP(c, hipMemcpyAsync(dX, L.col(w), (size_t)m * ld * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    CAL_HIP(c, copy_cols(c, dX, L.col(w), ld, n, m));
     Panel Qp = panel(), X = panel();
     if (w > 0) panel_add(Qp, L.col(0), ld, w);
     panel_add(X, dX, ld, m);
@@ -550,8 +550,7 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
             // [Q(:,1:s+1),R_] = projectAndNormalize({Q_conv},Q_,true) (restarted_ca_lanczos.m:291)
             CAL_TRY(ensure_work(c, s + 1, ld));
             double* dW = work_col(c, 0) + c->A.lpad;
-            CAL_HIP(c, hipMemcpyAsync(dW, L.col(0), (size_t)(s + 1) * ld * sizeof(double), hipMemcpyDeviceToDevice,
-                                      c->stream));
+            CAL_HIP(c, copy_cols(c, dW, L.col(0), ld, n, s + 1));
             Panel Qc = panel(), Xw = panel();
             if (L.next > 0) panel_add(Qc, L.dExt, ld, L.next);
             panel_add(Xw, dW, ld, s + 1);
@@ -595,8 +594,7 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
             CAL_TRY(ensure_work(c, 2 * s, ld));
             double* dW = work_col(c, 0) + c->A.lpad;
             double* dY = work_col(c, s) + c->A.lpad;
-            CAL_HIP(c, hipMemcpyAsync(dW, L.col((k - 1) * s + 1), (size_t)s * ld * sizeof(double),
-                                      hipMemcpyDeviceToDevice, c->stream));
+            CAL_HIP(c, copy_cols(c, dW, L.col((k - 1) * s + 1), ld, n, s));
             std::vector<double*> dQ{L.dExt ? L.dExt : L.col(0), L.col(0)};
             const int widths[2] = {L.next, (k - 2) * s};
             std::vector<std::vector<double>> RZ;
