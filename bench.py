@@ -50,7 +50,7 @@ def parse():
     p.add_argument("--basis", default="newton")
     p.add_argument("--orth", default="local")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-iters", type=int, default=2, help="outer iterations of the CPU sample")
+    p.add_argument("--cpu-iters", type=int, default=3, help="outer iterations of the CPU sample")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "spmv_traffic.json"))
     p.add_argument("--mpk-depth", type=int, default=8,
                    help="N > 1: ghost depth of the CA matrix-powers kernel (1 = one halo exchange per SpMV)")
@@ -124,9 +124,30 @@ def _blas_threads():
 
 
 def cpu_baseline(wl, s, iters, basis="newton"):
-    """The oracle restatement (NumPy/SciPy) timed on this host: Newton
-    prologue excluded, `iters` outer iterations of ca_lanczos_basic with
-    diagnostics off, on the same matrix and start vector."""
+    """The C/OpenMP restatement (oracle/c/ca_lanczos_omp.c, all host cores)
+    timed on this host: Newton prologue excluded, `iters` outer iterations of
+    ca_lanczos_basic 'local' (k = 1..iters, diagnostics off) on the same
+    matrix and start vector (SURVEY §8d CPU baseline (2))."""
+    from oracle import ca_lanczos_ref as ref
+    from oracle import omp
+    A = wl.full()
+    r = ref.matlab_rand(wl.n)
+    q = r / math.sqrt(r @ r)
+    Bk, _, _ = ref.newton_change_of_basis(A, q, s)
+    omp.lib()
+    t0 = time.perf_counter()
+    omp.ca_lanczos_local(A, q, Bk, s, iters, basis == "newton")
+    dt = time.perf_counter() - t0
+    th = omp.threads()
+    return {"value": iters / dt, "unit": "outer-iters/s", "cores": th, "kind": "port",
+            "sample": "oracle/c/ca_lanczos_omp.c (C/OpenMP, %d threads): %d outer iterations (k=1..%d, s=%d, "
+                      "Newton, 'local', Householder TSQR normalize, diagnostics off) on the same %s matrix; "
+                      "%.1f s" % (th, iters, iters, s, wl.name, dt)}
+
+
+def cpu_baseline_numpy(wl, s, iters, basis="newton"):
+    """The NumPy restatement (oracle/ca_lanczos_ref.py) on the same sample:
+    SciPy's CSR SpMV is single-threaded, LAPACK QR uses the BLAS threads."""
     from oracle import ca_lanczos_ref as ref
     blas_threads = _blas_threads()
     A = wl.full()
@@ -137,10 +158,9 @@ def cpu_baseline(wl, s, iters, basis="newton"):
     ref.ca_lanczos_basic(A, q, Bk, iters, s, basis, "local", diagnostics=False)
     dt = time.perf_counter() - t0
     return {"value": iters / dt, "unit": "outer-iters/s", "cores": int(blas_threads), "kind": "port",
-            "sample": "oracle/ca_lanczos_ref.py ca_lanczos_basic, %d outer iterations (k=1..%d, s=%d, "
-                      "Newton, 'local', diagnostics off) on the same %s matrix; SciPy CSR SpMV is "
-                      "single-threaded, LAPACK QR uses %d threads; %.1f s"
-                      % (iters, iters, s, wl.name, blas_threads, dt)}
+            "sample": "oracle/ca_lanczos_ref.py ca_lanczos_basic, %d outer iterations on the same %s matrix; "
+                      "SciPy CSR SpMV single-threaded, LAPACK QR %d threads; %.1f s"
+                      % (iters, wl.name, blas_threads, dt)}
 
 
 def cpu_baseline_irl(wl, s, max_lanczos, nw):
@@ -393,6 +413,7 @@ def main():
         line["spmv_host_roundtrip_ms"] = host_rt_ms
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(wl, s, args.cpu_iters, args.basis)
+        line["cpu_baseline_numpy"] = cpu_baseline_numpy(wl, s, 2, args.basis)
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()

@@ -1,0 +1,321 @@
+/* ca_lanczos_omp.c -- multithreaded C restatement of the reference's
+ * CA-Lanczos outer loop ('local' orthogonalisation, diagnostics off).
+ *
+ * TEST INFRASTRUCTURE ONLY (the CPU baseline of bench.py and a second oracle
+ * checked against oracle/ca_lanczos_ref.py by tests/test_oracle_c.py).
+ * Nothing in the product links it.  SURVEY §8d asks for this second CPU
+ * number: the NumPy restatement's SpMV is single-threaded, this one runs
+ * every n-length loop on all host cores with OpenMP.
+ *
+ * Follows, line by line in structure:
+ *   ca_lanczos.m:150-245   ca_lanczos_basic, orth 'local' (k = 1 normalize,
+ *                          k > 1 projectAndNormalize against the previous
+ *                          block, T update :200-223)
+ *   matrix_powers_newton.m:15-48 (real shifts, modifiedp = 1) and
+ *   matrix_powers_monomial.m:6-12 (through ca_lanczos.m:110-118)
+ *   projectAndNormalize.m:3-90 (doreorth = true, threshold 0.5 at :52)
+ *   project.m:7-58 (one block, doreorth = false)
+ *   normalize.m:3-36 / tsqr.m:7-12: Householder QR + sign fix.  The QR is a
+ *   TSQR (Householder per thread block, Householder of the stacked R
+ *   factors, explicit Q through the tree): R is unique once its diagonal is
+ *   made positive, so it equals MATLAB's qr(A,0) R up to rounding.
+ * The Newton shifts / change-of-basis matrix Bk come from the caller (the
+ * NumPy oracle's prologue, ca_lanczos.m:66-72).
+ */
+#include <math.h>
+#include <omp.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define IDX(i, j, ld) ((size_t)(i) + (size_t)(j) * (size_t)(ld))
+
+/* ---- dense helpers (column-major) ---------------------------------------- */
+
+/* LAPACK dlarfg on x[0..len): alpha = x[0]; returns tau, x[0] = beta,
+ * x[1..] = v(2:end) */
+static double house(double* x, size_t len, size_t inc) {
+    double xn = 0.0;
+    for (size_t i = 1; i < len; ++i) xn += x[i * inc] * x[i * inc];
+    xn = sqrt(xn);
+    if (xn == 0.0) return 0.0;
+    const double alpha = x[0];
+    const double beta = -copysign(hypot(alpha, xn), alpha);
+    const double sc = 1.0 / (alpha - beta);
+    for (size_t i = 1; i < len; ++i) x[i * inc] *= sc;
+    x[0] = beta;
+    return (beta - alpha) / beta;
+}
+
+/* Householder QR in place of A (rows x m, ld); tau[m] */
+static void geqr2(size_t rows, int m, double* A, size_t ld, double* tau) {
+    for (int j = 0; j < m; ++j) {
+        if ((size_t)j >= rows) {
+            tau[j] = 0.0;
+            continue;
+        }
+        double* col = A + IDX(j, j, ld);
+        tau[j] = house(col, rows - j, 1);
+        if (tau[j] == 0.0) continue;
+        for (int c = j + 1; c < m; ++c) {
+            double* cc = A + IDX(j, c, ld);
+            double d = cc[0];
+            for (size_t i = 1; i < rows - j; ++i) d += col[i] * cc[i];
+            d *= tau[j];
+            cc[0] -= d;
+            for (size_t i = 1; i < rows - j; ++i) cc[i] -= d * col[i];
+        }
+    }
+}
+
+/* apply H(0) ... H(m-1) (reflectors in A, tau) to C (rows x m, ldc): C = Q C */
+static void apply_q(size_t rows, int m, const double* A, size_t ld, const double* tau, double* C, size_t ldc,
+                    int ncol) {
+    for (int j = m - 1; j >= 0; --j) {
+        if (tau[j] == 0.0 || (size_t)j >= rows) continue;
+        const double* v = A + IDX(j, j, ld);
+        for (int c = 0; c < ncol; ++c) {
+            double* cc = C + IDX(j, c, ldc);
+            double d = cc[0];
+            for (size_t i = 1; i < rows - j; ++i) d += v[i] * cc[i];
+            d *= tau[j];
+            cc[0] -= d;
+            for (size_t i = 1; i < rows - j; ++i) cc[i] -= d * v[i];
+        }
+    }
+}
+
+/* tsqr.m:7-12: [Q,R] = qr(X,0), d = sign(diag(R)), R = diag(d) R, Q = Q diag(d).
+ * X (n x m, ld n) is overwritten by Q; R is m x m (ld m). */
+static void tsqr(size_t n, int m, double* X, double* R) {
+    int P = omp_get_max_threads();
+    if ((size_t)P * (size_t)m * 4 > n) P = 1;
+    double* Rs = calloc((size_t)P * m * m, sizeof(double));
+    double* taus = calloc((size_t)P * m, sizeof(double));
+#pragma omp parallel num_threads(P)
+    {
+        const int p = omp_get_thread_num();
+        const size_t r0 = n * (size_t)p / P, r1 = n * (size_t)(p + 1) / P;
+        double* Xb = X + r0;
+        geqr2(r1 - r0, m, Xb, n, taus + (size_t)p * m);
+        for (int j = 0; j < m; ++j)
+            for (int i = 0; i <= j; ++i) Rs[IDX((size_t)p * m + i, j, (size_t)P * m)] = Xb[IDX(i, j, n)];
+    }
+    /* QR of the stacked R factors */
+    const size_t PR = (size_t)P * m;
+    double* ttop = calloc(m, sizeof(double));
+    geqr2(PR, m, Rs, PR, ttop);
+    for (int j = 0; j < m; ++j)
+        for (int i = 0; i < m; ++i) R[IDX(i, j, m)] = i <= j ? Rs[IDX(i, j, PR)] : 0.0;
+    double* Qtop = calloc(PR * m, sizeof(double));
+    for (int j = 0; j < m; ++j) Qtop[IDX(j, j, PR)] = 1.0;
+    apply_q(PR, m, Rs, PR, ttop, Qtop, PR, m);
+    /* Q block p = H_p [Qtop block p; 0] */
+#pragma omp parallel num_threads(P)
+    {
+        const int p = omp_get_thread_num();
+        const size_t r0 = n * (size_t)p / P, r1 = n * (size_t)(p + 1) / P, rows = r1 - r0;
+        double* Xb = X + r0;
+        double* C = calloc(rows * m, sizeof(double));
+        for (int j = 0; j < m; ++j)
+            for (int i = 0; i < m && (size_t)i < rows; ++i) C[IDX(i, j, rows)] = Qtop[IDX((size_t)p * m + i, j, PR)];
+        apply_q(rows, m, Xb, n, taus + (size_t)p * m, C, rows, m);
+        for (int j = 0; j < m; ++j) memcpy(Xb + (size_t)j * n, C + (size_t)j * rows, rows * sizeof(double));
+        free(C);
+    }
+    /* sign fix (sign(0) = 0, as MATLAB) */
+    for (int j = 0; j < m; ++j) {
+        const double rj = R[IDX(j, j, m)];
+        const double d = rj > 0.0 ? 1.0 : (rj < 0.0 ? -1.0 : 0.0);
+        for (int c = 0; c < m; ++c) R[IDX(j, c, m)] *= d;
+        double* q = X + (size_t)j * n;
+#pragma omp parallel for schedule(static)
+        for (size_t i = 0; i < n; ++i) q[i] *= d;
+    }
+    free(Rs);
+    free(taus);
+    free(ttop);
+    free(Qtop);
+}
+
+/* G (w x m, ld w) = Qp' X, Qp n x w, X n x m (both ld n) */
+static void gemm_tn(size_t n, int w, int m, const double* Qp, const double* X, double* G) {
+    memset(G, 0, (size_t)w * m * sizeof(double));
+#pragma omp parallel
+    {
+        double* acc = calloc((size_t)w * m, sizeof(double));
+#pragma omp for schedule(static)
+        for (size_t i = 0; i < n; ++i)
+            for (int j = 0; j < m; ++j) {
+                const double x = X[IDX(i, j, n)];
+                for (int a = 0; a < w; ++a) acc[IDX(a, j, w)] += Qp[IDX(i, a, n)] * x;
+            }
+#pragma omp critical
+        for (size_t e = 0; e < (size_t)w * m; ++e) G[e] += acc[e];
+        free(acc);
+    }
+}
+
+/* X -= Qp G */
+static void gemm_sub(size_t n, int w, int m, const double* Qp, const double* G, double* X) {
+#pragma omp parallel for schedule(static)
+    for (size_t i = 0; i < n; ++i)
+        for (int j = 0; j < m; ++j) {
+            double s = 0.0;
+            for (int a = 0; a < w; ++a) s += Qp[IDX(i, a, n)] * G[IDX(a, j, w)];
+            X[IDX(i, j, n)] -= s;
+        }
+}
+
+static double col_norm(size_t n, const double* x) {
+    double s = 0.0;
+#pragma omp parallel for reduction(+ : s) schedule(static)
+    for (size_t i = 0; i < n; ++i) s += x[i] * x[i];
+    return sqrt(s);
+}
+
+/* X (r x m) <- X / R, R upper (m x m): forward substitution by columns */
+static void rdiv_upper(int r, int m, double* X, int ldx, const double* R, int ldr) {
+    for (int j = 0; j < m; ++j) {
+        for (int k = 0; k < j; ++k) {
+            const double f = R[IDX(k, j, ldr)];
+            for (int i = 0; i < r; ++i) X[IDX(i, j, ldx)] -= X[IDX(i, k, ldx)] * f;
+        }
+        const double d = R[IDX(j, j, ldr)];
+        for (int i = 0; i < r; ++i) X[IDX(i, j, ldx)] /= d;
+    }
+}
+
+/* y = A x [- shift x] */
+static void spmv(size_t n, const int64_t* rp, const int32_t* col, const double* val, const double* x, double* y,
+                 double shift, int shifted) {
+#pragma omp parallel for schedule(static)
+    for (size_t i = 0; i < n; ++i) {
+        double s = 0.0;
+        for (int64_t p = rp[i]; p < rp[i + 1]; ++p) s += val[p] * x[col[p]];
+        y[i] = shifted ? s - shift * x[i] : s;
+    }
+}
+
+/* ca_lanczos_basic, orth 'local', diagnostics off (ca_lanczos.m:150-245).
+ * q: normalised start vector; Bk (s+1) x s; T_out (st x st, ld st);
+ * reorth_out[t]: 1 where projectAndNormalize took its second pass. */
+int cal_omp_ca_lanczos_local(int64_t n_, const int64_t* rowptr, const int32_t* col, const double* val,
+                             const double* q, const double* Bk, int s, int t, int newton, double* T_out,
+                             int* reorth_out) {
+    if (n_ < 1 || s < 1 || t < 1) return -1;
+    const size_t n = (size_t)n_;
+    const int s1 = s + 1, st = s * t;
+    double* Q = malloc(n * (size_t)(st + 1) * sizeof(double));
+    double* V = malloc(n * (size_t)s1 * sizeof(double));
+    double* Y = malloc(n * (size_t)s * sizeof(double));
+    double* T = calloc((size_t)(st + 1) * (st + 1), sizeof(double));
+    double* b = calloc((size_t)t + 1, sizeof(double));
+    if (!Q || !V || !Y || !T || !b) return -2;
+    const int ldT = st + 1;
+    memcpy(Q, q, n * sizeof(double));
+    for (int k = 1; k <= t; ++k) {
+        /* matrix powers (ca_lanczos.m:110-118) */
+        memcpy(V, Q + (size_t)((k - 1) * s) * n, n * sizeof(double));
+        for (int i = 0; i < s; ++i)
+            spmv(n, rowptr, col, val, V + (size_t)i * n, V + (size_t)(i + 1) * n, newton ? Bk[IDX(i, i, s1)] : 0.0,
+                 newton);
+        if (k == 1) {
+            /* [Q(:,1:s+1),Rk] = normalize(V) ; T = Rk*Bk/Rk(1:s,1:s) (:176-182) */
+            double Rk[17 * 17], RB[17 * 16], R11[16 * 16];
+            tsqr(n, s1, V, Rk);
+            memcpy(Q, V, n * (size_t)s1 * sizeof(double));
+            for (int j = 0; j < s; ++j)
+                for (int i = 0; i < s1; ++i) {
+                    double a = 0.0;
+                    for (int l = 0; l < s1; ++l) a += Rk[IDX(i, l, s1)] * Bk[IDX(l, j, s1)];
+                    RB[IDX(i, j, s1)] = a;
+                }
+            for (int j = 0; j < s; ++j)
+                for (int i = 0; i < s; ++i) R11[IDX(i, j, s)] = Rk[IDX(i, j, s1)];
+            rdiv_upper(s1, s, RB, s1, R11, s);
+            for (int j = 0; j < s; ++j)
+                for (int i = 0; i < s1; ++i) T[IDX(i, j, ldT)] = RB[IDX(i, j, s1)];
+            b[0] = RB[IDX(s, s - 1, s1)];
+            reorth_out[0] = 0;
+            continue;
+        }
+        /* [Q_,Rk_] = projectAndNormalize({Q(:,(k-2)s+1:(k-1)s+1)}, V(:,2:s+1), true) (:187) */
+        const double* Qp = Q + (size_t)((k - 2) * s) * n;
+        double* X = V + n;
+        double before[16], after[16], RY[17 * 16], RZ[17 * 16], R[16 * 16];
+        for (int j = 0; j < s; ++j) before[j] = col_norm(n, X + (size_t)j * n);        /* :17-22 */
+        memcpy(Y, X, n * (size_t)s * sizeof(double));
+        gemm_tn(n, s1, s, Qp, Y, RY);                                                 /* project :25 */
+        gemm_sub(n, s1, s, Qp, RY, Y);
+        memcpy(X, Y, n * (size_t)s * sizeof(double));                                  /* keep Y */
+        tsqr(n, s, X, R);                                                              /* normalize :26 */
+        double worst = -1.0;
+        for (int j = 0; j < s; ++j) {
+            double a = 0.0;
+            for (int i = 0; i < s; ++i) a += R[IDX(i, j, s)] * R[IDX(i, j, s)];
+            after[j] = sqrt(a);                                                        /* :45-48 */
+            const double rel = fabs(before[j] - after[j]) / before[j];
+            if (rel > worst || (worst != worst)) worst = rel;
+        }
+        int reorth = worst > 0.5;                                                      /* :52 */
+        const double* Rkk_s = RY;
+        if (reorth) {
+            gemm_tn(n, s1, s, Qp, Y, RZ);                                              /* :63 */
+            gemm_sub(n, s1, s, Qp, RZ, Y);
+            tsqr(n, s, Y, R);                                                          /* :64 */
+            for (int e = 0; e < s1 * s; ++e) RZ[e] += RY[e];                           /* :71-73 */
+            Rkk_s = RZ;
+            memcpy(X, Y, n * (size_t)s * sizeof(double));
+        }
+        reorth_out[k - 1] = reorth;
+        memcpy(Q + (size_t)((k - 1) * s + 1) * n, X, n * (size_t)s * sizeof(double)); /* :188 */
+        /* T update (:200-223) */
+        double Rk[17 * 17], R11[16 * 16], Rkk11[16 * 16], t1[16 * 16], t3[16 * 16];
+        memset(Rk, 0, sizeof(Rk));
+        Rk[0] = 1.0;
+        for (int j = 1; j <= s; ++j) {
+            Rk[IDX(0, j, s1)] = Rkk_s[IDX(s, j - 1, s1)];
+            for (int i = 1; i <= s; ++i) Rk[IDX(i, j, s1)] = R[IDX(i - 1, j - 1, s)];
+        }
+        memset(Rkk11, 0, sizeof(Rkk11));
+        for (int j = 0; j < s; ++j)
+            for (int i = 0; i < s; ++i) R11[IDX(i, j, s)] = Rk[IDX(i, j, s1)];
+        for (int j = 1; j < s; ++j)
+            for (int i = 0; i < s; ++i) Rkk11[IDX(i, j, s)] = Rkk_s[IDX(i, j - 1, s1)];
+        const double rho = Rk[IDX(s, s, s1)], rho_t = Rk[IDX(s - 1, s - 1, s1)];
+        const double bk = Bk[IDX(s, s - 1, s1)], bprev = b[k - 2];
+        for (int j = 0; j < s; ++j)
+            for (int i = 0; i < s; ++i) {
+                double a = 0.0;
+                for (int l = 0; l < s; ++l) a += R11[IDX(i, l, s)] * Bk[IDX(l, j, s1)];
+                t1[IDX(i, j, s)] = a;
+            }
+        rdiv_upper(s, s, t1, s, R11, s);
+        memset(t3, 0, sizeof(t3));
+        for (int j = 0; j < s; ++j) t3[IDX(0, j, s)] = bprev * Rkk11[IDX(s - 1, j, s)];
+        rdiv_upper(s, s, t3, s, R11, s);
+        const int m0 = s * (k - 1);
+        for (int j = 0; j < s; ++j)
+            for (int i = 0; i < s; ++i) {
+                double v = t1[IDX(i, j, s)];
+                if (j == s - 1) v += (bk / rho_t) * Rk[IDX(i, s, s1)];
+                v -= t3[IDX(i, j, s)];
+                T[IDX(m0 + i, m0 + j, ldT)] = v;
+            }
+        b[k - 1] = bk * (rho / rho_t);                                                /* :214 */
+        T[IDX(m0 - 1, m0, ldT)] = bprev;
+        T[IDX(m0, m0 - 1, ldT)] = bprev;
+        T[IDX(m0 + s, m0 + s - 1, ldT)] = b[k - 1];
+    }
+    for (int j = 0; j < st; ++j)
+        for (int i = 0; i < st; ++i) T_out[IDX(i, j, st)] = T[IDX(i, j, ldT)];
+    free(Q);
+    free(V);
+    free(Y);
+    free(T);
+    free(b);
+    return 0;
+}
+
+int cal_omp_threads(void) { return omp_get_max_threads(); }
