@@ -63,13 +63,15 @@ def _worker(rank, world, port, case, out_q):
     check(ctx.h, lib.cal_spmv(ctx.h, ptr(xl), ptr(y)))
     ok_spmv = np.array_equal(y, (A @ x)[r0:r1])
     out = cal.ca_lanczos_ex(A, ref.matlab_rand(n)[r0:r1], s, it, "newton", orth, diagnostics=True, ctx=ctx)
-    out_q.put((rank, ok_spmv, info, out.T, out.ritz_rnorm, out.orth_err, list(out.reorth)))
+    out_q.put((rank, ok_spmv, info, out.T, out.ritz_rnorm, out.orth_err, list(out.reorth),
+               (out.info.get("n_orth_breaks"), out.info.get("n_ritz_locked"))))
     ctx.close()
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case", [(2, 32, 8, 48, "local"), (3, 10, 8, 32, "full")])
+@pytest.mark.parametrize("case", [(2, 32, 8, 48, "local"), (3, 10, 8, 32, "full"), (2, 24, 8, 64, "periodic"),
+                                  (2, 24, 8, 64, "selective")])
 def test_two_ranks_one_gpu_match_single(cal, ref, case):
     world = 2
     mpc = mp.get_context("spawn")
@@ -87,10 +89,11 @@ def test_two_ranks_one_gpu_match_single(cal, ref, case):
     r = ref.matlab_rand(A.shape[0])
     single = cal.ca_lanczos_ex(A, r, s, it, "newton", orth, diagnostics=True)
     normA = 4.0 * dim
-    for rank, ok_spmv, info, T, rn, oe, flags in res:
+    for rank, ok_spmv, info, T, rn, oe, flags, brk in res:
         assert ok_spmv, rank
         assert info["nghost"] > 0
         assert flags == list(single.reorth)
+        assert brk == (single.info.get("n_orth_breaks"), single.info.get("n_ritz_locked"))
         assert np.max(np.abs(T - single.T)) <= 1e-9 * normA
         big = single.ritz_rnorm[:, 0] > 1e-10
         assert np.all(np.abs(np.log(rn[big, 0] / single.ritz_rnorm[big, 0])) < np.log(1.5))
