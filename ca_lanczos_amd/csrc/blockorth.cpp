@@ -13,6 +13,7 @@
 //    on norms taken from the same Gram (before: diag X'X; after: diag of
 //    X'X - C'C = ||Y_i||^2), so the pass count follows the reference.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <vector>
 
@@ -391,6 +392,23 @@ static bool orth_device_ok(cal_ctx* c, const Panel& Qp, const Panel& X) {
            rowapply_ok(w + m, m, true, w);
 }
 
+// Spin on the published sequence word.  No HIP call in the fast path: a
+// stream query would enqueue a marker behind the prefetched matrix powers and
+// stall the next dispatch.  After 2 s without the word, synchronise the stream
+// (a faulted kernel reports here) and look once more.
+static int wait_published(cal_ctx* c, const unsigned long long* h_seq, unsigned long long seq) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spin = 1;; ++spin) {
+        if (__atomic_load_n(h_seq, __ATOMIC_ACQUIRE) == seq) return 0;
+        if ((spin & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+            CAL_HIP(c, hipStreamSynchronize(c->stream));
+            if (__atomic_load_n(h_seq, __ATOMIC_ACQUIRE) == seq) return 0;
+            return set_error(c, CAL_ERR_HIP, "block orthogonalisation: result never published");
+        }
+        __builtin_ia32_pause();
+    }
+}
+
 static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, bool doreorth, const PanelOut& Qout,
                        double* Rq, double* R, bool* reorth) {
     const int w = Qp.total, m = X.total, nq = w < 8 ? w : 8, wp = w + m;
@@ -414,9 +432,21 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
         CAL_HIP(c, launch_rowgram(ct, nt, w == 9, n, (int)blocks, c->d_partial, c->stream));
         timer_end(c, t);
     }
-    CAL_HIP(c, launch_reduce(c->d_partial, (int)blocks, 272, d_tile, c->stream));
-    CAL_TRY(allreduce_sum(c, d_tile, 272));
-    CAL_HIP(c, launch_orth_coef(0, d_tile, d_st, d_mbuf, d_out, w, m, WP, MO, doreorth ? 1 : 0, c->stream));
+    CAL_TRY(ensure_pub(c));
+    const unsigned long long seq = ++c->pub_seq;
+    double* h_out = c->h_pub;
+    unsigned long long* h_seq = reinterpret_cast<unsigned long long*>(c->h_pub + 516);
+    unsigned long long* d_seq = reinterpret_cast<unsigned long long*>(c->d_pub + 516);
+    // reduce the Gram partials, all-reduce the tile over the ranks, then the
+    // s x s algebra; phase 1 publishes R / RY / flags to h_out
+    auto coef = [&](int phase, int dore) -> int {
+        CAL_HIP(c, launch_reduce(c->d_partial, (int)blocks, 272, d_tile, c->stream));
+        CAL_TRY(allreduce_sum(c, d_tile, 272));
+        CAL_HIP(c, launch_orth_coef(phase, d_tile, d_st, d_mbuf, d_out, w, m, WP, MO, dore,
+                                    phase == 1 ? c->d_pub : nullptr, d_seq, seq, c->stream));
+        return 0;
+    };
+    CAL_TRY(coef(0, doreorth ? 1 : 0));
     ColList cw{};
     OutList ol{};
     for (int cc = 0; cc < 17; ++cc) cw.p[cc] = panel_slice(W, cc < wp ? cc : wp - 1, 1).ptr[0];
@@ -427,25 +457,22 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
         CAL_HIP(c, launch_rowapply(cw, d_mbuf, wp, m, ol, 2, w, n, (int)blocks, c->d_partial, c->stream));
         timer_end(c, t);
     }
-    CAL_HIP(c, launch_reduce(c->d_partial, (int)blocks, 272, d_tile, c->stream));
-    CAL_TRY(allreduce_sum(c, d_tile, 272));
-    CAL_HIP(c, launch_orth_coef(1, d_tile, d_st, d_mbuf, d_out, w, m, WP, MO, 0, c->stream));
+    CAL_TRY(coef(1, 0));
     // pass B: Q = [Qp | W M1] M2, one store
     {
         const int t = timer_begin(c, 2);
         CAL_HIP(c, launch_rowapply(cw, d_mbuf, wp, m, ol, 3, w, n, (int)((n + 255) / 256), c->d_partial, c->stream));
         timer_end(c, t);
     }
-    double* h_out = c->h_red + 3072;
-    CAL_HIP(c, hipMemcpyAsync(h_out, d_out, 516 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    if (!c->orth_event) CAL_HIP(c, hipEventCreateWithFlags(&c->orth_event, hipEventDisableTiming));
-    CAL_HIP(c, hipEventRecord(c->orth_event, c->stream));
     if (c->pre_wait) {  // e.g. the next step's matrix powers (lanczos_step)
         auto hook = std::move(c->pre_wait);
         c->pre_wait = nullptr;
         CAL_TRY(hook());
     }
-    CAL_HIP(c, hipEventSynchronize(c->orth_event));
+    // R, RY and the flags arrive in h_out when the phase-1 algebra ends (before
+    // pass B): poll the sequence word; if the stream drains without it, the
+    // kernels failed -- report the stream's error
+    CAL_TRY(wait_published(c, h_seq, seq));
     if (h_out[512] != 0.0 || h_out[513] != 0.0) return 1;
     std::copy(h_out, h_out + (size_t)m * m, R);
     std::copy(h_out + 256, h_out + 256 + (size_t)w * m, Rq);

@@ -204,8 +204,12 @@ hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, co
                            int64_t n, int blocks, double* partial, hipStream_t st);
 // s x s coefficients of the two-sweep block orthogonalisation (phase 0 after
 // the P1 Gram, phase 1 after pass A); see kernels.hip k_orth_coef.
+// Phase 1 with hout != nullptr also publishes out (R, RY, flags; 516
+// doubles) to the host-mapped hout and then stores seq to *hseq (system-scope
+// release): the host polls that word instead of copying and waiting.
 hipError_t launch_orth_coef(int phase, const double* tile, double* st, double* mbuf, double* out, int w, int m,
-                            int WP, int MO, int doreorth, hipStream_t stream);
+                            int WP, int MO, int doreorth, double* hout, unsigned long long* hseq,
+                            unsigned long long seq, hipStream_t stream);
 // Grid of the row-parallel Gram sweeps (k_rowapply with GRAM): 4 blocks of
 // 38 KB LDS per CU on 256 CUs.
 constexpr int kRowGramBlocks = 1024;
@@ -270,6 +274,12 @@ struct cal_ctx {
     std::function<int()> pre_wait;
     bool orth_redone = false;  // the last block was redone on the host path
     hipEvent_t orth_event = nullptr;
+    // device-coefficient block orthogonalisation: the pinned host-mapped
+    // result page the phase-1 kernel publishes R / RY / flags into (h_pub,
+    // device alias d_pub; the sequence word follows the 516 doubles)
+    double* h_pub = nullptr;
+    double* d_pub = nullptr;
+    unsigned long long pub_seq = 0;
 };
 
 // ---- helpers shared by the host-side translation units -----------------
@@ -292,6 +302,11 @@ int hip_fail(cal_ctx* c, hipError_t e, const char* what);
 // rowptr/col/val: n_rows stored rows, the local ones starting at stored row
 // ext_off; col: ids relative to the local origin (negative = left halo);
 // lpad/rext: halo extent on each side of the local rows in a vector column.
+// Pinned host-mapped result page of the device block orthogonalisation:
+// 516 doubles (R, RY, flags) then the 8-byte sequence word.
+constexpr int kPubDoubles = 520;
+int ensure_pub(cal_ctx* c);
+
 int upload_matrix(cal_ctx* c, int64_t n_rows, int64_t ext_off, int64_t n_local, int64_t n_global, int64_t row0,
                   int64_t nghost, int64_t lpad, int64_t rext, const std::vector<int>& rowptr,
                   const std::vector<int>& col, const double* val);

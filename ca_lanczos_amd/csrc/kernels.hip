@@ -912,7 +912,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     // Gram kinds: each wave transposes only its own 64 rows through the tile,
     // so wave-level syncs suffice, and the next iteration's rows are loaded
     // before this iteration's MFMA phase.
-    const int64_t stride = GRAM ? (int64_t)gridDim.x * 256 : n;
+    const int64_t nch = (n + 255) / 256;
+    const int64_t cstride = GRAM ? (int64_t)gridDim.x : nch;
+    auto chunk_base = [&](int64_t ci) { return ci * 256; };
     double pn[WPMAX];
     auto load_rows = [&](int64_t b, double* dst) {
         const int64_t r = b + tid;
@@ -920,15 +922,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
         for (int c = 0; c < WPMAX; ++c) dst[c] = pc[c][rr];
     };
-    load_rows((int64_t)blockIdx.x * 256, pn);
-    for (int64_t base = (int64_t)blockIdx.x * 256; base < n; base += stride) {
+    load_rows(chunk_base(blockIdx.x), pn);
+    for (int64_t ci = blockIdx.x; ci < nch; ci += cstride) {
         asm volatile("" ::: "memory");
+        const int64_t base = chunk_base(ci);
         const int64_t r = base + tid;
         const bool in = r < n;
         double p[WPMAX];
 #pragma unroll
         for (int c = 0; c < WPMAX; ++c) p[c] = in ? pn[c] : 0.0;
-        if (GRAM && base + stride < n) load_rows(base + stride, pn);
+        if (GRAM && ci + cstride < nch) load_rows(chunk_base(ci + cstride), pn);
         double y[MOUT];
 #pragma unroll
         for (int j = 0; j < MOUT; ++j) y[j] = 0.0;
@@ -1244,8 +1247,26 @@ hipError_t launch_spmv_resid(const SpmvArgs& a, const double* xi, double lr, dou
 // for term; products and sums in the same sequence), so both paths give the
 // same bits.
 // --------------------------------------------------------------------------
+// tools/coef_probe.hip builds with CAL_OC_PROF: clock64() marks per step
+#ifdef CAL_OC_PROF
+__device__ long long g_oc_marks[16];
+#define OC_MARK(i)                                           \
+    do {                                                     \
+        __syncthreads();                                     \
+        if (threadIdx.x == 0) g_oc_marks[i] = clock64();     \
+    } while (0)
+#else
+#define OC_MARK(i) \
+    do {           \
+    } while (0)
+#endif
 namespace {
 constexpr int kOcM = 16, kOcW = 9;
+#ifndef CAL_OC_THREADS
+#define CAL_OC_THREADS 256
+#endif
+constexpr int kOcThreads = CAL_OC_THREADS;  // >= kOcM * kOcM (oc_chol_inv8 clears R by thread)
+constexpr int kOcOut = 516;   // R (<= 16 x 16) at 0, RY at 256, flags at 512
 
 // Upper Cholesky of the m x m matrix in G (ld kOcM, destroyed) into R;
 // returns false (block-uniform) on a non-positive or non-finite pivot.
@@ -1278,23 +1299,95 @@ __device__ bool oc_chol(int m, double* G, double* R, int* flag) {
     return true;
 }
 
-// Ri = R^-1 (upper), column j by thread j with the host's back substitution.
+// Ri = R^-1 (upper), column j by lane j with the host's back substitution
+// (s = [i == j] - sum_{k=i+1..j} R(i,k) Ri(k,j), ascending k; Ri(i,j) = s /
+// R(i,i)).  The lane's own column stays in registers; i descends in lockstep
+// over all lanes, so the R(i,k) reads are LDS broadcasts.
 __device__ void oc_trinv(int m, const double* R, double* Ri) {
     const int tid = threadIdx.x;
-    for (int e = tid; e < kOcM * kOcM; e += blockDim.x) Ri[e] = 0.0;
-    __syncthreads();
-    if (tid < m) {
+    if (tid < kOcM) {
         const int j = tid;
-        for (int i = j; i >= 0; --i) {
+        double col[kOcM];
+#pragma unroll
+        for (int i = kOcM - 1; i >= 0; --i) {
             double s = (i == j) ? 1.0 : 0.0;
-            for (int k = i + 1; k <= j; ++k) {
-                const double t = R[i + k * kOcM] * Ri[k + j * kOcM];
-                s = s - t;
+#pragma unroll
+            for (int k = i + 1; k < kOcM; ++k) {
+                const double t = R[i + k * kOcM] * col[k];
+                const double u = s - t;
+                s = k <= j ? u : s;
             }
-            Ri[i + j * kOcM] = s / R[i + i * kOcM];
+            const double v = s / R[i + i * kOcM];
+            col[i] = (i <= j && j < m && i < m) ? v : 0.0;
         }
+#pragma unroll
+        for (int i = 0; i < kOcM; ++i) Ri[i + j * kOcM] = col[i];
     }
     __syncthreads();
+}
+
+// m <= 8: Cholesky and inverse in wave 0 with the matrix in registers, lane
+// l = r + 8c holding entry (r, c); same operations, in the same order, as
+// oc_chol / oc_trinv (and dense::chol_upper / tri_inv_upper on the host):
+//   R(j,j) = sqrt(G(j,j)), R(j,c) = G(j,c) / R(j,j),
+//   G(r,c) -= R(j,r) * R(j,c) for j < r <= c (ascending j),
+//   Ri(i,j) = ([i == j] - sum_{k=i+1..j} R(i,k) Ri(k,j)) / R(i,i).
+// R and Ri are written to LDS (ld kOcM); returns false (block-uniform) on a
+// non-positive or non-finite pivot.  Called by all threads of the block.
+__device__ bool oc_chol_inv8(int m, const double* G, double* R, double* Ri, int* flag) {
+    const int tid = threadIdx.x;
+    if (tid < 64) {
+        const int r = tid & 7, c = tid >> 3;
+        double g = (r < m && c < m) ? G[r + c * kOcM] : 0.0;
+        double rv = 0.0;  // R(r, c) once row r is final
+        int bad = 0;
+        for (int j = 0; j < m; ++j) {
+            const double sj = __shfl(g, j + 8 * j, 64);
+            if (!(sj > 0.0) || !isfinite(sj)) {
+                bad = 1;
+                break;
+            }
+            const double rjj = sqrt(sj);
+            if (r == j) rv = c == j ? rjj : (c > j && c < m ? g / rjj : 0.0);
+            const double rjr = __shfl(rv, j + 8 * r, 64);  // R(j, r)
+            const double rjc = __shfl(rv, j + 8 * c, 64);  // R(j, c)
+            if (r > j && c >= r) {
+                const double t = rjr * rjc;
+                g = g - t;
+            }
+        }
+        R[r + c * kOcM] = (r <= c && r < m && c < m) ? rv : 0.0;
+        if (tid == 0) *flag = bad;
+    }
+    __syncthreads();
+    if (*flag) return false;
+    if (tid < 8) {
+        const int j = tid;
+        double col[8];
+#pragma unroll
+        for (int i = 7; i >= 0; --i) {
+            double s = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+            for (int k = i + 1; k < 8; ++k) {
+                const double t = R[i + k * kOcM] * col[k];
+                const double u = s - t;
+                s = k <= j ? u : s;
+            }
+            const double v = s / R[i + i * kOcM];
+            col[i] = (i <= j && j < m && i < m) ? v : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) Ri[i + j * kOcM] = col[i];
+#pragma unroll
+        for (int i = 8; i < kOcM; ++i) Ri[i + j * kOcM] = 0.0;
+    } else if (tid < kOcM) {
+#pragma unroll
+        for (int i = 0; i < kOcM; ++i) Ri[i + tid * kOcM] = 0.0;
+    }
+    if (tid < kOcM * kOcM && (tid & 15) >= 8) R[tid] = 0.0;  // rows 8.. of R (columns < 16)
+    if (tid < kOcM * kOcM && (tid >> 4) >= 8) R[tid] = 0.0;
+    __syncthreads();
+    return true;
 }
 }  // namespace
 
@@ -1308,13 +1401,14 @@ __device__ void oc_trinv(int m, const double* R, double* Ri) {
 // (w x m) at 256, flags at 512: [0] phase-0 failure, [1] phase-1 failure,
 // [2] reorth.
 template <int PHASE>
-__global__ __launch_bounds__(256) void k_orth_coef(const double* __restrict__ tile, double* __restrict__ st,
-                                                   double* __restrict__ mbuf, double* __restrict__ out, int w, int m,
-                                                   int WP, int MO, int doreorth) {
+__device__ void orth_coef_body(const double* __restrict__ tile, double* __restrict__ st, double* __restrict__ mbuf,
+                               double* __restrict__ out, int w, int m, int WP, int MO, int doreorth) {
     __shared__ double G[kOcM * kOcM], R[kOcM * kOcM], Ri[kOcM * kOcM], C[kOcW * kOcM], Ra[kOcM * kOcM];
+    __shared__ double C0[PHASE == 1 ? kOcW * kOcM : 1];  // phase 1: phase 0's C (from st)
     __shared__ double nb[kOcM];
     __shared__ int flag;
     const int tid = threadIdx.x, nq = w < 8 ? w : 8, wp = w + m;
+    OC_MARK(0);
     // unpack the tile: G = block Gram (m x m), C = Qp' block (w x m)
     for (int e = tid; e < m * m; e += blockDim.x) {
         const int i = e % m, j = e / m;
@@ -1324,12 +1418,15 @@ __global__ __launch_bounds__(256) void k_orth_coef(const double* __restrict__ ti
         const int i = e % w, j = e / w;
         C[e] = i < 8 ? tile[i + (nq + j) * 16] : tile[256 + nq + j];
     }
-    if (PHASE == 1)
+    if (PHASE == 1) {
         for (int e = tid; e < m * m; e += blockDim.x) Ra[e % m + (e / m) * kOcM] = st[256 + e];
+        for (int e = tid; e < w * m; e += blockDim.x) C0[e] = st[e];
+    }
     __syncthreads();
+    OC_MARK(1);
     if (PHASE == 0 && tid < m) nb[tid] = sqrt(G[tid + tid * kOcM]);  // norms before (projectAndNormalize.m:17-22)
     // G -= C'C   (host: s = sum_k C(k,i) C(k,j); G(i,j) -= s)
-    double upd[2] = {0.0, 0.0};
+    double upd[kOcM * kOcM / kOcThreads];
     for (int e = tid, q = 0; e < m * m; e += blockDim.x, ++q) {
         const int i = e % m, j = e / m;
         double s = 0.0;
@@ -1342,20 +1439,31 @@ __global__ __launch_bounds__(256) void k_orth_coef(const double* __restrict__ ti
     __syncthreads();
     for (int e = tid, q = 0; e < m * m; e += blockDim.x, ++q) G[e % m + (e / m) * kOcM] = upd[q];
     __syncthreads();
-    if (PHASE == 0 && tid == 0) {
-        // rel = |before - after| / before, reorth = max(rel) > 0.5 (NaN-ignoring max)
-        double mx = NAN;
-        for (int i = 0; i < m; ++i) {
-            const double after = sqrt(fmax(G[i + i * kOcM], 0.0));
-            const double rel = fabs(nb[i] - after) / nb[i];
-            if (!isnan(rel) && (isnan(mx) || rel > mx)) mx = rel;
+    OC_MARK(2);
+    if (PHASE == 0) {
+        // rel = |before - after| / before per column (lane i), then the
+        // NaN-ignoring max in column order, reorth = max(rel) > 0.5
+        if (tid < m) {
+            const double after = sqrt(fmax(G[tid + tid * kOcM], 0.0));
+            nb[tid] = fabs(nb[tid] - after) / nb[tid];
         }
-        out[512 + 2] = (doreorth && mx > 0.5) ? 1.0 : 0.0;
+        __syncthreads();
+        if (tid == 0) {
+            double mx = NAN;
+            for (int i = 0; i < m; ++i) {
+                const double rel = nb[i];
+                if (!isnan(rel) && (isnan(mx) || rel > mx)) mx = rel;
+            }
+            out[512 + 2] = (doreorth && mx > 0.5) ? 1.0 : 0.0;
+        }
     }
-    const bool ok = oc_chol(m, G, R, &flag);
+    const bool fast = m <= 8;
+    const bool ok = fast ? oc_chol_inv8(m, G, R, Ri, &flag) : oc_chol(m, G, R, &flag);
+    OC_MARK(3);
     if (tid == 0) out[512 + PHASE] = ok ? 0.0 : 1.0;
     if (!ok) return;  // block-uniform: the host redoes the block on its own path
-    oc_trinv(m, R, Ri);
+    if (!fast) oc_trinv(m, R, Ri);
+    OC_MARK(4);
     if (PHASE == 0) {
         // M1 = Mz Ri, Mz = [-C; I] (wp x m); host: dense::matmul, p = 0..m-1
         for (int e = tid; e < WP * MO; e += blockDim.x) {
@@ -1375,56 +1483,87 @@ __global__ __launch_bounds__(256) void k_orth_coef(const double* __restrict__ ti
     } else {
         double* M2p = mbuf + WP * MO;
         double* M2y = M2p + WP * MO;
-        // M2 = [-C3 Rb^-1 ; Rb^-1]   (C3 is this phase's C)
-        for (int e = tid; e < WP * MO; e += blockDim.x) {
-            const int cc = e / MO, j = e % MO;
-            double v = 0.0;
-            if (cc < w && j < m) {
+        // four independent products over one flattened index (all waves busy):
+        //   M2p = -C3 Rb^-1 (WP x MO), M2y = Rb^-1 (MO x MO),
+        //   RY = C + C3 Ra (w x m), R = Rb Ra (m x m, upper)
+        const int n1 = WP * MO, n2 = n1 + MO * MO, n3 = n2 + w * m, n4 = n3 + m * m;
+        for (int f = tid; f < n4; f += blockDim.x) {
+            if (f < n1) {
+                const int e = f, cc = e / MO, j = e % MO;
+                double v = 0.0;
+                if (cc < w && j < m) {
+                    double s = 0.0;
+                    for (int k = 0; k <= j; ++k) {
+                        const double t = C[cc + k * w] * Ri[k + j * kOcM];
+                        s = s + t;
+                    }
+                    v = -s;
+                }
+                M2p[e] = v;
+            } else if (f < n2) {
+                const int e = f - n1, i = e / MO, j = e % MO;
+                M2y[e] = (i < m && j < m) ? Ri[i + j * kOcM] : 0.0;
+            } else if (f < n3) {
+                const int e = f - n2, i = e % w, j = e / w;
                 double s = 0.0;
                 for (int k = 0; k <= j; ++k) {
-                    const double t = C[cc + k * w] * Ri[k + j * kOcM];
+                    const double t = C[i + k * w] * Ra[k + j * kOcM];
                     s = s + t;
                 }
-                v = -s;
+                const double ctot = 0.0 + s;
+                out[256 + e] = C0[e] + ctot;
+            } else {
+                const int e = f - n3, i = e % m, j = e / m;
+                double s = 0.0;
+                for (int p = 0; p < m; ++p) {
+                    const double t = R[i + p * kOcM] * Ra[p + j * kOcM];
+                    s = s + t;
+                }
+                out[e] = i > j ? 0.0 : s;
             }
-            M2p[e] = v;
         }
-        for (int e = tid; e < MO * MO; e += blockDim.x) {
-            const int i = e / MO, j = e % MO;
-            M2y[e] = (i < m && j < m) ? Ri[i + j * kOcM] : 0.0;
-        }
-        // RY = C + C3 Ra (C from phase 0 in st), R = Rb Ra (upper)
-        for (int e = tid; e < w * m; e += blockDim.x) {
-            const int i = e % w, j = e / w;
-            double s = 0.0;
-            for (int k = 0; k <= j; ++k) {
-                const double t = C[i + k * w] * Ra[k + j * kOcM];
-                s = s + t;
-            }
-            const double ctot = 0.0 + s;
-            out[256 + e] = st[e] + ctot;
-        }
-        for (int e = tid; e < m * m; e += blockDim.x) {
-            const int i = e % m, j = e / m;
-            double s = 0.0;
-            for (int p = 0; p < m; ++p) {
-                const double t = R[i + p * kOcM] * Ra[p + j * kOcM];
-                s = s + t;
-            }
-            out[e] = i > j ? 0.0 : s;
-        }
+    }
+    OC_MARK(5);
+}
+
+// Phase 1 publishes the block's results to pinned host memory: the 516
+// doubles of out (R, RY, flags) are copied to hout, then the sequence number
+// is stored with system-scope release semantics -- the host polls it
+// (blockorth.cpp orth_device) instead of a device-to-host copy + event.
+__device__ void orth_publish(const double* __restrict__ out, double* __restrict__ hout,
+                             unsigned long long* __restrict__ hseq, unsigned long long seq) {
+    __syncthreads();  // out was written by the whole block
+    for (int e = threadIdx.x; e < kOcOut; e += blockDim.x) hout[e] = out[e];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(hseq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
+template <int PHASE>
+__global__ __launch_bounds__(kOcThreads) void k_orth_coef(const double* __restrict__ tile, double* __restrict__ st,
+                                                   double* __restrict__ mbuf, double* __restrict__ out, int w, int m,
+                                                   int WP, int MO, int doreorth, double* __restrict__ hout,
+                                                   unsigned long long* __restrict__ hseq, unsigned long long seq) {
+    orth_coef_body<PHASE>(tile, st, mbuf, out, w, m, WP, MO, doreorth);
+    if (PHASE == 1 && hout) orth_publish(out, hout, hseq, seq);
+}
+
 hipError_t launch_orth_coef(int phase, const double* tile, double* st, double* mbuf, double* out, int w, int m,
-                            int WP, int MO, int doreorth, hipStream_t stream) {
+                            int WP, int MO, int doreorth, double* hout, unsigned long long* hseq,
+                            unsigned long long seq, hipStream_t stream) {
     if (m < 1 || m > kOcM || w < 0 || w > kOcW) return hipErrorInvalidValue;
     if (phase == 0)
-        hipLaunchKernelGGL(k_orth_coef<0>, dim3(1), dim3(256), 0, stream, tile, st, mbuf, out, w, m, WP, MO, doreorth);
+        hipLaunchKernelGGL(k_orth_coef<0>, dim3(1), dim3(kOcThreads), 0, stream, tile, st, mbuf, out, w, m, WP, MO, doreorth,
+                           hout, hseq, seq);
     else
-        hipLaunchKernelGGL(k_orth_coef<1>, dim3(1), dim3(256), 0, stream, tile, st, mbuf, out, w, m, WP, MO, doreorth);
+        hipLaunchKernelGGL(k_orth_coef<1>, dim3(1), dim3(kOcThreads), 0, stream, tile, st, mbuf, out, w, m, WP, MO, doreorth,
+                           hout, hseq, seq);
     return hipGetLastError();
 }
+
 
 // y(r) = sum_j |A(r,j)| over the local CSR rows: the start vector of
 // normest (sum(abs(S))' = row sums for a symmetric A).

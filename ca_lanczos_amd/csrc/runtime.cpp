@@ -62,6 +62,17 @@ int ensure_red(cal_ctx* c, size_t doubles) {
     return 0;
 }
 
+int ensure_pub(cal_ctx* c) {
+    if (c->h_pub) return 0;
+    // coherent (uncached), mapped: GPU stores reach host memory directly
+    CAL_HIP(c, hipHostMalloc((void**)&c->h_pub, kPubDoubles * sizeof(double),
+                             hipHostMallocMapped | hipHostMallocCoherent));
+    std::fill(c->h_pub, c->h_pub + kPubDoubles, 0.0);
+    CAL_HIP(c, hipHostGetDevicePointer((void**)&c->d_pub, c->h_pub, 0));
+    c->pub_seq = 0;
+    return 0;
+}
+
 int ensure_work(cal_ctx* c, int cols, int64_t ld) {
     if (cols <= c->work_cols && ld == c->work_ld) return 0;
     if (c->d_work) CAL_HIP(c, hipFree(c->d_work));
@@ -555,6 +566,7 @@ void cal_destroy(cal_ctx* c) {
     }
     for (auto e : c->event_pool) hipEventDestroy(e);
     if (c->orth_event) hipEventDestroy(c->orth_event);
+    if (c->h_pub) hipHostFree(c->h_pub);
     hipStreamDestroy(c->stream);
     delete c;
 }

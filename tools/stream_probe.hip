@@ -57,6 +57,33 @@ __global__ __launch_bounds__(256) void k_apply2(Cols P, OCols Y, int64_t n) {
     }
 }
 
+
+// k_apply1 with the row blocks taken in descending order when REV (block b
+// -> row block nb-1-b): alternating the direction between consecutive sweeps
+// lets each sweep start on the lines the previous one touched last (MALL).
+template <bool STORE>
+__global__ __launch_bounds__(256) void k_apply1r(Cols P, OCols Y, int64_t n, int rev) {
+    const int64_t b = rev ? (int64_t)gridDim.x - 1 - blockIdx.x : blockIdx.x;
+    const int64_t r = b * 256 + threadIdx.x;
+    if (r >= n) return;
+    double y[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < 17; ++c) {
+        const double v = P.p[c][r];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = __builtin_fma(v, cM[c * 8 + j], y[j]);
+    }
+    if (STORE) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Y.p[j][r] = y[j];
+    } else {
+        double s = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += y[j];
+        if (s == 123.456) Y.p[0][r] = s;
+    }
+}
+
 typedef double d4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -108,6 +135,62 @@ __global__ __launch_bounds__(256) void k_gram17(Cols P, int64_t n, double* out) 
     if (v == 1.2345) out[0] = v;
 }
 
+// 2 rows per lane, 16-B loads; each wave transposes its rows through the
+// LDS tile in two halves (row 2t, then 2t+1) -- same LDS as k_gram17.
+// PF: the next iteration's rows are loaded before this one's LDS/MFMA work.
+template <int STAGE, bool PF>
+__global__ __launch_bounds__(256) void k_gram17x2(Cols P, int64_t n, double* out) {
+    __shared__ double tile[256 * 17];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, c16 = lane & 15, g = lane >> 4;
+    d4 acc = {0, 0, 0, 0};
+    double eacc = 0, junk = 0;
+    const int64_t np = n / 2;  // n even here
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    double2 pn[17];
+    auto load = [&](int64_t b, double2* dst) {
+        const int64_t t = b + tid < np ? b + tid : np - 1;
+#pragma unroll
+        for (int c = 0; c < 17; ++c) dst[c] = *reinterpret_cast<const double2*>(P.p[c] + 2 * t);
+    };
+    if (PF) load((int64_t)blockIdx.x * 256, pn);
+    for (int64_t base = (int64_t)blockIdx.x * 256; base < np; base += stride) {
+        double2 p[17];
+        if (PF) {
+#pragma unroll
+            for (int c = 0; c < 17; ++c) p[c] = pn[c];
+            if (base + stride < np) load(base + stride, pn);
+        } else {
+            load(base, p);
+        }
+        if (STAGE == 0) {
+#pragma unroll
+            for (int c = 0; c < 17; ++c) junk += p[c].x + p[c].y;
+            continue;
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            double* trow = tile + tid * 17;
+#pragma unroll
+            for (int c = 0; c < 17; ++c) trow[c] = h ? p[c].y : p[c].x;
+            wsync();
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int row = wave * 64 + 4 * k + g;
+                const double a = tile[row * 17 + c16];
+                if (STAGE == 2) {
+                    acc = mfma64(a, a, acc);
+                    eacc += tile[row * 17 + 16] * a;
+                } else {
+                    junk += a + tile[row * 17 + 16];
+                }
+            }
+            wsync();
+        }
+    }
+    const double v = acc[0] + acc[1] + acc[2] + acc[3] + eacc + junk;
+    if (v == 1.2345) out[0] = v;
+}
+
 int main() {
     const int64_t n = 215LL * 215 * 215, ld = (n + 63) / 64 * 64;
     double* buf;
@@ -139,6 +222,13 @@ int main() {
     const int g1 = (int)((n + 255) / 256), g2 = (int)((n / 2 + 255) / 256);
     time("apply 17->8 store, 8B/lane", 25.0 * 8 * n, [&] { hipLaunchKernelGGL(k_apply1<true>, dim3(g1), dim3(256), 0, 0, P, Y, n); });
     time("apply 17->8 store, 16B/lane", 25.0 * 8 * n, [&] { hipLaunchKernelGGL(k_apply2<true>, dim3(g2), dim3(256), 0, 0, P, Y, n); });
+    {
+        int dir = 0;
+        time("read 17 alternating direction", 17.0 * 8 * n, [&] { hipLaunchKernelGGL(k_apply1r<false>, dim3(g1), dim3(256), 0, 0, P, Y, n, dir); dir ^= 1; });
+        time("read 17 same direction (rev kernel)", 17.0 * 8 * n, [&] { hipLaunchKernelGGL(k_apply1r<false>, dim3(g1), dim3(256), 0, 0, P, Y, n, 0); });
+        time("apply 17->8 alternating direction", 25.0 * 8 * n, [&] { hipLaunchKernelGGL(k_apply1r<true>, dim3(g1), dim3(256), 0, 0, P, Y, n, dir); dir ^= 1; });
+        time("apply 17->8 same direction (rev kernel)", 25.0 * 8 * n, [&] { hipLaunchKernelGGL(k_apply1r<true>, dim3(g1), dim3(256), 0, 0, P, Y, n, 0); });
+    }
     time("read 17, 8B/lane", 17.0 * 8 * n, [&] { hipLaunchKernelGGL(k_apply1<false>, dim3(g1), dim3(256), 0, 0, P, Y, n); });
     time("read 17, 16B/lane", 17.0 * 8 * n, [&] { hipLaunchKernelGGL(k_apply2<false>, dim3(g2), dim3(256), 0, 0, P, Y, n); });
     for (int G : {768, 1024, 2048}) {
@@ -149,6 +239,17 @@ int main() {
         time(nm, 17.0 * 8 * n, [&] { hipLaunchKernelGGL(k_gram17<1>, dim3(G), dim3(256), 0, 0, P, n, buf); });
         snprintf(nm, 64, "gram17 +mfma G=%d", G);
         time(nm, 17.0 * 8 * n, [&] { hipLaunchKernelGGL(k_gram17<2>, dim3(G), dim3(256), 0, 0, P, n, buf); });
+    }
+    for (int G : {1024, 2048}) {
+        char nm[64];
+        snprintf(nm, 64, "gram17x2 loads G=%d", G);
+        time(nm, 17.0 * 8 * n, [&] { hipLaunchKernelGGL((k_gram17x2<0, false>), dim3(G), dim3(256), 0, 0, P, n, buf); });
+        snprintf(nm, 64, "gram17x2 +lds G=%d", G);
+        time(nm, 17.0 * 8 * n, [&] { hipLaunchKernelGGL((k_gram17x2<1, false>), dim3(G), dim3(256), 0, 0, P, n, buf); });
+        snprintf(nm, 64, "gram17x2 +mfma G=%d", G);
+        time(nm, 17.0 * 8 * n, [&] { hipLaunchKernelGGL((k_gram17x2<2, false>), dim3(G), dim3(256), 0, 0, P, n, buf); });
+        snprintf(nm, 64, "gram17x2 +mfma +pf G=%d", G);
+        time(nm, 17.0 * 8 * n, [&] { hipLaunchKernelGGL((k_gram17x2<2, true>), dim3(G), dim3(256), 0, 0, P, n, buf); });
     }
     CK(hipDeviceSynchronize());
     return 0;
