@@ -120,7 +120,7 @@ __global__ void k_gen7_pair(const double* __restrict__ x, double* __restrict__ y
 // pair kernel with the table machinery of k_spmv_pair: per-pair uint16 id,
 // LDS (offset code, value pair) table, MODE-1 centre load; ID: load ids,
 // TAB: offsets/values from the LDS table (else from kernel args)
-template <bool ID, bool TAB, bool CENTER, bool GFILL = false>
+template <bool ID, bool TAB, bool CENTER, bool GFILL = false, bool NTST = false>
 __global__ __launch_bounds__(256) void k_pairtab(const double* __restrict__ x, double* __restrict__ y,
                                                  const uint16_t* __restrict__ ids, int64_t n, Offs off,
                                                  const int* __restrict__ gtab_off = nullptr,
@@ -166,10 +166,45 @@ __global__ __launch_bounds__(256) void k_pairtab(const double* __restrict__ x, d
         y0 -= 0.5 * c.x;
         y1 -= 0.5 * c.y;
     }
-    double2 o;
-    o.x = y0;
-    o.y = y1;
-    *reinterpret_cast<double2*>(y + r) = o;
+    if (NTST) {
+        __builtin_nontemporal_store(y0, y + r);
+        __builtin_nontemporal_store(y1, y + r + 1);
+    } else {
+        double2 o;
+        o.x = y0;
+        o.y = y1;
+        *reinterpret_cast<double2*>(y + r) = o;
+    }
+}
+
+// the streaming sweeps between the powers: 17 columns read (Gram-like) or
+// 17 read + 8 written (apply-like); NTQ: non-temporal stores for all but the
+// last output column
+struct Col17 { const double* p[17]; };
+struct Col8 { double* p[8]; };
+template <bool STORE, bool NTQ>
+__global__ __launch_bounds__(256) void k_sweep17(Col17 P, Col8 Y, int64_t n) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= n) return;
+    double v[17];
+#pragma unroll
+    for (int c = 0; c < 17; ++c) v[c] = P.p[c][r];
+    double acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        acc[j] = 0;
+#pragma unroll
+        for (int c = 0; c < 17; ++c) acc[j] += v[c] * (0.01 * (c + j));
+    }
+    if (STORE) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (NTQ && j < 7) __builtin_nontemporal_store(acc[j], Y.p[j] + r);
+            else Y.p[j][r] = acc[j];
+        }
+    } else if (acc[0] == 1.2345) {
+        Y.p[0][r] = acc[1];
+    }
 }
 
 int main() {
@@ -260,6 +295,77 @@ int main() {
         time("7pt xcd persistent 2048", 16.0 * n, [&] { hipLaunchKernelGGL((k_gen7x<false, true>), dim3(2048), dim3(256), 0, 0, x, y, id, n, off, nch); });
         time("7pt xcd persistent 2048 + ids", 18.0 * n, [&] { hipLaunchKernelGGL((k_gen7x<true, true>), dim3(2048), dim3(256), 0, 0, x, y, id, n, off, nch); });
         time("7pt xcd persistent 8192 + ids", 18.0 * n, [&] { hipLaunchKernelGGL((k_gen7x<true, true>), dim3(8192), dim3(256), 0, 0, x, y, id, n, off, nch); });
+    }
+    // in-loop emulation: 8 powers rotating through 9 vectors, then a Gram-like
+    // read sweep, an apply-like read sweep and an apply sweep writing the new
+    // block whose last column is the next q
+    {
+        const int64_t ldv = ((n + 2 * P + 64) + 63) / 64 * 64;
+        double* pool;
+        CK(hipMalloc(&pool, (size_t)(9 + 17) * ldv * 8));
+        CK(hipMemset(pool, 0, (size_t)(9 + 17) * ldv * 8));
+        auto V = [&](int j) { return pool + (size_t)j * ldv + P + 32; };
+        auto Qc = [&](int j) { return pool + (size_t)(9 + j) * ldv + P + 32; };
+        std::vector<int> ho(256, 0);
+        std::vector<double2> hv(256, make_double2(0.0, 0.0));
+        const int64_t o7[7] = {-P, -N, -1, 0, 1, N, P};
+        Offs off{};
+        for (int e = 0; e < 7; ++e) {
+            off.d[e] = o7[e];
+            ho[e] = (int)o7[e] * 4 + 3;
+            hv[e] = make_double2(e == 3 ? 6.0 : -1.0, e == 3 ? 6.0 : -1.0);
+        }
+        int* go;
+        double2* gv;
+        CK(hipMalloc(&go, 256 * 4));
+        CK(hipMalloc(&gv, 256 * 16));
+        CK(hipMemcpy(go, ho.data(), 256 * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(gv, hv.data(), 256 * 16, hipMemcpyHostToDevice));
+        std::vector<hipEvent_t> ev(12);
+        for (auto& evk : ev) CK(hipEventCreate(&evk));
+        const int masks[] = {0x00, 0xFF, 0x80, 0xC0, 0xE0, 0xF0, 0xF8, 0x81, 0xE1};
+        for (int variant = 0; variant < (int)(sizeof(masks) / sizeof(int)); ++variant) {
+            const int ntmask = masks[variant];
+            const bool ntq = false;
+            double acc[11] = {0};
+            const int steps = 6;
+            for (int stp = 0; stp < steps; ++stp) {
+                CK(hipEventRecord(ev[0]));
+                for (int j = 0; j < 8; ++j) {
+                    if ((ntmask >> j) & 1)
+                        hipLaunchKernelGGL((k_pairtab<true, true, true, true, true>), dim3(g2), dim3(256), 0, 0, V(j), V(j + 1), id, n, off, go, gv);
+                    else
+                        hipLaunchKernelGGL((k_pairtab<true, true, true, true, false>), dim3(g2), dim3(256), 0, 0, V(j), V(j + 1), id, n, off, go, gv);
+                    CK(hipEventRecord(ev[j + 1]));
+                }
+                Col17 Pc;
+                Col8 Yc;
+                for (int c = 0; c < 9; ++c) Pc.p[c] = Qc(c);
+                for (int c = 0; c < 8; ++c) Pc.p[9 + c] = V(c + 1);
+                for (int c = 0; c < 7; ++c) Yc.p[c] = Qc(9 + c);
+                Yc.p[7] = V(0);
+                hipLaunchKernelGGL((k_sweep17<false, false>), dim3(g1), dim3(256), 0, 0, Pc, Yc, n);
+                CK(hipEventRecord(ev[9]));
+                hipLaunchKernelGGL((k_sweep17<false, false>), dim3(g1), dim3(256), 0, 0, Pc, Yc, n);
+                CK(hipEventRecord(ev[10]));
+                if (ntq) hipLaunchKernelGGL((k_sweep17<true, true>), dim3(g1), dim3(256), 0, 0, Pc, Yc, n);
+                else hipLaunchKernelGGL((k_sweep17<true, false>), dim3(g1), dim3(256), 0, 0, Pc, Yc, n);
+                CK(hipEventRecord(ev[11]));
+                CK(hipEventSynchronize(ev[11]));
+                if (stp == 0) continue;
+                for (int k = 0; k < 11; ++k) {
+                    float ms;
+                    CK(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+                    acc[k] += ms * 1e3 / (steps - 1);
+                }
+            }
+            double tot = 0;
+            for (int k = 0; k < 11; ++k) tot += acc[k];
+            printf("{\"inloop\": \"spmv nt mask 0x%02x\", \"spmv_us\": [", ntmask);
+            for (int k = 0; k < 8; ++k) printf("%.1f%s", acc[k], k < 7 ? ", " : "");
+            printf("], \"gram_us\": %.1f, \"gram2_us\": %.1f, \"apply_us\": %.1f, \"total_us\": %.1f}\n", acc[8], acc[9],
+                   acc[10], tot);
+        }
     }
     CK(hipDeviceSynchronize());
     return 0;
