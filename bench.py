@@ -374,6 +374,9 @@ def main():
     achieved = dom[0] / (dom[1] * 1e-3) / 1e9
     traffic = traffic_for(args, wl, world, dominant)
     n_reorth = int(np.sum(flags[W:W + K]))
+    # whole-step algorithmic HBM bytes of this implementation:
+    # s SpMVs + P1 + pass A (Gram sweeps) + pass B (chained apply), per rank
+    b_step = s * b_spmv_launch + 2 * b_gram + b_apply
     b_outer = s * (12 * nnz_total + 20 * n + 4) + 8 * n * (5 * s + 2)
     line = {
         "metric": "CA-Lanczos outer-iters/sec (n~10M, s=8)",
@@ -402,6 +405,9 @@ def main():
         "reorth_passes": "%d/%d" % (n_reorth, K),
         "csr_outer_algorithmic_GB": b_outer / 1e9,
         "kernel_ms_per_step": per_step,
+        "step_hbm": {"algorithmic_GB_per_rank": b_step / 1e9,
+                     "achieved_GBps_per_rank": b_step / (elapsed / K) / 1e9,
+                     "frac": b_step / (elapsed / K) / 1e9 / HBM_PEAK_GBS},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": dom[2], "bytes_per_launch": dom[0], "avg_launch_us": dom[1] * 1e3},
