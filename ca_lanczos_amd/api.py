@@ -503,26 +503,29 @@ IMPL_MAX_RESTARTS = 40  # impl_restarted_ca_lanczos.m:7
 
 
 def impl_restarted_ca_lanczos(A, r, max_lanczos, n_wanted_eigs=10, s=6, basis="newton", orth="full", tol=1.0e-6,
-                              ctx=None):
+                              ctx=None, return_Q=True):
     """``[conv_eigs,Q_conv,num_restarts] = impl_restarted_ca_lanczos(A,r,
     max_lanczos,n_wanted_eigs,s,basis,orth,tol)`` -- the implicit restart
     impl_restarted_ca_lanczos.m:4-226 sets out to implement (the file itself
     does not run).  Only orth 'full' is defined.
 
     Returns a dict: conv_eigs (n_wanted_eigs, descending), Q_conv
-    (n x n_wanted_eigs), num_restarts, converged, ritz_est (num_restarts x
-    n_wanted_eigs), norm_A."""
+    (n x n_wanted_eigs; None with return_Q=False: the Ritz vectors are formed
+    on the device but not copied to the host), num_restarts, converged,
+    ritz_est (num_restarts x n_wanted_eigs), norm_A."""
     ctx = ctx or context_for(A)
     r = f64(r).ravel()
     n = len(r)
     E = np.zeros(n_wanted_eigs)
-    V = np.zeros((n, n_wanted_eigs), order="F")
+    V = np.zeros((n, n_wanted_eigs), order="F") if return_Q else None
     est = np.zeros((IMPL_MAX_RESTARTS, n_wanted_eigs), order="F")
     info = _lib.RestartInfo()
     st = lib.cal_impl_restarted_ca_lanczos(ctx.h, ptr(r), int(max_lanczos), int(n_wanted_eigs), int(s),
-                                           basis.encode(), orth.encode(), float(tol), ptr(E), ptr(V), ptr(est),
+                                           basis.encode(), orth.encode(), float(tol), ptr(E),
+                                           ptr(V) if return_Q else None, ptr(est),
                                            ctypes.byref(info))
     check(ctx.h, st, "impl_restarted_ca_lanczos")
     k, nr = info.nconv, info.num_restarts
-    return dict(conv_eigs=E[:k].copy(), Q_conv=V[:, :k].copy(), num_restarts=nr, ritz_est=est[:nr].copy(),
+    return dict(conv_eigs=E[:k].copy(), Q_conv=V[:, :k].copy() if return_Q else None, num_restarts=nr,
+                ritz_est=est[:nr].copy(),
                 converged=bool(info.converged), norm_A=info.norm_A, ms=info.ms)

@@ -110,6 +110,25 @@ int gram_host(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* out
     return 0;
 }
 
+// Y = P * M with M (wp x wy, column-major) already on the device; store only.
+static int apply_dev(cal_ctx* c, int64_t n, const Panel& P, const double* dM, int wy, const PanelOut& Y) {
+    const int wp = P.total;
+    const int wpp = (wp + 3) & ~3;
+    int max_nty = 8192 / (wpp * 16);
+    if (wp < 1 || wy < 1 || max_nty < 1) return set_error(c, CAL_ERR_ARG, "apply: panel shape out of range");
+    max_nty = max_nty >= 8 ? 8 : (max_nty >= 4 ? 4 : (max_nty >= 2 ? 2 : 1));
+    const int cw_max = 16 * max_nty;
+    for (int y0 = 0; y0 < wy; y0 += cw_max) {
+        const int cw = std::min(cw_max, wy - y0);
+        const ApplyPlan pl = apply_plan(wp, cw, n, false, 0);
+        const int t = timer_begin(c, 2);
+        CAL_HIP(c, launch_apply(P, dM + (size_t)y0 * wp, wp, cw, panel_out_slice(Y, y0, cw), true, 0, n, pl,
+                                c->d_partial, c->stream));
+        timer_end(c, t);
+    }
+    return 0;
+}
+
 int apply_host(cal_ctx* c, int64_t n, const Panel& P, const double* M, int wy, const PanelOut* Y, double* gram,
                int wq, double* gramp) {
     const int wp = P.total;
@@ -653,27 +672,111 @@ int project_blocks(cal_ctx* c, int64_t n, int64_t ld, int nb, const std::vector<
 // project.m block MGS across blocks, then normalize; the second projection
 // of :52-73 when a column lost more than half its norm).  X is read from dX
 // and not modified; dY is an n x m work block; QZ goes to Qout.
+// ---- project.m without host round trips (projectAndNormalize's blocks) ----
+// Each block's Gram Q{i}'X is reduced on the device into a region of d_red,
+// the coefficient matrix [-R{i}; I] is formed there (k_form_projM) and the
+// update X - Q{i} R{i} is enqueued right behind it; R{i} goes to pinned host
+// memory with an async copy.  The caller reads the copies after its next host
+// wait (normalize_dev polls the block's published R), which the stream orders
+// after them.  Same kernels and coefficients as project_blocks: same bits.
+namespace {
+constexpr size_t kAsyncBase = 8192, kAsyncRegion = 8192;  // doubles; Gram at +0, M at +4096
+}
+
+static bool async_ok(int nb, const int* widths, int m) {
+    if (m < 1 || m > 16 || nb + 1 > 6) return false;
+    for (int i = 0; i < nb; ++i)
+        if (widths[i] > 128) return false;
+    return true;
+}
+
+// Gram A'B (A <= 128 columns, B <= 16) reduced (and all-reduced) into d_dst
+// (ld *ldc) and copied to h_dst; nothing waits.
+static int gram_async(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* d_dst, double* h_dst, int* ldc) {
+    const GramPlan pl = gram_plan(A.total, B.total, n);
+    CAL_TRY(ensure_partial(c, (size_t)pl.blocks * pl.entries));
+    const int t = timer_begin(c, 1);
+    CAL_HIP(c, launch_gram(A, B, n, pl, c->d_partial, c->stream));
+    timer_end(c, t);
+    CAL_HIP(c, launch_reduce(c->d_partial, pl.blocks, pl.entries, d_dst, c->stream));
+    CAL_TRY(allreduce_sum(c, d_dst, pl.entries));
+    CAL_HIP(c, hipMemcpyAsync(h_dst, d_dst, pl.entries * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    *ldc = 16 * pl.nta;
+    return 0;
+}
+
+// One block-MGS pass of project.m over the nb blocks (doreorth = false);
+// region r of d_red / h_red holds block r's Gram; ldc[r] its leading dimension.
+static int project_blocks_async(cal_ctx* c, int64_t n, int64_t ld, int nb, const std::vector<double*>& dQ,
+                                const int* widths, int m, double* dX, int region0, std::vector<int>& ldc) {
+    Panel X = panel();
+    panel_add(X, dX, ld, m);
+    const PanelOut Xo = panel_out(dX, ld, m);
+    ldc.assign(nb, 0);
+    for (int i = 0; i < nb; ++i) {
+        const int w = widths[i];
+        if (w <= 0) continue;
+        const size_t off = kAsyncBase + (size_t)(region0 + i) * kAsyncRegion;
+        Panel Qi = panel();
+        panel_add(Qi, dQ[i], ld, w);
+        CAL_TRY(gram_async(c, n, Qi, X, c->d_red + off, c->h_red + off, &ldc[i]));  // R{i} = Q{i}'*X
+        double* dM = c->d_red + off + 4096;
+        CAL_HIP(c, launch_form_projM(c->d_red + off, ldc[i], w, m, dM, c->stream));
+        Panel W = panel();
+        panel_add(W, dQ[i], ld, w);
+        panel_add(W, dX, ld, m);
+        CAL_TRY(apply_dev(c, n, W, dM, m, Xo));  // X = X - Q{i}*R{i}
+    }
+    return 0;
+}
+
+static void read_async_R(cal_ctx* c, int nb, const int* widths, int m, int region0, const std::vector<int>& ldc,
+                         std::vector<std::vector<double>>& R) {
+    for (int i = 0; i < nb; ++i) {
+        const int w = widths[i];
+        R[i].assign((size_t)std::max(w, 0) * m, 0.0);
+        const double* h = c->h_red + kAsyncBase + (size_t)(region0 + i) * kAsyncRegion;
+        for (int j = 0; j < m && w > 0; ++j)
+            for (int r = 0; r < w; ++r) R[i][r + (size_t)j * w] = h[r + (size_t)j * ldc[i]];
+    }
+}
+
 int project_and_normalize_blocks_dev(cal_ctx* c, int64_t n, int64_t ld, int nblocks, const std::vector<double*>& dQ,
                                      const int* widths, int m, const double* dX, bool doreorth, double* dY,
                                      const PanelOut& Qout, std::vector<std::vector<double>>& RZ, double* R,
                                      bool* reorth, int* rank) {
+    const bool async = async_ok(nblocks, widths, m);
     std::vector<double> before(m);
-    {
+    std::vector<std::vector<double>> RY(nblocks);
+    for (int i = 0; i < nblocks; ++i) RY[i].assign((size_t)std::max(widths[i], 0) * m, 0.0);
+    Panel Yp = panel();
+    panel_add(Yp, dY, ld, m);
+    bool sh = false;
+    int rk = m;
+    if (async) {
+        // (the regions lie above everything the synchronous paths stage in h_red)
+        CAL_TRY(ensure_red(c, kAsyncBase + (size_t)(nblocks + 1) * kAsyncRegion));
+        Panel Xp = panel();
+        panel_add(Xp, dX, ld, m);
+        int ldx = 0;
+        const size_t offx = kAsyncBase + (size_t)nblocks * kAsyncRegion;
+        CAL_TRY(gram_async(c, n, Xp, Xp, c->d_red + offx, c->h_red + offx, &ldx));  // norms before (:17-22)
+        CAL_HIP(c, copy_cols(c, dY, dX, ld, n, m));
+        std::vector<int> ldc;
+        CAL_TRY(project_blocks_async(c, n, ld, nblocks, dQ, widths, m, dY, 0, ldc));  // :25
+        CAL_TRY(normalize_dev(c, n, Yp, Qout, R, 1.0e-8, &rk, &sh));                   // :26 (waits)
+        for (int i = 0; i < m; ++i) before[i] = std::sqrt(c->h_red[offx + i + (size_t)i * ldx]);
+        read_async_R(c, nblocks, widths, m, 0, ldc, RY);
+    } else {
         Panel Xp = panel();
         panel_add(Xp, dX, ld, m);
         std::vector<double> G((size_t)m * m);
         CAL_TRY(gram_host(c, n, Xp, Xp, G.data()));
         for (int i = 0; i < m; ++i) before[i] = std::sqrt(G[i + (size_t)i * m]);   // :17-22
+        CAL_HIP(c, copy_cols(c, dY, dX, ld, n, m));
+        CAL_TRY(project_blocks(c, n, ld, nblocks, dQ, widths, m, dY, false, RY));  // :25
+        CAL_TRY(normalize_dev(c, n, Yp, Qout, R, 1.0e-8, &rk, &sh));  // :26
     }
-    CAL_HIP(c, copy_cols(c, dY, dX, ld, n, m));
-    std::vector<std::vector<double>> RY(nblocks);
-    for (int i = 0; i < nblocks; ++i) RY[i].assign((size_t)std::max(widths[i], 0) * m, 0.0);
-    CAL_TRY(project_blocks(c, n, ld, nblocks, dQ, widths, m, dY, false, RY));  // :25
-    Panel Yp = panel();
-    panel_add(Yp, dY, ld, m);
-    bool sh = false;
-    int rk = m;
-    CAL_TRY(normalize_dev(c, n, Yp, Qout, R, 1.0e-8, &rk, &sh));  // :26
     double mx = NAN;
     for (int i = 0; i < m; ++i) {  // :45-48 (after = ||R(:,i)||)
         double after = 0.0;
@@ -688,8 +791,15 @@ int project_and_normalize_blocks_dev(cal_ctx* c, int64_t n, int64_t ld, int nblo
         re = true;
         std::vector<std::vector<double>> R2(nblocks);
         for (int i = 0; i < nblocks; ++i) R2[i].assign((size_t)std::max(widths[i], 0) * m, 0.0);
-        CAL_TRY(project_blocks(c, n, ld, nblocks, dQ, widths, m, dY, false, R2));
-        CAL_TRY(normalize_dev(c, n, Yp, Qout, R, 1.0e-8, &rk, &sh));
+        if (async) {
+            std::vector<int> ldc;
+            CAL_TRY(project_blocks_async(c, n, ld, nblocks, dQ, widths, m, dY, 0, ldc));
+            CAL_TRY(normalize_dev(c, n, Yp, Qout, R, 1.0e-8, &rk, &sh));
+            read_async_R(c, nblocks, widths, m, 0, ldc, R2);
+        } else {
+            CAL_TRY(project_blocks(c, n, ld, nblocks, dQ, widths, m, dY, false, R2));
+            CAL_TRY(normalize_dev(c, n, Yp, Qout, R, 1.0e-8, &rk, &sh));
+        }
         for (int i = 0; i < nblocks; ++i)
             for (size_t e = 0; e < R2[i].size(); ++e) RZ[i][e] = R2[i][e] + RY[i][e];
     }

@@ -220,6 +220,11 @@ hipError_t launch_dot(const double* x, const double* y, int64_t n, double* parti
 int dot_blocks(int64_t n);
 hipError_t launch_axpy_sub(double* y, const double* x, double a, int64_t n, hipStream_t st);  // y -= a*x
 hipError_t launch_div(double* y, const double* x, double b, int64_t n, hipStream_t st);      // y = x / b
+hipError_t launch_form_projM(const double* G, int ldg, int w, int m, double* M, hipStream_t st);
+// y -= a * x, a = *pa (take_sqrt: sqrt(*pa)) read on the device
+hipError_t launch_axpy_sub_dev(double* y, const double* x, const double* pa, bool take_sqrt, int64_t n,
+                               hipStream_t st);
+hipError_t launch_div_sqrt(double* y, const double* x, const double* nn, int64_t n, hipStream_t st);  // y = x / sqrt(*nn)
 hipError_t launch_abs_rowsum(const int* rowptr, const double* val, int64_t n, double* y, hipStream_t st);
 hipError_t launch_gather(double* dst, const double* src, const int* idx, int64_t cnt, hipStream_t st);
 // fused SpMV + Ritz residual partials for one Ritz pair (diagnostics)

@@ -1565,6 +1565,58 @@ hipError_t launch_orth_coef(int phase, const double* tile, double* st, double* m
 }
 
 
+// M = [-G(0:w, 0:m); I_m] ((w + m) x m, column-major) from a reduced Gram
+// block G (ld ldg): the coefficients of X - Q R (project.m:30) formed on the
+// device, the same values the host path stages (blockorth.cpp project_blocks).
+__global__ __launch_bounds__(256) void k_form_projM(const double* __restrict__ G, int ldg, int w, int m,
+                                                   double* __restrict__ M) {
+    const int e = blockIdx.x * 256 + threadIdx.x, rows = w + m;
+    if (e >= rows * m) return;
+    const int r = e % rows, j = e / rows;
+    M[e] = r < w ? -G[r + (int64_t)j * ldg] : (r - w == j ? 1.0 : 0.0);
+}
+
+hipError_t launch_form_projM(const double* G, int ldg, int w, int m, double* M, hipStream_t st) {
+    const int cnt = (w + m) * m;
+    if (cnt <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_form_projM, dim3((cnt + 255) / 256), dim3(256), 0, st, G, ldg, w, m, M);
+    return hipGetLastError();
+}
+
+// y -= a * x with a = *pa (or sqrt(*pa)) still on the device: the Lanczos
+// recurrence's alpha / beta updates without a host round trip (same ops as
+// k_axpy_sub with the host's value)
+__global__ __launch_bounds__(256) void k_axpy_sub_dev(double* __restrict__ y, const double* __restrict__ x,
+                                                     const double* __restrict__ pa, int take_sqrt, int64_t n) {
+    const double a = take_sqrt ? sqrt(*pa) : *pa;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const double t = a * x[i];
+        y[i] = y[i] - t;
+    }
+}
+
+hipError_t launch_axpy_sub_dev(double* y, const double* x, const double* pa, bool take_sqrt, int64_t n,
+                               hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_axpy_sub_dev, dim3(vec_blocks(n)), dim3(256), 0, st, y, x, pa, take_sqrt ? 1 : 0, n);
+    return hipGetLastError();
+}
+
+// ||x|| on the device: y = x / sqrt(*nn) (normest's x = x / norm(x) with the
+// norm still on the device; sqrt and the division as the host would do them)
+__global__ __launch_bounds__(256) void k_div_sqrt(double* __restrict__ y, const double* __restrict__ x,
+                                                 const double* __restrict__ nn, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) y[i] = x[i] / sqrt(*nn);
+}
+
+hipError_t launch_div_sqrt(double* y, const double* x, const double* nn, int64_t n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_div_sqrt, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, y, x, nn, n);
+    return hipGetLastError();
+}
+
 // y(r) = sum_j |A(r,j)| over the local CSR rows: the start vector of
 // normest (sum(abs(S))' = row sums for a symmetric A).
 __global__ __launch_bounds__(256) void k_abs_rowsum(const int* __restrict__ rowptr, const double* __restrict__ val,

@@ -98,10 +98,18 @@ static int enqueue_powers(cal_ctx* c, LanczosState& L, int k) {
 
 // ---- normest(A) (MATLAB built-in; ca_lanczos.m:258,370) ---------------------
 // Power iteration on A'A = A^2 (A symmetric) from x = sum(abs(A))', until the
-// estimate changes by <= tol * e (tol 1e-6, at most 100 iterations).
+// estimate changes by <= tol * e (tol 1e-6, at most 100 iterations).  The
+// iterations run in chunks of kNormestChunk with no host round trip: each
+// leaves ||x||^2 and ||Sx||^2 in d_red and rescales x by the device-side norm
+// (the host's sqrt and division, same bits); the host then replays MATLAB's
+// stopping test over the chunk and stops at the same iteration with the same
+// e -- extra iterations of the last chunk are discarded.
 static int normest_dev(cal_ctx* c, double* out) {
+    constexpr int kNormestChunk = 8;
+    constexpr size_t kNrm = 4096;  // d_red / h_red offset (orth_device uses [0, 4096))
     const int64_t n = c->A.n_local, ld = c->A.ld;
     CAL_TRY(ensure_work(c, 2, ld));
+    CAL_TRY(ensure_red(c, kNrm + 2 * kNormestChunk));
     double* x = work_col(c, 0) + c->A.lpad;
     double* y = work_col(c, 1) + c->A.lpad;
     CAL_HIP(c, launch_abs_rowsum(c->A.rowptr + c->A.ext_off, c->A.val, n, x, c->stream));
@@ -113,20 +121,40 @@ static int normest_dev(cal_ctx* c, double* out) {
         return 0;
     }
     CAL_HIP(c, launch_div(x, x, e, n, c->stream));
+    const int nb = dot_blocks(n);
+    CAL_TRY(ensure_partial(c, nb));
+    auto dot_dev = [&](const double* a, double* dst) -> int {
+        CAL_HIP(c, launch_dot(a, a, n, c->d_partial, nb, c->stream));
+        CAL_HIP(c, launch_reduce(c->d_partial, nb, 1, dst, c->stream));
+        return allreduce_sum(c, dst, 1);
+    };
+    double* d_nrm = c->d_red + kNrm;
+    const double* h_nrm = c->h_red + kNrm;
     double e0 = 0.0;
-    for (int cnt = 0; std::fabs(e - e0) > 1.0e-6 * e && cnt <= 100; ++cnt) {
-        e0 = e;
-        CAL_TRY(spmv_dev(c, x, y, 0, 0.0, 0.0, nullptr));  // Sx = S*x
-        CAL_TRY(spmv_dev(c, y, x, 0, 0.0, 0.0, nullptr));  // x = S'*Sx
-        double nx = 0.0, ny = 0.0;
-        CAL_TRY(dot_host(c, n, x, x, &nx));
-        CAL_TRY(dot_host(c, n, y, y, &ny));
-        nx = std::sqrt(nx);
-        e = nx / std::sqrt(ny);
-        CAL_HIP(c, launch_div(x, x, nx, n, c->stream));
+    int cnt = 0;
+    for (;;) {
+        for (int i = 0; i < kNormestChunk; ++i) {
+            CAL_TRY(spmv_dev(c, x, y, 0, 0.0, 0.0, nullptr));  // Sx = S*x
+            CAL_TRY(spmv_dev(c, y, x, 0, 0.0, 0.0, nullptr));  // x = S'*Sx
+            CAL_TRY(dot_dev(x, d_nrm + 2 * i));
+            CAL_TRY(dot_dev(y, d_nrm + 2 * i + 1));
+            CAL_HIP(c, launch_div_sqrt(x, x, d_nrm + 2 * i, n, c->stream));  // x = x / norm(x)
+        }
+        CAL_HIP(c, hipMemcpyAsync(c->h_red + kNrm, d_nrm, 2 * kNormestChunk * sizeof(double), hipMemcpyDeviceToHost,
+                                  c->stream));
+        CAL_HIP(c, hipStreamSynchronize(c->stream));
+        c->small_pending = false;
+        for (int i = 0; i < kNormestChunk; ++i) {
+            if (!(std::fabs(e - e0) > 1.0e-6 * e && cnt <= 100)) {
+                *out = e;
+                return 0;
+            }
+            e0 = e;
+            const double nx = std::sqrt(h_nrm[2 * i]);
+            e = nx / std::sqrt(h_nrm[2 * i + 1]);
+            ++cnt;
+        }
     }
-    *out = e;
-    return 0;
 }
 
 // ---- periodic: the omega recurrence (ca_lanczos.m:464-549) -----------------
@@ -192,34 +220,60 @@ static int newton_prologue(cal_ctx* c, LanczosState& L, bool cgs = true) {
     double nrm2 = 0.0;
     CAL_TRY(dot_host(c, n, L.col(0), L.col(0), &nrm2));
     CAL_HIP(c, launch_div(Qc(0), L.col(0), std::sqrt(nrm2), n, c->stream));
-    std::vector<double> alpha(m), beta(m);
+    // the 2s steps run without host round trips: alpha_j and beta_j^2 stay
+    // on the device (d_red [kAB, kAB + 2m)) and feed the updates directly; the
+    // CGS coefficients become [-R; 1] on the device (k_form_projM).  Same
+    // kernels and operations as the host-driven loop: same bits.
+    constexpr size_t kAB = 4096 + 64;  // above normest's chunk, below the async projection regions
+    CAL_TRY(ensure_red(c, kAB + 2 * m + 2048));
+    double* d_ab = c->d_red + kAB;      // alpha at [0, m), beta^2 at [m, 2m)
+    double* d_cg = d_ab + 2 * m;        // CGS Gram (ld 16 * nta), M at +1024
+    const int nbd = dot_blocks(n);
+    CAL_TRY(ensure_partial(c, nbd));
+    auto dot_dev = [&](const double* a, const double* b, double* dst) -> int {
+        CAL_HIP(c, launch_dot(a, b, n, c->d_partial, nbd, c->stream));
+        CAL_HIP(c, launch_reduce(c->d_partial, nbd, 1, dst, c->stream));
+        return allreduce_sum(c, dst, 1);
+    };
     for (int j = 0; j < m; ++j) {
         CAL_TRY(spmv_dev(c, Qc(j), r, 0, 0.0, 0.0, nullptr));  // :103
-        if (j > 0) CAL_HIP(c, launch_axpy_sub(r, Qc(j - 1), beta[j - 1], n, c->stream));  // :105
-        CAL_TRY(dot_host(c, n, r, Qc(j), &alpha[j]));                                       // :107
-        CAL_HIP(c, launch_axpy_sub(r, Qc(j), alpha[j], n, c->stream));                      // :108
-        double rr = 0.0;
-        CAL_TRY(dot_host(c, n, r, r, &rr));
-        beta[j] = std::sqrt(rr);  // :109
-        if (!(beta[j] > 0.0) || !std::isfinite(beta[j])) {
-            L.breakdown = true;
-            return set_error(c, CAL_ERR_NUMERIC, "Lanczos breakdown (beta = 0) in the Newton prologue");
-        }
-        CAL_HIP(c, launch_div(Qc(j + 1), r, beta[j], n, c->stream));  // :110
+        if (j > 0) CAL_HIP(c, launch_axpy_sub_dev(r, Qc(j - 1), d_ab + m + j - 1, true, n, c->stream));  // :105
+        CAL_TRY(dot_dev(r, Qc(j), d_ab + j));                                                          // :107
+        CAL_HIP(c, launch_axpy_sub_dev(r, Qc(j), d_ab + j, false, n, c->stream));                      // :108
+        CAL_TRY(dot_dev(r, r, d_ab + m + j));                                                          // :109
+        CAL_HIP(c, launch_div_sqrt(Qc(j + 1), r, d_ab + m + j, n, c->stream));                         // :110
         if (!cgs) continue;  // lanczos(...,'local') (restarted_ca_lanczos.m:65)
         // one CGS pass against Q(:,1:j) (lanczos.m:62-66)
         Panel Qj = panel();
         panel_add(Qj, Qc(0), ld, j + 1);
         Panel qn = panel();
         panel_add(qn, Qc(j + 1), ld, 1);
-        std::vector<double> Rkk(j + 1), M(j + 2);
-        CAL_TRY(gram_host(c, n, Qj, qn, Rkk.data()));
-        for (int i = 0; i <= j; ++i) M[i] = -Rkk[i];
-        M[j + 1] = 1.0;
+        const GramPlan pl = gram_plan(j + 1, 1, n);
+        CAL_TRY(ensure_partial(c, (size_t)pl.blocks * pl.entries));
+        CAL_HIP(c, launch_gram(Qj, qn, n, pl, c->d_partial, c->stream));
+        CAL_HIP(c, launch_reduce(c->d_partial, pl.blocks, pl.entries, d_cg, c->stream));
+        CAL_TRY(allreduce_sum(c, d_cg, pl.entries));
+        double* dM = d_cg + 1024;
+        CAL_HIP(c, launch_form_projM(d_cg, 16 * pl.nta, j + 1, 1, dM, c->stream));
         Panel W = panel();
         panel_add(W, Qc(0), ld, j + 2);  // [Q(:,1:j) | q_{j+1}] contiguous
-        PanelOut out = panel_out(Qc(j + 1), ld, 1);
-        CAL_TRY(apply_host(c, n, W, M.data(), 1, &out, nullptr, 0, nullptr));
+        const ApplyPlan ap = apply_plan(j + 2, 1, n, false, 0);
+        CAL_HIP(c, launch_apply(W, dM, j + 2, 1, panel_out(Qc(j + 1), ld, 1), true, 0, n, ap, c->d_partial,
+                                c->stream));
+    }
+    std::vector<double> alpha(m), beta(m);
+    {
+        CAL_HIP(c, hipMemcpyAsync(c->h_red + kAB, d_ab, 2 * m * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        CAL_HIP(c, hipStreamSynchronize(c->stream));
+        c->small_pending = false;
+        for (int j = 0; j < m; ++j) {
+            alpha[j] = c->h_red[kAB + j];
+            beta[j] = std::sqrt(c->h_red[kAB + m + j]);
+            if (!(beta[j] > 0.0) || !std::isfinite(beta[j])) {
+                L.breakdown = true;
+                return set_error(c, CAL_ERR_NUMERIC, "Lanczos breakdown (beta = 0) in the Newton prologue");
+            }
+        }
     }
     // eig(T) of the 2s x 2s symmetric tridiagonal (ca_lanczos.m:69): ascending
     std::vector<double> w(m);
@@ -1219,7 +1273,9 @@ int cal_impl_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, 
     std::stable_sort(sel.begin(), sel.end(), [&](int a, int b2) { return wk[a] > wk[b2]; });
     const int nw = (int)sel.size();
     for (int i = 0; i < nw; ++i) conv_eigs[i] = wk[sel[i]];
-    if (Q_conv) {
+    {
+        // the Ritz vectors Q_conv = V_k Y_k(:, sel) are formed on the device
+        // (work columns 0..nw-1); Q_conv == NULL keeps them there
         std::vector<double> Ms((size_t)k * nw);
         for (int j = 0; j < nw; ++j)
             for (int i = 0; i < k; ++i) Ms[i + (size_t)j * k] = Yk[i + (size_t)sel[j] * k];
@@ -1228,8 +1284,9 @@ int cal_impl_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, 
         panel_add(P, L->col(0), ld, k);
         PanelOut Y = panel_out(work_col(c, 0) + c->A.lpad, ld, nw);
         CAL_TRY(apply_host(c, n, P, Ms.data(), nw, &Y, nullptr, 0, nullptr));
-        CAL_HIP(c, hipMemcpy2DAsync(Q_conv, n * sizeof(double), work_col(c, 0) + c->A.lpad, ld * sizeof(double),
-                                    n * sizeof(double), nw, hipMemcpyDeviceToHost, c->stream));
+        if (Q_conv)
+            CAL_HIP(c, hipMemcpy2DAsync(Q_conv, n * sizeof(double), work_col(c, 0) + c->A.lpad, ld * sizeof(double),
+                                        n * sizeof(double), nw, hipMemcpyDeviceToHost, c->stream));
         CAL_HIP(c, hipStreamSynchronize(c->stream));
     }
     if (info) {
