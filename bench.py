@@ -335,6 +335,11 @@ def main():
     gram_avg_ms = gram_ms / max(gram_cnt, 1)
     csr_spmv = None
     host_rt_ms = None
+    pat_spmv = None
+    if world == 1 and rank == 0 and ctx.spmv_format()[0] == "pattern":
+        # the bench's own SpMV kernel back to back on one x / y pair (the
+        # Infinity Cache holds both): the kernel's rate outside the loop
+        pat_spmv = ctx.bench_spmv(20, 1.0)
     if world == 1 and rank == 0:
         # the same SpMV in plain CSR (12 B/nonzero), device-resident, for reference
         ctx2 = cal.Context(device=local, spmv_format="csr")
@@ -412,6 +417,10 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": dom[2], "bytes_per_launch": dom[0], "avg_launch_us": dom[1] * 1e3},
     }
+    if pat_spmv is not None:
+        line["spmv_kernel_back_to_back"] = {"avg_us": pat_spmv[0] * 1e3, "min_us": pat_spmv[1] * 1e3,
+                                            "gbps": b_spmv_launch / (pat_spmv[0] * 1e-3) / 1e9,
+                                            "bytes_per_launch": b_spmv_launch}
     if csr_spmv is not None:
         line["spmv_csr_kernel"] = {"avg_us": csr_spmv[0] * 1e3, "min_us": csr_spmv[1] * 1e3,
                                    "gbps": b_csr / (csr_spmv[0] * 1e-3) / 1e9, "bytes_per_launch": b_csr}
