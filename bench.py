@@ -285,8 +285,31 @@ def traffic_for(args, wl, world, cls):
     return None
 
 
+_JSON_FD = None
+
+
+def _quiet_stdout():
+    """Send everything written to fd 1 (gloo's connection banners, HIP/RCCL
+    messages, from every rank) to stderr; emit() writes the one JSON line to
+    the original stdout."""
+    global _JSON_FD
+    sys.stdout.flush()
+    _JSON_FD = os.dup(1)
+    os.dup2(2, 1)
+
+
+def emit(line):
+    data = (json.dumps(line) + "\n").encode()
+    if _JSON_FD is None:
+        sys.stdout.write(data.decode())
+        sys.stdout.flush()
+    else:
+        os.write(_JSON_FD, data)
+
+
 def main():
     args = parse()
+    _quiet_stdout()
     if args.driver == "irl":
         return main_irl(args)
     E = setup(args)
@@ -429,7 +452,7 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(wl, s, args.cpu_iters, args.basis)
         line["cpu_baseline_numpy"] = cpu_baseline_numpy(wl, s, 2, args.basis)
-    print(json.dumps(line), flush=True)
+    emit(line)
     if dist is not None:
         dist.barrier()
 
@@ -522,7 +545,7 @@ def main_irl(args):
     }
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_irl(wl, s, ml, nw)
-    print(json.dumps(line), flush=True)
+    emit(line)
     if dist is not None:
         dist.barrier()
 
