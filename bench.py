@@ -34,6 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
+MFMA_F64_PEAK_TF = 78.6  # MI355X FP64 matrix peak (AMD spec sheet; the guide lists no f64 row)
 
 
 def parse():
@@ -439,6 +440,13 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": dom[2], "bytes_per_launch": dom[0], "avg_launch_us": dom[1] * 1e3},
+        # the Gram sweeps' matrix-core work: one 16x16 f64 tile Gram per row
+        # (v_mfma_f64_16x16x4f64; rocprofv3 SQ_INSTS_VALU_MFMA_MOPS_F64 x 512
+        # = 512 n per launch, profiles/r01/pmc/bench_mfma_counters_v11.csv)
+        "gram_mfma": {"flops_per_launch": 512 * n_loc, "tflops": 512 * n_loc / (gram_avg_ms * 1e-3) / 1e12,
+                      "peak_tflops": MFMA_F64_PEAK_TF,
+                      "frac": 512 * n_loc / (gram_avg_ms * 1e-3) / 1e12 / MFMA_F64_PEAK_TF,
+                      "bound_by_hbm_tflops": 512.0 / b_gram * n_loc * 6.29},
     }
     if pat_spmv is not None:
         line["spmv_kernel_back_to_back"] = {"avg_us": pat_spmv[0] * 1e3, "min_us": pat_spmv[1] * 1e3,
