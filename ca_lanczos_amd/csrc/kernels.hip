@@ -25,27 +25,24 @@ typedef double d2 __attribute__((ext_vector_type(2)));
 constexpr int kSpmvThreads = 256;
 constexpr int kSpmvNnz = 2048;  // LDS-staged nonzeros per row block (16 KiB)
 
-__device__ __forceinline__ const double* pcol(const Panel& P, int c) {
+// Column c of a panel.  The segment table is taken by value and read with
+// static indices only: binding a reference to a by-value kernel argument
+// makes the compiler copy the struct to scratch in every thread (184 B per
+// thread, re-read per column).
+template <typename T, typename PT>
+__device__ __forceinline__ T* seg_col(const PT P, int c) {
+    T* res = P.ptr[0];
+    int base = 0;
 #pragma unroll
-    for (int s = 0; s < kMaxSeg; ++s) {
-        if (s < P.nseg) {
-            if (c < P.ncol[s]) return P.ptr[s] + (int64_t)c * P.ld[s];
-            c -= P.ncol[s];
-        }
+    for (int q = 0; q < kMaxSeg; ++q) {
+        const int nq = q < P.nseg ? P.ncol[q] : 0;
+        if (c >= base && c < base + nq) res = P.ptr[q] + (int64_t)(c - base) * P.ld[q];
+        base += nq;
     }
-    return P.ptr[0];
+    return res;
 }
-
-__device__ __forceinline__ double* pcol_out(const PanelOut& P, int c) {
-#pragma unroll
-    for (int s = 0; s < kMaxSeg; ++s) {
-        if (s < P.nseg) {
-            if (c < P.ncol[s]) return P.ptr[s] + (int64_t)c * P.ld[s];
-            c -= P.ncol[s];
-        }
-    }
-    return P.ptr[0];
-}
+__device__ __forceinline__ const double* pcol(const Panel P, int c) { return seg_col<const double>(P, c); }
+__device__ __forceinline__ double* pcol_out(const PanelOut P, int c) { return seg_col<double>(P, c); }
 
 __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -742,8 +739,98 @@ ApplyPlan apply_plan(int wp, int wy, int64_t n, bool gram, int wq) {
     return p;
 }
 
+// Store-only apply Y = P M with one row per lane: every column load and
+// store is a contiguous 512-B wave access (the tile layout of k_apply reads
+// 16 row runs per instruction and reaches 3.3-3.8 TB/s on the restart
+// drivers' wide panels; tools/wide_probe.hip).  M (wp x wy, column-major) is
+// staged row-major in LDS for broadcast reads.  y_j = fma(p_c, M(c,j), y_j)
+// over c ascending.  Y may alias columns of P: a lane reads all of its row
+// before it writes it.
+template <int WY>
+__global__ __launch_bounds__(256) void k_apply_rows(Panel P, const double* __restrict__ M, int wp, int wy,
+                                                    PanelOut Y, int64_t n) {
+    extern __shared__ __attribute__((aligned(16))) double Mr[];  // [wp][WY]
+    for (int e = threadIdx.x; e < wp * WY; e += 256) {
+        const int c = e / WY, j = e % WY;
+        Mr[e] = j < wy ? M[(int64_t)j * wp + c] : 0.0;
+    }
+    __syncthreads();
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= n) return;
+    // segment tables copied field by field with static indices (a reference
+    // to the by-value kernel argument would copy it to scratch per thread)
+    const double* sp[kMaxSeg];
+    int64_t sl[kMaxSeg];
+    int sb[kMaxSeg + 1];
+    sb[0] = 0;
+#pragma unroll
+    for (int q = 0; q < kMaxSeg; ++q) {
+        sp[q] = P.ptr[q];
+        sl[q] = P.ld[q];
+        sb[q + 1] = sb[q] + (q < P.nseg ? P.ncol[q] : 0);
+    }
+    auto colp = [&](int c) {
+        const double* res = sp[0] + r;
+#pragma unroll
+        for (int q = 0; q < kMaxSeg; ++q)
+            if (c >= sb[q] && c < sb[q + 1]) res = sp[q] + (int64_t)(c - sb[q]) * sl[q] + r;
+        return res;
+    };
+    double y[WY];
+#pragma unroll
+    for (int j = 0; j < WY; ++j) y[j] = 0.0;
+    constexpr int G = 8;  // columns whose loads are in flight together
+    for (int c0 = 0; c0 < wp; c0 += G) {
+        double p[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u) p[u] = *colp(c0 + u < wp ? c0 + u : c0);
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            if (c0 + u < wp) {
+                const double* mrow = Mr + (c0 + u) * WY;
+#pragma unroll
+                for (int j = 0; j < WY; ++j) y[j] = __builtin_fma(p[u], mrow[j], y[j]);
+            }
+        }
+    }
+    double* yp[kMaxSeg];
+    int64_t yl[kMaxSeg];
+    int yb[kMaxSeg + 1];
+    yb[0] = 0;
+#pragma unroll
+    for (int q = 0; q < kMaxSeg; ++q) {
+        yp[q] = Y.ptr[q];
+        yl[q] = Y.ld[q];
+        yb[q + 1] = yb[q] + (q < Y.nseg ? Y.ncol[q] : 0);
+    }
+#pragma unroll
+    for (int j = 0; j < WY; ++j) {
+        if (j < wy) {
+            double* dst = yp[0] + r;
+#pragma unroll
+            for (int q = 0; q < kMaxSeg; ++q)
+                if (j >= yb[q] && j < yb[q + 1]) dst = yp[q] + (int64_t)(j - yb[q]) * yl[q] + r;
+            *dst = y[j];
+        }
+    }
+}
+
 hipError_t launch_apply(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y, bool store,
                         int wq, int64_t n, const ApplyPlan& pl, double* partial, hipStream_t st) {
+    if (store && !pl.gram && !pl.gramp && wy <= 16 && wp <= 256) {
+        const dim3 g((unsigned)((n + 255) / 256)), b(256);
+        const int WY = wy <= 1 ? 1 : (wy <= 2 ? 2 : (wy <= 4 ? 4 : (wy <= 8 ? 8 : 16)));
+        const size_t sh = sizeof(double) * (size_t)wp * WY;
+        if (n <= 0) return hipSuccess;
+        switch (WY) {
+            case 1: hipLaunchKernelGGL((k_apply_rows<1>), g, b, sh, st, P, dM, wp, wy, Y, n); break;
+            case 2: hipLaunchKernelGGL((k_apply_rows<2>), g, b, sh, st, P, dM, wp, wy, Y, n); break;
+            case 4: hipLaunchKernelGGL((k_apply_rows<4>), g, b, sh, st, P, dM, wp, wy, Y, n); break;
+            case 8: hipLaunchKernelGGL((k_apply_rows<8>), g, b, sh, st, P, dM, wp, wy, Y, n); break;
+            default: hipLaunchKernelGGL((k_apply_rows<16>), g, b, sh, st, P, dM, wp, wy, Y, n); break;
+        }
+        return hipGetLastError();
+    }
     dim3 g(pl.blocks), b(256);
     const size_t sh = pl.lds_bytes;
 #define CAL_APPLY(NTY, RUN, G, GP, S) \
