@@ -5,16 +5,23 @@
 // the SpMV and the Newton matrix-powers recurrence are bit-identical to a
 // sequential CSR SpMV.  MFMA accumulates inside the matrix core.
 //
-// Kernels (DESIGN.md §Kernels):
-//   k_spmv      CSR-stream SpMV: coalesced val/col loads of a row block,
-//               products staged in LDS, sequential per-row sums (bit-exact),
-//               fused Newton shift epilogue (matrix_powers_newton.m:31-47).
-//   k_gram      tall-skinny C = A^T B with v_mfma_f64_16x16x4_f64, per-lane
-//               row runs (16-B loads), deterministic block partials.
-//   k_apply     tall-skinny Y = P M (MFMA), optional fused Y^T Y and
-//               Psub^T Y Grams on the accumulator registers, in-place safe.
-//   k_reduce    fixed-order sum of block partials.
-//   k_dot, k_axpy_sub, k_div, k_gather, k_spmv_resid: small vector kernels.
+// Kernels (DESIGN.md §3):
+//   k_spmv          CSR-stream SpMV: coalesced val/col loads of a row block,
+//                   products staged in LDS, sequential per-row sums
+//                   (bit-exact), fused Newton shift (matrix_powers_newton.m:31-47).
+//   k_spmv_pat_lds, k_spmv_pair
+//                   row-pattern SpMV (lossless pattern table, one / two rows
+//                   per lane), same arithmetic, same shift epilogue.
+//   k_rowapply      the hot block-orthogonalisation sweeps (s <= 8): Gram
+//                   tiles through LDS onto v_mfma_f64_16x16x4f64, the
+//                   coefficient apply in registers, the chained pass B.
+//   k_orth_coef     the s x s algebra between the sweeps; publishes R / RY.
+//   k_gram, k_apply tall-skinny C = A^T B / Y = P M (+ Grams) on MFMA tiles
+//                   for the generic widths ('full', restarts).
+//   k_apply_rows    row-parallel store-only Y = P M (wide panels).
+//   k_reduce        fixed-order sum of block partials.
+//   k_dot, k_axpy_sub(_dev), k_div(_sqrt), k_gather, k_spmv_resid,
+//   k_form_projM, k_abs_rowsum: small vector kernels.
 #include "cal_internal.hpp"
 
 namespace cal {
@@ -947,9 +954,11 @@ hipError_t launch_tilegram(const Panel& T, const double* E, int64_t n, int block
 }
 
 // k_rowapply: lane <-> row.  Y = P * M with P of wp <= WPMAX columns and
-// M zero-padded to WPMAX x MOUT (row-major in global memory, wave-uniform
-// index -> scalar loads).  Every column load is a contiguous 512-B wave
-// access; padded columns reload a valid column (cache hit) times zero.
+// M zero-padded to WPMAX x MOUT (row-major), staged in LDS and read as
+// broadcasts (scalar loads of M measured 9 us faster for pass A alone but
+// slower for pass B, and no different in the loop).  Every column load is a
+// contiguous 512-B wave access; padded columns reload a valid column (cache
+// hit) times zero.
 // GRAM: the stored rows [Qp(0:nq) | Y(0:m)] (nq = min(wq, 8)) are
 // transposed through LDS into one 16-column tile and accumulated with
 // v_mfma_f64_16x16x4 (tile^T tile); Qp column 8 (if wq == 9) is the extra
