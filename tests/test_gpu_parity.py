@@ -504,3 +504,18 @@ def test_impl_restarted_rejects(cal, ref):
         cal.impl_restarted_ca_lanczos(A, r, 40, 4, 4, "newton", "bogus")
     with pytest.raises(cal.CalError):
         cal.impl_restarted_ca_lanczos(A, r, 12, 8, 4, "newton", "full")
+
+
+@pytest.mark.parametrize("s,basis", [(1, "newton"), (2, "monomial"), (3, "newton"), (5, "newton"), (6, "monomial"),
+                                     (9, "newton"), (12, "newton"), (15, "newton")])
+def test_ca_lanczos_block_sizes(cal, ref, s, basis):
+    """Every block size the ABI accepts (1 <= s <= 15): s + 1 > 9 leaves the
+    device-coefficient fast path for the generic sweeps; s = 1 is plain
+    Lanczos with one-column blocks.  Same bars as the s = 4 / 8 cases."""
+    N = 20
+    A = cal.matrices.laplacian_2d(N)
+    r = ref.matlab_rand(N * N)
+    it = s * 5
+    out = cal.ca_lanczos_ex(A, r, s, it, basis, "local")
+    exp = ref.ca_lanczos(A, r, s, it, basis, "local")
+    _compare_lanczos(out, exp, 8.0)
