@@ -519,3 +519,26 @@ def test_ca_lanczos_block_sizes(cal, ref, s, basis):
     out = cal.ca_lanczos_ex(A, r, s, it, basis, "local")
     exp = ref.ca_lanczos(A, r, s, it, basis, "local")
     _compare_lanczos(out, exp, 8.0)
+
+
+@pytest.mark.parametrize("s,basis", [(2, "monomial"), (4, "monomial"), (4, "newton")])
+@pytest.mark.parametrize("start", ["e1", "two"])
+def test_ca_lanczos_exhausted_krylov_space(cal, ref, s, basis, start):
+    """A start vector inside a 1- or 2-dimensional invariant subspace exhausts
+    the Krylov space inside the first block: R of normalize is singular
+    (normalize.m:18-35 only flags the rank) and ca_lanczos.m:176-223 then
+    divides by it.  The oracle raises on these inputs (MATLAB warns and
+    returns Inf/NaN); the HIP path must not hand back an unflagged T: it
+    either raises with a negative status or reports the rank deficiency /
+    breakdown in info."""
+    n = 100
+    A = cal.matrices.diagonal(np.arange(1.0, n + 1.0))
+    r = np.eye(n)[0] + (np.eye(n)[5] if start == "two" else 0.0)
+    with pytest.raises(np.linalg.LinAlgError):
+        ref.ca_lanczos(A, r, s, 3 * s, basis, "local", diagnostics=False)
+    try:
+        out = cal.ca_lanczos_ex(A, r, s, 3 * s, basis, "local", diagnostics=False)
+    except cal.CalError as e:
+        assert e.status < 0
+        return
+    assert out.info["n_rank_deficient"] >= 1 or out.info["breakdown"] == 1
