@@ -13,7 +13,8 @@ resident in HBM before the timed region.
 Workloads: lap2d_N / lap3d_N (Dirichlet Laplacians), circuit_N (the
 G3_circuit stand-in, matrices.circuit_like) or --matrix FILE (.mtx/.mat).
 N > 1 runs one rank per GPU (torch.distributed.run): contiguous row slabs
-(z-slabs for the Laplacians) of the same matrix, RCCL halo exchange per SpMV
+(z-slabs for the Laplacians) of the same matrix, one deep RCCL halo exchange
+per outer iteration (CA matrix powers, overlapped with the interior powers)
 and RCCL allreduce of the Gram blocks (strong scaling, whole-job rate).
 --driver irl times whole impl_restarted_ca_lanczos solves instead of
 ca_lanczos outer iterations (a secondary line; the default is the headline).
@@ -423,8 +424,11 @@ def main():
         "config": {"workload": wl.desc % (n, nnz_total),
                    "s": s, "basis": args.basis, "orth": args.orth, "parallelism": "row-slab x%d" % world,
                    "comm": (args.comm if world > 1 else "none"),
-                   "halo": ("CA matrix powers: one %d-band deep exchange per outer iteration (band %d rows)"
-                            % (s, mpk["band_l"]) if mpk["depth"] > 1 and s <= mpk["depth"]
+                   "halo": ("CA matrix powers: one %d-band deep exchange per outer iteration (band %d rows)%s"
+                            % (s, mpk["band_l"],
+                               ", overlapped with the interior powers" if args.comm == "rccl"
+                               and os.environ.get("CAL_MPK_OVERLAP", "1") != "0" else "")
+                            if mpk["depth"] > 1 and s <= mpk["depth"]
                             else "one exchange per SpMV") if world > 1 else "none"},
         "spmv_format": ("%s (%d row patterns, %d entries; %d pair patterns, %d entries, %d split pairs)"
                         % (fmt, npat, nent, npairpat, npent, nsplit)) if fmt == "pattern" else fmt,

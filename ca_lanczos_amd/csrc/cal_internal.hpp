@@ -103,6 +103,10 @@ struct PatArgs {
     int pcanon;            // every pair pattern has exactly pmaxlen entries (canonical slots)
     int pslot[8];          // canonical slot offsets (the matrix's distinct col - row, ascending)
     int64_t xlo, xhi;      // addressable range of a vector column around its origin
+    // two-range launch (pair kernel): compact pair index t >= gap_at maps to
+    // stored pair t + gap, i.e. rows [0, 2 gap_at) and [2 (gap_at + gap),
+    // 2 gap + n) relative to the origin; n counts the rows of both ranges
+    int64_t gap_at = 0, gap = 0;
 };
 constexpr int kPairSplit = 0xFFFF;
 
@@ -325,7 +329,7 @@ int spmv_range(cal_ctx* c, int64_t o, int64_t len, const double* x, double* y, i
 int powers_dev(cal_ctx* c, int s, const double* q, double* const* Y, const double* shift, const double* im2,
                const double* const* xprev);
 // Halo exchange of the d-deep ghost zone of x (contiguous row ranges; mpk only).
-int halo_exchange_deep(cal_ctx* c, double* x, int d);
+int halo_exchange_deep(cal_ctx* c, double* x, int d, hipStream_t st);
 // copy the n local rows of m columns (leading dimension ld) on the context
 // stream; src/dst are local-origin pointers (a whole-column copy from there
 // would run lpad entries past the last column)

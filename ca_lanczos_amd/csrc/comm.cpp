@@ -30,8 +30,13 @@ static int ensure_stage(cal_ctx* c, size_t doubles) {
 
 void comm_destroy(cal_ctx* c) {
     if (!c->comm) return;
-    if (c->comm->nccl) ncclCommDestroy(c->comm->nccl);
-    if (c->comm->h_stage) hipHostFree(c->comm->h_stage);
+    Comm* m = c->comm;
+    if (m->stream) hipStreamSynchronize(m->stream);
+    if (m->nccl) ncclCommDestroy(m->nccl);
+    if (m->h_stage) hipHostFree(m->h_stage);
+    if (m->ev_q) hipEventDestroy(m->ev_q);
+    if (m->ev_halo) hipEventDestroy(m->ev_halo);
+    if (m->stream) hipStreamDestroy(m->stream);
     delete c->comm;
     c->comm = nullptr;
 }
@@ -95,7 +100,7 @@ int halo_exchange(cal_ctx* c, double* x) {
 // from each q > me [max(st[q], row1), min(st[q+1], row1 + d br)); every piece
 // is a contiguous run of the column on both sides, so RCCL sends and
 // receives in place (no pack kernel).  Peers ascending on every rank.
-int halo_exchange_deep(cal_ctx* c, double* x, int d) {
+int halo_exchange_deep(cal_ctx* c, double* x, int d, hipStream_t hs_st) {
     Comm* m = c->comm;
     DevMatrix& A = c->A;
     if (!m || m->nranks <= 1) return 0;
@@ -132,8 +137,8 @@ int halo_exchange_deep(cal_ctx* c, double* x, int d) {
     if (m->kind == 1) {
         CAL_NCCL(c, ncclGroupStart());
         for (const Piece& p : pieces) {
-            if (p.s_cnt > 0) CAL_NCCL(c, ncclSend(x + p.s_off, (size_t)p.s_cnt, ncclDouble, p.peer, m->nccl, c->stream));
-            if (p.r_cnt > 0) CAL_NCCL(c, ncclRecv(x + p.r_off, (size_t)p.r_cnt, ncclDouble, p.peer, m->nccl, c->stream));
+            if (p.s_cnt > 0) CAL_NCCL(c, ncclSend(x + p.s_off, (size_t)p.s_cnt, ncclDouble, p.peer, m->nccl, hs_st));
+            if (p.r_cnt > 0) CAL_NCCL(c, ncclRecv(x + p.r_off, (size_t)p.r_cnt, ncclDouble, p.peer, m->nccl, hs_st));
         }
         CAL_NCCL(c, ncclGroupEnd());
         return 0;
@@ -232,6 +237,17 @@ int cal_comm_init_rccl(cal_ctx* c, int nranks, int rank, const void* id128) {
     if (r != ncclSuccess) {
         delete m;
         return nccl_fail(c, r, "ncclCommInitRank");
+    }
+    // the halo stream (high priority: its RCCL kernel is dispatched between
+    // the interior matrix-powers blocks) and its two events
+    int lo = 0, hi = 0;
+    hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (hipStreamCreateWithPriority(&m->stream, hipStreamNonBlocking, hi) != hipSuccess ||
+        hipEventCreateWithFlags(&m->ev_q, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&m->ev_halo, hipEventDisableTiming) != hipSuccess) {
+        c->comm = m;
+        comm_destroy(c);
+        return set_error(c, CAL_ERR_HIP, "halo stream / events");
     }
     c->comm = m;
     return 0;

@@ -26,6 +26,10 @@ struct Comm {
     void* user = nullptr;
     double* h_stage = nullptr;  // pinned
     size_t stage_cap = 0;
+    // RCCL: the deep halo exchange runs here, overlapped with the interior
+    // matrix powers (runtime.cpp powers_dev); ev_q: q ready, ev_halo: received
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_q = nullptr, ev_halo = nullptr;
 };
 
 void comm_destroy(cal_ctx* c);

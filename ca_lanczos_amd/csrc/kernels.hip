@@ -291,16 +291,18 @@ __global__ __launch_bounds__(256) void k_spmv_pair(PatArgs a, const uint16_t* __
     int2* s_pinfo = reinterpret_cast<int2*>(s_pv + a.npent);
     int* s_poff = reinterpret_cast<int*>(s_pinfo + (CANON ? 0 : a.nppat));
     const int tid = threadIdx.x;
-    const int64_t npairs = (a.n + 1) >> 1;
-    const int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 256 + tid;
-    const int id = ppat[t < npairs ? t : npairs - 1];
+    const int64_t npairs = (a.n + 1) >> 1;  // compact pairs (both ranges)
+    const int64_t tc = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 256 + tid;
+    const int64_t tcl = tc < npairs ? tc : npairs - 1;
+    const int64_t t = tcl + (tcl >= a.gap_at ? a.gap : 0);  // stored pair (skips the gap)
+    const int id = ppat[t];
     // canonical slots: slot e always loads x[r + pslot[e] .. +1] (clamped to
     // the column; a slot no row of the pair uses is discarded), so the x
     // loads depend on neither the id nor the table and leave first
     double2 xc[CANON ? MAXLEN : 1];
     double2 xs = make_double2(0.0, 0.0), xp = make_double2(0.0, 0.0);  // shift terms
     {
-        const int64_t r0 = 2 * (t < npairs ? t : npairs - 1);
+        const int64_t r0 = 2 * t;
         if (CANON) {
 #pragma unroll
             for (int e = 0; e < MAXLEN; ++e) {
@@ -320,7 +322,7 @@ __global__ __launch_bounds__(256) void k_spmv_pair(PatArgs a, const uint16_t* __
     if (!CANON)
         for (int i = tid; i < a.nppat; i += 256) s_pinfo[i] = ppinfo[i];
     __syncthreads();
-    if (t >= npairs) return;
+    if (tc >= npairs) return;
     const int64_t r = 2 * t;
     if (id != kPairSplit) {  // both rows exist (the lone last row is split)
         // canonical tables: every pair pattern has MAXLEN entries in one
@@ -366,7 +368,7 @@ __global__ __launch_bounds__(256) void k_spmv_pair(PatArgs a, const uint16_t* __
         return;
     }
     // split pair: each row on its own from the row tables
-    for (int k = 0; k < 2 && r + k < a.n; ++k) {
+    for (int k = 0; k < 2 && r + k < a.n + 2 * a.gap; ++k) {
         const int64_t rr = r + k;
         const int2 pi = a.pinfo[a.pat[rr]];
         double sum = 0.0;
@@ -389,12 +391,18 @@ __global__ __launch_bounds__(256) void k_spmv_pair(PatArgs a, const uint16_t* __
 
 constexpr size_t kPatLdsMax = 64 * 1024;
 
+// the pair kernel needs 16-B aligned columns, rows <= 8 entries and an LDS-sized pair table
+bool spmv_pat_pair_path(const PatArgs& a) {
+    const bool al16 = (((uintptr_t)a.x | (uintptr_t)a.y | (uintptr_t)(a.mode == 2 ? a.xprev : nullptr)) & 15) == 0;
+    const size_t lds2 = (size_t)a.npent * 20 + (size_t)a.nppat * 8 + 16;
+    return a.ppat && al16 && a.maxlen <= 8 && lds2 <= kPatLdsMax;
+}
+
 template <int MODE>
 static hipError_t launch_pat_mode(const PatArgs& a, hipStream_t st) {
     const size_t lds = (size_t)a.npat * 8 + (size_t)a.nent * 12 + 16;
-    const bool al16 = (((uintptr_t)a.x | (uintptr_t)a.y | (uintptr_t)(MODE == 2 ? a.xprev : nullptr)) & 15) == 0;
     const size_t lds2 = (size_t)a.npent * 20 + (size_t)a.nppat * 8 + 16;
-    if (a.ppat && al16 && a.maxlen <= 8 && lds2 <= kPatLdsMax) {
+    if (spmv_pat_pair_path(a)) {
         const int64_t npairs = (a.n + 1) / 2;
         dim3 g((unsigned)((npairs + 255) / 256)), b(256);
 #define CAL_PR(ML)                                                                                           \
@@ -447,6 +455,24 @@ static hipError_t launch_pat_mode(const PatArgs& a, hipStream_t st) {
 
 hipError_t launch_spmv_pat(const PatArgs& a, hipStream_t st) {
     if (a.nblk <= 0) return hipSuccess;
+    if (a.gap != 0 && !spmv_pat_pair_path(a)) {  // the row kernels take one range: two launches
+        PatArgs b = a, h = a;
+        b.gap_at = b.gap = h.gap_at = h.gap = 0;
+        b.n = 2 * a.gap_at;
+        b.nblk = (int)((b.n + 255) / 256);
+        const int64_t sh = 2 * (a.gap_at + a.gap);
+        h.n = a.n - 2 * a.gap_at;
+        h.nblk = (int)((h.n + 255) / 256);
+        h.pat += sh;
+        h.x += sh;
+        h.y += sh;
+        if (h.xprev) h.xprev += sh;
+        if (h.ppat) h.ppat += sh / 2;
+        h.xlo -= sh;
+        h.xhi -= sh;
+        hipError_t e = launch_spmv_pat(b, st);
+        return e != hipSuccess ? e : launch_spmv_pat(h, st);
+    }
     switch (a.mode) {
         case 0: return launch_pat_mode<0>(a, st);
         case 1: return launch_pat_mode<1>(a, st);

@@ -1,6 +1,7 @@
 // runtime.cpp -- context lifecycle, device buffers, matrix upload, timers.
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <unordered_map>
 #include <vector>
@@ -417,11 +418,8 @@ int upload_matrix(cal_ctx* c, int64_t n_rows, int64_t ext_off, int64_t n_local, 
     return 0;
 }
 
-int spmv_range(cal_ctx* c, int64_t o, int64_t len, const double* x, double* y, int mode, double shift, double im2,
-               const double* xprev) {
-    const DevMatrix& A = c->A;
-    if (o < 0 || (o & 1) || len < 0 || o + len > A.n_rows)
-        return set_error(c, CAL_ERR_ARG, "spmv_range: bad stored-row range");
+static PatArgs pat_args(const DevMatrix& A, int64_t o, int64_t len, const double* x, double* y, int mode,
+                        double shift, double im2, const double* xprev) {
     const int64_t d = o - A.ext_off;  // launch origin relative to the local origin
     PatArgs p;
     p.pat = A.pat + o;
@@ -450,6 +448,33 @@ int spmv_range(cal_ctx* c, int64_t o, int64_t len, const double* x, double* y, i
     for (int k = 0; k < 8; ++k) p.pslot[k] = A.pslot[k];
     p.xlo = -(A.lpad + d);
     p.xhi = A.ld - (A.lpad + d);
+    return p;
+}
+
+int spmv_range(cal_ctx* c, int64_t o, int64_t len, const double* x, double* y, int mode, double shift, double im2,
+               const double* xprev) {
+    const DevMatrix& A = c->A;
+    if (o < 0 || (o & 1) || len < 0 || o + len > A.n_rows)
+        return set_error(c, CAL_ERR_ARG, "spmv_range: bad stored-row range");
+    const PatArgs p = pat_args(A, o, len, x, y, mode, shift, im2, xprev);
+    const int t = timer_begin(c, 0);
+    CAL_HIP(c, launch_spmv_pat(p, c->stream));
+    timer_end(c, t);
+    return 0;
+}
+
+// Two stored-row ranges [o1, o1 + len1) and [o2, o2 + len2) in one launch
+// (the pair kernel skips the gap; the row kernels take two launches).
+int spmv_range2(cal_ctx* c, int64_t o1, int64_t len1, int64_t o2, int64_t len2, const double* x, double* y, int mode,
+                double shift, double im2, const double* xprev) {
+    const DevMatrix& A = c->A;
+    if (len1 == 0) return spmv_range(c, o2, len2, x, y, mode, shift, im2, xprev);
+    if (len2 == 0) return spmv_range(c, o1, len1, x, y, mode, shift, im2, xprev);
+    if (o1 < 0 || (o1 & 1) || (len1 & 1) || (o2 & 1) || len2 < 0 || o2 < o1 + len1 || o2 + len2 > A.n_rows)
+        return set_error(c, CAL_ERR_ARG, "spmv_range2: bad stored-row ranges");
+    PatArgs p = pat_args(A, o1, len1 + len2, x, y, mode, shift, im2, xprev);
+    p.gap_at = len1 / 2;
+    p.gap = (o2 - o1) / 2 - p.gap_at;
     const int t = timer_begin(c, 0);
     CAL_HIP(c, launch_spmv_pat(p, c->stream));
     timer_end(c, t);
@@ -486,28 +511,92 @@ int spmv_dev(cal_ctx* c, const double* x, double* y, int mode, double shift, dou
 // length up to even: the extra edge rows are computed from stale halo data
 // and never read by a valid row of the next power (they lie one row outside
 // its reach), and masked loads keep them from leaking into their pair rows.
+//
+// Overlap (RCCL): the exchange runs on the communicator's stream while the
+// compute stream works through the interior trapezoid -- power j on
+// [row0 + j bl, row1 - j br), which reads only power j-1's interior and, for
+// j = 1, q's own rows.  The boundary pieces [glo_j, row0 + j bl) and
+// [row1 - j br, ghi_j) follow the exchange, both sides in one launch, after
+// every interior power: they read the boundary of power j-1 and the interior
+// next to it.  A boundary launch recomputes at most one interior edge row
+// (the even rounding) from valid data, so its bits do not change; the
+// interior launch's own extra edge row is stale until that boundary launch
+// overwrites it and is outside the next interior power's reach.
+struct PowRange {
+    int64_t o, len;  // stored rows, o even
+};
+
+static PowRange stored_range(const DevMatrix& A, int64_t glo, int64_t ghi) {
+    int64_t o = glo - A.row0 + A.ext_off;
+    const int64_t e = ghi - A.row0 + A.ext_off;
+    o &= ~(int64_t)1;
+    int64_t len = std::max<int64_t>(0, e - o);
+    if ((len & 1) && o + len < A.n_rows) ++len;
+    return {o, len};
+}
+
+// 0 off, 1 on (default for RCCL), from CAL_MPK_OVERLAP; CAL_MPK_FAKE_BAND=b
+// splits a single rank's powers the same way with band b (launch-cost and
+// two-range-kernel checks: no exchange is involved, the bits are unchanged)
+static int mpk_overlap_env() {
+    const char* e = std::getenv("CAL_MPK_OVERLAP");
+    return e ? std::atoi(e) : -1;
+}
+static int64_t mpk_fake_band() {
+    const char* e = std::getenv("CAL_MPK_FAKE_BAND");
+    return e ? (int64_t)std::atoll(e) : (int64_t)0;
+}
+
 int powers_dev(cal_ctx* c, int s, const double* q, double* const* Y, const double* shift, const double* im2,
                const double* const* xprev) {
     const DevMatrix& A = c->A;
     auto mode_of = [&](int j) { return shift ? ((im2 && im2[j] != 0.0) ? 2 : 1) : 0; };
-    if (!(A.mpk && A.use_pat && s <= A.mpk_depth && s > 1)) {
+    auto launch = [&](int j, const PowRange& r1, const PowRange& r2) {  // power j (1-based)
+        return spmv_range2(c, r1.o, r1.len, r2.o, r2.len, j == 1 ? q : Y[j - 2], Y[j - 1], mode_of(j - 1),
+                           shift ? shift[j - 1] : 0.0, im2 ? im2[j - 1] : 0.0, xprev ? xprev[j - 1] : nullptr);
+    };
+    const int64_t row1 = A.row0 + A.n_local;
+    const bool mpk = A.mpk && A.use_pat && s <= A.mpk_depth && s > 1;
+    const int64_t fake = (!mpk && A.use_pat && s > 1 && !A.mpk && A.nghost == 0) ? mpk_fake_band() : 0;
+    if (!mpk && fake <= 0) {
         for (int j = 0; j < s; ++j)
             CAL_TRY(spmv_dev(c, j == 0 ? q : Y[j - 1], Y[j], mode_of(j), shift ? shift[j] : 0.0,
                              im2 ? im2[j] : 0.0, xprev ? xprev[j] : nullptr));
         return 0;
     }
-    CAL_TRY(halo_exchange_deep(c, const_cast<double*>(q), s));
-    const int64_t row1 = A.row0 + A.n_local;
+    // global rows of power j and whether each side waits for the exchange
+    const int64_t bl = mpk ? A.band_l : fake, br = mpk ? A.band_r : fake;
+    auto glo = [&](int j) { return mpk ? std::max(A.ext_lo, A.row0 - (int64_t)(s - j) * bl) : A.row0; };
+    auto ghi = [&](int j) { return mpk ? std::min(A.ext_hi, row1 + (int64_t)(s - j) * br) : row1; };
+    const bool dep_lo = mpk ? A.ext_lo < A.row0 : true, dep_hi = mpk ? A.ext_hi > row1 : true;
+    auto ilo = [&](int j) { return dep_lo ? A.row0 + (int64_t)j * bl : glo(j); };
+    auto ihi = [&](int j) { return dep_hi ? row1 - (int64_t)j * br : ghi(j); };
+    Comm* m = c->comm;
+    const bool rccl = mpk && m && m->kind == 1 && m->stream && m->ev_q && m->ev_halo;
+    const int ov = mpk_overlap_env();
+    const bool split = (fake > 0 || (mpk && (ov == 1 || (ov < 0 && rccl)))) && (dep_lo || dep_hi) &&
+                       ilo(s) + 4 < ihi(s);
+    if (!split) {
+        CAL_TRY(halo_exchange_deep(c, const_cast<double*>(q), s, c->stream));
+        for (int j = 1; j <= s; ++j) CAL_TRY(launch(j, stored_range(A, glo(j), ghi(j)), PowRange{0, 0}));
+        return 0;
+    }
+    if (rccl) {  // exchange on the communicator's stream, behind q
+        CAL_HIP(c, hipEventRecord(m->ev_q, c->stream));
+        CAL_HIP(c, hipStreamWaitEvent(m->stream, m->ev_q, 0));
+        CAL_TRY(halo_exchange_deep(c, const_cast<double*>(q), s, m->stream));
+        CAL_HIP(c, hipEventRecord(m->ev_halo, m->stream));
+    } else if (mpk) {
+        CAL_TRY(halo_exchange_deep(c, const_cast<double*>(q), s, c->stream));
+    }
+    for (int j = 1; j <= s; ++j) CAL_TRY(launch(j, stored_range(A, ilo(j), ihi(j)), PowRange{0, 0}));
+    if (rccl) CAL_HIP(c, hipStreamWaitEvent(c->stream, m->ev_halo, 0));
     for (int j = 1; j <= s; ++j) {
-        const int64_t glo = std::max(A.ext_lo, A.row0 - (int64_t)(s - j) * A.band_l);
-        const int64_t ghi = std::min(A.ext_hi, row1 + (int64_t)(s - j) * A.band_r);
-        int64_t o = glo - A.ext_lo + A.ext_dummy;  // stored index
-        const int64_t e = ghi - A.ext_lo + A.ext_dummy;
-        o &= ~(int64_t)1;
-        int64_t len = e - o;
-        if ((len & 1) && o + len < A.n_rows) ++len;
-        CAL_TRY(spmv_range(c, o, len, j == 1 ? q : Y[j - 2], Y[j - 1], mode_of(j - 1), shift ? shift[j - 1] : 0.0,
-                           im2 ? im2[j - 1] : 0.0, xprev ? xprev[j - 1] : nullptr));
+        const PowRange lo = dep_lo ? stored_range(A, glo(j), ilo(j)) : PowRange{0, 0};
+        const PowRange hi = dep_hi ? stored_range(A, ihi(j), ghi(j)) : PowRange{0, 0};
+        if (lo.len > 0 && hi.len > 0 && hi.o < lo.o + lo.len)
+            return set_error(c, CAL_ERR_ARG, "powers_dev: boundary ranges overlap");
+        CAL_TRY(launch(j, lo, hi));
     }
     return 0;
 }

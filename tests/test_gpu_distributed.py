@@ -162,7 +162,10 @@ def _mpk_worker(rank, world, port, case, out_q):
     b = cal.matrices.slab_bounds(n, world, N ** (dim - 1))
     r0, r1 = b[rank], b[rank + 1]
     res = {}
-    for depth in (8, 1):
+    # (depth, CAL_MPK_OVERLAP): 1 splits the powers into the interior
+    # trapezoid and the boundary pieces after the exchange (the RCCL default)
+    for key, depth, ov in (("8", 8, "0"), ("8s", 8, "1"), ("1", 1, "0")):
+        os.environ["CAL_MPK_OVERLAP"] = ov
         ctx = cal.Context(0, mpk_depth=depth)
         ctx.comm_init_host(world, rank, allreduce, exchange)
         ctx.set_matrix_slab(n, r0, A[r0:r1])
@@ -171,7 +174,7 @@ def _mpk_worker(rank, world, port, case, out_q):
         Vn = cal.matrix_powers_newton(None, v, s, lam, 1, ctx=ctx)
         Vm = cal.matrix_powers_monomial(None, v / np.linalg.norm(v), s, ctx=ctx)
         out = cal.ca_lanczos_ex(A, ref.matlab_rand(n)[r0:r1], s, it, "newton", orth, diagnostics=False, ctx=ctx)
-        res[depth] = (ctx.mpk_info(), Vn, Vm, out.T, list(out.reorth))
+        res[key] = (ctx.mpk_info(), Vn, Vm, out.T, list(out.reorth))
         ctx.close()
     out_q.put((rank, r0, r1, res))
     dist.barrier()
@@ -179,14 +182,17 @@ def _mpk_worker(rank, world, port, case, out_q):
 
 
 @pytest.mark.parametrize("world,case", [(2, (3, 12, 8, 40, "local")), (3, (3, 10, 8, 32, "local")),
-                                        (3, (2, 30, 6, 36, "full"))])
+                                        (3, (2, 30, 6, 36, "full")), (2, (3, 40, 8, 40, "local")),
+                                        (3, (2, 61, 6, 36, "local"))])
 def test_mpk_deep_ghost_zone(cal, ref, world, case):
     """Distributed matrix powers with one s-deep halo exchange (the stored
     ghost-zone rows are recomputed redundantly) are bit-identical to the
     single-GPU powers on every rank's rows, and the whole CA-Lanczos run is
     bit-identical to the one-exchange-per-SpMV distributed run.  World 3 on
     10 or 30 planes: the 8-plane ghost zone spans two ranks and is clipped at
-    the domain ends."""
+    the domain ends.  The split schedule (interior trapezoid, then both
+    boundary pieces in one two-range launch) gives the same bits; it needs
+    more than 2 s planes per slab (lap3d 40 on 2 ranks, lap2d 61 on 3)."""
     mpc = mp.get_context("spawn")
     q = mpc.Queue()
     port = _free_port()
@@ -204,13 +210,16 @@ def test_mpk_deep_ghost_zone(cal, ref, world, case):
     lam = np.array([7.5, 0.5, 3.0, 11.0, 1.5, 5.0, 9.0, 2.5])[:s]
     Vn = ref.matrix_powers_newton(A, v, s, lam, 1)
     for rank, r0, r1, rr in res:
-        info8, info1 = rr[8][0], rr[1][0]
+        info8, info1 = rr["8"][0], rr["1"][0]
         assert info8["depth"] == 8 and info1["depth"] == 1
         assert info8["band_l"] == N ** (dim - 1) and info8["n_rows"] > r1 - r0
-        assert np.array_equal(rr[8][1], Vn[r0:r1]), rank            # newton powers, oracle bits
-        assert np.array_equal(rr[8][1], rr[1][1]) and np.array_equal(rr[8][2], rr[1][2])
-        assert np.array_equal(rr[8][3], rr[1][3]) and rr[8][4] == rr[1][4]   # whole run
-    assert all(np.array_equal(res[0][3][8][3], x[3][8][3]) for x in res)
+        assert np.array_equal(rr["8"][1], Vn[r0:r1]), rank            # newton powers, oracle bits
+        assert np.array_equal(rr["8"][1], rr["1"][1]) and np.array_equal(rr["8"][2], rr["1"][2])
+        assert np.array_equal(rr["8"][3], rr["1"][3]) and rr["8"][4] == rr["1"][4]   # whole run
+        for k in range(1, 4):                                          # the split schedule
+            assert np.array_equal(rr["8s"][k], rr["8"][k]), (rank, k)
+        assert rr["8s"][4] == rr["8"][4]
+    assert all(np.array_equal(res[0][3]["8"][3], x[3]["8"][3]) for x in res)
 
 
 def _restart_worker(rank, world, port, out_q):

@@ -542,3 +542,37 @@ def test_ca_lanczos_exhausted_krylov_space(cal, ref, s, basis, start):
         assert e.status < 0
         return
     assert out.info["n_rank_deficient"] >= 1 or out.info["breakdown"] == 1
+
+
+@pytest.mark.parametrize("basis", ["newton", "monomial"])
+def test_matrix_powers_split_schedule(cal, ref, monkeypatch, basis):
+    """The multi-GPU matrix-powers schedule on one rank (CAL_MPK_FAKE_BAND):
+    each power as its interior range, then both boundary pieces in one
+    two-range pair-kernel launch.  No exchange is involved, so the powers
+    and the whole CA-Lanczos run must keep the unsplit bits."""
+    N, s = 30, 8
+    A = cal.matrices.laplacian_3d(N)
+    n = A.shape[0]
+    v = ref.matlab_rand(n, seed=3)
+    r = ref.matlab_rand(n)
+    lam = np.linspace(0.5, 11.5, s)
+
+    def run():
+        ctx = cal.Context().set_matrix(A)
+        V = (cal.matrix_powers_newton(A, v, s, lam, 1, ctx=ctx) if basis == "newton"
+             else cal.matrix_powers_monomial(A, v / np.linalg.norm(v), s, ctx=ctx))
+        out = cal.ca_lanczos_ex(A, r, s, 4 * s, basis, "local", diagnostics=False, ctx=ctx)
+        ctx.close()
+        return V, out
+
+    V0, o0 = run()
+    # the stencil's band, and wider ones (odd: ragged even rounding); a fake
+    # band below the matrix's own would read unfinished rows by design
+    for band in (N * N, N * N + 1, 3 * N * N + 7):
+        monkeypatch.setenv("CAL_MPK_FAKE_BAND", str(band))
+        V1, o1 = run()
+        assert np.array_equal(V1, V0), band
+        assert np.array_equal(o1.T, o0.T) and list(o1.reorth) == list(o0.reorth), band
+    monkeypatch.delenv("CAL_MPK_FAKE_BAND")
+    if basis == "newton":
+        assert np.array_equal(V0, ref.matrix_powers_newton(A, v, s, lam, 1))
