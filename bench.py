@@ -52,6 +52,8 @@ def parse():
     p.add_argument("--basis", default="newton")
     p.add_argument("--orth", default="local")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--basis-gb", type=float, default=200.0,
+                   help="per-GPU budget for the Krylov basis Q; longer runs continue in restarted epochs")
     p.add_argument("--cpu-iters", type=int, default=8, help="outer iterations of the C/OpenMP CPU sample")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "spmv_traffic.json"))
     p.add_argument("--mpk-depth", type=int, default=8,
@@ -326,16 +328,31 @@ def main():
     # launch adds ~6 us per kernel boundary); KT more steps then run with the
     # HIP-event kernel timers for the per-kernel figures and the roofline.
     KT = max(1, min(K, 5))
-    ctx.lanczos_begin(r_full[r0:r1], s, W + K + KT, args.basis, args.orth)
-    for _ in range(W):
+    # Q holds s*t + 1 columns of the local slab.  A run longer than a 200 GB
+    # basis (about 300 outer iterations of lap3d_215 on one GPU) continues in
+    # epochs: a new epoch restarts the Krylov space from the same vector, and
+    # its Newton prologue is timed when it falls inside the timed region.
+    t_epoch = min(W + K + KT, max(4, int(args.basis_gb * 1e9 / ((r1 - r0) * 8.0 * (s + 1)))))
+    ep = {"left": 0, "flags": []}
+
+    def step():
+        if ep["left"] == 0:
+            if ep.get("begun"):
+                ep["flags"] += list(ctx.lanczos_get()[3])
+            ctx.lanczos_begin(r_full[r0:r1], s, t_epoch, args.basis, args.orth)
+            ep["left"], ep["begun"] = t_epoch, True
         ctx.lanczos_step(False)
+        ep["left"] -= 1
+
+    for _ in range(W):
+        step()
     ctx.synchronize()
     if dist is not None:
         dist.barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
     for _ in range(K):
-        ctx.lanczos_step(False)
+        step()
     ctx.synchronize()
     t1 = time.perf_counter()
     if dist is not None:
@@ -344,13 +361,14 @@ def main():
     ctx.timer_enable(True)
     ctx.timer_reset()
     for _ in range(KT):
-        ctx.lanczos_step(False)
+        step()
     ctx.synchronize()
     spmv_cnt, spmv_ms = ctx.timer_read("spmv")
     gram_cnt, gram_ms = ctx.timer_read("gram")
     apply_cnt, apply_ms = ctx.timer_read("apply")
     ctx.timer_enable(False)
     T, _, _, flags, info = ctx.lanczos_get()
+    flags = np.concatenate([np.asarray(ep["flags"], dtype=flags.dtype), flags])
     elapsed, spmv_avg_ms = max_over_ranks(dist, [elapsed, spmv_ms / max(spmv_cnt, 1)])
 
     fmt, npat, nent = ctx.spmv_format()
