@@ -299,3 +299,52 @@ class MPKSlab:
             V.append(y)
             x = y
         return np.stack([v[self.r0 - self.wlo:self.r1 - self.wlo] for v in V], axis=1)
+
+    def split_ok(self, s):
+        """Every power keeps a non-empty interior (more than 2s bands per slab)."""
+        lo = self.r0 + s * self.bl if self.elo < self.r0 else self.r0
+        hi = self.r1 - s * self.br if self.ehi > self.r1 else self.r1
+        return lo < hi
+
+    def powers_split(self, q_local, s, shifts=None):
+        """The overlapped schedule of runtime.cpp powers_dev: every power's
+        interior [r0 + j bl, r1 - j br) is computed before the exchange, from
+        a window whose ghost zone is still NaN, then each power's two
+        boundary pieces after it.  A NaN in the result would mean the
+        interior read a ghost row it does not own yet."""
+        assert s <= self.D and self.split_ok(s)
+        wl = self.whi - self.wlo
+        V = [np.full(wl, np.nan) for _ in range(s + 1)]
+        V[0][self.r0 - self.wlo:self.r1 - self.wlo] = q_local
+        dep_lo, dep_hi = self.elo < self.r0, self.ehi > self.r1
+
+        def glo(j):
+            return max(self.elo, self.r0 - (s - j) * self.bl)
+
+        def ghi(j):
+            return min(self.ehi, self.r1 + (s - j) * self.br)
+
+        def ilo(j):
+            return self.r0 + j * self.bl if dep_lo else glo(j)
+
+        def ihi(j):
+            return self.r1 - j * self.br if dep_hi else ghi(j)
+
+        def run(j, lo, hi):
+            if hi <= lo:
+                return
+            x = V[j - 1]
+            y = self.ext[lo - self.elo:hi - self.elo] @ x
+            if shifts is not None:
+                y = y - shifts[j - 1] * x[lo - self.wlo:hi - self.wlo]
+            V[j][lo - self.wlo:hi - self.wlo] = y
+
+        for j in range(1, s + 1):  # interior trapezoid, exchange in flight
+            run(j, ilo(j), ihi(j))
+        V[0][:] = np.where(np.isnan(V[0]), self.deep_halo(q_local, s), V[0])
+        for j in range(1, s + 1):  # boundary pieces after the exchange
+            if dep_lo:
+                run(j, glo(j), ilo(j))
+            if dep_hi:
+                run(j, ihi(j), ghi(j))
+        return np.stack([v[self.r0 - self.wlo:self.r1 - self.wlo] for v in V], axis=1)

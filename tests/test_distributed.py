@@ -89,19 +89,27 @@ def _mpk_worker(rank, world, port, case, out_q):
     m = dr.MPKSlab(A[r0:r1], bounds, rank, D)
     q = ref.matlab_rand(n, seed=3)
     lam = np.linspace(0.5, 4.0 * dim - 0.5, s)
-    out_q.put((rank, r0, r1, m.bl, m.elo, m.ehi, m.powers(q[r0:r1], s, lam), m.powers(q[r0:r1], s)))
+    # every rank takes part in the exchanges, so the split runs on all or none
+    import torch
+    ok = torch.tensor([1.0 if m.split_ok(s) else 0.0])
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    split = (m.powers_split(q[r0:r1], s, lam), m.powers_split(q[r0:r1], s)) if ok.item() > 0 else None
+    out_q.put((rank, r0, r1, m.bl, m.elo, m.ehi, m.powers(q[r0:r1], s, lam), m.powers(q[r0:r1], s), split))
     dist.barrier()
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world,case", [(2, (3, 9, 8, 8)), (3, (3, 8, 6, 8)), (4, (2, 24, 8, 8)),
-                                        (3, (2, 20, 4, 6))])
+                                        (3, (2, 20, 4, 6)), (2, (2, 40, 8, 8)), (3, (2, 61, 6, 8)),
+                                        (4, (2, 90, 8, 8))])
 def test_mpk_deep_ghost_zone_restatement(ref, world, case):
     """The CA matrix-powers scheme of comm.cpp / runtime.cpp (ghost rows
     fetched from owners, one s-band exchange, shrinking ranges) on gloo:
     the powers equal the global Newton / monomial powers bit for bit on
     every slab, including ghost zones that span several ranks (3-4 ranks on
-    8-9 planes with an 8-plane zone) and clip at the domain ends."""
+    8-9 planes with an 8-plane zone) and clip at the domain ends.  Slabs of
+    more than 2s planes also run the overlapped schedule (interior powers
+    before the exchange, from a NaN ghost zone): same bits, no NaN."""
     ctx = mp.get_context("spawn")
     qq = ctx.Queue()
     port = _free_port()
@@ -118,8 +126,14 @@ def test_mpk_deep_ghost_zone_restatement(ref, world, case):
     lam = np.linspace(0.5, 4.0 * dim - 0.5, s)
     Vn = ref.matrix_powers_newton(A, q, s, lam, 1)
     Vm = np.hstack([q[:, None], ref.matrix_powers_monomial(A, q, s)])
-    for rank, r0, r1, bl, elo, ehi, Pn, Pm in res:
+    nsplit = 0
+    for rank, r0, r1, bl, elo, ehi, Pn, Pm, split in res:
         assert bl == N ** (dim - 1)
         assert elo == max(0, r0 - (D - 1) * bl) and ehi == min(A.shape[0], r1 + (D - 1) * bl)
         assert np.array_equal(Pn, Vn[r0:r1]), rank
         assert np.array_equal(Pm, Vm[r0:r1]), rank
+        if split is not None:
+            nsplit += 1
+            assert np.array_equal(split[0], Pn) and np.array_equal(split[1], Pm), rank
+    if min(x[2] - x[1] for x in res) > 2 * s * N ** (dim - 1):  # every slab thick enough
+        assert nsplit == world
