@@ -557,7 +557,7 @@ int powers_dev(cal_ctx* c, int s, const double* q, double* const* Y, const doubl
     };
     const int64_t row1 = A.row0 + A.n_local;
     const bool mpk = A.mpk && A.use_pat && s <= A.mpk_depth && s > 1;
-    const int64_t fake = (!mpk && A.use_pat && s > 1 && !A.mpk && A.nghost == 0) ? mpk_fake_band() : 0;
+    const int64_t fake = (!mpk && !A.mpk && A.use_pat && s > 1 && A.nghost == 0) ? mpk_fake_band() : 0;
     if (!mpk && fake <= 0) {
         for (int j = 0; j < s; ++j)
             CAL_TRY(spmv_dev(c, j == 0 ? q : Y[j - 1], Y[j], mode_of(j), shift ? shift[j] : 0.0,
