@@ -1,0 +1,49 @@
+"""bench.py's output contract, on a small workload: one JSON line on stdout
+with the fields the driver reads, the roofline and CPU-baseline objects, and
+the epoch path that keeps long runs inside the basis budget."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args, timeout=240):
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT, capture_output=True,
+                       text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout[-2000:]  # exactly one line on stdout
+    return json.loads(lines[0])
+
+
+def test_bench_contract_fields():
+    d = _bench("--workload", "lap3d_40", "--steps", "3", "--warmup", "1", "--cpu-iters", "2")
+    assert d["metric"].startswith("CA-Lanczos outer-iters/sec") and d["unit"] == "outer-iters/s"
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    assert abs(d["value"] - 1e3 / d["ms_per_step"]) <= 1e-6 * d["value"]
+    assert (d["n_gpus"], d["steps"], d["warmup"]) == (1, 3, 1)
+    assert d["higher_is_better"] is True and d["scaling"] == "strong" and d["vs_baseline"] is None
+    assert d["dtype"] == "f64" and d["data"].startswith("synthetic")
+    assert d["config"]["workload"].startswith("lap3d_40") and d["config"]["s"] == 8
+    rf = d["roofline"]
+    assert {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(rf)
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    assert rf["achieved"] > 0 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
+    cb = d["cpu_baseline"]
+    assert {"value", "unit", "cores", "kind", "sample"} <= set(cb)
+    assert cb["value"] > 0 and cb["unit"] == "outer-iters/s" and cb["kind"] in ("port", "reference")
+    assert d["reorth_passes"].endswith("/3")
+
+
+def test_bench_epochs_keep_the_line_valid():
+    """A basis budget of 20 MB holds only a few outer iterations of lap3d_40:
+    the run continues in restarted epochs and still prints one valid line."""
+    d = _bench("--workload", "lap3d_40", "--steps", "12", "--warmup", "2", "--no-cpu-baseline",
+               "--basis-gb", "0.02")
+    assert d["value"] > 0 and d["steps"] == 12
+    assert d["reorth_passes"].endswith("/12")
