@@ -47,3 +47,24 @@ def test_bench_epochs_keep_the_line_valid():
                "--basis-gb", "0.02")
     assert d["value"] > 0 and d["steps"] == 12
     assert d["reorth_passes"].endswith("/12")
+
+
+def test_bench_two_ranks_one_line():
+    """The driver's N > 1 launch (torch.distributed.run, one rank per GPU),
+    rehearsed with 2 ranks on one GPU over the host-staged communicator:
+    rank 0 prints the only line, the whole-job rate, no CPU baseline."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "3", "--warmup", "1", "--workload", "lap3d_40", "--comm", "host"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["parallelism"] == "row-slab x2"
+    assert d["config"]["comm"] == "host" and "cpu_baseline" not in d
