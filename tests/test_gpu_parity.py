@@ -576,3 +576,31 @@ def test_matrix_powers_split_schedule(cal, ref, monkeypatch, basis):
     monkeypatch.delenv("CAL_MPK_FAKE_BAND")
     if basis == "newton":
         assert np.array_equal(V0, ref.matrix_powers_newton(A, v, s, lam, 1))
+
+
+def test_matrix_powers_split_schedule_row_kernel(cal, ref, monkeypatch):
+    """The split schedule when the pair kernel does not apply (27-point
+    stencil: rows of 27 entries, beyond the pair kernel's 8): the two-range
+    launch falls back to two row-kernel launches.  Same bits as unsplit."""
+    import scipy.sparse as sp
+    N, s = 24, 8
+    T = sp.diags([np.ones(N - 1), 4.0 * np.ones(N), np.ones(N - 1)], [-1, 0, 1])
+    A = sp.kron(sp.kron(T, T), T).tocsr()
+    A.sort_indices()
+    n = A.shape[0]
+    v = ref.matlab_rand(n, seed=4)
+    lam = np.linspace(8.5, 200.0, s)
+
+    def run():
+        ctx = cal.Context().set_matrix(A)
+        assert ctx.spmv_format()[0] == "pattern"
+        V = cal.matrix_powers_newton(A, v, s, lam, 1, ctx=ctx)
+        ctx.close()
+        return V
+
+    V0 = run()
+    monkeypatch.setenv("CAL_MPK_FAKE_BAND", str(N * N + N + 1))
+    V1 = run()
+    monkeypatch.delenv("CAL_MPK_FAKE_BAND")
+    assert np.array_equal(V1, V0)
+    assert np.array_equal(V0, ref.matrix_powers_newton(A, v, s, lam, 1))
