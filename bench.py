@@ -479,12 +479,33 @@ def main():
                                    "gbps": b_csr / (csr_spmv[0] * 1e-3) / 1e9, "bytes_per_launch": b_csr}
     if host_rt_ms is not None:
         line["spmv_host_roundtrip_ms"] = host_rt_ms
+    if world == 1 and args.orth == "local":
+        line["diagnostics_on"] = diagnostics_run(ctx, r_full[r0:r1], s, args)
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(wl, s, args.cpu_iters, args.basis)
         line["cpu_baseline_numpy"] = cpu_baseline_numpy(wl, s, 2, args.basis)
     emit(line)
     if dist is not None:
         dist.barrier()
+
+
+def diagnostics_run(ctx, r, s, args, t=15):
+    """The reference-faithful cost: ca_lanczos.m computes the
+    Ritz residual norms and the orthogonality error at every outer iteration
+    (compute_ritz_rnorm / compute_orth_err, ca_lanczos.m:88-107,229-235).
+    t outer iterations with both on; the Newton prologue (in begin) excluded."""
+    ctx.lanczos_begin(r, s, t, args.basis, args.orth)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(t):
+        ctx.lanczos_step(True)
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    info = ctx.lanczos_get()[4]
+    ctx.lanczos_end()
+    return {"outer_iters": t, "ms": dt * 1e3, "outer_iters_per_s": t / dt, "diag_ms": info.diag_ms,
+            "what": "Ritz residual norms of all s*k Ritz pairs (eig of T, x = Q*Vp(:,i), ||Ax - lx||) and "
+                    "the orthogonality error after every outer iteration, as the reference always runs"}
 
 
 def main_irl(args):

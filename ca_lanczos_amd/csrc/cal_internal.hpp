@@ -232,6 +232,12 @@ hipError_t launch_div_sqrt(double* y, const double* x, const double* nn, int64_t
 hipError_t launch_abs_rowsum(const int* rowptr, const double* val, int64_t n, double* y, hipStream_t st);
 hipError_t launch_gather(double* dst, const double* src, const int* idx, int64_t cnt, hipStream_t st);
 // fused SpMV + Ritz residual partials for one Ritz pair (diagnostics)
+int spmv_pair_resid_blocks(const PatArgs& a);
+hipError_t launch_spmv_pair_resid(const PatArgs& a, double lr, double* partial, hipStream_t st);
+// Ritz residual partials of a real Ritz value on the pair patterns (local
+// rows; x's halo already exchanged): *blocks = 0 when the path does not apply
+int spmv_resid_pair_dev(cal_ctx* c, const double* x, double lr, double* partial, int* blocks);
+int spmv_resid_pair_blocks(cal_ctx* c);
 hipError_t launch_spmv_resid(const SpmvArgs& a, const double* xi, double lr, double li, int64_t nrows,
                              double* partial, int blocks, hipStream_t st);
 

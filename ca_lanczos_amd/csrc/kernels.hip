@@ -163,6 +163,13 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
+// fixed-order butterfly sum over the 64 lanes of a wave
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = v + __shfl_xor(v, off, 64);
+    return v;
+}
+
 template <int MODE, int MAXLEN>
 __global__ __launch_bounds__(256) void k_spmv_pat(PatArgs a) {
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -389,6 +396,89 @@ __global__ __launch_bounds__(256) void k_spmv_pair(PatArgs a, const uint16_t* __
     }
 }
 
+// Ritz residual partials ||A x - l x||^2 and ||l x||^2 for a real Ritz value
+// l (compute_ritz_rnorm, ca_lanczos.m:88-97) on the canonical pair patterns:
+// the products and their order are k_spmv_pair's MODE 1 (y = A x - l x),
+// nothing is stored, and each block leaves its two sums entry-major in
+// partial[e * gridDim.x + block] (e = 0 residual, 1 scale).
+template <int MAXLEN>
+__global__ __launch_bounds__(256) void k_spmv_pair_resid(PatArgs a, const uint16_t* __restrict__ ppat,
+                                                        const int* __restrict__ ppoff,
+                                                        const double2* __restrict__ ppval,
+                                                        double* __restrict__ partial) {
+    extern __shared__ __attribute__((aligned(16))) double lds_pair[];
+    double2* s_pv = reinterpret_cast<double2*>(lds_pair);
+    int* s_poff = reinterpret_cast<int*>(s_pv + a.npent);
+    __shared__ double ws[2][4];
+    const int tid = threadIdx.x;
+    const int64_t npairs = (a.n + 1) >> 1;
+    const int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 256 + tid;
+    const int64_t tcl = t < npairs ? t : npairs - 1;
+    const int id = ppat[tcl];
+    const int64_t r0 = 2 * tcl;
+    double2 xc[MAXLEN];
+#pragma unroll
+    for (int e = 0; e < MAXLEN; ++e) {
+        int64_t ad = r0 + a.pslot[e];
+        ad = ad < a.xlo ? a.xlo : (ad > a.xhi - 2 ? a.xhi - 2 : ad);
+        xc[e] = ld16(a.x + ad);
+    }
+    const double2 xs = ld16(a.x + (r0 < a.xhi - 2 ? r0 : a.xhi - 2));
+    for (int i = tid; i < a.npent; i += 256) {
+        s_pv[i] = ppval[i];
+        s_poff[i] = ppoff[i];
+    }
+    __syncthreads();
+    double num = 0.0, den = 0.0;
+    if (t < npairs) {
+        if (id != kPairSplit) {
+            const int base = id * MAXLEN;
+            double y0 = 0.0, y1 = 0.0;
+#pragma unroll
+            for (int e = 0; e < MAXLEN; ++e) {
+                const int code = s_poff[base + e];
+                const double2 v = s_pv[base + e];
+                const double t0 = v.x * xc[e].x, t1 = v.y * xc[e].y;
+                double a0 = y0 + t0, a1 = y1 + t1;
+                asm volatile("" : "+v"(a0), "+v"(a1));
+                y0 = (code & 1) ? a0 : y0;
+                y1 = (code & 2) ? a1 : y1;
+            }
+            const double u0 = a.shift * xs.x, u1 = a.shift * xs.y;
+            y0 = y0 - u0;
+            y1 = y1 - u1;
+            num = y0 * y0 + y1 * y1;
+            den = u0 * u0 + u1 * u1;
+        } else {  // split pair: each row from the row tables
+            for (int k = 0; k < 2 && r0 + k < a.n; ++k) {
+                const int64_t rr = r0 + k;
+                const int2 pi = a.pinfo[a.pat[rr]];
+                double sum = 0.0;
+                for (int e = 0; e < pi.y; ++e) {
+                    const double tv = a.pval[pi.x + e] * a.x[rr + a.pdelta[pi.x + e]];
+                    sum = sum + tv;
+                }
+                const double u = a.shift * a.x[rr];
+                const double y = sum - u;
+                num = num + y * y;
+                den = den + u * u;
+            }
+        }
+    }
+    num = wave_sum(num);
+    den = wave_sum(den);
+    const int lane = tid & 63, wave = tid >> 6;
+    if (lane == 0) {
+        ws[0][wave] = num;
+        ws[1][wave] = den;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        partial[blockIdx.x] = ((ws[0][0] + ws[0][1]) + ws[0][2]) + ws[0][3];
+        partial[gridDim.x + blockIdx.x] = ((ws[1][0] + ws[1][1]) + ws[1][2]) + ws[1][3];
+    }
+}
+
 constexpr size_t kPatLdsMax = 64 * 1024;
 
 // the pair kernel needs 16-B aligned columns, rows <= 8 entries and an LDS-sized pair table
@@ -450,6 +540,36 @@ static hipError_t launch_pat_mode(const PatArgs& a, hipStream_t st) {
         case 16: hipLaunchKernelGGL((k_spmv_pat<MODE, 16>), g, b, 0, st, a); break;
         default: hipLaunchKernelGGL((k_spmv_pat<MODE, 32>), g, b, 0, st, a); break;
     }
+    return hipGetLastError();
+}
+
+// blocks of the pair residual launch (0: the pair path does not apply)
+int spmv_pair_resid_blocks(const PatArgs& a) {
+    if (!spmv_pat_pair_path(a) || !a.pcanon || a.gap != 0) return 0;
+    return (int)(((a.n + 1) / 2 + 255) / 256);
+}
+
+hipError_t launch_spmv_pair_resid(const PatArgs& a, double lr, double* partial, hipStream_t st) {
+    PatArgs b = a;
+    b.shift = lr;
+    const int blocks = spmv_pair_resid_blocks(b);
+    if (blocks <= 0) return hipErrorInvalidValue;
+    const size_t lds = (size_t)b.npent * 20 + 16;
+    dim3 g(blocks), bl(256);
+#define CAL_PRR(ML) \
+    hipLaunchKernelGGL((k_spmv_pair_resid<ML>), g, bl, lds, st, b, b.ppat, b.ppoff, b.ppval, partial)
+    switch (b.pmaxlen) {
+        case 1: CAL_PRR(1); break;
+        case 2: CAL_PRR(2); break;
+        case 3: CAL_PRR(3); break;
+        case 4: CAL_PRR(4); break;
+        case 5: CAL_PRR(5); break;
+        case 6: CAL_PRR(6); break;
+        case 7: CAL_PRR(7); break;
+        case 8: CAL_PRR(8); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef CAL_PRR
     return hipGetLastError();
 }
 
@@ -1213,11 +1333,6 @@ hipError_t launch_rowgram(const ColList& P, int nt, bool has_extra, int64_t n, i
 // --------------------------------------------------------------------------
 // fixed-order partial reduction and small vector kernels
 // --------------------------------------------------------------------------
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = v + __shfl_xor(v, off, 64);
-    return v;
-}
 
 // One block per entry: partials are entry-major (part[e*nparts + p]), so the
 // 256 threads read one contiguous run; fixed-order strided sums, then a fixed

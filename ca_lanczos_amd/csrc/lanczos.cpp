@@ -338,14 +338,26 @@ static int ritz_diagnostics(cal_ctx* c, LanczosState& L) {
     PanelOut X = panel_out(work_col(c, 0) + c->A.lpad, ld, sk);
     CAL_TRY(apply_host(c, n, Qp, V.data(), sk, &X, nullptr, 0, nullptr));
     // ||A x - l x|| / ||l x|| per Ritz pair: fused SpMV + residual partials
-    const int nb = 256;
-    CAL_TRY(ensure_partial(c, (size_t)nb * 2 * sk));
+    // (real Ritz values on the pair patterns; complex pairs and CSR matrices
+    // on the row kernel)
+    const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (n + 255) / 256));
+    const int64_t pstride = 2 * (int64_t)std::max(nb, spmv_resid_pair_blocks(c));
+    CAL_TRY(ensure_partial(c, (size_t)pstride * sk));
     CAL_TRY(ensure_red(c, 2 * sk));
     for (int i = 0; i < sk; ++i) {
         const RitzPair& p = pairs[i];
         double* xr = work_col(c, p.cr) + c->A.lpad;
         double* xi = p.ci >= 0 ? work_col(c, p.ci) + c->A.lpad : nullptr;
+        double* part = c->d_partial + (size_t)i * pstride;
         CAL_TRY(halo_exchange(c, xr));
+        if (!xi) {
+            int nbk = 0;
+            CAL_TRY(spmv_resid_pair_dev(c, xr, p.lr, part, &nbk));
+            if (nbk > 0) {
+                CAL_HIP(c, launch_reduce(part, nbk, 2, c->d_red + 2 * i, c->stream));
+                continue;
+            }
+        }
         if (xi) CAL_TRY(halo_exchange(c, xi));
         SpmvArgs a{};
         a.rowptr = c->A.rowptr + c->A.ext_off;  // local rows of a stored slab
@@ -353,9 +365,9 @@ static int ritz_diagnostics(cal_ctx* c, LanczosState& L) {
         a.val = c->A.val;
         a.x = xr;
         const int t = timer_begin(c, 3);
-        CAL_HIP(c, launch_spmv_resid(a, xi, p.lr, p.li, n, c->d_partial + (size_t)i * nb * 2, nb, c->stream));
+        CAL_HIP(c, launch_spmv_resid(a, xi, p.lr, p.li, n, part, nb, c->stream));
         timer_end(c, t);
-        CAL_HIP(c, launch_reduce(c->d_partial + (size_t)i * nb * 2, nb, 2, c->d_red + 2 * i, c->stream));
+        CAL_HIP(c, launch_reduce(part, nb, 2, c->d_red + 2 * i, c->stream));
     }
     CAL_TRY(allreduce_sum(c, c->d_red, 2 * sk));
     CAL_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, 2 * sk * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -833,17 +845,23 @@ namespace {
 // ||A x - l x|| / ||l x|| of one device vector (ld layout, lpad origin)
 int rel_residual(cal_ctx* c, double* x, double l, double* out) {
     const int64_t n = c->A.n_local;
-    const int nb = 256;
-    CAL_TRY(ensure_partial(c, (size_t)nb * 2));
+    const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (n + 255) / 256));
+    CAL_TRY(ensure_partial(c, (size_t)2 * std::max(nb, spmv_resid_pair_blocks(c))));
     CAL_TRY(ensure_red(c, 2));
     CAL_TRY(halo_exchange(c, x));
-    SpmvArgs a{};
-    a.rowptr = c->A.rowptr + c->A.ext_off;  // local rows of a stored slab
-    a.col = c->A.col;
-    a.val = c->A.val;
-    a.x = x;
-    CAL_HIP(c, launch_spmv_resid(a, nullptr, l, 0.0, n, c->d_partial, nb, c->stream));
-    CAL_HIP(c, launch_reduce(c->d_partial, nb, 2, c->d_red, c->stream));
+    int nbk = 0;
+    CAL_TRY(spmv_resid_pair_dev(c, x, l, c->d_partial, &nbk));
+    if (nbk > 0) {
+        CAL_HIP(c, launch_reduce(c->d_partial, nbk, 2, c->d_red, c->stream));
+    } else {
+        SpmvArgs a{};
+        a.rowptr = c->A.rowptr + c->A.ext_off;  // local rows of a stored slab
+        a.col = c->A.col;
+        a.val = c->A.val;
+        a.x = x;
+        CAL_HIP(c, launch_spmv_resid(a, nullptr, l, 0.0, n, c->d_partial, nb, c->stream));
+        CAL_HIP(c, launch_reduce(c->d_partial, nb, 2, c->d_red, c->stream));
+    }
     CAL_TRY(allreduce_sum(c, c->d_red, 2));
     CAL_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     CAL_HIP(c, hipStreamSynchronize(c->stream));

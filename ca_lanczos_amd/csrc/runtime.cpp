@@ -463,6 +463,28 @@ int spmv_range(cal_ctx* c, int64_t o, int64_t len, const double* x, double* y, i
     return 0;
 }
 
+int spmv_resid_pair_blocks(cal_ctx* c) {
+    const DevMatrix& A = c->A;
+    if (!c->has_A || !A.use_pat || !A.use_pair) return 0;
+    // alignment is that of the work columns (16-B aligned origins)
+    const PatArgs p = pat_args(A, A.ext_off, A.n_local, nullptr, nullptr, 1, 0.0, 0.0, nullptr);
+    return spmv_pair_resid_blocks(p);
+}
+
+int spmv_resid_pair_dev(cal_ctx* c, const double* x, double lr, double* partial, int* blocks) {
+    const DevMatrix& A = c->A;
+    *blocks = 0;
+    if (!c->has_A || !A.use_pat || !A.use_pair) return 0;
+    const PatArgs p = pat_args(A, A.ext_off, A.n_local, x, nullptr, 1, lr, 0.0, nullptr);
+    const int nb = spmv_pair_resid_blocks(p);
+    if (nb <= 0) return 0;
+    const int t = timer_begin(c, 3);
+    CAL_HIP(c, launch_spmv_pair_resid(p, lr, partial, c->stream));
+    timer_end(c, t);
+    *blocks = nb;
+    return 0;
+}
+
 // Two stored-row ranges [o1, o1 + len1) and [o2, o2 + len2) in one launch
 // (the pair kernel skips the gap; the row kernels take two launches).
 int spmv_range2(cal_ctx* c, int64_t o1, int64_t len1, int64_t o2, int64_t len2, const double* x, double* y, int mode,
