@@ -76,12 +76,17 @@ int ensure_pub(cal_ctx* c) {
 
 int ensure_work(cal_ctx* c, int cols, int64_t ld) {
     if (cols <= c->work_cols && ld == c->work_ld) return 0;
+    // grow by half again (the Ritz diagnostics ask for s more columns every
+    // outer iteration; each reallocation frees, i.e. synchronises, and zeroes)
+    int alloc = cols;
+    if (ld == c->work_ld) alloc = std::max(cols, c->work_cols + c->work_cols / 2);
+    alloc = (alloc + 15) & ~15;
     if (c->d_work) CAL_HIP(c, hipFree(c->d_work));
     c->d_work = nullptr;
     c->work_cols = 0;
-    CAL_HIP(c, hipMalloc((void**)&c->d_work, (size_t)cols * ld * sizeof(double)));
-    CAL_HIP(c, hipMemsetAsync(c->d_work, 0, (size_t)cols * ld * sizeof(double), c->stream));
-    c->work_cols = cols;
+    CAL_HIP(c, hipMalloc((void**)&c->d_work, (size_t)alloc * ld * sizeof(double)));
+    CAL_HIP(c, hipMemsetAsync(c->d_work, 0, (size_t)alloc * ld * sizeof(double), c->stream));
+    c->work_cols = alloc;
     c->work_ld = ld;
     return 0;
 }
