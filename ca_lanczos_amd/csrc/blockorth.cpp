@@ -117,7 +117,7 @@ static int apply_dev(cal_ctx* c, int64_t n, const Panel& P, const double* dM, in
     int max_nty = 8192 / (wpp * 16);
     if (wp < 1 || wy < 1 || max_nty < 1) return set_error(c, CAL_ERR_ARG, "apply: panel shape out of range");
     max_nty = max_nty >= 8 ? 8 : (max_nty >= 4 ? 4 : (max_nty >= 2 ? 2 : 1));
-    const int cw_max = 16 * max_nty;
+    const int cw_max = std::max(16 * max_nty, apply_rows_max_wy(wp));  // store only
     for (int y0 = 0; y0 < wy; y0 += cw_max) {
         const int cw = std::min(cw_max, wy - y0);
         const ApplyPlan pl = apply_plan(wp, cw, n, false, 0);
@@ -139,9 +139,10 @@ int apply_host(cal_ctx* c, int64_t n, const Panel& P, const double* M, int wy, c
     int max_nty = 8192 / (wpp * 16);
     if (max_nty < 1) return set_error(c, CAL_ERR_UNSUPPORTED, "apply: panel wider than 512 columns");
     max_nty = max_nty >= 8 ? 8 : (max_nty >= 4 ? 4 : (max_nty >= 2 ? 2 : 1));
-    const int cw_max = 16 * max_nty;
-    CAL_TRY(stage_small(c, M, (size_t)wp * wy));
     const bool want = gram || gramp;
+    // store-only chunks as wide as the row-parallel apply takes
+    const int cw_max = (!want && Y) ? std::max(16 * max_nty, apply_rows_max_wy(wp)) : 16 * max_nty;
+    CAL_TRY(stage_small(c, M, (size_t)wp * wy));
     ApplyPlan last{};
     for (int y0 = 0; y0 < wy; y0 += cw_max) {
         const int cw = std::min(cw_max, wy - y0);

@@ -187,6 +187,8 @@ struct ApplyPlan {
     int64_t entries;  // per-block partial entries (gram + gramp)
 };
 ApplyPlan apply_plan(int wp, int wy, int64_t n, bool gram, int wq);
+int apply_rows_max_wy(int wp);  // widest output chunk of the row-parallel store-only apply
+bool apply_rows_ok(int wp, int wy);
 hipError_t launch_apply(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y, bool store,
                         int wq, int64_t n, const ApplyPlan& pl, double* partial, hipStream_t st);
 hipError_t launch_reduce(const double* partial, int nparts, int64_t nent, double* out, hipStream_t st);

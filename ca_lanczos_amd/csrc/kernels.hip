@@ -22,6 +22,8 @@
 //   k_reduce        fixed-order sum of block partials.
 //   k_dot, k_axpy_sub(_dev), k_div(_sqrt), k_gather, k_spmv_resid,
 //   k_form_projM, k_abs_rowsum: small vector kernels.
+#include <cstdlib>
+
 #include "cal_internal.hpp"
 
 namespace cal {
@@ -968,11 +970,25 @@ __global__ __launch_bounds__(256) void k_apply_rows(Panel P, const double* __res
     }
 }
 
+// the row-parallel store-only apply: <= 16 outputs for any panel up to 256
+// columns, wider output chunks (32, 64) while M fits 64 KB of LDS
+int apply_rows_max_wy(int wp) {
+    if (wp < 1 || wp > 256) return 0;
+    static const bool wide = [] {  // CAL_APPLY_ROWS_WIDE=0: <= 16 outputs (A/B)
+        const char* e = std::getenv("CAL_APPLY_ROWS_WIDE");
+        return !e || std::atoi(e) != 0;
+    }();
+    int wy = 16;
+    while (wide && wy < 64 && (size_t)wp * (2 * wy) * sizeof(double) <= 65536) wy *= 2;
+    return wy;
+}
+bool apply_rows_ok(int wp, int wy) { return wy >= 1 && wy <= apply_rows_max_wy(wp); }
+
 hipError_t launch_apply(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y, bool store,
                         int wq, int64_t n, const ApplyPlan& pl, double* partial, hipStream_t st) {
-    if (store && !pl.gram && !pl.gramp && wy <= 16 && wp <= 256) {
+    if (store && !pl.gram && !pl.gramp && apply_rows_ok(wp, wy)) {
         const dim3 g((unsigned)((n + 255) / 256)), b(256);
-        const int WY = wy <= 1 ? 1 : (wy <= 2 ? 2 : (wy <= 4 ? 4 : (wy <= 8 ? 8 : 16)));
+        const int WY = wy <= 1 ? 1 : (wy <= 2 ? 2 : (wy <= 4 ? 4 : (wy <= 8 ? 8 : (wy <= 16 ? 16 : (wy <= 32 ? 32 : 64)))));
         const size_t sh = sizeof(double) * (size_t)wp * WY;
         if (n <= 0) return hipSuccess;
         switch (WY) {
@@ -980,7 +996,9 @@ hipError_t launch_apply(const Panel& P, const double* dM, int wp, int wy, const 
             case 2: hipLaunchKernelGGL((k_apply_rows<2>), g, b, sh, st, P, dM, wp, wy, Y, n); break;
             case 4: hipLaunchKernelGGL((k_apply_rows<4>), g, b, sh, st, P, dM, wp, wy, Y, n); break;
             case 8: hipLaunchKernelGGL((k_apply_rows<8>), g, b, sh, st, P, dM, wp, wy, Y, n); break;
-            default: hipLaunchKernelGGL((k_apply_rows<16>), g, b, sh, st, P, dM, wp, wy, Y, n); break;
+            case 16: hipLaunchKernelGGL((k_apply_rows<16>), g, b, sh, st, P, dM, wp, wy, Y, n); break;
+            case 32: hipLaunchKernelGGL((k_apply_rows<32>), g, b, sh, st, P, dM, wp, wy, Y, n); break;
+            default: hipLaunchKernelGGL((k_apply_rows<64>), g, b, sh, st, P, dM, wp, wy, Y, n); break;
         }
         return hipGetLastError();
     }
