@@ -344,6 +344,9 @@ static int ritz_diagnostics(cal_ctx* c, LanczosState& L) {
     const int64_t pstride = 2 * (int64_t)std::max(nb, spmv_resid_pair_blocks(c));
     CAL_TRY(ensure_partial(c, (size_t)pstride * sk));
     CAL_TRY(ensure_red(c, 2 * sk));
+    // partial blocks per pair; when every pair fills its stride the sums are
+    // reduced in one launch (entry 2i+e at (2i+e) * pstride/2)
+    std::vector<int> nparts(sk, 0);
     for (int i = 0; i < sk; ++i) {
         const RitzPair& p = pairs[i];
         double* xr = work_col(c, p.cr) + c->A.lpad;
@@ -354,7 +357,7 @@ static int ritz_diagnostics(cal_ctx* c, LanczosState& L) {
             int nbk = 0;
             CAL_TRY(spmv_resid_pair_dev(c, xr, p.lr, part, &nbk));
             if (nbk > 0) {
-                CAL_HIP(c, launch_reduce(part, nbk, 2, c->d_red + 2 * i, c->stream));
+                nparts[i] = nbk;
                 continue;
             }
         }
@@ -367,7 +370,13 @@ static int ritz_diagnostics(cal_ctx* c, LanczosState& L) {
         const int t = timer_begin(c, 3);
         CAL_HIP(c, launch_spmv_resid(a, xi, p.lr, p.li, n, part, nb, c->stream));
         timer_end(c, t);
-        CAL_HIP(c, launch_reduce(part, nb, 2, c->d_red + 2 * i, c->stream));
+        nparts[i] = nb;
+    }
+    if (std::all_of(nparts.begin(), nparts.end(), [&](int v) { return 2 * (int64_t)v == pstride; })) {
+        CAL_HIP(c, launch_reduce(c->d_partial, (int)(pstride / 2), 2 * sk, c->d_red, c->stream));
+    } else {
+        for (int i = 0; i < sk; ++i)
+            CAL_HIP(c, launch_reduce(c->d_partial + (size_t)i * pstride, nparts[i], 2, c->d_red + 2 * i, c->stream));
     }
     CAL_TRY(allreduce_sum(c, c->d_red, 2 * sk));
     CAL_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, 2 * sk * sizeof(double), hipMemcpyDeviceToHost, c->stream));
