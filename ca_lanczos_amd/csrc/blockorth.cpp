@@ -693,7 +693,7 @@ static bool async_ok(int nb, const int* widths, int m) {
 
 // Gram A'B (A <= 128 columns, B <= 16) reduced (and all-reduced) into d_dst
 // (ld *ldc) and copied to h_dst; nothing waits.
-static int gram_async(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* d_dst, double* h_dst, int* ldc) {
+int gram_async(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* d_dst, double* h_dst, int* ldc) {
     const GramPlan pl = gram_plan(A.total, B.total, n);
     CAL_TRY(ensure_partial(c, (size_t)pl.blocks * pl.entries));
     const int t = timer_begin(c, 1);

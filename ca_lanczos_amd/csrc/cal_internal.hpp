@@ -234,6 +234,9 @@ hipError_t launch_div_sqrt(double* y, const double* x, const double* nn, int64_t
 hipError_t launch_abs_rowsum(const int* rowptr, const double* val, int64_t n, double* y, hipStream_t st);
 hipError_t launch_gather(double* dst, const double* src, const int* idx, int64_t cnt, hipStream_t st);
 // fused SpMV + Ritz residual partials for one Ritz pair (diagnostics)
+// Gram A'B (A <= 128 columns, B <= 16) reduced, all-reduced and copied to
+// h_dst (ld *ldc) asynchronously: valid after the stream's next wait
+int gram_async(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* d_dst, double* h_dst, int* ldc);
 int spmv_pair_resid_blocks(const PatArgs& a);
 hipError_t launch_spmv_pair_resid(const PatArgs& a, double lr, double* partial, hipStream_t st);
 // Ritz residual partials of a real Ritz value on the pair patterns (local

@@ -311,6 +311,21 @@ static void matlab_sort_desc(std::vector<RitzPair>& v, bool cplx) {
 static int ritz_diagnostics(cal_ctx* c, LanczosState& L) {
     const int s = L.s, k = L.k, sk = s * k;
     const int64_t n = c->A.n_local, ld = c->A.ld;
+    // the orthogonality error's Gram (compute_orth_err, ca_lanczos.m:99-107)
+    // runs on the GPU while the host solves eig(T): enqueued here, read after
+    // the residuals' wait below
+    const int jq = sk + 1;
+    const int wa = jq > s + 1 ? jq - s - 1 : s + 1;
+    Panel OA = panel(), OB = panel();
+    panel_add(OA, L.col(0), ld, wa);
+    panel_add(OB, L.col(jq > s + 1 ? wa : 0), ld, s + 1);
+    constexpr size_t kOrthRegion = 8192 + 7 * 8192;  // above the projections' async regions
+    const bool oe_async = wa <= 128;
+    int oe_ld = 0;
+    if (oe_async) {
+        CAL_TRY(ensure_red(c, kOrthRegion + 8192));
+        CAL_TRY(gram_async(c, n, OA, OB, c->d_red + kOrthRegion, c->h_red + kOrthRegion, &oe_ld));
+    }
     // eig(T(1:sk,1:sk)) (ca_lanczos.m:229)
     std::vector<double> Tk((size_t)sk * sk), wr(sk), wi(sk), V((size_t)sk * sk);
     for (int j = 0; j < sk; ++j)
@@ -386,21 +401,18 @@ static int ritz_diagnostics(cal_ctx* c, LanczosState& L) {
     for (int i = 0; i < sk; ++i) rn[i] = std::sqrt(c->h_red[2 * i]) / std::sqrt(c->h_red[2 * i + 1]);
     L.rn.push_back(rn);
     // orthogonality error (compute_orth_err, ca_lanczos.m:99-107)
-    const int j = sk + 1;
+    std::vector<double> G((size_t)wa * (s + 1));
+    if (oe_async) {
+        const double* h = c->h_red + kOrthRegion;  // the stream is synchronised above
+        for (int jj = 0; jj <= s; ++jj)
+            for (int ii = 0; ii < wa; ++ii) G[ii + (size_t)jj * wa] = h[ii + (size_t)jj * oe_ld];
+    } else {
+        CAL_TRY(gram_host(c, n, OA, OB, G.data()));
+    }
     double oe = 0.0;
-    if (j > s + 1) {
-        const int wa = j - s - 1;
-        Panel A1 = panel(), B1 = panel();
-        panel_add(A1, L.col(0), ld, wa);
-        panel_add(B1, L.col(wa), ld, s + 1);
-        std::vector<double> G((size_t)wa * (s + 1));
-        CAL_TRY(gram_host(c, n, A1, B1, G.data()));
+    if (jq > s + 1) {
         for (double g : G) oe = std::max(oe, std::fabs(g));
     } else {
-        Panel A1 = panel();
-        panel_add(A1, L.col(0), ld, s + 1);
-        std::vector<double> G((size_t)(s + 1) * (s + 1));
-        CAL_TRY(gram_host(c, n, A1, A1, G.data()));
         for (int jj = 0; jj <= s; ++jj)
             for (int ii = 0; ii <= s; ++ii)
                 oe = std::max(oe, std::fabs(G[ii + (size_t)jj * (s + 1)] - (ii == jj ? 1.0 : 0.0)));
