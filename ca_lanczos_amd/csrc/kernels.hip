@@ -11,14 +11,19 @@
 //                   (bit-exact), fused Newton shift (matrix_powers_newton.m:31-47).
 //   k_spmv_pat_lds, k_spmv_pair
 //                   row-pattern SpMV (lossless pattern table, one / two rows
-//                   per lane), same arithmetic, same shift epilogue.
+//                   per lane), same arithmetic, same shift epilogue; the pair
+//                   kernel also takes two row ranges (the split matrix powers).
+//   k_spmv_pair_resid
+//                   Ritz residual sums ||A x - l x||^2, ||l x||^2 on the pair
+//                   patterns (compute_ritz_rnorm), nothing stored.
 //   k_rowapply      the hot block-orthogonalisation sweeps (s <= 8): Gram
 //                   tiles through LDS onto v_mfma_f64_16x16x4f64, the
 //                   coefficient apply in registers, the chained pass B.
 //   k_orth_coef     the s x s algebra between the sweeps; publishes R / RY.
 //   k_gram, k_apply tall-skinny C = A^T B / Y = P M (+ Grams) on MFMA tiles
 //                   for the generic widths ('full', restarts).
-//   k_apply_rows    row-parallel store-only Y = P M (wide panels).
+//   k_apply_rows    row-parallel store-only Y = P M (wide panels, up to 64
+//                   outputs per launch).
 //   k_reduce        fixed-order sum of block partials.
 //   k_dot, k_axpy_sub(_dev), k_div(_sqrt), k_gather, k_spmv_resid,
 //   k_form_projM, k_abs_rowsum: small vector kernels.
