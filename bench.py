@@ -40,7 +40,8 @@ MFMA_F64_PEAK_TF = 78.6  # MI355X FP64 matrix peak (AMD spec sheet; the guide li
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")),
+                   help="ranks (one per GPU); without a launcher bench.py starts torch.distributed.run itself")
     p.add_argument("--steps", type=int, default=15)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--workload", default="lap3d_215", help="lap2d_N | lap3d_N | circuit_N")
@@ -117,6 +118,32 @@ class Workload:
             return self._A
         rowptr, col, val = self.rows(0, self.n)
         return sp.csr_matrix((val, col.astype(np.int32), rowptr), shape=(self.n, self.n))
+
+
+def host_info():
+    """CPU model (lscpu's 'Model name' from /proc/cpuinfo), the host cores this
+    process may use and the ROCm release of the image (BASELINE.md's line)."""
+    model = "?"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    rocm = "?"
+    for p in ("/opt/rocm/.info/version", "/opt/rocm/.info/version-dev"):
+        try:
+            rocm = open(p).read().strip()
+            break
+        except OSError:
+            pass
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        cores = os.cpu_count()
+    import torch
+    return {"cpu_model": model, "cpu_cores_visible": cores, "rocm": rocm, "torch": torch.__version__}
 
 
 def _blas_threads():
@@ -311,8 +338,40 @@ def emit(line):
         os.write(_JSON_FD, data)
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` without a launcher: start N ranks (one process per
+    GPU) under torch.distributed.run as a CHILD process -- this process has
+    not touched the GPU and is not replaced -- relay the rank-0 JSON line and
+    return the child's exit code."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    proc = subprocess.run(cmd, env=env, stdout=subprocess.PIPE)
+    sys.stdout.write(proc.stdout.decode())
+    sys.stdout.flush()
+    return proc.returncode
+
+
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        return launch_ranks(args)
+    if world_env is not None and int(world_env) != args.gpus:
+        sys.stderr.write("bench.py: --gpus %d but WORLD_SIZE=%s\n" % (args.gpus, world_env))
+        return 2
     _quiet_stdout()
     if args.driver == "irl":
         return main_irl(args)
@@ -374,6 +433,7 @@ def main():
     fmt, npat, nent = ctx.spmv_format()
     npairpat, npent, nsplit = ctx.spmv_pair_info()
     mpk = ctx.mpk_info()
+    sched = ctx.mpk_schedule()  # what the last timed step's matrix powers actually did
     apply_avg_ms = apply_ms / max(apply_cnt, 1)
     gram_avg_ms = gram_ms / max(gram_cnt, 1)
     csr_spmv = None
@@ -442,17 +502,13 @@ def main():
         "config": {"workload": wl.desc % (n, nnz_total),
                    "s": s, "basis": args.basis, "orth": args.orth, "parallelism": "row-slab x%d" % world,
                    "comm": (args.comm if world > 1 else "none"),
-                   "halo": ("CA matrix powers: one %d-band deep exchange per outer iteration (band %d rows)%s"
-                            % (s, mpk["band_l"],
-                               ", overlapped with the interior powers" if args.comm == "rccl"
-                               and os.environ.get("CAL_MPK_OVERLAP", "1") != "0" else "")
-                            if mpk["depth"] > 1 and s <= mpk["depth"]
-                            else "one exchange per SpMV") if world > 1 else "none"},
+                   "halo": ("%s (CA matrix powers depth %d, band %d rows)"
+                            % (ctx.MPK_SCHEDULES.get(sched, "?"), mpk["depth"], mpk["band_l"]))
+                           if world > 1 else "none"},
         "spmv_format": ("%s (%d row patterns, %d entries; %d pair patterns, %d entries, %d split pairs)"
                         % (fmt, npat, nent, npairpat, npent, nsplit)) if fmt == "pattern" else fmt,
         "spmv_gbps": spmv_gbps,
         "spmv_avg_us": spmv_avg_ms * 1e3,
-        "spmv_csr_equiv_gbps": b_csr / (spmv_avg_ms * 1e-3) / 1e9,
         "reorth_passes": "%d/%d" % (n_reorth, K),
         "csr_outer_algorithmic_GB": b_outer / 1e9,
         "kernel_ms_per_step": per_step,
@@ -479,6 +535,7 @@ def main():
                                    "gbps": b_csr / (csr_spmv[0] * 1e-3) / 1e9, "bytes_per_launch": b_csr}
     if host_rt_ms is not None:
         line["spmv_host_roundtrip_ms"] = host_rt_ms
+    line["host"] = host_info()
     if world == 1 and args.orth == "local":
         line["diagnostics_on"] = diagnostics_run(ctx, r_full[r0:r1], s, args)
     if world == 1 and not args.no_cpu_baseline:
@@ -594,6 +651,7 @@ def main_irl(args):
                      "kernel": "SpMV (%s) inside the IRL" % fmt, "bytes_per_launch": b_spmv,
                      "avg_launch_us": spmv_avg_ms * 1e3},
     }
+    line["host"] = host_info()
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_irl(wl, s, ml, nw)
     emit(line)
@@ -602,4 +660,4 @@ def main_irl(args):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

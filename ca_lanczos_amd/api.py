@@ -26,7 +26,7 @@ class Context:
     the device-resident CA-Lanczos state."""
 
     def __init__(self, device: int | None = None, spmv_format: str | None = None, orth_coef: str | None = None,
-                 mpk_depth: int | None = None):
+                 mpk_depth: int | None = None, normalize: str | None = None):
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", "0"))
         h = ctypes.c_void_p()
@@ -43,6 +43,19 @@ class Context:
             self.set_orth_coef(orth_coef)
         if mpk_depth is not None:
             self.set_mpk_depth(mpk_depth)
+        if normalize or os.environ.get("CAL_NORMALIZE"):
+            self.set_normalize(normalize or os.environ["CAL_NORMALIZE"])
+
+    def set_normalize(self, kind: str):
+        """normalize (tsqr.m) backend: "auto", "tsqr" (Householder TSQR
+        everywhere) or "cholqr2" (cal_set_normalize)."""
+        check(self.h, lib.cal_set_normalize(self.h, kind.encode()), "normalize backend")
+        return self
+
+    def normalize_backend(self):
+        v = ctypes.c_int()
+        check(self.h, lib.cal_get_normalize(self.h, ctypes.byref(v)))
+        return ("auto", "tsqr", "cholqr2")[v.value]
 
     def set_mpk_depth(self, depth: int):
         """Ghost depth of the distributed CA matrix-powers kernel (next
@@ -55,6 +68,16 @@ class Context:
         d, bl, br, nr = ctypes.c_int(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         check(self.h, lib.cal_mpk_info(self.h, ctypes.byref(d), ctypes.byref(bl), ctypes.byref(br), ctypes.byref(nr)))
         return dict(depth=d.value, band_l=bl.value, band_r=br.value, n_rows=nr.value)
+
+    MPK_SCHEDULES = {-1: "none", 0: "one exchange per SpMV", 1: "one deep exchange",
+                     2: "one deep exchange overlapped with the interior powers",
+                     3: "split schedule, synchronous exchange"}
+
+    def mpk_schedule(self):
+        """Schedule the last matrix-powers call took (cal_mpk_schedule)."""
+        v = ctypes.c_int()
+        check(self.h, lib.cal_mpk_schedule(self.h, ctypes.byref(v)))
+        return v.value
 
     def set_orth_coef(self, where: str):
         """Run the block-orthogonalisation s x s algebra on the "device"

@@ -36,6 +36,17 @@ int download(cal_ctx* c, double* h, const double* d, int64_t dld, int64_t n, int
     return 0;
 }
 
+// marks a tier-1 call for its duration (normalize backend choice, use_tsqr)
+struct Tier1 {
+    cal_ctx* c;
+    explicit Tier1(cal_ctx* cc) : c(cc) {
+        if (c) c->tier1 = true;
+    }
+    ~Tier1() {
+        if (c) c->tier1 = false;
+    }
+};
+
 int check_ctx(cal_ctx* c, bool need_A) {
     if (!c) return CAL_ERR_ARG;
     hipSetDevice(c->device);
@@ -136,8 +147,10 @@ int cal_matrix_powers_newton(cal_ctx* c, const double* v, int s, const double* l
 }
 
 int cal_tsqr(cal_ctx* c, int64_t n, int m, const double* A, double* Q, double* R) {
+    Tier1 t1(c);
     CAL_TRY(check_ctx(c, false));
-    if (!A || !Q || !R || n < 1 || m < 1 || m > 16) return set_error(c, CAL_ERR_ARG, "tsqr: need 1 <= m <= 16");
+    if (!A || !Q || !R || m < 1 || n < m) return set_error(c, CAL_ERR_ARG, "tsqr: need an n x m A with n >= m >= 1");
+    if (!tsqr_ok(m)) return set_error(c, CAL_ERR_UNSUPPORTED, "tsqr: at most 32 columns on the device");
     const int64_t ld = ld_for(n);
     CAL_TRY(ensure_scratch(c, (size_t)2 * m * ld));
     double* dX = c->d_scratch;
@@ -145,16 +158,15 @@ int cal_tsqr(cal_ctx* c, int64_t n, int m, const double* A, double* Q, double* R
     CAL_TRY(upload(c, dX, ld, A, n, m));
     Panel X = panel();
     panel_add(X, dX, ld, m);
-    int rank = 0;
-    bool sh = false;
-    CAL_TRY(normalize_dev(c, n, X, panel_out(dQ, ld, m), R, 1.0e-8, &rank, &sh));
-    CAL_TRY(download(c, Q, dQ, ld, n, m));
-    return sh ? CAL_WARN_RANK_DEFICIENT : 0;
+    // Householder TSQR whatever the normalize setting: tsqr.m is qr(A,0)
+    CAL_TRY(tsqr_dev(c, n, X, nullptr, m, panel_out(dQ, ld, m), R));
+    return download(c, Q, dQ, ld, n, m);
 }
 
 int cal_normalize(cal_ctx* c, int64_t n, int m, const double* X, double tol, double* Q, double* R, int* rank) {
+    Tier1 t1(c);
     CAL_TRY(check_ctx(c, false));
-    if (!X || !Q || !R || n < 1 || m < 1 || m > 16) return set_error(c, CAL_ERR_ARG, "normalize: need 1 <= m <= 16");
+    if (!X || !Q || !R || n < 1 || m < 1 || m > 32) return set_error(c, CAL_ERR_ARG, "normalize: need 1 <= m <= 32");
     const int64_t ld = ld_for(n);
     CAL_TRY(ensure_scratch(c, (size_t)2 * m * ld));
     double* dX = c->d_scratch;
@@ -192,6 +204,7 @@ int cal_cholqr(cal_ctx* c, int64_t n, int m, const double* X, double* Q, double*
 
 int cal_project(cal_ctx* c, int64_t n, int nblocks, const double* const* Q, const int* widths, int m, const double* X,
                 int doreorth, double* Xout, double* const* R) {
+    Tier1 t1(c);
     CAL_TRY(check_ctx(c, false));
     if (nblocks < 0 || (nblocks > 0 && (!Q || !widths)) || !X || !Xout || n < 1 || m < 1 || m > 16)
         return set_error(c, CAL_ERR_ARG, "project: bad arguments");
@@ -221,6 +234,7 @@ int cal_project(cal_ctx* c, int64_t n, int nblocks, const double* const* Q, cons
 
 int cal_project_and_normalize(cal_ctx* c, int64_t n, int nblocks, const double* const* Q, const int* widths, int m,
                               const double* X, int doreorth, double* QZ, double* const* RZ, int* reorth, int* rank) {
+    Tier1 t1(c);
     CAL_TRY(check_ctx(c, false));
     if (nblocks < 0 || (nblocks > 0 && (!Q || !widths)) || !X || !QZ || n < 1 || m < 1 || m > 16)
         return set_error(c, CAL_ERR_ARG, "projectAndNormalize: bad arguments");

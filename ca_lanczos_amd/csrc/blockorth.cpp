@@ -503,7 +503,20 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
 int normalize_dev(cal_ctx* c, int64_t n, const Panel& X, const PanelOut& Qout, double* R, double tol, int* rank,
                   bool* shifted) {
     const int m = X.total;
-    if (m < 1 || m > 16) return set_error(c, CAL_ERR_ARG, "normalize: 1..16 columns supported");
+    if (use_tsqr(c, m, c->tier1)) {  // tsqr.m: Householder TSQR
+        CAL_TRY(tsqr_dev(c, n, X, nullptr, m, Qout, R));
+        if (shifted) *shifted = false;
+        if (rank) *rank = rank_from_R(m, R, tol);
+        return 0;
+    }
+    auto via_tsqr = [&]() -> int {
+        CAL_TRY(tsqr_dev(c, n, X, nullptr, m, Qout, R));
+        if (shifted) *shifted = false;
+        if (rank) *rank = rank_from_R(m, R, tol);
+        return 0;
+    };
+    if (m > 16 && tsqr_ok(m)) return via_tsqr();  // the CholQR kernels take <= 16 columns
+    if (m < 1 || m > 16) return set_error(c, CAL_ERR_ARG, "normalize: 1..32 columns supported");
     if (orth_device_ok(c, panel(), X)) {
         bool ro = false;
         const int st = orth_device(c, n, panel(), X, false, Qout, nullptr, R, &ro);
@@ -514,6 +527,9 @@ int normalize_dev(cal_ctx* c, int64_t n, const Panel& X, const PanelOut& Qout, d
             return 0;
         }
         c->orth_redone = true;
+        // the device Cholesky failed (kappa(X) > ~1e8): Householder TSQR gives
+        // the reference's R for any kappa ("cholqr2" keeps shifted CholQR3)
+        if (c->normalize_kind != 2) return via_tsqr();
     }
     std::vector<double> G((size_t)m * m), Mz((size_t)m * m, 0.0), Ctot;
     if (X.nseg <= kMaxSeg) {
@@ -523,6 +539,10 @@ int normalize_dev(cal_ctx* c, int64_t n, const Panel& X, const PanelOut& Qout, d
             for (int i = 0; i < m; ++i) G[i + (size_t)j * m] = G16[i + j * 16];
     } else {
         CAL_TRY(gram_host(c, n, X, X, G.data()));
+    }
+    if (c->normalize_kind != 2) {
+        std::vector<double> Rc((size_t)m * m);
+        if (!dense::chol_upper(m, G.data(), m, Rc.data(), m)) return via_tsqr();
     }
     for (int i = 0; i < m; ++i) Mz[i + (size_t)i * m] = 1.0;
     bool sh = false;

@@ -246,6 +246,36 @@ int spmv_resid_pair_blocks(cal_ctx* c);
 hipError_t launch_spmv_resid(const SpmvArgs& a, const double* xi, double lr, double li, int64_t nrows,
                              double* partial, int blocks, hipStream_t st);
 
+// ---- Householder TSQR (tsqr.hip / tsqr.cpp) ------------------------------
+constexpr int kTsqrMaxCols = 33;
+struct TsqrCols {
+    const double* p[kTsqrMaxCols];
+};
+struct TsqrQ {
+    double* p[32];
+};
+// One level of the TSQR tree.  Level 0 reads the panel (direct columns, or
+// Z = P M formed per row with M wp x m column-major); higher levels read the
+// stack of the level below: one m x m column-major block per tile (block
+// layout).  UP writes each tile's R as a block of `out`; DOWN reads the
+// tile's S block from `S` (null at the root: the sign fix) and writes Q rows
+// (level 0: TsqrQ columns; higher levels: `out` in block layout).
+struct TsqrLevelArgs {
+    int64_t rows = 0;
+    int m = 0;
+    int wp = 0;
+    const double* M = nullptr;
+    const double* in = nullptr;
+    double* out = nullptr;
+    const double* S = nullptr;
+};
+int tsqr_mm(int m);          // register tile width (8, 16, 32; 0: m > 32)
+int tsqr_tile_rows(int m);   // rows per tile (4096 / tsqr_mm)
+bool tsqr_form_ok(int wp, int m);
+// src: 0 stack, 1 direct columns, 2 formed
+hipError_t launch_tsqr(bool down, int src, const TsqrLevelArgs& a, const TsqrCols& P, const TsqrQ& Q,
+                       hipStream_t st);
+
 }  // namespace cal
 
 // Per-launch kernel timer (HIP events on the launching stream).
@@ -287,7 +317,12 @@ struct cal_ctx {
     std::vector<hipEvent_t> event_pool;
 
     int spmv_format = 0;  // 0 auto, 1 CSR, 2 row-pattern (applies at the next set_matrix)
-    int mpk_depth_req = 8;  // ghost depth of the distributed matrix-powers kernel (next set_matrix; 1 = off)
+    int mpk_depth_req = 8;
+    // schedule of the last powers_dev call (cal_mpk_schedule): 0 one halo
+    // exchange per SpMV, 1 one deep exchange, 2 deep exchange on the RCCL
+    // stream overlapped with the interior powers, 3 split schedule with a
+    // synchronous exchange; -1 none yet
+    int powers_schedule = -1;  // ghost depth of the distributed matrix-powers kernel (next set_matrix; 1 = off)
     bool orth_coef_device = true;  // block-orth s x s algebra on the device (blockorth.cpp)
     // set by lanczos_step: work to enqueue after a block orthogonalisation is
     // enqueued and before the host waits for its R (orth_device)
@@ -300,6 +335,14 @@ struct cal_ctx {
     double* h_pub = nullptr;
     double* d_pub = nullptr;
     unsigned long long pub_seq = 0;
+    // normalize (tsqr.m) backend: 0 "auto" (Householder TSQR for the tier-1
+    // calls, CholQR2 in the CA-Lanczos loop with TSQR when its Cholesky
+    // fails), 1 "tsqr" (Householder TSQR everywhere), 2 "cholqr2" (CholQR2
+    // everywhere, shifted CholQR3 when its Cholesky fails)
+    int normalize_kind = 0;
+    bool tier1 = false;  // inside a host-pointer (tier-1) entry point (api.cpp)
+    double* d_tsqr = nullptr;  // TSQR tree workspace
+    size_t tsqr_cap = 0;
 };
 
 // ---- helpers shared by the host-side translation units -----------------
@@ -399,5 +442,17 @@ int halo_exchange(cal_ctx* c, double* x);
 int spmv_dev(cal_ctx* c, const double* x, double* y, int mode, double shift, double im2,
              const double* xprev);
 int allreduce_sum(cal_ctx* c, double* d_buf, int64_t count);
+// d_recv[p * count + i] = rank p's d_send[i] (in rank order, every rank)
+int allgather(cal_ctx* c, const double* d_send, double* d_recv, int64_t count);
+
+// Householder TSQR of Z (tsqr.m:7-12): Z = W (direct, dM null, W.total = m)
+// or Z = W * M (dM: W.total x m column-major on the device, formed per row).
+// Q -> Qout (n x m), R -> host (m x m, diag >= 0, the reference's sign fix).
+// Multi-GPU: the tree's root is taken over all ranks (allgather + redundant
+// top levels).  Runs c->pre_wait before its one host wait.  m <= 32.
+int tsqr_dev(cal_ctx* c, int64_t n, const Panel& W, const double* dM, int m, const PanelOut& Qout, double* R);
+bool tsqr_ok(int m);
+// whether normalize / projectAndNormalize use TSQR here (tier1: a host-pointer call)
+bool use_tsqr(const cal_ctx* c, int m, bool tier1);
 
 }  // namespace cal

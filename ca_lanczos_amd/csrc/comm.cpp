@@ -56,6 +56,27 @@ int allreduce_sum(cal_ctx* c, double* d_buf, int64_t count) {
     return 0;
 }
 
+int allgather(cal_ctx* c, const double* d_send, double* d_recv, int64_t count) {
+    Comm* m = c->comm;
+    if (!m || m->nranks <= 1) {
+        if (count > 0 && d_recv != d_send)
+            CAL_HIP(c, hipMemcpyAsync(d_recv, d_send, count * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+        return 0;
+    }
+    if (count <= 0) return 0;
+    if (m->kind == 1) {
+        CAL_NCCL(c, ncclAllGather(d_send, d_recv, (size_t)count, ncclDouble, m->nccl, c->stream));
+        return 0;
+    }
+    // host-staged: every rank contributes its block into zeros, then a sum
+    // (x + 0 == x: the gather is exact)
+    const int64_t tot = count * m->nranks;
+    CAL_HIP(c, hipMemsetAsync(d_recv, 0, tot * sizeof(double), c->stream));
+    CAL_HIP(c, hipMemcpyAsync(d_recv + count * m->rank, d_send, count * sizeof(double), hipMemcpyDeviceToDevice,
+                              c->stream));
+    return allreduce_sum(c, d_recv, tot);
+}
+
 int halo_exchange(cal_ctx* c, double* x) {
     Comm* m = c->comm;
     DevMatrix& A = c->A;

@@ -454,8 +454,12 @@ __global__ __launch_bounds__(256) void k_spmv_pair_resid(PatArgs a, const uint16
             const double u0 = a.shift * xs.x, u1 = a.shift * xs.y;
             y0 = y0 - u0;
             y1 = y1 - u1;
-            num = y0 * y0 + y1 * y1;
-            den = u0 * u0 + u1 * u1;
+            // an odd local slab's last row pairs with the first stored ghost
+            // row (distributed layout, not split): that row belongs to the
+            // next rank and must not enter this rank's sums
+            const bool two = r0 + 1 < a.n;
+            num = y0 * y0 + (two ? y1 * y1 : 0.0);
+            den = u0 * u0 + (two ? u1 * u1 : 0.0);
         } else {  // split pair: each row from the row tables
             for (int k = 0; k < 2 && r0 + k < a.n; ++k) {
                 const int64_t rr = r0 + k;

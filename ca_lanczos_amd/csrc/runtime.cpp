@@ -4,6 +4,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <unordered_map>
+#include <string>
 #include <vector>
 
 #include "cal_internal.hpp"
@@ -586,6 +587,7 @@ int powers_dev(cal_ctx* c, int s, const double* q, double* const* Y, const doubl
     const bool mpk = A.mpk && A.use_pat && s <= A.mpk_depth && s > 1;
     const int64_t fake = (!mpk && !A.mpk && A.use_pat && s > 1 && A.nghost == 0) ? mpk_fake_band() : 0;
     if (!mpk && fake <= 0) {
+        c->powers_schedule = 0;
         for (int j = 0; j < s; ++j)
             CAL_TRY(spmv_dev(c, j == 0 ? q : Y[j - 1], Y[j], mode_of(j), shift ? shift[j] : 0.0,
                              im2 ? im2[j] : 0.0, xprev ? xprev[j] : nullptr));
@@ -603,6 +605,7 @@ int powers_dev(cal_ctx* c, int s, const double* q, double* const* Y, const doubl
     const int ov = mpk_overlap_env();
     const bool split = (fake > 0 || (mpk && (ov == 1 || (ov < 0 && rccl)))) && (dep_lo || dep_hi) &&
                        ilo(s) + 4 < ihi(s);
+    c->powers_schedule = split ? (rccl ? 2 : 3) : 1;
     if (!split) {
         CAL_TRY(halo_exchange_deep(c, const_cast<double*>(q), s, c->stream));
         for (int j = 1; j <= s; ++j) CAL_TRY(launch(j, stored_range(A, glo(j), ghi(j)), PowRange{0, 0}));
@@ -816,6 +819,29 @@ int cal_mpk_info(cal_ctx* c, int* depth, int64_t* band_l, int64_t* band_r, int64
     if (band_l) *band_l = c->A.band_l;
     if (band_r) *band_r = c->A.band_r;
     if (n_rows) *n_rows = c->A.n_rows;
+    return 0;
+}
+
+int cal_set_normalize(cal_ctx* c, const char* kind) {
+    if (!c || !kind) return CAL_ERR_ARG;
+    std::string k(kind);
+    for (auto& ch : k) ch = (char)tolower(ch);
+    if (k == "auto") c->normalize_kind = 0;
+    else if (k == "tsqr") c->normalize_kind = 1;
+    else if (k == "cholqr2") c->normalize_kind = 2;
+    else return set_error(c, CAL_ERR_ARG, "normalize backend must be auto, tsqr or cholqr2");
+    return 0;
+}
+
+int cal_get_normalize(cal_ctx* c, int* kind) {
+    if (!c || !kind) return CAL_ERR_ARG;
+    *kind = c->normalize_kind;
+    return 0;
+}
+
+int cal_mpk_schedule(cal_ctx* c, int* schedule) {
+    if (!c || !schedule) return CAL_ERR_ARG;
+    *schedule = c->powers_schedule;
     return 0;
 }
 

@@ -1,0 +1,329 @@
+// tsqr.hip -- Householder TSQR on gfx950 (tsqr.m:7-12: [Q,R] = qr(A,0) with
+// the positive-diagonal sign fix).
+//
+// A tall n x m panel (m <= 32) is cut into tiles of TR = 4096/MM rows (MM =
+// 8, 16 or 32 >= m): one wave per tile holds it in registers (64 doubles per
+// lane: lane l owns rows l + 64 i) and factors it with LAPACK's reflectors
+// (dlarfg: beta = -sign(alpha) ||x||, tau = (beta - alpha) / beta,
+// v = x / (alpha - beta)).  Every reflector needs ONE wave-wide reduction of
+// the vector [||x_below||^2, x'y_{j+1}, ..., x'y_{m-1}] -- all of it is known
+// before the reflector is -- done as a fixed DPP butterfly (quad_perm,
+// half/full row mirror, row_bcast 15/31) ending in lane 63, so the result is
+// bitwise reproducible.  The tile R factors are stacked (one m x m block per
+// tile) and the same kernel factors the stack, level by level, until one tile
+// remains: that is the TSQR reduction tree (multi-GPU: each rank's local root
+// is all-gathered and the global levels run redundantly on every rank).
+//
+// Q is formed top-down without storing reflectors: each tile RECOMPUTES its
+// factorisation from its (unchanged) input -- the same code on the same bits
+// gives the same reflectors -- builds its explicit Q factor in place
+// (dorg2r), and multiplies it by the m x m block S its parent handed down
+// (the root's S is diag(sign(diag R)), the sign fix of tsqr.m:9-12).  At
+// level 0 the product is the output Q; above it, it is the S of the children.
+//
+// HBM traffic at level 0: the panel is read twice (factor, then recompute +
+// form) and Q written once; the stack levels are 1/TR-th of that.
+#include "cal_internal.hpp"
+
+namespace cal {
+
+namespace {
+
+// DPP move of a double (two 32-bit halves); disabled rows yield 0
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWMASK, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWMASK, 0xF, false);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_readlane((int)b, lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// sum over the 64 lanes, returned wave-uniform; fixed order
+__device__ __forceinline__ double wave_allsum(double v) {
+    v = v + dpp_f64<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+    v = v + dpp_f64<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+    v = v + dpp_f64<0x141, 0xF>(v);  // row_half_mirror
+    v = v + dpp_f64<0x140, 0xF>(v);  // row_mirror
+    v = v + dpp_f64<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
+    v = v + dpp_f64<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
+    return readlane_f64(v, 63);
+}
+
+// Householder QR of the register tile a (rows lane + 64 i, m <= MM columns,
+// zero outside): R in the upper triangle of rows 0..m-1 (row j = lane j, i = 0;
+// R(j,j) also in beta[j]), reflector j below the diagonal of column j, tau[j].
+template <int MM, int RPL>
+__device__ __forceinline__ void tile_geqr2(double (&a)[RPL][MM], double (&tau)[MM], double (&beta)[MM], int m,
+                                           int lane) {
+#pragma unroll
+    for (int j = 0; j < MM; ++j) {
+        tau[j] = 0.0;
+        beta[j] = 0.0;
+        if (j < m) {
+        double d[MM];
+#pragma unroll
+        for (int c = j; c < MM; ++c) d[c] = 0.0;
+#pragma unroll
+        for (int i = 0; i < RPL; ++i) {
+            const bool below = lane + 64 * i > j;
+            const double x = below ? a[i][j] : 0.0;
+#pragma unroll
+            for (int c = j; c < MM; ++c) {
+                const double t = x * a[i][c];
+                d[c] = d[c] + t;
+            }
+        }
+#pragma unroll
+        for (int c = j; c < MM; ++c)
+            if (c < m) d[c] = wave_allsum(d[c]);
+        const double alpha = readlane_f64(a[0][j], j);
+        double t = 0.0, b = alpha, scal = 0.0;
+        if (d[j] != 0.0) {  // dlarfg: xnorm == 0 -> H = I
+            const double aa = alpha * alpha;
+            const double nrm = sqrt(aa + d[j]);
+            b = alpha >= 0.0 ? -nrm : nrm;
+            t = (b - alpha) / b;
+            scal = 1.0 / (alpha - b);
+        }
+        tau[j] = t;
+        beta[j] = b;
+        // tau * w_c, w_c = v'y_c = y_c(j) + scal * x'y_c (v_j = 1), in place of d
+#pragma unroll
+        for (int c = j + 1; c < MM; ++c) {
+            if (c < m) {
+                const double u = scal * d[c];
+                const double w = readlane_f64(a[0][c], j) + u;
+                d[c] = t * w;
+            } else {
+                d[c] = 0.0;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < RPL; ++i) {
+            const int row = lane + 64 * i;
+            if (row > j) {
+                const double v = scal * a[i][j];
+                a[i][j] = v;
+#pragma unroll
+                for (int c = j + 1; c < MM; ++c) {
+                    const double u = d[c] * v;
+                    a[i][c] = a[i][c] - u;
+                }
+            } else if (row == j) {  // the pivot row: y_c(j) - tau w_c
+                a[i][j] = b;
+#pragma unroll
+                for (int c = j + 1; c < MM; ++c) a[i][c] = a[i][c] - d[c];
+            }
+        }
+        }
+    }
+}
+
+// Explicit Q = H_0 ... H_{m-1} [I; 0] in place over the reflectors (dorg2r).
+template <int MM, int RPL>
+__device__ __forceinline__ void tile_org2r(double (&a)[RPL][MM], const double (&tau)[MM], int m, int lane) {
+#pragma unroll
+    for (int jj = 0; jj < MM; ++jj) {
+        const int j = MM - 1 - jj;
+        if (j < m) {
+        const double t = tau[j];
+        if (j < m - 1) {
+            // w_c = v' q_c over rows >= j (v_j = 1), c = j+1..m-1
+            double d[MM];
+#pragma unroll
+            for (int c = j + 1; c < MM; ++c) d[c] = 0.0;
+#pragma unroll
+            for (int i = 0; i < RPL; ++i) {
+                const int row = lane + 64 * i;
+                const double v = row > j ? a[i][j] : (row == j ? 1.0 : 0.0);
+#pragma unroll
+                for (int c = j + 1; c < MM; ++c) {
+                    const double u = v * a[i][c];
+                    d[c] = d[c] + u;
+                }
+            }
+#pragma unroll
+            for (int c = j + 1; c < MM; ++c) d[c] = c < m ? t * wave_allsum(d[c]) : 0.0;
+#pragma unroll
+            for (int i = 0; i < RPL; ++i) {
+                const int row = lane + 64 * i;
+                if (row >= j) {
+                    const double v = row > j ? a[i][j] : 1.0;
+#pragma unroll
+                    for (int c = j + 1; c < MM; ++c) {
+                        const double u = d[c] * v;
+                        a[i][c] = a[i][c] - u;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < RPL; ++i) {
+            const int row = lane + 64 * i;
+            const double v = a[i][j];
+            const double mt = -t;
+            a[i][j] = row > j ? mt * v : (row == j ? 1.0 - t : 0.0);
+        }
+        }
+    }
+}
+
+// SRC: 0 stack (block layout), 1 direct columns, 2 formed Z = P M (WP columns)
+template <int MM, int SRC, int WP, bool DOWN>
+__global__ __launch_bounds__(256) void k_tsqr(TsqrLevelArgs a, TsqrCols P, TsqrQ Q, int64_t ntiles) {
+    constexpr int RPL = 64 / MM, TR = 64 * RPL;
+    __shared__ double Ms[SRC == 2 ? WP * MM : 1];
+    __shared__ double Ss[DOWN ? 4 * MM * MM : 1];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int m = a.m;
+    if (SRC == 2) {
+        for (int e = threadIdx.x; e < WP * MM; e += 256) {
+            const int k = e / MM, c = e % MM;
+            Ms[e] = (k < a.wp && c < m) ? a.M[k + (int64_t)c * a.wp] : 0.0;
+        }
+        __syncthreads();
+    }
+    const int64_t tile = (int64_t)blockIdx.x * 4 + wave;
+    if (tile >= ntiles) return;  // whole waves
+    const int64_t base = tile * TR;
+    const int64_t mm = (int64_t)m * m;
+    double x[RPL][MM];
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+        const int64_t r = base + lane + 64 * i;
+        const bool in = r < a.rows;
+        const int64_t rc = in ? r : 0;
+        if (SRC == 0) {
+            const int64_t blk = rc / m, rr = rc - blk * m;
+            const double* src = a.in + blk * mm + rr;
+#pragma unroll
+            for (int c = 0; c < MM; ++c) {
+                const double v = src[(int64_t)(c < m ? c : 0) * m];
+                x[i][c] = (in && c < m) ? v : 0.0;
+            }
+        } else if (SRC == 1) {
+#pragma unroll
+            for (int c = 0; c < MM; ++c) {
+                const double v = P.p[c][rc];  // host pads p[c >= m] with a valid column
+                x[i][c] = (in && c < m) ? v : 0.0;
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < MM; ++c) x[i][c] = 0.0;
+#pragma unroll
+            for (int k = 0; k < WP; ++k) {
+                const double p = P.p[k][rc];  // host pads p[k >= wp] (zero rows of M)
+#pragma unroll
+                for (int c = 0; c < MM; ++c) x[i][c] = __builtin_fma(p, Ms[k * MM + c], x[i][c]);
+            }
+#pragma unroll
+            for (int c = 0; c < MM; ++c) x[i][c] = in ? x[i][c] : 0.0;
+        }
+    }
+    double tau[MM], beta[MM];
+    tile_geqr2<MM, RPL>(x, tau, beta, m, lane);
+    if (!DOWN) {
+        // R of this tile -> block `tile` of the next level's stack
+        if (lane < m) {
+            double* dst = a.out + tile * mm + lane;
+#pragma unroll
+            for (int c = 0; c < MM; ++c)
+                if (c < m) dst[(int64_t)c * m] = c < lane ? 0.0 : x[0][c];
+        }
+        return;
+    }
+    double* S = Ss + wave * MM * MM;
+    if (a.S) {
+        const double* src = a.S + tile * mm;
+        for (int e = lane; e < MM * MM; e += 64) {
+            const int k = e % MM, c = e / MM;
+            S[e] = (k < m && c < m) ? src[k + (int64_t)c * m] : 0.0;
+        }
+    } else {  // root: S = diag(sign(diag R)) (tsqr.m:9-12; sign(0) = 0); lane k writes row k
+#pragma unroll
+        for (int c = 0; c < MM; ++c) {
+            const double sg = beta[c] > 0.0 ? 1.0 : (beta[c] < 0.0 ? -1.0 : 0.0);
+            if (lane < MM) S[lane + c * MM] = (lane == c && c < m) ? sg : 0.0;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    tile_org2r<MM, RPL>(x, tau, m, lane);
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+        const int64_t r = base + lane + 64 * i;
+        double o[MM];
+#pragma unroll
+        for (int c = 0; c < MM; ++c) o[c] = 0.0;
+#pragma unroll
+        for (int k = 0; k < MM; ++k) {
+            if (k < m) {
+#pragma unroll
+                for (int c = 0; c < MM; ++c) {
+                    const double u = x[i][k] * S[k + c * MM];
+                    o[c] = o[c] + u;
+                }
+            }
+        }
+        if (r < a.rows) {
+            if (SRC == 0) {
+                const int64_t blk = r / m, rr = r - blk * m;
+                double* dst = a.out + blk * mm + rr;
+#pragma unroll
+                for (int c = 0; c < MM; ++c)
+                    if (c < m) dst[(int64_t)c * m] = o[c];
+            } else {
+#pragma unroll
+                for (int c = 0; c < MM; ++c)
+                    if (c < m) Q.p[c][r] = o[c];
+            }
+        }
+    }
+}
+
+}  // namespace
+
+int tsqr_mm(int m) { return m <= 8 ? 8 : (m <= 16 ? 16 : (m <= 32 ? 32 : 0)); }
+int tsqr_tile_rows(int m) {
+    const int mm = tsqr_mm(m);
+    return mm ? 4096 / mm : 0;
+}
+bool tsqr_form_ok(int wp, int m) { return (m <= 8 && wp <= 17) || (m > 8 && m <= 16 && wp <= 33); }
+
+hipError_t launch_tsqr(bool down, int src, const TsqrLevelArgs& a, const TsqrCols& P, const TsqrQ& Q,
+                       hipStream_t st) {
+    const int MM = tsqr_mm(a.m);
+    if (!MM || a.rows <= 0) return hipErrorInvalidValue;
+    const int64_t tiles = (a.rows + 4096 / MM - 1) / (4096 / MM);
+    const dim3 g((unsigned)((tiles + 3) / 4)), b(256);
+#define CAL_TQ(MMV, SRCV, WPV)                                                                             \
+    do {                                                                                                   \
+        if (down) hipLaunchKernelGGL((k_tsqr<MMV, SRCV, WPV, true>), g, b, 0, st, a, P, Q, tiles);          \
+        else hipLaunchKernelGGL((k_tsqr<MMV, SRCV, WPV, false>), g, b, 0, st, a, P, Q, tiles);              \
+    } while (0)
+    if (src == 2) {
+        if (MM == 8 && a.wp <= 17) CAL_TQ(8, 2, 17);
+        else if (MM == 16 && a.wp <= 33) CAL_TQ(16, 2, 33);
+        else return hipErrorInvalidValue;
+    } else if (src == 1) {
+        if (MM == 8) CAL_TQ(8, 1, 0);
+        else if (MM == 16) CAL_TQ(16, 1, 0);
+        else CAL_TQ(32, 1, 0);
+    } else {
+        if (MM == 8) CAL_TQ(8, 0, 0);
+        else if (MM == 16) CAL_TQ(16, 0, 0);
+        else CAL_TQ(32, 0, 0);
+    }
+#undef CAL_TQ
+    return hipGetLastError();
+}
+
+}  // namespace cal

@@ -80,6 +80,11 @@ int cal_matrix_info(cal_ctx* ctx, int64_t* n_local, int64_t* nnz_local, int64_t*
  * the active depth (1 = off), the global band and the stored row count. */
 int cal_set_mpk_depth(cal_ctx* ctx, int depth);
 int cal_mpk_info(cal_ctx* ctx, int* depth, int64_t* band_l, int64_t* band_r, int64_t* n_rows);
+/* Schedule the last matrix-powers call took: 0 one halo exchange per SpMV,
+ * 1 one deep exchange, 2 one deep exchange on the RCCL stream overlapped
+ * with the interior powers, 3 the split schedule with a synchronous
+ * exchange; -1 before the first call. */
+int cal_mpk_schedule(cal_ctx* ctx, int* schedule);
 /* Device storage of A, chosen at the next cal_set_matrix_*: "auto" (default:
  * row patterns when A has <= 65535 distinct rows of <= 32 entries, else
  * CSR), "csr", or "pattern".  Both are lossless and give bit-identical SpMV
@@ -93,6 +98,16 @@ int cal_spmv_pair_info(cal_ctx* ctx, int* npairpatterns, int* nentries, int64_t*
  * "device" (default: one kernel, no host round trip inside a block) or
  * "host".  Both give bit-identical results; "host" exists for testing. */
 int cal_set_orth_coef(cal_ctx* ctx, const char* where);
+/* Backend of normalize (tsqr.m) on the device: "auto" (default: Householder
+ * TSQR for the host-pointer calls cal_tsqr / cal_normalize /
+ * cal_project_and_normalize; CholQR2 fused into the CA-Lanczos sweeps, with
+ * Householder TSQR whenever its Cholesky fails, i.e. kappa > ~1e8), "tsqr"
+ * (Householder TSQR everywhere, the reference's algorithm; multi-GPU: the
+ * local trees' roots are all-gathered over RCCL), "cholqr2" (CholQR2
+ * everywhere, shifted CholQR3 when its Cholesky fails).  cal_tsqr is always
+ * Householder TSQR.  get: 0 auto, 1 tsqr, 2 cholqr2. */
+int cal_set_normalize(cal_ctx* ctx, const char* kind);
+int cal_get_normalize(cal_ctx* ctx, int* kind);
 /* Device-resident SpMV timing: `reps` launches of y = (A - shift I) x on
  * HBM-resident vectors (x = ones), HIP events around each launch on the
  * context stream; returns the mean and the minimum kernel time. */
@@ -110,7 +125,8 @@ int cal_matrix_powers_newton(cal_ctx* ctx, const double* v, int s, const double*
                              const double* lambda_im, int modifiedp, double* V);
 
 /* ---- a5-a9: tall-skinny block orthogonalisation ------------------------- */
-/* [Q,R] = tsqr(A): A n x m -> Q n x m, R m x m upper, diag(R) >= 0.   tsqr.m:7-12 */
+/* [Q,R] = tsqr(A): A n x m -> Q n x m, R m x m upper, diag(R) >= 0.   tsqr.m:7-12
+ * Householder TSQR (LAPACK reflectors per tile, reduction tree), m <= 32, n >= m. */
 int cal_tsqr(cal_ctx* ctx, int64_t n, int m, const double* A, double* Q, double* R);
 /* [Q,R] = cholqr(X): G = X'X, R = chol(G), Q = X/R.                  cholqr.m:3-8 */
 int cal_cholqr(cal_ctx* ctx, int64_t n, int m, const double* X, double* Q, double* R);
