@@ -184,7 +184,7 @@ int cal_normalize(cal_ctx* c, int64_t n, int m, const double* X, double tol, dou
 
 int cal_cholqr(cal_ctx* c, int64_t n, int m, const double* X, double* Q, double* R) {
     CAL_TRY(check_ctx(c, false));
-    if (!X || !Q || !R || n < 1 || m < 1 || m > 16) return set_error(c, CAL_ERR_ARG, "cholqr: need 1 <= m <= 16");
+    if (!X || !Q || !R || n < 1 || m < 1 || m > 32) return set_error(c, CAL_ERR_ARG, "cholqr: need 1 <= m <= 32");
     const int64_t ld = ld_for(n);
     CAL_TRY(ensure_scratch(c, (size_t)2 * m * ld));
     double* dX = c->d_scratch;
@@ -206,7 +206,7 @@ int cal_project(cal_ctx* c, int64_t n, int nblocks, const double* const* Q, cons
                 int doreorth, double* Xout, double* const* R) {
     Tier1 t1(c);
     CAL_TRY(check_ctx(c, false));
-    if (nblocks < 0 || (nblocks > 0 && (!Q || !widths)) || !X || !Xout || n < 1 || m < 1 || m > 16)
+    if (nblocks < 0 || (nblocks > 0 && (!Q || !widths)) || !X || !Xout || n < 1 || m < 1 || m > 32)
         return set_error(c, CAL_ERR_ARG, "project: bad arguments");
     const int64_t ld = ld_for(n);
     int wtot = 0;
@@ -236,7 +236,7 @@ int cal_project_and_normalize(cal_ctx* c, int64_t n, int nblocks, const double* 
                               const double* X, int doreorth, double* QZ, double* const* RZ, int* reorth, int* rank) {
     Tier1 t1(c);
     CAL_TRY(check_ctx(c, false));
-    if (nblocks < 0 || (nblocks > 0 && (!Q || !widths)) || !X || !QZ || n < 1 || m < 1 || m > 16)
+    if (nblocks < 0 || (nblocks > 0 && (!Q || !widths)) || !X || !QZ || n < 1 || m < 1 || m > 32)
         return set_error(c, CAL_ERR_ARG, "projectAndNormalize: bad arguments");
     const int64_t ld = ld_for(n);
     int wtot = 0, nonempty = 0, only = -1;

@@ -74,7 +74,23 @@ static int stage_small(cal_ctx* c, const double* M, size_t count) {
     return 0;
 }
 
+static int gram_host16(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* out);
+
+// out (wa x wb) = A'B, B in chunks of <= 16 columns (the MFMA Gram's B tile)
 int gram_host(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* out) {
+    const int wa = A.total, wb = B.total;
+    if (wb <= 16) return gram_host16(c, n, A, B, out);
+    for (int j0 = 0; j0 < wb; j0 += 16) {
+        const int nb = std::min(16, wb - j0);
+        std::vector<double> t((size_t)wa * nb);
+        CAL_TRY(gram_host16(c, n, A, panel_slice(B, j0, nb), t.data()));
+        for (int j = 0; j < nb; ++j)
+            for (int i = 0; i < wa; ++i) out[i + (size_t)(j0 + j) * wa] = t[i + (size_t)j * wa];
+    }
+    return 0;
+}
+
+static int gram_host16(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* out) {
     const int wa = A.total, wb = B.total;
     if (wb > 16 || wb < 1 || wa < 1) return set_error(c, CAL_ERR_ARG, "gram: panel widths out of range");
     if (A.nseg > kMaxSeg || B.nseg > kMaxSeg) return set_error(c, CAL_ERR_ARG, "gram: too many segments");
@@ -552,11 +568,112 @@ int normalize_dev(cal_ctx* c, int64_t n, const Panel& X, const PanelOut& Qout, d
     return 0;
 }
 
+// n x m device block for the TSQR paths (materialised Y / Z when the tile
+// kernel cannot form them on the fly)
+static int ensure_zbuf(cal_ctx* c, int64_t n, int m, double** p, int64_t* ld) {
+    *ld = ((std::max<int64_t>(n, 1) + 63) / 64) * 64;
+    const size_t need = (size_t)(*ld) * m;
+    if (need > c->zbuf_cap) {
+        if (c->d_zbuf) CAL_HIP(c, hipFree(c->d_zbuf));
+        c->d_zbuf = nullptr;
+        CAL_HIP(c, hipMalloc((void**)&c->d_zbuf, need * sizeof(double)));
+        c->zbuf_cap = need;
+    }
+    *p = c->d_zbuf;
+    return 0;
+}
+
+// projectAndNormalize.m:3-90 against one block with the Householder TSQR
+// normalize (tsqr.m): C = Qp'X and X'X from one Gram sweep; the reorth test
+// of :45-52 on the algebraic norms ||Y_i||^2 = diag(X'X - C'C); on reorth the
+// second projection C2 = Qp'Y (:63, Y = X - Qp C formed on the fly) and
+// RZ = C + C2 (:71-73); then TSQR of Z = X - Qp RZ, formed per row inside the
+// tile kernel (or materialised first for shapes it does not instantiate).
+static int pn_tsqr(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, bool doreorth, const PanelOut& Qout,
+                   double* Rq, double* R, PNResult* res) {
+    const int w = Qp.total, m = X.total, wp = w + m;
+    if (!tsqr_ok(m)) return set_error(c, CAL_ERR_UNSUPPORTED, "projectAndNormalize (tsqr): at most 32 columns");
+    const Panel W = panel_concat(Qp, X);
+    std::vector<double> G1((size_t)wp * m);
+    CAL_TRY(gram_host(c, n, W, X, G1.data()));
+    std::vector<double> C((size_t)std::max(w, 1) * m, 0.0), before(m);
+    double mx = NAN;
+    for (int j = 0; j < m; ++j) {
+        for (int i = 0; i < w; ++i) C[i + (size_t)j * w] = G1[i + (size_t)j * wp];
+        double cc = 0.0;
+        for (int k = 0; k < w; ++k) cc += C[k + (size_t)j * w] * C[k + (size_t)j * w];
+        const double xx = G1[w + j + (size_t)j * wp];
+        before[j] = std::sqrt(xx);
+        const double after = std::sqrt(std::max(xx - cc, 0.0));
+        const double rel = std::fabs(before[j] - after) / before[j];
+        if (!std::isnan(rel) && (std::isnan(mx) || rel > mx)) mx = rel;
+    }
+    const bool reorth = w > 0 && doreorth && mx > 0.5;
+    auto coef = [&](const std::vector<double>& Ct) {
+        std::vector<double> M((size_t)wp * m, 0.0);
+        for (int j = 0; j < m; ++j) {
+            for (int i = 0; i < w; ++i) M[i + (size_t)j * wp] = -Ct[i + (size_t)j * w];
+            M[w + j + (size_t)j * wp] = 1.0;
+        }
+        return M;
+    };
+    std::vector<double> Ct = C, C2;
+    if (reorth) {  // C2 = Qp'Y, Y = W [-C; I]
+        std::vector<double> M = coef(C);
+        C2.assign((size_t)w * m, 0.0);
+        if (w <= 16 && m <= 16) {
+            CAL_TRY(apply_host(c, n, W, M.data(), m, nullptr, nullptr, w, C2.data()));
+        } else {
+            double* dY;
+            int64_t ldy;
+            CAL_TRY(ensure_zbuf(c, n, m, &dY, &ldy));
+            const PanelOut Yo = panel_out(dY, ldy, m);
+            CAL_TRY(apply_host(c, n, W, M.data(), m, &Yo, nullptr, 0, nullptr));
+            CAL_TRY(gram_host(c, n, Qp, as_panel(Yo), C2.data()));
+        }
+        for (size_t e = 0; e < C2.size(); ++e) Ct[e] = C[e] + C2[e];
+    }
+    if (w == 0) {
+        CAL_TRY(tsqr_dev(c, n, X, nullptr, m, Qout, R));
+    } else {
+        // Z = Y - Qp C2 on the rounded Y = X - Qp C, as the reference
+        // projects the stored Y again (:63)
+        std::vector<double> M = coef(C);
+        if (reorth)
+            for (int j = 0; j < m; ++j)
+                for (int i = 0; i < w; ++i) M.push_back(-C2[i + (size_t)j * w]);
+        if (tsqr_form_ok(wp, m) && W.nseg <= kMaxSeg) {
+            CAL_TRY(stage_small(c, M.data(), M.size()));
+            CAL_TRY(tsqr_dev(c, n, W, c->d_small, m, Qout, R, reorth ? c->d_small + (size_t)wp * m : nullptr,
+                             reorth ? w : 0));
+        } else {
+            double* dZ;
+            int64_t ldz;
+            CAL_TRY(ensure_zbuf(c, n, m, &dZ, &ldz));
+            const PanelOut Zo = panel_out(dZ, ldz, m);
+            CAL_TRY(apply_host(c, n, W, M.data(), m, &Zo, nullptr, 0, nullptr));
+            if (reorth) {
+                Panel W2 = panel_concat(Qp, as_panel(Zo));
+                CAL_TRY(apply_host(c, n, W2, coef(C2).data(), m, &Zo, nullptr, 0, nullptr));
+            }
+            CAL_TRY(tsqr_dev(c, n, as_panel(Zo), nullptr, m, Qout, R));
+        }
+    }
+    for (size_t e = 0; e < (size_t)w * m; ++e) Rq[e] = Ct[e];
+    if (res) {
+        res->reorth = reorth;
+        res->rank = rank_from_R(m, R, 1.0e-8);
+        res->chol_shifted = false;
+    }
+    return 0;
+}
+
 int project_and_normalize_dev(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, bool doreorth,
                               const PanelOut& Qout, double* Rq, double* R, PNResult* res) {
     const int w = Qp.total, m = X.total;
-    if (m < 1 || m > 16) return set_error(c, CAL_ERR_ARG, "projectAndNormalize: 1..16 columns supported");
     if (Qp.nseg + X.nseg > kMaxSeg) return set_error(c, CAL_ERR_ARG, "projectAndNormalize: too many segments");
+    if (use_tsqr(c, m, c->tier1) || (m > 16 && tsqr_ok(m))) return pn_tsqr(c, n, Qp, X, doreorth, Qout, Rq, R, res);
+    if (m < 1 || m > 16) return set_error(c, CAL_ERR_ARG, "projectAndNormalize: 1..32 columns supported");
     if (orth_device_ok(c, Qp, X)) {
         bool ro = false;
         const int st = orth_device(c, n, Qp, X, doreorth, Qout, Rq, R, &ro);
@@ -570,6 +687,8 @@ int project_and_normalize_dev(cal_ctx* c, int64_t n, const Panel& Qp, const Pane
             return 0;
         }
         c->orth_redone = true;
+        // a device Cholesky failed (kappa > ~1e8): the Householder TSQR path
+        if (c->normalize_kind != 2 && tsqr_ok(m)) return pn_tsqr(c, n, Qp, X, doreorth, Qout, Rq, R, res);
     }
     const Panel W = panel_concat(Qp, X);
     const int wp = w + m;
@@ -621,6 +740,7 @@ int project_and_normalize_dev(cal_ctx* c, int64_t n, const Panel& Qp, const Pane
     }
     std::vector<double> Rtmp((size_t)m * m);
     if (!dense::chol_upper(m, GZ.data(), m, Rtmp.data(), m)) {
+        if (c->normalize_kind != 2 && tsqr_ok(m)) return pn_tsqr(c, n, Qp, X, doreorth, Qout, Rq, R, res);
         // the algebraic Gram lost definiteness (heavy cancellation): Y'Y directly
         CAL_TRY(apply_host(c, n, W, Mz.data(), m, nullptr, GZ.data(), 0, nullptr));
     }
@@ -714,6 +834,7 @@ static bool async_ok(int nb, const int* widths, int m) {
 // Gram A'B (A <= 128 columns, B <= 16) reduced (and all-reduced) into d_dst
 // (ld *ldc) and copied to h_dst; nothing waits.
 int gram_async(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* d_dst, double* h_dst, int* ldc) {
+    if (B.total > 16 || A.total > 128) return set_error(c, CAL_ERR_ARG, "gram_async: A <= 128, B <= 16 columns");
     const GramPlan pl = gram_plan(A.total, B.total, n);
     CAL_TRY(ensure_partial(c, (size_t)pl.blocks * pl.entries));
     const int t = timer_begin(c, 1);

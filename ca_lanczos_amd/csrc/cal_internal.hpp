@@ -268,6 +268,8 @@ struct TsqrLevelArgs {
     const double* in = nullptr;
     double* out = nullptr;
     const double* S = nullptr;
+    const double* M2 = nullptr;  // formed mode: Z = (P M) + P(:, 0:w2) M2 (w2 x m)
+    int w2 = 0;
 };
 int tsqr_mm(int m);          // register tile width (8, 16, 32; 0: m > 32)
 int tsqr_tile_rows(int m);   // rows per tile (4096 / tsqr_mm)
@@ -343,6 +345,8 @@ struct cal_ctx {
     bool tier1 = false;  // inside a host-pointer (tier-1) entry point (api.cpp)
     double* d_tsqr = nullptr;  // TSQR tree workspace
     size_t tsqr_cap = 0;
+    double* d_zbuf = nullptr;  // n x m block of the TSQR paths (blockorth.cpp)
+    size_t zbuf_cap = 0;
 };
 
 // ---- helpers shared by the host-side translation units -----------------
@@ -446,11 +450,13 @@ int allreduce_sum(cal_ctx* c, double* d_buf, int64_t count);
 int allgather(cal_ctx* c, const double* d_send, double* d_recv, int64_t count);
 
 // Householder TSQR of Z (tsqr.m:7-12): Z = W (direct, dM null, W.total = m)
-// or Z = W * M (dM: W.total x m column-major on the device, formed per row).
+// or Z = W * M (dM: W.total x m column-major on the device, formed per row),
+// optionally followed by Z += W(:, 0:w2) * M2 on the rounded W * M (dM2).
 // Q -> Qout (n x m), R -> host (m x m, diag >= 0, the reference's sign fix).
 // Multi-GPU: the tree's root is taken over all ranks (allgather + redundant
 // top levels).  Runs c->pre_wait before its one host wait.  m <= 32.
-int tsqr_dev(cal_ctx* c, int64_t n, const Panel& W, const double* dM, int m, const PanelOut& Qout, double* R);
+int tsqr_dev(cal_ctx* c, int64_t n, const Panel& W, const double* dM, int m, const PanelOut& Qout, double* R,
+             const double* dM2 = nullptr, int w2 = 0);
 bool tsqr_ok(int m);
 // whether normalize / projectAndNormalize use TSQR here (tier1: a host-pointer call)
 bool use_tsqr(const cal_ctx* c, int m, bool tier1);

@@ -27,6 +27,10 @@
 
 namespace cal {
 
+// block size limit: the k = 1 block has s + 1 <= 32 columns (the TSQR tile)
+// and the Newton prologue's 2s shifts fit cal_lanczos_info.shifts[64]
+constexpr int kMaxS = 31;
+
 struct LanczosState {
     int s = 0, max_outer = 0, k = 0;
     bool newton = false, full = false;
@@ -320,7 +324,7 @@ static int ritz_diagnostics(cal_ctx* c, LanczosState& L) {
     panel_add(OA, L.col(0), ld, wa);
     panel_add(OB, L.col(jq > s + 1 ? wa : 0), ld, s + 1);
     constexpr size_t kOrthRegion = 8192 + 7 * 8192;  // above the projections' async regions
-    const bool oe_async = wa <= 128;
+    const bool oe_async = wa <= 128 && s + 1 <= 16;
     int oe_ld = 0;
     if (oe_async) {
         CAL_TRY(ensure_red(c, kOrthRegion + 8192));
@@ -736,8 +740,8 @@ void cal_lanczos_free_state(cal_ctx* c) {
 int cal_lanczos_begin(cal_ctx* c, const double* r, int s, int max_outer, const char* basis, const char* orth) {
     if (!c) return CAL_ERR_ARG;
     if (!c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
-    if (!r || s < 1 || s > 15 || max_outer < 1 || !basis)
-        return set_error(c, CAL_ERR_ARG, "cal_lanczos_begin: need r, 1 <= s <= 15, max_outer >= 1");
+    if (!r || s < 1 || s > kMaxS || max_outer < 1 || !basis)
+        return set_error(c, CAL_ERR_ARG, "cal_lanczos_begin: need r, 1 <= s <= 31, max_outer >= 1");
     std::string o = orth ? orth : "local", b = basis;
     for (auto& ch : o) ch = (char)tolower(ch);
     for (auto& ch : b) ch = (char)tolower(ch);
@@ -898,7 +902,7 @@ int cal_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, int n
                              const char* orth, double tol, int diagnostics, double* conv_eigs, double* Q_conv,
                              double* rnorms, double* orth_err, cal_restart_info* info) {
     constexpr int kMaxRestarts = 200;  // restarted_ca_lanczos.m:6
-    if (!c || !r || n_wanted < 1 || s < 1 || s > 15 || !basis || !orth || !conv_eigs)
+    if (!c || !r || n_wanted < 1 || s < 1 || s > kMaxS || !basis || !orth || !conv_eigs)
         return set_error(c, CAL_ERR_ARG, "restarted_ca_lanczos: bad arguments");
     if (!c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
     std::string o(orth), b(basis);
@@ -1198,7 +1202,7 @@ int cal_impl_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, 
                                   double* ritz_est, cal_restart_info* info) {
     constexpr int kMaxRestarts = 40;  // impl_restarted_ca_lanczos.m:7
     if (!c) return CAL_ERR_ARG;
-    if (!r || n_wanted < 1 || s < 1 || s > 15 || !basis || !orth || !conv_eigs)
+    if (!r || n_wanted < 1 || s < 1 || s > kMaxS || !basis || !orth || !conv_eigs)
         return set_error(c, CAL_ERR_ARG, "impl_restarted_ca_lanczos: bad arguments");
     if (!c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
     std::string o(orth), b(basis);

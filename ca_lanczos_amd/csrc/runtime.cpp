@@ -685,6 +685,8 @@ void cal_destroy(cal_ctx* c) {
     }
     for (auto e : c->event_pool) hipEventDestroy(e);
     if (c->orth_event) hipEventDestroy(c->orth_event);
+    if (c->d_tsqr) hipFree(c->d_tsqr);
+    if (c->d_zbuf) hipFree(c->d_zbuf);
     if (c->h_pub) hipHostFree(c->h_pub);
     hipStreamDestroy(c->stream);
     delete c;

@@ -179,7 +179,8 @@ __device__ __forceinline__ void tile_org2r(double (&a)[RPL][MM], const double (&
 template <int MM, int SRC, int WP, bool DOWN>
 __global__ __launch_bounds__(256) void k_tsqr(TsqrLevelArgs a, TsqrCols P, TsqrQ Q, int64_t ntiles) {
     constexpr int RPL = 64 / MM, TR = 64 * RPL;
-    __shared__ double Ms[SRC == 2 ? WP * MM : 1];
+    // formed mode: M (wp x m) at [0, WP*MM), the second projection M2 (w2 x m) after it
+    __shared__ double Ms[SRC == 2 ? 2 * WP * MM : 1];
     __shared__ double Ss[DOWN ? 4 * MM * MM : 1];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int m = a.m;
@@ -187,6 +188,7 @@ __global__ __launch_bounds__(256) void k_tsqr(TsqrLevelArgs a, TsqrCols P, TsqrQ
         for (int e = threadIdx.x; e < WP * MM; e += 256) {
             const int k = e / MM, c = e % MM;
             Ms[e] = (k < a.wp && c < m) ? a.M[k + (int64_t)c * a.wp] : 0.0;
+            Ms[WP * MM + e] = (a.M2 && k < a.w2 && c < m) ? a.M2[k + (int64_t)c * a.w2] : 0.0;
         }
         __syncthreads();
     }
@@ -222,6 +224,19 @@ __global__ __launch_bounds__(256) void k_tsqr(TsqrLevelArgs a, TsqrCols P, TsqrQ
                 const double p = P.p[k][rc];  // host pads p[k >= wp] (zero rows of M)
 #pragma unroll
                 for (int c = 0; c < MM; ++c) x[i][c] = __builtin_fma(p, Ms[k * MM + c], x[i][c]);
+            }
+            if (a.M2) {
+                // projectAndNormalize.m:63: Z = Y - Qp C2 on the ROUNDED
+                // Y = X - Qp C (one combined coefficient would lose C2 below
+                // u |C|); Qp = the first w2 panel columns (reloaded: cache hits)
+#pragma unroll
+                for (int k = 0; k < WP; ++k) {
+                    if (k < a.w2) {
+                        const double p = P.p[k][rc];
+#pragma unroll
+                        for (int c = 0; c < MM; ++c) x[i][c] = __builtin_fma(p, Ms[WP * MM + k * MM + c], x[i][c]);
+                    }
+                }
             }
 #pragma unroll
             for (int c = 0; c < MM; ++c) x[i][c] = in ? x[i][c] : 0.0;

@@ -50,7 +50,8 @@ int ensure_tsqr(cal_ctx* c, size_t doubles) {
 
 }  // namespace
 
-int tsqr_dev(cal_ctx* c, int64_t n, const Panel& W, const double* dM, int m, const PanelOut& Qout, double* R) {
+int tsqr_dev(cal_ctx* c, int64_t n, const Panel& W, const double* dM, int m, const PanelOut& Qout, double* R,
+             const double* dM2, int w2) {
     if (!tsqr_ok(m)) return set_error(c, CAL_ERR_UNSUPPORTED, "tsqr: 1..32 columns on the device");
     const int wp = W.total;
     const bool form = dM != nullptr;
@@ -127,6 +128,8 @@ int tsqr_dev(cal_ctx* c, int64_t n, const Panel& W, const double* dM, int m, con
         a.in = L.in;
         a.out = down ? L.down : L.up;
         a.S = L.S;
+        a.M2 = dM2;
+        a.w2 = w2;
         return a;
     };
     // up the tree

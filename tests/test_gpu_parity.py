@@ -286,8 +286,8 @@ def test_ca_lanczos_bad_args(cal):
         cal.ca_lanczos(A, np.ones(64), 4, 16, "newton", "bogus")
     with pytest.raises(cal.CalError):
         cal.ca_lanczos(A, np.ones(64), 4, 16, "chebyshev", "local")
-    with pytest.raises(cal.CalError):  # s > 15: s + 1 exceeds the 16-column block kernels
-        cal.ca_lanczos(A, np.ones(64), 17, 34, "newton", "local")
+    with pytest.raises(cal.CalError):  # s > 31: s + 1 exceeds the 32-column TSQR tile
+        cal.ca_lanczos(A, np.ones(64), 32, 64, "newton", "local")
 
 
 @pytest.mark.gpu
@@ -507,15 +507,20 @@ def test_impl_restarted_rejects(cal, ref):
 
 
 @pytest.mark.parametrize("s,basis", [(1, "newton"), (2, "monomial"), (3, "newton"), (5, "newton"), (6, "monomial"),
-                                     (9, "newton"), (12, "newton"), (15, "newton")])
+                                     (9, "newton"), (12, "newton"), (15, "newton"), (16, "newton"),
+                                     (20, "newton"), (24, "newton")])
 def test_ca_lanczos_block_sizes(cal, ref, s, basis):
-    """Every block size the ABI accepts (1 <= s <= 15): s + 1 > 9 leaves the
-    device-coefficient fast path for the generic sweeps; s = 1 is plain
-    Lanczos with one-column blocks.  Same bars as the s = 4 / 8 cases."""
+    """Block sizes 1 <= s <= 24 (the ABI takes s <= 31): s + 1 > 9 leaves the
+    device-coefficient fast path for the generic sweeps; s + 1 > 16 takes the
+    Householder TSQR normalize (32-column tiles); s = 1 is plain Lanczos with
+    one-column blocks.  s = 4, 8, 12, 16 with 120 steps is the reference's
+    own harness (test_ca_lanczos.m:29-41).  Same bars as the s = 4 / 8 cases."""
     N = 20
     A = cal.matrices.laplacian_2d(N)
     r = ref.matlab_rand(N * N)
-    it = s * 5
+    # at most 8 outer iterations: 'local' loses orthogonality on this 400-row
+    # problem and by k ~ 10 the reorth test sits on its 0.5 threshold
+    it = min(120, 8 * s) if s >= 12 else s * 5
     out = cal.ca_lanczos_ex(A, r, s, it, basis, "local")
     exp = ref.ca_lanczos(A, r, s, it, basis, "local")
     _compare_lanczos(out, exp, 8.0)
@@ -604,3 +609,52 @@ def test_matrix_powers_split_schedule_row_kernel(cal, ref, monkeypatch):
     monkeypatch.delenv("CAL_MPK_FAKE_BAND")
     assert np.array_equal(V1, V0)
     assert np.array_equal(V0, ref.matrix_powers_newton(A, v, s, lam, 1))
+
+
+@pytest.mark.parametrize("s,tol_T", [(8, 1e-8), (10, 1e-7)])
+def test_ca_lanczos_monomial_full_sweep(cal, ref, s, tol_T):
+    """The reference's monomial sweep (test_ca_lanczos_convergence_orthogonality.m:
+    54-55: s = 1..10, 'full', 120 steps, A / norm(A,'inf'), r0 = rand) on a
+    matrix the image can build, diag(linspace(1,100,500)) / 100.  At s = 10 the
+    monomial basis has kappa(V) far beyond u^(-1/2): CholQR2's Cholesky fails
+    and the block takes the Householder TSQR.  Bars: 1e-15 perturbations of r
+    move the oracle's own T by 3e-11 (s = 8) / 6e-10 (s = 10) and its top ten
+    Ritz values by 3e-12 / 5e-11; T within tol_T, top ten Ritz values within
+    1e-9, identical reorth flags, orthogonality error < 1e-13."""
+    import scipy.sparse as sp
+    n = 500
+    A = sp.diags(ref.matlab_linspace(1.0, 100.0, n) / 100.0).tocsr()
+    r = ref.matlab_rand(n)
+    out = cal.ca_lanczos_ex(A, r, s, 120, "monomial", "full", diagnostics=True)
+    exp = ref.ca_lanczos(A, r, s, 120, "monomial", "full", diagnostics=True)
+    assert list(out.reorth) == list(exp.reorth)
+    assert out.T.shape == exp.T.shape
+    assert np.max(np.abs(out.T - exp.T)) <= tol_T
+    w = np.sort(np.linalg.eigvals(out.T).real)[-10:]
+    we = np.sort(np.linalg.eigvals(exp.T).real)[-10:]
+    assert np.max(np.abs(w - we)) <= 1e-9
+    assert np.max(out.orth_err) < 1e-13
+
+
+@pytest.mark.parametrize("cond", [1e8, 1e11, 1e14])
+def test_project_and_normalize_ill_conditioned(cal, ref, cond):
+    """projectAndNormalize (Householder TSQR normalize) on a block whose
+    projected part has kappa up to 1e14: R within 20 m kappa u ||Y||, QZ
+    orthonormal to 1e-13 (Householder), identical reorth flag.  Orthogonality
+    to Qp of the directions with singular values ~ kappa^-1 ||Y|| is lost to
+    O(u kappa) in any normalize-after-project scheme, the reference's too: it
+    must be within 10x the oracle's own (+ 1e-13)."""
+    rng = np.random.RandomState(int(np.log10(cond)))
+    n, w, m = 20000, 9, 8
+    Qp, _ = np.linalg.qr(rng.randn(n, w))
+    Y = _rand_block(n, m, 7, cond)
+    Y = Y - Qp @ (Qp.T @ Y)
+    X = Y + Qp @ rng.randn(w, m) * 0.3
+    QZ, RZ, re, rank = cal.projectAndNormalize_ex([Qp], X)
+    QZr, RZr, info = ref.projectAndNormalize_ex([Qp], X)
+    assert re == info.reorth
+    ny = np.linalg.norm(Y, 2)
+    assert np.max(np.abs(RZ[1] - RZr[1])) <= 20 * m * cond * 2.0 ** -53 * ny
+    assert np.max(np.abs(RZ[0] - RZr[0])) <= 1e-12 * np.linalg.norm(X, 2)
+    assert np.linalg.norm(QZ.T @ QZ - np.eye(m), 2) <= 1e-13
+    assert np.max(np.abs(QZ.T @ Qp)) <= 10 * np.max(np.abs(QZr.T @ Qp)) + 1e-13
