@@ -59,6 +59,10 @@ def parse():
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "spmv_traffic.json"))
     p.add_argument("--mpk-depth", type=int, default=8,
                    help="N > 1: ghost depth of the CA matrix-powers kernel (1 = one halo exchange per SpMV)")
+    p.add_argument("--normalize", default="auto", choices=["auto", "tsqr", "cholqr2"],
+                   help="normalize (tsqr.m) backend of the headline: auto = CholQR2 fused into the sweeps "
+                        "(Householder TSQR when its Cholesky fails), tsqr = Householder TSQR tree")
+    p.add_argument("--no-legs", action="store_true", help="skip the secondary TSQR / CSR legs")
     p.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                    help="N > 1 transport: RCCL (default) or host-staged gloo callbacks (rehearsal of the "
                         "distributed bench with several ranks on one GPU)")
@@ -243,7 +247,7 @@ def setup(args):
 
     ndev = ctypes.c_int(0)
     cal._lib.lib.cal_device_count(ctypes.byref(ndev))
-    ctx = cal.Context(device=local % max(ndev.value, 1), mpk_depth=args.mpk_depth)
+    ctx = cal.Context(device=local % max(ndev.value, 1), mpk_depth=args.mpk_depth, normalize=args.normalize)
     bounds = slab_bounds(n, world, wl.plane)
     r0, r1 = bounds[rank], bounds[rank + 1]
     rowptr, col, val = wl.rows(r0, r1)
@@ -439,6 +443,14 @@ def main():
     csr_spmv = None
     host_rt_ms = None
     pat_spmv = None
+    csr_leg = None
+    # the same outer iteration with the Householder TSQR normalize (tsqr.m,
+    # BASELINE configs 3/4: "TSQR" / "RCCL TSQR tree"), every rank
+    tsqr_leg = None
+    if args.normalize != "tsqr" and not args.no_legs:
+        ctx.set_normalize("tsqr")
+        tsqr_leg = timed_leg(ctx, r_full[r0:r1], s, min(K, 10), min(W, 2), args.basis, args.orth, dist)
+        ctx.set_normalize(args.normalize)
     if world == 1 and rank == 0 and ctx.spmv_format()[0] == "pattern":
         # the bench's own SpMV kernel back to back on one x / y pair (the
         # Infinity Cache holds both): the kernel's rate outside the loop
@@ -448,6 +460,10 @@ def main():
         ctx2 = cal.Context(device=local, spmv_format="csr")
         ctx2.set_matrix(wl.full())
         csr_spmv = ctx2.bench_spmv(20, 1.0)
+        if not args.no_legs:
+            # the whole outer iteration with A in plain CSR (12 B / nonzero):
+            # SURVEY §8d's 619 / 691 outer-it/s bound is for this format
+            csr_leg = timed_leg(ctx2, r_full[r0:r1], s, min(K, 10), min(W, 2), args.basis, args.orth, None)
         ctx2.close()
         # tier-1 host-pointer SpMV (MATLAB-boundary semantics: PCIe in and out)
         v = np.ones(n)
@@ -472,7 +488,8 @@ def main():
     b_apply = (2 * s + 1 + s) * 8 * n_loc
     b_gram = (2 * s + 1) * 8 * n_loc
     spmv_gbps = b_spmv_launch / (spmv_avg_ms * 1e-3) / 1e9
-    per_step = {"spmv": spmv_ms / KT, "gram": gram_ms / KT, "apply": apply_ms / KT}
+    # (the first timed step's powers were prefetched untimed: SpMV = avg launch x s)
+    per_step = {"spmv": spmv_avg_ms * s, "gram": gram_ms / KT, "apply": apply_ms / KT}
     dominant = max(per_step, key=per_step.get)
     dom = {"spmv": (b_spmv_launch, spmv_avg_ms, ("k_spmv_pair (row-pattern SpMV, two rows per lane, + Newton shift)"
                                                  if npairpat else "k_spmv_pat_lds (row-pattern SpMV + Newton shift)")
@@ -501,6 +518,10 @@ def main():
         "data": wl.data,
         "config": {"workload": wl.desc % (n, nnz_total),
                    "s": s, "basis": args.basis, "orth": args.orth, "parallelism": "row-slab x%d" % world,
+                   "normalize": {"auto": "CholQR2 fused into the block-orthogonalisation sweeps (Householder TSQR "
+                                         "when its Cholesky fails; tsqr_step times the TSQR leg)",
+                                 "cholqr2": "CholQR2 (shifted CholQR3 fallback)",
+                                 "tsqr": "Householder TSQR tree"}[args.normalize],
                    "comm": (args.comm if world > 1 else "none"),
                    "halo": ("%s (CA matrix powers depth %d, band %d rows)"
                             % (ctx.MPK_SCHEDULES.get(sched, "?"), mpk["depth"], mpk["band_l"]))
@@ -530,6 +551,19 @@ def main():
         line["spmv_kernel_back_to_back"] = {"avg_us": pat_spmv[0] * 1e3, "min_us": pat_spmv[1] * 1e3,
                                             "gbps": b_spmv_launch / (pat_spmv[0] * 1e-3) / 1e9,
                                             "bytes_per_launch": b_spmv_launch}
+    if tsqr_leg is not None:
+        # per step: P1 Gram + pass-A projection Gram + TSQR up (leaf sweep
+        # "gram") + TSQR down (leaf sweep "apply") + tree levels ("other")
+        tsqr_leg["normalize"] = "Householder TSQR (tile QR per wave, stacked-R tree%s)" % (
+            ", RCCL allgather of the rank roots" if world > 1 else "")
+        line["tsqr_step"] = tsqr_leg
+    if csr_leg is not None:
+        csr_leg["spmv_format"] = "csr"
+        csr_leg["spmv_avg_us"] = csr_leg["kernel_avg_launch_us"]["spmv"]
+        csr_leg["spmv_gbps"] = b_csr / (csr_leg["spmv_avg_us"] * 1e-6) / 1e9
+        csr_leg["spmv_frac"] = csr_leg["spmv_gbps"] / HBM_PEAK_GBS
+        csr_leg["survey_bound_outer_iters_per_s"] = HBM_PEAK_GBS * 1e9 / (b_outer + 8 * n * (2 * s + 1))
+        line["csr_step"] = csr_leg
     if csr_spmv is not None:
         line["spmv_csr_kernel"] = {"avg_us": csr_spmv[0] * 1e3, "min_us": csr_spmv[1] * 1e3,
                                    "gbps": b_csr / (csr_spmv[0] * 1e-3) / 1e9, "bytes_per_launch": b_csr}
@@ -544,6 +578,45 @@ def main():
     emit(line)
     if dist is not None:
         dist.barrier()
+
+
+def timed_leg(ctx, r, s, K, W, basis, orth, dist):
+    """A secondary leg on the same workload: a fresh run, W warm-up and K
+    timed outer iterations (barrier + synchronize on both sides, max over
+    ranks), then one more with the per-kernel HIP-event timers."""
+    KT = 3
+    ctx.lanczos_begin(r, s, W + K + KT, basis, orth)
+    for _ in range(W):
+        ctx.lanczos_step(False)
+    ctx.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        ctx.lanczos_step(False)
+    ctx.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+    ctx.timer_enable(True)
+    ctx.timer_reset()
+    for _ in range(KT):
+        ctx.lanczos_step(False)
+    ctx.synchronize()
+    tm = {k: ctx.timer_read(k) for k in ("spmv", "gram", "apply", "other")}
+    ctx.timer_enable(False)
+    flags = ctx.lanczos_get()[3]
+    ctx.lanczos_end()
+    elapsed = max_over_ranks(dist, [elapsed])[0]
+    # the first timed step's matrix powers were prefetched by the untimed step
+    # before it: SpMV per step = average launch x s
+    per = {k: v[1] / KT for k, v in tm.items()}
+    per["spmv"] = tm["spmv"][1] / max(tm["spmv"][0], 1) * s
+    return {"outer_iters_per_s": K / elapsed, "ms_per_step": 1e3 * elapsed / K, "steps": K,
+            "reorth_passes": "%d/%d" % (int(np.sum(flags[W:W + K])), K),
+            "kernel_ms_per_step": per,
+            "kernel_avg_launch_us": {k: 1e3 * v[1] / max(v[0], 1) for k, v in tm.items()},
+            "kernel_launches": {k: v[0] for k, v in tm.items()}}
 
 
 def diagnostics_run(ctx, r, s, args, t=15):
