@@ -68,3 +68,24 @@ def test_bench_two_ranks_one_line():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["parallelism"] == "row-slab x2"
     assert d["config"]["comm"] == "host" and "cpu_baseline" not in d
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`bench.py --gpus 2` with no launcher (the driver's BENCH command shape)
+    starts the two ranks itself -- it must not silently measure one GPU.
+    Host-staged communicator: both ranks share the test box's GPU.  The TSQR
+    leg runs on both ranks (its tree's root all-gathered)."""
+    d = _bench("--gpus", "2", "--steps", "3", "--warmup", "1", "--workload", "lap3d_40", "--comm", "host",
+               timeout=300)
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["parallelism"] == "row-slab x2"
+    assert d["config"]["comm"] == "host" and "cpu_baseline" not in d
+    assert "tsqr_step" in d and d["tsqr_step"]["outer_iters_per_s"] > 0
+    assert d["tsqr_step"]["reorth_passes"] == d["reorth_passes"].replace("/3", "/3")
+
+
+def test_bench_rejects_mismatched_world():
+    """--gpus N under a launcher with another WORLD_SIZE exits non-zero."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and p.stdout.strip() == ""
