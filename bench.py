@@ -55,7 +55,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--basis-gb", type=float, default=200.0,
                    help="per-GPU budget for the Krylov basis Q; longer runs continue in restarted epochs")
-    p.add_argument("--cpu-iters", type=int, default=8, help="outer iterations of the C/OpenMP CPU sample")
+    p.add_argument("--cpu-iters", type=int, default=15, help="outer iterations of the C/OpenMP CPU sample")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "spmv_traffic.json"))
     p.add_argument("--mpk-depth", type=int, default=8,
                    help="N > 1: ghost depth of the CA matrix-powers kernel (1 = one halo exchange per SpMV)")

@@ -16,7 +16,7 @@
  *   projectAndNormalize.m:3-90 (doreorth = true, threshold 0.5 at :52)
  *   project.m:7-58 (one block, doreorth = false)
  *   normalize.m:3-36 / tsqr.m:7-12: Householder QR + sign fix.  The QR is a
- *   TSQR (Householder per thread block, Householder of the stacked R
+ *   TSQR (Householder per 2048-row tile, Householder of the stacked R
  *   factors, explicit Q through the tree): R is unique once its diagonal is
  *   made positive, so it equals MATLAB's qr(A,0) R up to rounding.
  * The Newton shifts / change-of-basis matrix Bk come from the caller (the
@@ -86,23 +86,24 @@ static void apply_q(size_t rows, int m, const double* A, size_t ld, const double
 }
 
 /* tsqr.m:7-12: [Q,R] = qr(X,0), d = sign(diag(R)), R = diag(d) R, Q = Q diag(d).
- * X (n x m, ld n) is overwritten by Q; R is m x m (ld m). */
+ * X (n x m, ld n) is overwritten by Q; R is m x m (ld m).  Two-level TSQR:
+ * Householder QR of cache-sized row tiles (in parallel), Householder QR of
+ * the stacked tile R factors, then each tile's Q applied to its block of the
+ * stack's Q. */
+#define TSQR_TILE 2048
 static void tsqr(size_t n, int m, double* X, double* R) {
-    int P = omp_get_max_threads();
-    if ((size_t)P * (size_t)m * 4 > n) P = 1;
-    double* Rs = calloc((size_t)P * m * m, sizeof(double));
-    double* taus = calloc((size_t)P * m, sizeof(double));
-#pragma omp parallel num_threads(P)
-    {
-        const int p = omp_get_thread_num();
-        const size_t r0 = n * (size_t)p / P, r1 = n * (size_t)(p + 1) / P;
+    const size_t nt = (n + TSQR_TILE - 1) / TSQR_TILE, PR = nt * (size_t)m;
+    double* Rs = calloc(PR * m, sizeof(double));
+    double* taus = calloc(nt * m, sizeof(double));
+#pragma omp parallel for schedule(dynamic, 4)
+    for (size_t t = 0; t < nt; ++t) {
+        const size_t r0 = t * TSQR_TILE, rows = (r0 + TSQR_TILE <= n ? TSQR_TILE : n - r0);
         double* Xb = X + r0;
-        geqr2(r1 - r0, m, Xb, n, taus + (size_t)p * m);
+        geqr2(rows, m, Xb, n, taus + t * m);
         for (int j = 0; j < m; ++j)
-            for (int i = 0; i <= j; ++i) Rs[IDX((size_t)p * m + i, j, (size_t)P * m)] = Xb[IDX(i, j, n)];
+            for (int i = 0; i <= j && (size_t)i < rows; ++i) Rs[IDX(t * m + i, j, PR)] = Xb[IDX(i, j, n)];
     }
     /* QR of the stacked R factors */
-    const size_t PR = (size_t)P * m;
     double* ttop = calloc(m, sizeof(double));
     geqr2(PR, m, Rs, PR, ttop);
     for (int j = 0; j < m; ++j)
@@ -110,61 +111,84 @@ static void tsqr(size_t n, int m, double* X, double* R) {
     double* Qtop = calloc(PR * m, sizeof(double));
     for (int j = 0; j < m; ++j) Qtop[IDX(j, j, PR)] = 1.0;
     apply_q(PR, m, Rs, PR, ttop, Qtop, PR, m);
-    /* Q block p = H_p [Qtop block p; 0] */
-#pragma omp parallel num_threads(P)
+    /* Q tile t = H_t [Qtop block t; 0] */
+#pragma omp parallel
     {
-        const int p = omp_get_thread_num();
-        const size_t r0 = n * (size_t)p / P, r1 = n * (size_t)(p + 1) / P, rows = r1 - r0;
-        double* Xb = X + r0;
-        double* C = calloc(rows * m, sizeof(double));
-        for (int j = 0; j < m; ++j)
-            for (int i = 0; i < m && (size_t)i < rows; ++i) C[IDX(i, j, rows)] = Qtop[IDX((size_t)p * m + i, j, PR)];
-        apply_q(rows, m, Xb, n, taus + (size_t)p * m, C, rows, m);
-        for (int j = 0; j < m; ++j) memcpy(Xb + (size_t)j * n, C + (size_t)j * rows, rows * sizeof(double));
+        double* C = malloc((size_t)TSQR_TILE * m * sizeof(double));
+#pragma omp for schedule(dynamic, 4)
+        for (size_t t = 0; t < nt; ++t) {
+            const size_t r0 = t * TSQR_TILE, rows = (r0 + TSQR_TILE <= n ? TSQR_TILE : n - r0);
+            double* Xb = X + r0;
+            memset(C, 0, rows * m * sizeof(double));
+            for (int j = 0; j < m; ++j)
+                for (int i = 0; i < m && (size_t)i < rows; ++i) C[IDX(i, j, rows)] = Qtop[IDX(t * m + i, j, PR)];
+            apply_q(rows, m, Xb, n, taus + t * m, C, rows, m);
+            for (int j = 0; j < m; ++j) memcpy(Xb + (size_t)j * n, C + (size_t)j * rows, rows * sizeof(double));
+        }
         free(C);
     }
     /* sign fix (sign(0) = 0, as MATLAB) */
+    double d[64];
     for (int j = 0; j < m; ++j) {
         const double rj = R[IDX(j, j, m)];
-        const double d = rj > 0.0 ? 1.0 : (rj < 0.0 ? -1.0 : 0.0);
-        for (int c = 0; c < m; ++c) R[IDX(j, c, m)] *= d;
-        double* q = X + (size_t)j * n;
-#pragma omp parallel for schedule(static)
-        for (size_t i = 0; i < n; ++i) q[i] *= d;
+        d[j] = rj > 0.0 ? 1.0 : (rj < 0.0 ? -1.0 : 0.0);
+        for (int c = 0; c < m; ++c) R[IDX(j, c, m)] *= d[j];
     }
+#pragma omp parallel for schedule(static)
+    for (size_t i = 0; i < n; ++i)
+        for (int j = 0; j < m; ++j) X[IDX(i, j, n)] *= d[j];
     free(Rs);
     free(taus);
     free(ttop);
     free(Qtop);
 }
 
-/* G (w x m, ld w) = Qp' X, Qp n x w, X n x m (both ld n) */
+/* G (w x m, ld w) = Qp' X, Qp n x w, X n x m (both ld n): row blocks, each a
+ * set of contiguous column segments (dot products over the block) */
+#define GEMM_BLK 1024
 static void gemm_tn(size_t n, int w, int m, const double* Qp, const double* X, double* G) {
     memset(G, 0, (size_t)w * m * sizeof(double));
+    const size_t nb = (n + GEMM_BLK - 1) / GEMM_BLK;
 #pragma omp parallel
     {
         double* acc = calloc((size_t)w * m, sizeof(double));
 #pragma omp for schedule(static)
-        for (size_t i = 0; i < n; ++i)
+        for (size_t b = 0; b < nb; ++b) {
+            const size_t i0 = b * GEMM_BLK, i1 = i0 + GEMM_BLK < n ? i0 + GEMM_BLK : n;
             for (int j = 0; j < m; ++j) {
-                const double x = X[IDX(i, j, n)];
-                for (int a = 0; a < w; ++a) acc[IDX(a, j, w)] += Qp[IDX(i, a, n)] * x;
+                const double* x = X + (size_t)j * n;
+                for (int a = 0; a < w; ++a) {
+                    const double* q = Qp + (size_t)a * n;
+                    double sum = 0.0;
+                    for (size_t i = i0; i < i1; ++i) sum += q[i] * x[i];
+                    acc[IDX(a, j, w)] += sum;
+                }
             }
+        }
 #pragma omp critical
         for (size_t e = 0; e < (size_t)w * m; ++e) G[e] += acc[e];
         free(acc);
     }
 }
 
-/* X -= Qp G */
+/* X -= Qp G, by row blocks and columns */
 static void gemm_sub(size_t n, int w, int m, const double* Qp, const double* G, double* X) {
+    const size_t nb = (n + GEMM_BLK - 1) / GEMM_BLK;
 #pragma omp parallel for schedule(static)
-    for (size_t i = 0; i < n; ++i)
+    for (size_t b = 0; b < nb; ++b) {
+        const size_t i0 = b * GEMM_BLK, i1 = i0 + GEMM_BLK < n ? i0 + GEMM_BLK : n;
+        double s[GEMM_BLK];
         for (int j = 0; j < m; ++j) {
-            double s = 0.0;
-            for (int a = 0; a < w; ++a) s += Qp[IDX(i, a, n)] * G[IDX(a, j, w)];
-            X[IDX(i, j, n)] -= s;
+            for (size_t i = i0; i < i1; ++i) s[i - i0] = 0.0;
+            for (int a = 0; a < w; ++a) {
+                const double* q = Qp + (size_t)a * n;
+                const double g = G[IDX(a, j, w)];
+                for (size_t i = i0; i < i1; ++i) s[i - i0] += q[i] * g;
+            }
+            double* x = X + (size_t)j * n;
+            for (size_t i = i0; i < i1; ++i) x[i] -= s[i - i0];
         }
+    }
 }
 
 static double col_norm(size_t n, const double* x) {
