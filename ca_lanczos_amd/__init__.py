@@ -18,6 +18,7 @@ from .api import (  # noqa: F401
     default_context,
     eig,
     leja,
+    matlab_rand,
     matrix_powers_monomial,
     matrix_powers_newton,
     newton_basis_matrix,

@@ -91,6 +91,7 @@ SIGNATURES = [
     ("cal_cholqr", c_int, [c_void_p, c_int64, c_int, dp, dp, dp]),
     ("cal_project", c_int, [c_void_p, c_int64, c_int, POINTER(dp), ip, c_int, dp, c_int, dp, POINTER(dp)]),
     ("cal_normalize", c_int, [c_void_p, c_int64, c_int, dp, c_double, dp, dp, ip]),
+    ("cal_normalize_opt", c_int, [c_void_p, c_int64, c_int, dp, c_char_p, c_double, dp, dp, ip]),
     ("cal_project_and_normalize", c_int,
      [c_void_p, c_int64, c_int, POINTER(dp), ip, c_int, dp, c_int, dp, POINTER(dp), ip, ip]),
     ("cal_ca_lanczos", c_int,
@@ -114,6 +115,7 @@ SIGNATURES = [
     ("cal_leja", c_int, [c_int, dp, dp, dp, dp, ip]),
     ("cal_newton_basis_matrix", c_int, [c_int, dp, dp, c_int, dp]),
     ("cal_eig", c_int, [c_int, dp, c_int, dp, dp, dp]),
+    ("cal_matlab_rand", c_int, [c_int64, ctypes.c_uint, dp]),
     ("cal_tridiag_eigvals", c_int, [c_int, dp, dp, dp]),
     ("cal_qrstep", c_int, [c_int, dp, c_int, dp, c_int, c_double]),
 ]

@@ -135,6 +135,20 @@ class Context:
         self.n = A.shape[0]
         return self
 
+    def set_matrix_csc(self, A):
+        """MATLAB's sparse storage (mxGetJc / mxGetIr / mxGetPr: CSC with int64
+        mwIndex arrays) through cal_set_matrix_csc, the entry a MEX shim uses."""
+        A = sp.csc_matrix(A)
+        A.sort_indices()
+        jc = np.ascontiguousarray(A.indptr, dtype=np.int64)
+        ir = np.ascontiguousarray(A.indices, dtype=np.int64)
+        pr = np.ascontiguousarray(A.data, dtype=np.float64)
+        check(self.h, lib.cal_set_matrix_csc(self.h, A.shape[0], jc.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                             ir.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), ptr(pr)),
+              "set_matrix_csc")
+        self.n = A.shape[0]
+        return self
+
     def set_matrix_slab(self, n_global, row0, A_rows):
         """Distributed: rows [row0, row0+nlocal) of A (global column ids)."""
         A_rows = sp.csr_matrix(A_rows)
@@ -349,17 +363,25 @@ def project(Q, X, doreorth=False):
 
 
 def normalize(X, opt="None", tol=1.0e-8):
-    """``[Q,R,rank] = normalize(X,opt,tol)`` -- normalize.m:3-36."""
-    if str(opt).lower() == "randomizenullspace":
-        raise NotImplementedError("normalize(...,'randomizeNullSpace') is not on the hot path")
+    """``[Q,R,rank] = normalize(X,opt,tol)`` -- normalize.m:3-36; opt
+    'randomizeNullSpace' runs normalize.m:28-31,38-51 (the null-space
+    columns drawn from a fresh MATLAB rand stream, seed 5489)."""
     ctx = default_context()
     X = f64(X)
     n, m = X.shape
     Q = np.zeros((n, m), order="F")
     R = np.zeros((m, m), order="F")
     rank = ctypes.c_int()
-    check(ctx.h, lib.cal_normalize(ctx.h, n, m, ptr(X), tol, ptr(Q), ptr(R), ctypes.byref(rank)), "normalize")
+    check(ctx.h, lib.cal_normalize_opt(ctx.h, n, m, ptr(X), str(opt).encode(), tol, ptr(Q), ptr(R),
+                                       ctypes.byref(rank)), "normalize")
     return Q, R, rank.value
+
+
+def matlab_rand(count, seed=5489):
+    """MATLAB ``rand`` of a fresh session (rng(seed,'twister')): cal_matlab_rand."""
+    out = np.zeros(int(count))
+    check(None, lib.cal_matlab_rand(int(count), int(seed), ptr(out)), "matlab_rand")
+    return out
 
 
 def projectAndNormalize_ex(Q, X, doreorth=True):

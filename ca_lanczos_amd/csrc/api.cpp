@@ -4,10 +4,12 @@
 // SpMV.m, matrix_powers_*.m, tsqr.m, cholqr.m, project.m, normalize.m and
 // projectAndNormalize.m binds; the device-resident tier is lanczos.cpp.
 #include <algorithm>
+#include <random>
 #include <cmath>
 #include <string>
 #include <vector>
 
+#include "../../include/calanczos_host.h"
 #include "cal_internal.hpp"
 #include "dense.hpp"
 
@@ -164,22 +166,75 @@ int cal_tsqr(cal_ctx* c, int64_t n, int m, const double* A, double* Q, double* R
 }
 
 int cal_normalize(cal_ctx* c, int64_t n, int m, const double* X, double tol, double* Q, double* R, int* rank) {
+    return cal_normalize_opt(c, n, m, X, "None", tol, Q, R, rank);
+}
+
+int cal_normalize_opt(cal_ctx* c, int64_t n, int m, const double* X, const char* opt, double tol, double* Q,
+                      double* R, int* rank) {
     Tier1 t1(c);
     CAL_TRY(check_ctx(c, false));
     if (!X || !Q || !R || n < 1 || m < 1 || m > 32) return set_error(c, CAL_ERR_ARG, "normalize: need 1 <= m <= 32");
+    std::string o = opt ? opt : "None";
+    for (auto& ch : o) ch = (char)tolower(ch);
+    const bool randomize = o == "randomizenullspace";  // normalize.m:28 strcmpi
     const int64_t ld = ld_for(n);
-    CAL_TRY(ensure_scratch(c, (size_t)2 * m * ld));
+    CAL_TRY(ensure_scratch(c, (size_t)3 * m * ld));
     double* dX = c->d_scratch;
     double* dQ = c->d_scratch + (size_t)m * ld;
+    double* dW = c->d_scratch + (size_t)2 * m * ld;
     CAL_TRY(upload(c, dX, ld, X, n, m));
     Panel P = panel();
     panel_add(P, dX, ld, m);
     int rk = 0;
     bool sh = false;
-    CAL_TRY(normalize_dev(c, n, P, panel_out(dQ, ld, m), R, tol > 0 ? tol : 1.0e-8, &rk, &sh));
+    CAL_TRY(normalize_dev(c, n, P, panel_out(dQ, ld, m), R, tol > 0 ? tol : 1.0e-8, &rk, &sh));  // :14-24
     if (rank) *rank = rk;
+    if (randomize && rk < m) {
+        // :29-31: [U,S,W] = svd(R); R = S*W'; Q = Q*U; randomizeNullSpace(Q, rank)
+        std::vector<double> U((size_t)m * m), S(m), W((size_t)m * m);
+        dense::svd(m, R, m, U.data(), S.data(), W.data());
+        for (int j = 0; j < m; ++j)
+            for (int i = 0; i < m; ++i) R[i + (size_t)j * m] = S[i] * W[j + (size_t)i * m];
+        Panel Qp = panel();
+        panel_add(Qp, dQ, ld, m);
+        const PanelOut Wo = panel_out(dW, ld, m);
+        CAL_TRY(apply_host(c, n, Qp, U.data(), m, &Wo, nullptr, 0, nullptr));
+        // :43-50: Q(:,null) = rand(nrows, ncols-rank); project against Q(:,1:rank); tsqr
+        const int k = m - rk;
+        std::vector<double> h((size_t)n * k);
+        cal_matlab_rand(n * k, 5489, h.data());
+        double* dN = dW + (size_t)rk * ld;
+        CAL_TRY(upload(c, dN, ld, h.data(), n, k));
+        if (rk > 0) {
+            std::vector<double*> blocks{dW};
+            const int widths[1] = {rk};
+            std::vector<std::vector<double>> R_(1);
+            CAL_TRY(project_blocks(c, n, ld, 1, blocks, widths, k, dN, false, R_));
+        }
+        Panel Np = panel();
+        panel_add(Np, dN, ld, k);
+        std::vector<double> Rn((size_t)k * k);
+        if (tsqr_ok(k)) {
+            CAL_TRY(tsqr_dev(c, n, Np, nullptr, k, panel_out(dN, ld, k), Rn.data()));
+        } else {
+            CAL_TRY(normalize_wide_dev(c, n, ld, dN, k, dN, dX));
+        }
+        CAL_TRY(download(c, Q, dW, ld, n, m));
+        return CAL_WARN_RANK_DEFICIENT;
+    }
     CAL_TRY(download(c, Q, dQ, ld, n, m));
     return rk < m ? CAL_WARN_RANK_DEFICIENT : 0;
+}
+
+// MATLAB rand (MT19937 genrand_res53) of a fresh stream seeded `seed`
+int cal_matlab_rand(int64_t count, unsigned seed, double* out) {
+    if (count < 0 || (count > 0 && !out)) return CAL_ERR_ARG;
+    std::mt19937 g(seed);
+    for (int64_t i = 0; i < count; ++i) {
+        const uint32_t a = g() >> 5, b = g() >> 6;
+        out[i] = (a * 67108864.0 + b) / 9007199254740992.0;
+    }
+    return 0;
 }
 
 int cal_cholqr(cal_ctx* c, int64_t n, int m, const double* X, double* Q, double* R) {

@@ -147,6 +147,89 @@ void singular_values(int m, const double* A, int lda, double* sv) {
     std::sort(sv, sv + m, [](double x, double y) { return x > y; });
 }
 
+// Full SVD of a small square matrix by one-sided Jacobi: A V = U S with the
+// singular values descending; U's columns for zero singular values are
+// completed to an orthonormal basis.
+void svd(int m, const double* A, int lda, double* U, double* S, double* V) {
+    std::vector<double> W((size_t)m * m), Vw((size_t)m * m, 0.0);
+    for (int j = 0; j < m; ++j) {
+        for (int i = 0; i < m; ++i) W[i + (size_t)j * m] = A[i + (size_t)j * lda];
+        Vw[j + (size_t)j * m] = 1.0;
+    }
+    const double eps = std::ldexp(1.0, -52);
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        double off = 0.0;
+        for (int p = 0; p < m - 1; ++p)
+            for (int q = p + 1; q < m; ++q) {
+                double a = 0, b = 0, c = 0;
+                for (int i = 0; i < m; ++i) {
+                    const double up = W[i + (size_t)p * m], uq = W[i + (size_t)q * m];
+                    a += up * up;
+                    b += uq * uq;
+                    c += up * uq;
+                }
+                if (std::fabs(c) <= eps * std::sqrt(a * b) || c == 0.0) continue;
+                off = std::max(off, std::fabs(c) / std::sqrt(a * b));
+                const double zeta = (b - a) / (2.0 * c);
+                const double t = (zeta >= 0 ? 1.0 : -1.0) / (std::fabs(zeta) + std::sqrt(1.0 + zeta * zeta));
+                const double cs = 1.0 / std::sqrt(1.0 + t * t), sn = cs * t;
+                for (int i = 0; i < m; ++i) {
+                    const double up = W[i + (size_t)p * m], uq = W[i + (size_t)q * m];
+                    W[i + (size_t)p * m] = cs * up - sn * uq;
+                    W[i + (size_t)q * m] = sn * up + cs * uq;
+                    const double vp = Vw[i + (size_t)p * m], vq = Vw[i + (size_t)q * m];
+                    Vw[i + (size_t)p * m] = cs * vp - sn * vq;
+                    Vw[i + (size_t)q * m] = sn * vp + cs * vq;
+                }
+            }
+        if (off <= eps) break;
+    }
+    std::vector<double> sv(m);
+    std::vector<int> ord(m);
+    for (int j = 0; j < m; ++j) {
+        double s2 = 0;
+        for (int i = 0; i < m; ++i) s2 += W[i + (size_t)j * m] * W[i + (size_t)j * m];
+        sv[j] = std::sqrt(s2);
+        ord[j] = j;
+    }
+    std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return sv[x] > sv[y]; });
+    const double small = sv[ord[0]] * m * eps;
+    int nz = 0;
+    for (int k = 0; k < m; ++k) {
+        const int j = ord[k];
+        S[k] = sv[j];
+        for (int i = 0; i < m; ++i) V[i + (size_t)k * m] = Vw[i + (size_t)j * m];
+        if (sv[j] > small && sv[j] > 0.0) {
+            for (int i = 0; i < m; ++i) U[i + (size_t)k * m] = W[i + (size_t)j * m] / sv[j];
+            nz = k + 1;
+        } else {
+            for (int i = 0; i < m; ++i) U[i + (size_t)k * m] = 0.0;
+        }
+    }
+    // complete U: Gram-Schmidt (twice) of unit vectors against the columns so far
+    int next_e = 0;
+    for (int k = nz; k < m; ++k) {
+        for (; next_e < m; ++next_e) {
+            std::vector<double> u(m, 0.0);
+            u[next_e] = 1.0;
+            for (int pass = 0; pass < 2; ++pass)
+                for (int c = 0; c < k; ++c) {
+                    double d = 0;
+                    for (int i = 0; i < m; ++i) d += U[i + (size_t)c * m] * u[i];
+                    for (int i = 0; i < m; ++i) u[i] -= d * U[i + (size_t)c * m];
+                }
+            double nu = 0;
+            for (int i = 0; i < m; ++i) nu += u[i] * u[i];
+            nu = std::sqrt(nu);
+            if (nu > 0.5) {
+                for (int i = 0; i < m; ++i) U[i + (size_t)k * m] = u[i] / nu;
+                ++next_e;
+                break;
+            }
+        }
+    }
+}
+
 // Symmetric eigenproblem: Householder reduction to tridiagonal form with the
 // transformations accumulated (EISPACK tred2), then the implicit QL iteration
 // with Wilkinson-type shifts applied to the accumulated vectors (tql2).

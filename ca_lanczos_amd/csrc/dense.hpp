@@ -22,6 +22,9 @@ void rdiv_upper(int r, int m, double* X, int ldx, const double* R, int ldr);
 bool tridiag_eigvals(int n, const double* d, const double* e, double* w);
 // Singular values of a small square matrix (one-sided Jacobi), descending.
 void singular_values(int m, const double* A, int lda, double* sv);
+// Full SVD A = U diag(S) V' of a small square matrix (one-sided Jacobi),
+// singular values descending; U completed to orthonormal for zero values.
+void svd(int m, const double* A, int lda, double* U, double* S, double* V);
 // General real eigenproblem (Householder Hessenberg reduction + shifted QR,
 // EISPACK orthes/hqr2 algorithm).  A (n x n) is not modified.  On return
 // wr/wi hold the eigenvalues; V (n x n) holds real vectors in the column of a

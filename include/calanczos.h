@@ -136,6 +136,13 @@ int cal_project(cal_ctx* ctx, int64_t n, int nblocks, const double* const* Q, co
 /* [Q,R,rank] = normalize(X,'None',tol).                               normalize.m:3-36 */
 int cal_normalize(cal_ctx* ctx, int64_t n, int m, const double* X, double tol, double* Q, double* R,
                   int* rank);
+/* [Q,R,rank] = normalize(X,opt,tol), opt "None" or "randomizeNullSpace"
+ * (normalize.m:28-31,38-51: when rank < m, R = S*W' and Q = Q*U from svd(R),
+ * then the null-space columns are replaced by rand (a fresh MT19937 stream,
+ * seed 5489 -- cal_matlab_rand), projected against Q(:,1:rank) and tsqr'd).
+ * Returns CAL_WARN_RANK_DEFICIENT when rank < m.  m <= 32. */
+int cal_normalize_opt(cal_ctx* ctx, int64_t n, int m, const double* X, const char* opt, double tol, double* Q,
+                      double* R, int* rank);
 /* [QZ,RZ] = projectAndNormalize(Q,X,doreorth); RZ has nblocks+1 entries:
  * RZ[i] widths[i] x m, RZ[nblocks] m x m.  *reorth = 1 when the reference
  * would disp('second').                                    projectAndNormalize.m:3-90 */

@@ -29,6 +29,9 @@ int cal_newton_basis_matrix(int s, const double* lam_re, const double* lam_im, i
 /* [V,D] = eig(T) for the Ritz analysis (ca_lanczos.m:229): symmetric solver
  * when T is exactly symmetric, general (Hessenberg QR) otherwise.  V is n x n
  * column-major; complex pairs are stored as (real, imag) column pairs. */
+/* MATLAB rand of a fresh session with rng(seed,'twister'): MT19937
+ * genrand_res53, `count` values in column-major order. */
+int cal_matlab_rand(int64_t count, unsigned seed, double* out);
 int cal_eig(int n, const double* T, int ldt, double* wr, double* wi, double* V);
 
 /* Eigenvalues of the symmetric tridiagonal T = diag(alpha) + diag(beta,+-1),

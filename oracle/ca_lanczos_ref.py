@@ -264,7 +264,7 @@ def _randomize_null_space(Q, rank, rng):
     nrows, ncols = Q.shape
     null = list(range(rank, ncols))
     Q = Q.copy()
-    Q[:, null] = rng.random_sample((nrows, len(null)))
+    Q[:, null] = rng.random_sample(nrows * len(null)).reshape((nrows, len(null)), order="F")  # MATLAB fills by columns
     Q[:, null], _ = project([Q[:, :rank]], Q[:, null])
     Q[:, null], _ = tsqr(Q[:, null])
     return Q

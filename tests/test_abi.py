@@ -123,3 +123,12 @@ def test_qrstep_matches_oracle_up_to_signs(cal, ref):
             assert np.max(np.abs(W * sg - Wr)) < 1e-9
             assert np.max(np.abs(H * np.outer(sg, sg) - Hr)) < 1e-9 * np.abs(H0).max()
             assert np.max(np.abs(np.tril(H, -2))) == 0.0
+
+
+def test_matlab_rand_matches_mt19937(cal, ref):
+    """cal_matlab_rand (the null-space fill of normalize's randomizeNullSpace)
+    is MATLAB's rand of a fresh session: MT19937 genrand_res53, the oracle's
+    RandomState(seed).random_sample."""
+    for seed in (5489, 7):
+        assert np.array_equal(cal.matlab_rand(1000, seed), ref.matlab_rand(1000, seed=seed))
+

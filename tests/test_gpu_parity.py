@@ -658,3 +658,48 @@ def test_project_and_normalize_ill_conditioned(cal, ref, cond):
     assert np.max(np.abs(RZ[0] - RZr[0])) <= 1e-12 * np.linalg.norm(X, 2)
     assert np.linalg.norm(QZ.T @ QZ - np.eye(m), 2) <= 1e-13
     assert np.max(np.abs(QZ.T @ Qp)) <= 10 * np.max(np.abs(QZr.T @ Qp)) + 1e-13
+
+
+def test_set_matrix_csc_matlab_layout(cal, ref):
+    """The MEX entry for A: MATLAB's CSC arrays (int64 mwIndex jc / ir, pr)
+    through cal_set_matrix_csc.  SpMV bit-identical to the CSR entry and to
+    the oracle; a whole ca_lanczos run identical bit for bit."""
+    import scipy.sparse as sp
+    rng = np.random.RandomState(4)
+    n = 2000
+    B = sp.random(n, n, density=0.003, random_state=rng, format="csr")
+    A = (B + B.T + sp.diags(np.full(n, 4.0))).tocsr()
+    A.sort_indices()
+    c1 = cal.Context().set_matrix_csc(A.tocsc())
+    c2 = cal.Context().set_matrix(A)
+    v = ref.matlab_rand(n, seed=3) - 0.5
+    y1 = c1.spmv(v)
+    assert np.array_equal(y1, c2.spmv(v)) and np.array_equal(y1, ref.SpMV(A, v))
+    r = ref.matlab_rand(n)
+    o1 = cal.ca_lanczos_ex(A, r, 8, 48, "newton", "local", diagnostics=True, ctx=c1)
+    o2 = cal.ca_lanczos_ex(A, r, 8, 48, "newton", "local", diagnostics=True, ctx=c2)
+    assert np.array_equal(o1.T, o2.T) and np.array_equal(o1.Q, o2.Q)
+    assert np.array_equal(o1.ritz_rnorm, o2.ritz_rnorm)
+    c1.close()
+    c2.close()
+
+
+def test_normalize_randomize_null_space(cal, ref):
+    """normalize(X,'randomizeNullSpace') (normalize.m:28-31,38-51) on a rank-5
+    block of 8 columns: same rank; R = S W' and Q(:,1:rank) = Q U match the
+    oracle up to the sign of each singular pair; the null-space columns
+    (MATLAB rand of a fresh stream, projected, tsqr'd) match to 1e-10; Q
+    orthonormal to 1e-13 and Q R = X to 1e-12 ||X||."""
+    rng = np.random.RandomState(21)
+    n, m, rk = 5000, 8, 5
+    X = np.asfortranarray(rng.randn(n, rk) @ rng.randn(rk, m))
+    Q, R, rank = cal.normalize(X, "randomizeNullSpace")
+    Qr, Rr, rank_r = ref.normalize(X, "randomizeNullSpace")
+    assert rank == rank_r == rk
+    nx = np.linalg.norm(X, 2)
+    assert np.linalg.norm(Q.T @ Q - np.eye(m), 2) <= 1e-13
+    assert np.linalg.norm(Q @ R - X, 2) <= 1e-12 * nx
+    sg = np.sign(np.sum(Q[:, :rk] * Qr[:, :rk], axis=0))
+    assert np.max(np.abs(Q[:, :rk] * sg - Qr[:, :rk])) <= 1e-10
+    assert np.max(np.abs(R[:rk] * sg[:, None] - Rr[:rk])) <= 1e-10 * nx
+    assert np.max(np.abs(Q[:, rk:] - Qr[:, rk:])) <= 1e-10
