@@ -127,7 +127,7 @@ static int gram_host16(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, do
 }
 
 // Y = P * M with M (wp x wy, column-major) already on the device; store only.
-static int apply_dev(cal_ctx* c, int64_t n, const Panel& P, const double* dM, int wy, const PanelOut& Y) {
+int apply_dev(cal_ctx* c, int64_t n, const Panel& P, const double* dM, int wy, const PanelOut& Y) {
     const int wp = P.total;
     const int wpp = (wp + 3) & ~3;
     int max_nty = 8192 / (wpp * 16);

@@ -239,6 +239,18 @@ hipError_t launch_gather(double* dst, const double* src, const int* idx, int64_t
 int gram_async(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* d_dst, double* h_dst, int* ldc);
 int spmv_pair_resid_blocks(const PatArgs& a);
 hipError_t launch_spmv_pair_resid(const PatArgs& a, double lr, double* partial, hipStream_t st);
+// the same for npr real Ritz pairs in one launch: x_i = X + col[i] * ldx,
+// l_i = lam[i]; sums of pair i at partial[(2 out[i] + e) * pstride + block]
+hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64_t ldx, const int* col,
+                                        const double* lam, const int* out, int npr, double* partial,
+                                        int64_t pstride, hipStream_t st);
+int spmv_resid_pair_multi_dev(cal_ctx* c, const double* X, int64_t ldx, const int* col, const double* lam,
+                              const int* out, int npr, double* partial, int64_t pstride);
+// store-only Y = P M on the matrix cores (one segment each, 16-B aligned,
+// Y not aliasing P; M wp x wy column-major on the device)
+bool apply_mt_ok(int wp, int wy);
+hipError_t launch_apply_mt(const double* P, int64_t ldp, const double* dM, int wp, int wy, double* Y, int64_t ldy,
+                           int64_t n, hipStream_t st);
 // Ritz residual partials of a real Ritz value on the pair patterns (local
 // rows; x's halo already exchanged): *blocks = 0 when the path does not apply
 int spmv_resid_pair_dev(cal_ctx* c, const double* x, double lr, double* partial, int* blocks);
@@ -417,6 +429,8 @@ int gram_host(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* out
 // and gramp (Psub^T Y, wq x wy where Psub = first wq columns of P), on host.
 int apply_host(cal_ctx* c, int64_t n, const Panel& P, const double* M, int wy, const PanelOut* Y, double* gram,
                int wq, double* gramp);
+// Y = P * M, M (wp x wy) already on the device; store only
+int apply_dev(cal_ctx* c, int64_t n, const Panel& P, const double* dM, int wy, const PanelOut& Y);
 // Reorthogonalisation helpers used by the driver and the C ABI.
 struct PNResult {
     bool reorth = false;

@@ -27,7 +27,9 @@
 //   k_reduce        fixed-order sum of block partials.
 //   k_dot, k_axpy_sub(_dev), k_div(_sqrt), k_gather, k_spmv_resid,
 //   k_form_projM, k_abs_rowsum: small vector kernels.
+#include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "cal_internal.hpp"
 
@@ -490,6 +492,111 @@ __global__ __launch_bounds__(256) void k_spmv_pair_resid(PatArgs a, const uint16
     }
 }
 
+// k_spmv_pair_resid over many Ritz pairs in one launch: blockIdx.y takes
+// pairs [CPB y, CPB y + CPB) of the list (x = X + col[i] * ldx, l = lam[i]);
+// the pair ids and the table are loaded once per block and reused for every
+// pair.  Per pair the products, the per-lane sums, the wave sums and the
+// block sum are those of k_spmv_pair_resid, so are the bits; the block's
+// two sums go to partial[(2 out[i] + e) * pstride + blockIdx.x].
+template <int MAXLEN, int CPB>
+__global__ __launch_bounds__(256) void k_spmv_pair_resid_multi(PatArgs a, const uint16_t* __restrict__ ppat,
+                                                              const int* __restrict__ ppoff,
+                                                              const double2* __restrict__ ppval,
+                                                              const double* __restrict__ X, int64_t ldx,
+                                                              const int* __restrict__ col,
+                                                              const double* __restrict__ lam,
+                                                              const int* __restrict__ out, int npairs_ritz,
+                                                              double* __restrict__ partial, int64_t pstride) {
+    extern __shared__ __attribute__((aligned(16))) double lds_pair[];
+    double2* s_pv = reinterpret_cast<double2*>(lds_pair);
+    int* s_poff = reinterpret_cast<int*>(s_pv + a.npent);
+    __shared__ double ws[CPB][2][4];
+    const int tid = threadIdx.x;
+    const int64_t npairs = (a.n + 1) >> 1;
+    const int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 256 + tid;
+    const int64_t tcl = t < npairs ? t : npairs - 1;
+    const int id = ppat[tcl];
+    const int64_t r0 = 2 * tcl;
+    for (int i = tid; i < a.npent; i += 256) {
+        s_pv[i] = ppval[i];
+        s_poff[i] = ppoff[i];
+    }
+    __syncthreads();
+    const int i0 = blockIdx.y * CPB;
+    const int nq = npairs_ritz - i0 < CPB ? npairs_ritz - i0 : CPB;  // uniform over the block
+    const int lane = tid & 63, wave = tid >> 6;
+    const bool two = r0 + 1 < a.n;  // see k_spmv_pair_resid (odd distributed slab)
+    const int base = id != kPairSplit ? id * MAXLEN : 0;
+    // the pair's table entries, read from LDS once for all CPB columns
+    int code[MAXLEN];
+    double2 v[MAXLEN];
+#pragma unroll
+    for (int e = 0; e < MAXLEN; ++e) {
+        code[e] = s_poff[base + e];
+        v[e] = s_pv[base + e];
+    }
+    // one column at a time (two columns' loads in flight measured slower:
+    // 2.9 vs 2.2 ms per 64 columns at n = 9.94 M)
+    for (int q = 0; q < nq; ++q) {
+        const double* x = X + (int64_t)col[i0 + q] * ldx;
+        const double l = lam[i0 + q];
+        double2 xc[MAXLEN];
+#pragma unroll
+        for (int e = 0; e < MAXLEN; ++e) {
+            int64_t ad = r0 + a.pslot[e];
+            ad = ad < a.xlo ? a.xlo : (ad > a.xhi - 2 ? a.xhi - 2 : ad);
+            xc[e] = ld16(x + ad);
+        }
+        const double2 xs = ld16(x + (r0 < a.xhi - 2 ? r0 : a.xhi - 2));
+        double nu = 0.0, de = 0.0;
+        if (t < npairs) {
+            if (id != kPairSplit) {
+                double y0 = 0.0, y1 = 0.0;
+#pragma unroll
+                for (int e = 0; e < MAXLEN; ++e) {
+                    const double t0 = v[e].x * xc[e].x, t1 = v[e].y * xc[e].y;
+                    double a0 = y0 + t0, a1 = y1 + t1;
+                    asm volatile("" : "+v"(a0), "+v"(a1));
+                    y0 = (code[e] & 1) ? a0 : y0;
+                    y1 = (code[e] & 2) ? a1 : y1;
+                }
+                const double u0 = l * xs.x, u1 = l * xs.y;
+                y0 = y0 - u0;
+                y1 = y1 - u1;
+                nu = y0 * y0 + (two ? y1 * y1 : 0.0);
+                de = u0 * u0 + (two ? u1 * u1 : 0.0);
+            } else {
+                for (int k = 0; k < 2 && r0 + k < a.n; ++k) {
+                    const int64_t rr = r0 + k;
+                    const int2 pi = a.pinfo[a.pat[rr]];
+                    double sum = 0.0;
+                    for (int e = 0; e < pi.y; ++e) {
+                        const double tv = a.pval[pi.x + e] * x[rr + a.pdelta[pi.x + e]];
+                        sum = sum + tv;
+                    }
+                    const double u = l * x[rr];
+                    const double y = sum - u;
+                    nu = nu + y * y;
+                    de = de + u * u;
+                }
+            }
+        }
+        nu = wave_sum(nu);
+        de = wave_sum(de);
+        if (lane == 0) {
+            ws[q][0][wave] = nu;
+            ws[q][1][wave] = de;
+        }
+    }
+    __syncthreads();
+    if (tid < 2 * CPB) {
+        const int q = tid >> 1, e = tid & 1;
+        if (i0 + q < npairs_ritz)
+            partial[(2 * (int64_t)out[i0 + q] + e) * pstride + blockIdx.x] =
+                ((ws[q][e][0] + ws[q][e][1]) + ws[q][e][2]) + ws[q][e][3];
+    }
+}
+
 constexpr size_t kPatLdsMax = 64 * 1024;
 
 // the pair kernel needs 16-B aligned columns, rows <= 8 entries and an LDS-sized pair table
@@ -581,6 +688,45 @@ hipError_t launch_spmv_pair_resid(const PatArgs& a, double lr, double* partial, 
         default: return hipErrorInvalidValue;
     }
 #undef CAL_PRR
+    return hipGetLastError();
+}
+
+hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64_t ldx, const int* col,
+                                        const double* lam, const int* out, int npr, double* partial,
+                                        int64_t pstride, hipStream_t st) {
+    // Ritz pairs per block (CAL_RESID_CPB = 2 / 4 / 8 for A/B): more pairs
+    // share the table reads, fewer keep the blocks in flight on fewer columns
+    static const int cpb = [] {
+        const char* e = std::getenv("CAL_RESID_CPB");
+        const int v = e ? std::atoi(e) : 4;
+        return v == 2 || v == 8 ? v : 4;
+    }();
+    const int blocks = spmv_pair_resid_blocks(a);
+    if (blocks <= 0 || pstride < blocks) return hipErrorInvalidValue;
+    if (npr <= 0) return hipSuccess;
+    const size_t lds = (size_t)a.npent * 20 + 16;
+    auto go = [&](auto cpb_c) {
+        constexpr int CPB = decltype(cpb_c)::value;
+        dim3 g(blocks, (npr + CPB - 1) / CPB), bl(256);
+#define CAL_PRM(ML)                                                                                                \
+    hipLaunchKernelGGL((k_spmv_pair_resid_multi<ML, CPB>), g, bl, lds, st, a, a.ppat, a.ppoff, a.ppval, X, ldx, col, \
+                       lam, out, npr, partial, pstride)
+        switch (a.pmaxlen) {
+            case 1: CAL_PRM(1); break;
+            case 2: CAL_PRM(2); break;
+            case 3: CAL_PRM(3); break;
+            case 4: CAL_PRM(4); break;
+            case 5: CAL_PRM(5); break;
+            case 6: CAL_PRM(6); break;
+            case 7: CAL_PRM(7); break;
+            default: CAL_PRM(8); break;
+        }
+#undef CAL_PRM
+    };
+    if (a.pmaxlen > 8) return hipErrorInvalidValue;
+    if (cpb == 2) go(std::integral_constant<int, 2>{});
+    else if (cpb == 8) go(std::integral_constant<int, 8>{});
+    else go(std::integral_constant<int, 4>{});
     return hipGetLastError();
 }
 
@@ -711,6 +857,99 @@ __global__ __launch_bounds__(256) void k_gram(Panel A, Panel B, int64_t n, doubl
     }
 }
 
+// k_gram with coalesced loads: the same rows feed the same MFMAs in the same
+// order (so the same bits), but a block's 16 RUN rows (its four waves' row
+// runs of one grid step) are first loaded column by column with one row per
+// lane -- 512 contiguous bytes per wave instruction instead of 16 column
+// pieces -- and staged in LDS ([row][col], odd leading dimension), then read
+// back in k_gram's operand layout: lane (c16, g) of wave w takes row
+// w*4RUN + g*RUN + m of column 16t + c16 for MFMA m of tile t.  The B tile
+// is read once per row block into registers; A goes through LDS 16 columns
+// at a time, the next chunk's loads in flight during the current MFMAs.
+template <int NTA, int RUN>
+__global__ __launch_bounds__(256) void k_gram_lds(Panel A, Panel B, int64_t n, double* __restrict__ partial) {
+    constexpr int R = 16 * RUN;   // rows per block step
+    constexpr int LD = 17;        // [row][col] leading dimension (odd: conflict-free row-major writes)
+    constexpr int PER = R / 16;   // values per thread per 16-column chunk
+    // dynamic LDS: the two staging buffers, later reused for the wave partials
+    extern __shared__ __attribute__((aligned(16))) double lds_g[];
+    double* sT[2] = {lds_g, lds_g + R * LD};
+    auto red = reinterpret_cast<double (*)[NTA][64][4]>(lds_g);  // [3][NTA][64][4]
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int c16 = lane & 15, g = lane >> 4;
+    // loader mapping: chunk element e = tid + 256 q -> column e / R (uniform
+    // over a wave, R >= 64: scalar pointer arithmetic), row e % R
+    const int lrow0 = tid % R;
+    d4 acc[NTA];
+#pragma unroll
+    for (int t = 0; t < NTA; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+    const int orow = wave * 4 * RUN + g * RUN;  // this lane's operand rows: orow + m
+    const int64_t stride = (int64_t)gridDim.x * R;
+    double v[PER];
+    auto load = [&](int c, int64_t rb) {
+        const int64_t rr = rb + lrow0;
+        const bool in = rr < n;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int cc = __builtin_amdgcn_readfirstlane((tid + 256 * q) / R) + (c > 0 ? 16 * (c - 1) : 0);
+            const bool on = cc < (c == 0 ? B.total : A.total);
+            const double* pc = c == 0 ? pcol(B, on ? cc : 0) : pcol(A, on ? cc : 0);
+            const double x = pc[in ? rr : 0];
+            v[q] = (on && in) ? x : 0.0;
+        }
+    };
+    int64_t rb0 = (int64_t)blockIdx.x * R;
+    if (rb0 < n) load(0, rb0);
+    for (; rb0 < n; rb0 += stride) {
+        double bv[RUN];
+#pragma unroll
+        for (int c = 0; c <= NTA; ++c) {
+            // buffer c & 1: its last reader was chunk c - 2, done before the
+            // barrier after chunk c - 1's write (and the step-end barrier)
+            double* s = sT[c & 1];
+#pragma unroll
+            for (int q = 0; q < PER; ++q) s[lrow0 * LD + (tid + 256 * q) / R] = v[q];
+            // the next chunk's loads are in flight across the barrier and the MFMAs
+            if (c < NTA) load(c + 1, rb0);
+            else if (rb0 + stride < n) load(0, rb0 + stride);
+            __syncthreads();
+            if (c == 0) {
+#pragma unroll
+                for (int m = 0; m < RUN; ++m) bv[m] = s[(orow + m) * LD + c16];
+            } else {
+#pragma unroll
+                for (int m = 0; m < RUN; ++m) acc[c - 1] = mfma64(s[(orow + m) * LD + c16], bv[m], acc[c - 1]);
+            }
+        }
+        __syncthreads();  // the next step's chunk 0 rewrites buffer 0
+    }
+    __syncthreads();  // (no step ran) the staging buffers become the partials
+    if (wave > 0) {
+#pragma unroll
+        for (int t = 0; t < NTA; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[wave - 1][t][lane][r] = acc[t][r];
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const int ldc = 16 * NTA;
+        double* out = partial + blockIdx.x;
+        const int64_t nb = gridDim.x;
+#pragma unroll
+        for (int t = 0; t < NTA; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                double v = acc[t][r];
+                v = v + red[0][t][lane][r];
+                v = v + red[1][t][lane][r];
+                v = v + red[2][t][lane][r];
+                const int i = t * 16 + g + 4 * r, j = c16;
+                out[(int64_t)(j * ldc + i) * nb] = v;
+            }
+    }
+}
+
 GramPlan gram_plan(int wa, int wb, int64_t n) {
     (void)wb;
     GramPlan p;
@@ -725,9 +964,38 @@ GramPlan gram_plan(int wa, int wb, int64_t n) {
     return p;
 }
 
+template <int NTA, int RUN>
+static void launch_gram_lds(const Panel& A, const Panel& B, int64_t n, int blocks, double* partial, hipStream_t st) {
+    const size_t lds = std::max((size_t)2 * 16 * RUN * 17, (size_t)3 * NTA * 64 * 4) * sizeof(double);
+    hipLaunchKernelGGL((k_gram_lds<NTA, RUN>), dim3(blocks), dim3(256), lds, st, A, B, n, partial);
+}
+
+bool gram_lds_on() {  // CAL_GRAM_LDS=0: the direct-load k_gram (A/B; same bits)
+    static const bool on = [] {
+        const char* e = std::getenv("CAL_GRAM_LDS");
+        return !e || std::atoi(e) != 0;
+    }();
+    return on;
+}
+
 hipError_t launch_gram(const Panel& A, const Panel& B, int64_t n, const GramPlan& pl, double* partial,
                        hipStream_t st) {
     dim3 g(pl.blocks), b(256);
+    // the staged loads pay from 33 A columns on (tools/gram_probe.hip: +5-15 %
+    // at 48-128 columns; RUN = 16 stages 256-row blocks in 70 KB of LDS and
+    // loses to the direct loads at <= 32 columns)
+    if (gram_lds_on() && pl.nta >= 3) {
+        switch (pl.nta) {
+            case 3: launch_gram_lds<3, 8>(A, B, n, pl.blocks, partial, st); break;
+            case 4: launch_gram_lds<4, 8>(A, B, n, pl.blocks, partial, st); break;
+            case 5: launch_gram_lds<5, 4>(A, B, n, pl.blocks, partial, st); break;
+            case 6: launch_gram_lds<6, 4>(A, B, n, pl.blocks, partial, st); break;
+            case 7: launch_gram_lds<7, 4>(A, B, n, pl.blocks, partial, st); break;
+            case 8: launch_gram_lds<8, 4>(A, B, n, pl.blocks, partial, st); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     switch (pl.nta) {
         case 1: hipLaunchKernelGGL((k_gram<1, 16>), g, b, 0, st, A, B, n, partial); break;
         case 2: hipLaunchKernelGGL((k_gram<2, 16>), g, b, 0, st, A, B, n, partial); break;
@@ -1037,6 +1305,130 @@ hipError_t launch_apply(const Panel& P, const double* dM, int wp, int wy, const 
         }
     }
 #undef CAL_APPLY
+    return hipGetLastError();
+}
+
+// Store-only Y = P M for wide outputs (the Ritz vectors X = Q(:,1:sk) Vp of
+// compute_ritz_rnorm, ca_lanczos.m:93) on the matrix cores with the operand
+// roles transposed: D = M^T P^T.  Lane l feeds A = M(4kc + (l>>4), 16ty +
+// (l&15)) from LDS and B = P(r0 + 2(l&15) + t, 4kc + (l>>4)) (one 16-B load
+// per lane for t = 0, 1), so accumulator register r of tile (ty, t) holds
+// Y(r0 + 2(l&15) + t, 16ty + (l>>4) + 4r): every store writes 256 contiguous
+// bytes of one column.  The k_apply_rows kernel above pays one LDS broadcast
+// read per two FMAs and stalls on the LDS return path at ~25 TF; here one LDS
+// read feeds two 16x16x4 MFMAs (tools/ritz_apply_probe.hip, n = 9.94 M:
+// 120 x 120 in 6.6 ms vs 12.5 ms).  Each output is the k-ascending FMA chain
+// starting from 0, as k_apply_rows computes it (the probe compares bitwise).
+// One segment each; Y must not alias P.  Grid: blockIdx.y = 16*NT-column group.
+template <int NT, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_apply_mt(const double* __restrict__ P, int64_t ldp,
+                                                         const double* __restrict__ M, int wp, int wy,
+                                                         double* __restrict__ Y, int64_t ldy, int64_t n) {
+    extern __shared__ __attribute__((aligned(16))) double Ms[];  // [wpp][16 NT]
+    constexpr int ldm = 16 * NT;
+    const int wpp = (wp + 3) & ~3;
+    const int c0 = blockIdx.y * ldm;
+    for (int e = threadIdx.x; e < wpp * ldm; e += 64 * WAVES) {
+        const int k = e / ldm, j = e % ldm;
+        Ms[e] = (k < wp && c0 + j < wy) ? M[(int64_t)(c0 + j) * wp + k] : 0.0;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int c16 = lane & 15, g = lane >> 4;
+    const int nkc = wpp / 4;
+    const int64_t stride = (int64_t)gridDim.x * WAVES * 32;
+    for (int64_t r0 = ((int64_t)blockIdx.x * WAVES + wave) * 32; r0 < n; r0 += stride) {
+        const bool full = r0 + 32 <= n;
+        const int64_t rb = r0 + 2 * c16;
+        d4 acc[NT][2];
+#pragma unroll
+        for (int ty = 0; ty < NT; ++ty) acc[ty][0] = acc[ty][1] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+        for (int kc = 0; kc < nkc; ++kc) {
+            const int c = 4 * kc + g;
+            const bool con = c < wp;
+            const double* pc = P + (int64_t)(con ? c : 0) * ldp;
+            double b0, b1;
+            if (full) {
+                const d2 x = *reinterpret_cast<const d2*>(pc + rb);
+                b0 = x[0];
+                b1 = x[1];
+            } else {
+                b0 = rb < n ? pc[rb] : 0.0;
+                b1 = rb + 1 < n ? pc[rb + 1] : 0.0;
+            }
+            b0 = con ? b0 : 0.0;
+            b1 = con ? b1 : 0.0;
+#pragma unroll
+            for (int ty = 0; ty < NT; ++ty) {
+                const double a = Ms[c * ldm + 16 * ty + c16];
+                acc[ty][0] = mfma64(a, b0, acc[ty][0]);
+                acc[ty][1] = mfma64(a, b1, acc[ty][1]);
+            }
+        }
+#pragma unroll
+        for (int ty = 0; ty < NT; ++ty)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int j = c0 + 16 * ty + g + 4 * r;
+                if (j < wy) {
+                    double* yc = Y + (int64_t)j * ldy;
+                    if (full) {
+                        d2 x;
+                        x[0] = acc[ty][0][r];
+                        x[1] = acc[ty][1][r];
+                        *reinterpret_cast<d2*>(yc + rb) = x;
+                    } else {
+                        if (rb < n) yc[rb] = acc[ty][0][r];
+                        if (rb + 1 < n) yc[rb + 1] = acc[ty][1][r];
+                    }
+                }
+            }
+    }
+}
+
+// 16-column tiles per block: ceil(wy / 16) up to 8 (no idle tiles), fewer
+// until M (wpp x 16 NT doubles) fits the 160 KB of LDS of one CU (0: never)
+static int apply_mt_nt(int wp, int wy) {
+    const size_t wpp = (size_t)((wp + 3) & ~3);
+    int nt = std::min(8, (wy + 15) / 16);
+    while (nt > 1 && wpp * 16 * nt * sizeof(double) > 160 * 1024) --nt;
+    return wpp * 16 * nt * sizeof(double) <= 160 * 1024 ? nt : 0;
+}
+
+bool apply_mt_ok(int wp, int wy) { return wp >= 1 && wy >= 1 && apply_mt_nt(wp, wy) > 0; }
+
+hipError_t launch_apply_mt(const double* P, int64_t ldp, const double* dM, int wp, int wy, double* Y, int64_t ldy,
+                           int64_t n, hipStream_t st) {
+    if (!apply_mt_ok(wp, wy) || (((uintptr_t)P | (uintptr_t)Y | (uintptr_t)(ldp * 8) | (uintptr_t)(ldy * 8)) & 15))
+        return hipErrorInvalidValue;
+    if (n <= 0) return hipSuccess;
+    const int wpp = (wp + 3) & ~3;
+    // probe (n = 9.94 M): <= 32 outputs 4 waves, 4 blocks per CU; wider 8
+    // waves, 2 blocks per CU (1 at 128 outputs); fewer when M does not fit
+    auto go = [&](auto nt_c, auto waves_c, int per_cu) {
+        constexpr int NT = decltype(nt_c)::value, WAVES = decltype(waves_c)::value;
+        const size_t lds = (size_t)wpp * 16 * NT * sizeof(double);
+        const int fit = (int)((160 * 1024) / lds);
+        const int bpc = std::max(1, std::min(per_cu, fit));
+        int64_t blocks = (n + 32 * WAVES - 1) / (32 * WAVES);
+        if (blocks > 256 * bpc) blocks = 256 * bpc;
+        const unsigned groups = (unsigned)((wy + 16 * NT - 1) / (16 * NT));
+        hipLaunchKernelGGL((k_apply_mt<NT, WAVES>), dim3((unsigned)blocks, groups), dim3(64 * WAVES), lds, st, P, ldp,
+                           dM, wp, wy, Y, ldy, n);
+    };
+    using I = std::integral_constant<int, 4>;
+    using E = std::integral_constant<int, 8>;
+    switch (apply_mt_nt(wp, wy)) {
+        case 1: go(std::integral_constant<int, 1>{}, I{}, 4); break;
+        case 2: go(std::integral_constant<int, 2>{}, I{}, 4); break;
+        case 3: go(std::integral_constant<int, 3>{}, E{}, 2); break;
+        case 4: go(std::integral_constant<int, 4>{}, E{}, 2); break;
+        case 5: go(std::integral_constant<int, 5>{}, E{}, 2); break;
+        case 6: go(std::integral_constant<int, 6>{}, E{}, 2); break;
+        case 7: go(std::integral_constant<int, 7>{}, E{}, 2); break;
+        default: go(std::integral_constant<int, 8>{}, E{}, 1); break;
+    }
     return hipGetLastError();
 }
 

@@ -31,6 +31,30 @@ namespace cal {
 // and the Newton prologue's 2s shifts fit cal_lanczos_info.shifts[64]
 constexpr int kMaxS = 31;
 
+// Ritz pair of T(1:sk,1:sk) (compute_ritz_rnorm, ca_lanczos.m:88-97)
+struct RitzPair {
+    double lr, li;
+    int cr, ci;  // columns of the real / imaginary part in V (ci = -1: real)
+};
+
+// The diagnostics of one outer iteration (ca_lanczos.m:227-236), run one
+// iteration late: eig(T_k) is solved on the host while the GPU runs step
+// k + 1's matrix powers and the previous iteration's diagnostics kernels
+// (diagnostics on).
+struct DiagJob {
+    int k = 0;  // outer iteration described; 0: empty
+    std::vector<RitzPair> pairs;  // MATLAB's descending sort
+    std::vector<double> V;        // eigenvectors of T_k (sk x sk)
+    struct OeChunk {
+        int a0, na, b0, nb, ldc;
+        size_t off;  // doubles into the result region
+    };
+    std::vector<OeChunk> oe;
+    int wa = 0;
+    std::vector<int> sep;  // pairs reduced on their own (row kernel)
+    hipEvent_t ev = nullptr;
+};
+
 struct LanczosState {
     int s = 0, max_outer = 0, k = 0;
     bool newton = false, full = false;
@@ -59,6 +83,14 @@ struct LanczosState {
     std::vector<double> oe;
     cal_lanczos_info info{};
     bool breakdown = false;
+    // deferred diagnostics: `ready` solved on the host, `pending` on the stream
+    DiagJob ready, pending;
+    double* d_dres = nullptr;  // results: residual sums (2 sk), then the orth-error Grams
+    double* h_dres = nullptr;  // pinned
+    size_t dres_cap = 0;
+    double* d_din = nullptr;   // inputs: Vp (sk x sk), Ritz values, pair columns / slots
+    double* h_din = nullptr;   // pinned
+    size_t din_cap = 0;
     int64_t lpad = 0;  // local origin inside each column (left halo space)
     double* col(int j) { return dQ + (size_t)j * ld + lpad; }
     double* vcolumn(int j, int par = 0) { return dV + ((size_t)par * (s + 1) + j) * ld + lpad; }
@@ -297,12 +329,19 @@ static int newton_prologue(cal_ctx* c, LanczosState& L, bool cgs = true) {
     return 0;
 }
 
-// ---- Ritz residuals (compute_ritz_rnorm, ca_lanczos.m:88-97) --------------
-struct RitzPair {
-    double lr, li;
-    int cr, ci;  // columns of the real / imaginary part in V (ci = -1: real)
-};
-
+// ---- Ritz diagnostics (compute_ritz_rnorm / compute_orth_err, -----------
+// ca_lanczos.m:88-107,227-236), deferred by one outer iteration.
+//   diag_prepare(k): eig(T(1:sk,1:sk)) and MATLAB's descending sort, on the
+//     host, right after step k's T extension (the GPU meanwhile runs step
+//     k + 1's prefetched matrix powers and step k - 1's diagnostics kernels);
+//   diag_launch: the orthogonality error's Grams of Q(:,1:sk+1), X = Q(:,1:sk)
+//     Vp on the matrix cores, the residual sums of all sk pairs (real pairs on
+//     the pair patterns in one launch), one reduction, async copies to pinned
+//     memory, an event; enqueued in step k + 1 before anything there rewrites
+//     Q(:,1:sk+1) (periodic);
+//   diag_collect: reads the results once the event has passed (in step k + 2
+//     after the block orthogonalisation's wait, i.e. without waiting).
+// The last step (and cal_lanczos_get) flush what is left.
 static void matlab_sort_desc(std::vector<RitzPair>& v, bool cplx) {
     std::stable_sort(v.begin(), v.end(), [&](const RitzPair& a, const RitzPair& b) {
         if (!cplx) return a.lr > b.lr;
@@ -312,31 +351,16 @@ static void matlab_sort_desc(std::vector<RitzPair>& v, bool cplx) {
     });
 }
 
-static int ritz_diagnostics(cal_ctx* c, LanczosState& L) {
-    const int s = L.s, k = L.k, sk = s * k;
-    const int64_t n = c->A.n_local, ld = c->A.ld;
-    // the orthogonality error's Gram (compute_orth_err, ca_lanczos.m:99-107)
-    // runs on the GPU while the host solves eig(T): enqueued here, read after
-    // the residuals' wait below
-    const int jq = sk + 1;
-    const int wa = jq > s + 1 ? jq - s - 1 : s + 1;
-    Panel OA = panel(), OB = panel();
-    panel_add(OA, L.col(0), ld, wa);
-    panel_add(OB, L.col(jq > s + 1 ? wa : 0), ld, s + 1);
-    constexpr size_t kOrthRegion = 8192 + 7 * 8192;  // above the projections' async regions
-    const bool oe_async = wa <= 128 && s + 1 <= 16;
-    int oe_ld = 0;
-    if (oe_async) {
-        CAL_TRY(ensure_red(c, kOrthRegion + 8192));
-        CAL_TRY(gram_async(c, n, OA, OB, c->d_red + kOrthRegion, c->h_red + kOrthRegion, &oe_ld));
-    }
-    // eig(T(1:sk,1:sk)) (ca_lanczos.m:229)
-    std::vector<double> Tk((size_t)sk * sk), wr(sk), wi(sk), V((size_t)sk * sk);
+static int diag_prepare(cal_ctx* c, LanczosState& L, DiagJob& J) {
+    const int sk = L.s * L.k;
+    std::vector<double> Tk((size_t)sk * sk), wr(sk), wi(sk);
     for (int j = 0; j < sk; ++j)
         for (int i = 0; i < sk; ++i) Tk[i + (size_t)j * sk] = L.T[i + (size_t)j * L.Tld];
-    if (cal_eig(sk, Tk.data(), sk, wr.data(), wi.data(), V.data()) != 0)
+    J.V.assign((size_t)sk * sk, 0.0);
+    // [Vp,Dp] = eig(T(1:s*k,1:s*k)) (ca_lanczos.m:229)
+    if (cal_eig(sk, Tk.data(), sk, wr.data(), wi.data(), J.V.data()) != 0)
         return set_error(c, CAL_ERR_NUMERIC, "eig(T) did not converge");
-    std::vector<RitzPair> pairs;
+    J.pairs.clear();
     bool cplx = false;
     for (int j = 0; j < sk; ++j) {
         if (wi[j] != 0.0) {
@@ -344,85 +368,173 @@ static int ritz_diagnostics(cal_ctx* c, LanczosState& L) {
             // V(:,j) + i V(:,j+1) belongs to wr + i|wi|; the conjugate uses the
             // conjugate vector (same residual norm)
             const int jr = wi[j] > 0 ? j : j - 1;
-            pairs.push_back({wr[j], wi[j], jr, jr + 1});
+            J.pairs.push_back({wr[j], wi[j], jr, jr + 1});
         } else {
-            pairs.push_back({wr[j], 0.0, j, -1});
+            J.pairs.push_back({wr[j], 0.0, j, -1});
         }
     }
-    matlab_sort_desc(pairs, cplx);
-    // X = Q(:,1:sk) * V on the GPU (MFMA apply), into work columns
-    CAL_TRY(ensure_work(c, sk, ld));
-    Panel Qp = panel();
-    panel_add(Qp, L.col(0), ld, sk);
-    PanelOut X = panel_out(work_col(c, 0) + c->A.lpad, ld, sk);
-    CAL_TRY(apply_host(c, n, Qp, V.data(), sk, &X, nullptr, 0, nullptr));
-    // ||A x - l x|| / ||l x|| per Ritz pair: fused SpMV + residual partials
-    // (real Ritz values on the pair patterns; complex pairs and CSR matrices
-    // on the row kernel)
-    const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (n + 255) / 256));
-    const int64_t pstride = 2 * (int64_t)std::max(nb, spmv_resid_pair_blocks(c));
-    CAL_TRY(ensure_partial(c, (size_t)pstride * sk));
-    CAL_TRY(ensure_red(c, 2 * sk));
-    // partial blocks per pair; when every pair fills its stride the sums are
-    // reduced in one launch (entry 2i+e at (2i+e) * pstride/2)
-    std::vector<int> nparts(sk, 0);
-    for (int i = 0; i < sk; ++i) {
-        const RitzPair& p = pairs[i];
-        double* xr = work_col(c, p.cr) + c->A.lpad;
-        double* xi = p.ci >= 0 ? work_col(c, p.ci) + c->A.lpad : nullptr;
-        double* part = c->d_partial + (size_t)i * pstride;
-        CAL_TRY(halo_exchange(c, xr));
-        if (!xi) {
-            int nbk = 0;
-            CAL_TRY(spmv_resid_pair_dev(c, xr, p.lr, part, &nbk));
-            if (nbk > 0) {
-                nparts[i] = nbk;
-                continue;
-            }
+    matlab_sort_desc(J.pairs, cplx);
+    J.k = L.k;
+    return 0;
+}
+
+static int grow_pinned(cal_ctx* c, double** d, double** h, size_t* cap, size_t need) {
+    if (need <= *cap) return 0;
+    if (*d) CAL_HIP(c, hipFree(*d));
+    if (*h) CAL_HIP(c, hipHostFree(*h));
+    *d = *h = nullptr;
+    const size_t n = std::max(need, *cap + *cap / 2);
+    CAL_HIP(c, hipMalloc((void**)d, n * sizeof(double)));
+    CAL_HIP(c, hipHostMalloc((void**)h, n * sizeof(double), hipHostMallocDefault));
+    *cap = n;
+    return 0;
+}
+
+static int diag_launch(cal_ctx* c, LanczosState& L, DiagJob& J) {
+    const int s = L.s, sk = s * J.k;
+    const int64_t n = c->A.n_local, ld = c->A.ld;
+    // compute_orth_err(Q(:,1:sk+1), s): Q(:,1:j-s-1)'Q(:,j-s:j) for j > s+1,
+    // else Q'Q - I; Grams in chunks of 128 x 16 columns (gram_async)
+    const int jq = sk + 1;
+    J.wa = jq > s + 1 ? jq - s - 1 : s + 1;
+    const int bcol = jq > s + 1 ? J.wa : 0;
+    J.oe.clear();
+    size_t off = (size_t)2 * sk;
+    for (int a0 = 0; a0 < J.wa; a0 += 128)
+        for (int b0 = 0; b0 < s + 1; b0 += 16) {
+            const int na = std::min(128, J.wa - a0), nb = std::min(16, s + 1 - b0);
+            const GramPlan pl = gram_plan(na, nb, n);
+            J.oe.push_back({a0, na, b0, nb, 16 * pl.nta, off});
+            off += (size_t)pl.entries;
         }
+    CAL_TRY(grow_pinned(c, &L.d_dres, &L.h_dres, &L.dres_cap, off));
+    for (const auto& ch : J.oe) {
+        Panel OA = panel(), OB = panel();
+        panel_add(OA, L.col(ch.a0), ld, ch.na);
+        panel_add(OB, L.col(bcol + ch.b0), ld, ch.nb);
+        int ldc = 0;
+        CAL_TRY(gram_async(c, n, OA, OB, L.d_dres + ch.off, L.h_dres + ch.off, &ldc));
+    }
+    // X = Q(:,1:sk) * Vp (ca_lanczos.m:93) into work columns
+    const int npr = (int)std::count_if(J.pairs.begin(), J.pairs.end(), [](const RitzPair& p) { return p.ci < 0; });
+    const size_t o_lam = (size_t)sk * sk, o_col = o_lam + sk, o_out = o_col + (sk + 1) / 2;
+    CAL_TRY(grow_pinned(c, &L.d_din, &L.h_din, &L.din_cap, o_out + (sk + 1) / 2));
+    std::copy(J.V.begin(), J.V.end(), L.h_din);
+    double* h_lam = L.h_din + o_lam;
+    int* h_col = reinterpret_cast<int*>(L.h_din + o_col);
+    int* h_out = reinterpret_cast<int*>(L.h_din + o_out);
+    J.sep.clear();
+    const int nbp = spmv_resid_pair_blocks(c);  // 0: no pair path (row kernel for every pair)
+    for (int i = 0, q = 0; i < sk; ++i) {
+        const RitzPair& p = J.pairs[i];
+        if (nbp > 0 && p.ci < 0) {
+            h_lam[q] = p.lr;
+            h_col[q] = p.cr;
+            h_out[q] = i;
+            ++q;
+        } else {
+            J.sep.push_back(i);
+        }
+    }
+    CAL_HIP(c, hipMemcpyAsync(L.d_din, L.h_din, (o_out + (sk + 1) / 2) * sizeof(double), hipMemcpyHostToDevice,
+                              c->stream));
+    // sized for the last iteration at once (each growth frees and zeroes)
+    CAL_TRY(ensure_work(c, std::max(sk, s * L.max_outer), ld));
+    double* X = work_col(c, 0) + c->A.lpad;
+    if (apply_mt_ok(sk, sk)) {
+        const int t = timer_begin(c, 2);
+        hipError_t e = launch_apply_mt(L.col(0), ld, L.d_din, sk, sk, X, ld, n, c->stream);
+        timer_end(c, t);
+        if (e != hipSuccess) return hip_fail(c, e, "launch_apply_mt (Ritz vectors)");
+    } else {  // sk > 1280: the generic apply in column chunks
+        Panel Qp = panel();
+        panel_add(Qp, L.col(0), ld, sk);
+        CAL_TRY(apply_dev(c, n, Qp, L.d_din, sk, panel_out(X, ld, sk)));
+    }
+    // ||A x - l x||^2, ||l x||^2 per pair (ca_lanczos.m:94): entry 2i + e
+    const int nbr = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (n + 255) / 256));
+    const bool batched = nbp > 0;
+    const size_t sep0 = batched ? (size_t)2 * sk * nbp : 0;  // row-kernel partials
+    CAL_TRY(ensure_partial(c, sep0 + (size_t)2 * sk * nbr));
+    if (batched && npr > 0) {
+        for (int i = 0; i < sk; ++i)
+            if (J.pairs[i].ci < 0) CAL_TRY(halo_exchange(c, X + (int64_t)J.pairs[i].cr * ld));
+        const int t = timer_begin(c, 3);
+        CAL_TRY(spmv_resid_pair_multi_dev(c, X, ld, reinterpret_cast<const int*>(L.d_din + o_col), L.d_din + o_lam,
+                                          reinterpret_cast<const int*>(L.d_din + o_out), npr, c->d_partial, nbp));
+        timer_end(c, t);
+    }
+    for (size_t q = 0; q < J.sep.size(); ++q) {
+        const RitzPair& p = J.pairs[J.sep[q]];
+        double* xr = X + (int64_t)p.cr * ld;
+        double* xi = p.ci >= 0 ? X + (int64_t)p.ci * ld : nullptr;
+        CAL_TRY(halo_exchange(c, xr));
         if (xi) CAL_TRY(halo_exchange(c, xi));
         SpmvArgs a{};
         a.rowptr = c->A.rowptr + c->A.ext_off;  // local rows of a stored slab
         a.col = c->A.col;
         a.val = c->A.val;
         a.x = xr;
+        // no pair path: every pair entry-major at stride nbr (one reduction)
+        double* part = c->d_partial + sep0 + (batched ? q : (size_t)J.sep[q]) * 2 * nbr;
         const int t = timer_begin(c, 3);
-        CAL_HIP(c, launch_spmv_resid(a, xi, p.lr, p.li, n, part, nb, c->stream));
+        CAL_HIP(c, launch_spmv_resid(a, xi, p.lr, p.li, n, part, nbr, c->stream));
         timer_end(c, t);
-        nparts[i] = nb;
     }
-    if (std::all_of(nparts.begin(), nparts.end(), [&](int v) { return 2 * (int64_t)v == pstride; })) {
-        CAL_HIP(c, launch_reduce(c->d_partial, (int)(pstride / 2), 2 * sk, c->d_red, c->stream));
+    if (batched) {
+        if (npr > 0) CAL_HIP(c, launch_reduce(c->d_partial, nbp, 2 * sk, L.d_dres, c->stream));
+        for (size_t q = 0; q < J.sep.size(); ++q)
+            CAL_HIP(c, launch_reduce(c->d_partial + sep0 + q * 2 * nbr, nbr, 2, L.d_dres + 2 * J.sep[q], c->stream));
     } else {
-        for (int i = 0; i < sk; ++i)
-            CAL_HIP(c, launch_reduce(c->d_partial + (size_t)i * pstride, nparts[i], 2, c->d_red + 2 * i, c->stream));
+        CAL_HIP(c, launch_reduce(c->d_partial, nbr, 2 * sk, L.d_dres, c->stream));
     }
-    CAL_TRY(allreduce_sum(c, c->d_red, 2 * sk));
-    CAL_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, 2 * sk * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    CAL_HIP(c, hipStreamSynchronize(c->stream));
-    c->small_pending = false;
-    std::vector<double> rn(sk);
-    for (int i = 0; i < sk; ++i) rn[i] = std::sqrt(c->h_red[2 * i]) / std::sqrt(c->h_red[2 * i + 1]);
-    L.rn.push_back(rn);
-    // orthogonality error (compute_orth_err, ca_lanczos.m:99-107)
-    std::vector<double> G((size_t)wa * (s + 1));
-    if (oe_async) {
-        const double* h = c->h_red + kOrthRegion;  // the stream is synchronised above
-        for (int jj = 0; jj <= s; ++jj)
-            for (int ii = 0; ii < wa; ++ii) G[ii + (size_t)jj * wa] = h[ii + (size_t)jj * oe_ld];
-    } else {
-        CAL_TRY(gram_host(c, n, OA, OB, G.data()));
-    }
-    double oe = 0.0;
-    if (jq > s + 1) {
-        for (double g : G) oe = std::max(oe, std::fabs(g));
-    } else {
-        for (int jj = 0; jj <= s; ++jj)
-            for (int ii = 0; ii <= s; ++ii)
-                oe = std::max(oe, std::fabs(G[ii + (size_t)jj * (s + 1)] - (ii == jj ? 1.0 : 0.0)));
-    }
-    L.oe.push_back(oe);
+    CAL_TRY(allreduce_sum(c, L.d_dres, 2 * sk));
+    CAL_HIP(c, hipMemcpyAsync(L.h_dres, L.d_dres, 2 * sk * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (!J.ev) CAL_HIP(c, hipEventCreateWithFlags(&J.ev, hipEventDisableTiming));
+    CAL_HIP(c, hipEventRecord(J.ev, c->stream));
     return 0;
+}
+
+static int diag_collect(cal_ctx* c, LanczosState& L, DiagJob& J) {
+    const int s = L.s, k = J.k, sk = s * k;
+    CAL_HIP(c, hipEventSynchronize(J.ev));
+    std::vector<double> rn(sk);
+    for (int i = 0; i < sk; ++i) rn[i] = std::sqrt(L.h_dres[2 * i]) / std::sqrt(L.h_dres[2 * i + 1]);
+    double oe = 0.0;
+    const bool off_diag = sk + 1 > s + 1;
+    for (const auto& ch : J.oe)
+        for (int jj = 0; jj < ch.nb; ++jj)
+            for (int ii = 0; ii < ch.na; ++ii) {
+                double g = L.h_dres[ch.off + ii + (size_t)jj * ch.ldc];
+                if (!off_diag && ch.a0 + ii == ch.b0 + jj) g -= 1.0;
+                oe = std::max(oe, std::fabs(g));
+            }
+    if ((int)L.rn.size() < k) L.rn.resize(k);
+    if ((int)L.oe.size() < k) L.oe.resize(k, 0.0);
+    L.rn[k - 1] = rn;
+    L.oe[k - 1] = oe;
+    J.k = 0;
+    return 0;
+}
+
+// everything still deferred: the stream is drained
+static int diag_flush(cal_ctx* c, LanczosState& L) {
+    if (L.pending.k) CAL_TRY(diag_collect(c, L, L.pending));
+    if (L.ready.k) {
+        std::swap(L.pending, L.ready);
+        CAL_TRY(diag_launch(c, L, L.pending));
+        CAL_TRY(diag_collect(c, L, L.pending));
+    }
+    return 0;
+}
+
+static void diag_free(LanczosState& L) {
+    if (L.ready.ev) hipEventDestroy(L.ready.ev);
+    if (L.pending.ev) hipEventDestroy(L.pending.ev);
+    if (L.d_dres) hipFree(L.d_dres);
+    if (L.h_dres) hipHostFree(L.h_dres);
+    if (L.d_din) hipFree(L.d_din);
+    if (L.h_din) hipHostFree(L.h_din);
 }
 
 // ---- T extension (ca_lanczos.m:176-223) -----------------------------------
@@ -614,7 +726,7 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
     // (stream-ordered after this step's pass B) and the fixed shifts, so they
     // are enqueued (into the other V buffer) before the host waits for this
     // step's R: the GPU runs them while the host extends T and returns.
-    const bool prefetch = !diagnostics && L.mode == 0 && !L.restart_inner && k + 1 <= L.max_outer;
+    const bool prefetch = L.mode == 0 && !L.restart_inner && k + 1 <= L.max_outer;
     c->orth_redone = false;
     if (prefetch)
         c->pre_wait = [c, &L, k]() {
@@ -710,13 +822,27 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
         L.info.breakdown = 1;
         return set_error(c, CAL_WARN_BREAKDOWN, "CA-Lanczos breakdown: rho_t = Rk(s,s) = 0");
     }
+    // deferred diagnostics (see diag_prepare): step k-2's results are in (the
+    // wait for this block's R passed their event); step k-1's kernels go on
+    // the stream before periodic_update rewrites Q(:,(k-1)s+1:ks+1)
+    double td = now_ms();
+    if (L.pending.k) CAL_TRY(diag_collect(c, L, L.pending));
+    if (L.ready.k) {
+        std::swap(L.pending, L.ready);
+        CAL_TRY(diag_launch(c, L, L.pending));
+    }
+    double tdiag = now_ms() - td;
     if (L.mode == 2) CAL_TRY(periodic_update(c, L));
     if (L.mode == 3) CAL_TRY(selective_update(c, L));
-    const double t1 = now_ms();
-    if (diagnostics) CAL_TRY(ritz_diagnostics(c, L));
+    td = now_ms();
+    if (diagnostics) {
+        CAL_TRY(diag_prepare(c, L, L.ready));  // eig(T_k) on the host, GPU busy
+        if (k == L.max_outer) CAL_TRY(diag_flush(c, L));
+    }
     const double t2 = now_ms();
+    tdiag += t2 - td;
     L.info.loop_ms += t2 - t0;
-    L.info.diag_ms += t2 - t1;
+    L.info.diag_ms += tdiag;
     L.info.t = k;
     return 0;
 }
@@ -733,6 +859,7 @@ void cal_lanczos_free_state(cal_ctx* c) {
     if (c->lz->dV) hipFree(c->lz->dV);
     if (c->lz->dQR) hipFree(c->lz->dQR);
     if (c->lz->dQRy) hipFree(c->lz->dQRy);
+    diag_free(*c->lz);
     delete c->lz;
     c->lz = nullptr;
 }
@@ -806,8 +933,12 @@ int cal_lanczos_get(cal_ctx* c, double* T, int ldt, double* rn, double* oe, int*
     if (!c || !c->lz) return CAL_ERR_ARG;
     LanczosState& L = *c->lz;
     const int k = L.k, sk = L.s * L.k;
+    if (T && ldt < sk) return set_error(c, CAL_ERR_ARG, "cal_lanczos_get: ldt < s*k");
+    if (L.pending.k || L.ready.k) {  // diagnostics still deferred (a run stopped early)
+        hipSetDevice(c->device);
+        CAL_TRY(diag_flush(c, L));
+    }
     if (T) {
-        if (ldt < sk) return set_error(c, CAL_ERR_ARG, "cal_lanczos_get: ldt < s*k");
         for (int j = 0; j < sk; ++j)
             for (int i = 0; i < sk; ++i) T[i + (size_t)j * ldt] = L.T[i + (size_t)j * L.Tld];
     }

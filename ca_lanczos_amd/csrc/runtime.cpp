@@ -491,6 +491,15 @@ int spmv_resid_pair_dev(cal_ctx* c, const double* x, double lr, double* partial,
     return 0;
 }
 
+int spmv_resid_pair_multi_dev(cal_ctx* c, const double* X, int64_t ldx, const int* col, const double* lam,
+                              const int* out, int npr, double* partial, int64_t pstride) {
+    const DevMatrix& A = c->A;
+    if (!c->has_A || !A.use_pat || !A.use_pair) return set_error(c, CAL_ERR_ARG, "pair residuals: no pair patterns");
+    const PatArgs p = pat_args(A, A.ext_off, A.n_local, X, nullptr, 1, 0.0, 0.0, nullptr);
+    CAL_HIP(c, launch_spmv_pair_resid_multi(p, X, ldx, col, lam, out, npr, partial, pstride, c->stream));
+    return 0;
+}
+
 // Two stored-row ranges [o1, o1 + len1) and [o2, o2 + len2) in one launch
 // (the pair kernel skips the gap; the row kernels take two launches).
 int spmv_range2(cal_ctx* c, int64_t o1, int64_t len1, int64_t o2, int64_t len2, const double* x, double* y, int mode,
