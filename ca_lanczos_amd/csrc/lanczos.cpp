@@ -629,7 +629,9 @@ static int extend_T(cal_ctx* c, LanczosState& L, const std::vector<double>& Rkk_
 // selective (ca_lanczos.m:321-340): the Ritz pairs of T(1:sk,1:sk) with
 // b(k)|Vp(sk,i)| < normest(A) sqrt(eps) (unit-norm eigenvectors, as MATLAB's
 // eig returns them); when their count grows, QR = normalize(Q(:,1:sk) Vp(:,conv)).
-// Deviation: complex pairs are not considered (they would make QR complex).
+// A converged complex-conjugate pair (the test is the same for both) enters
+// as Q Re(v), Q Im(v): the real span of the reference's complex QR columns
+// Q v, Q conj(v), so the count and the projections are the reference's.
 static int selective_update(cal_ctx* c, LanczosState& L) {
     const int s = L.s, k = L.k, sk = s * k;
     const int64_t n = c->A.n_local, ld = c->A.ld;
@@ -640,9 +642,21 @@ static int selective_update(cal_ctx* c, LanczosState& L) {
         return set_error(c, CAL_ERR_NUMERIC, "eig(T) did not converge");
     const double thresh = L.norm_A * std::sqrt(std::numeric_limits<double>::epsilon());
     const double bk = L.b.back();
-    std::vector<int> conv;
+    std::vector<int> conv;  // columns of V: real pairs, or (Re v, Im v) of a complex pair
     for (int j = 0; j < sk; ++j) {
-        if (wi[j] != 0.0) continue;
+        if (wi[j] != 0.0) {  // V(:,j) + i V(:,j+1) belongs to wr(j) + i wi(j), wi(j) > 0, and its conjugate
+            double nv = 0.0;
+            for (int i = 0; i < sk; ++i)
+                nv += V[i + (size_t)j * sk] * V[i + (size_t)j * sk] + V[i + (size_t)(j + 1) * sk] * V[i + (size_t)(j + 1) * sk];
+            nv = std::sqrt(nv);
+            const double last = std::hypot(V[(sk - 1) + (size_t)j * sk], V[(sk - 1) + (size_t)(j + 1) * sk]);
+            if (bk * (last / nv) < thresh) {
+                conv.push_back(j);
+                conv.push_back(j + 1);
+            }
+            ++j;
+            continue;
+        }
         double nv = 0.0;
         for (int i = 0; i < sk; ++i) nv += V[i + (size_t)j * sk] * V[i + (size_t)j * sk];
         nv = std::sqrt(nv);

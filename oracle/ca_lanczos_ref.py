@@ -762,9 +762,11 @@ def ca_lanczos_selective(A, q, Bk, t, s, basis, diagnostics=True):
     """ca_lanczos.m:248-359: local block orthogonalisation against the
     previous block and the converged Ritz vectors QR; QR is rebuilt (all
     converged Ritz vectors, in eig order, then normalize) whenever the count
-    b(k)|Vp(sk,i)| < normest(A) sqrt(eps) grows.  Deviation: only real
-    eigenpairs of T are considered (a complex pair would make the reference's
-    QR complex)."""
+    b(k)|Vp(sk,i)| < normest(A) sqrt(eps) grows (:321-340).  A converged
+    complex-conjugate pair (|Vp(sk,i)| is the same for both) makes the
+    reference's QR(:,i:i+1) = Q [v, conj(v)] complex; its span is the real
+    span of Q Re(v), Q Im(v), which is what is locked here (same count, same
+    projections in exact arithmetic, real arithmetic throughout)."""
     n = len(q)
     rnorm = np.zeros((t, t * s))
     ortherr = np.zeros(t)
@@ -776,7 +778,7 @@ def ca_lanczos_selective(A, q, Bk, t, s, basis, diagnostics=True):
     norm_A = normest(A)
     norm_sqrt_eps = norm_A * math.sqrt(np.finfo(float).eps)     # :258
     nritz = 0
-    breaks, reorth, ritz, nritz_hist = [], [], [], []
+    breaks, reorth, ritz, nritz_hist, ncplx_hist = [], [], [], [], []
     k = 0
     while k < t:
         k += 1
@@ -796,15 +798,22 @@ def ca_lanczos_selective(A, q, Bk, t, s, basis, diagnostics=True):
             Q[:, (k - 1) * s + 1 : k * s + 1] = Q_[:, :s]
             T = _extend_T(T, b, k, s, Bk, Rk_[0], Rk_[2])         # Rk_s = Rk_{3} (:291)
         w, Vp = matlab_eig(T[: s * k, : s * k])                 # :321
-        real = np.isreal(w) if np.iscomplexobj(w) else np.ones(len(w), bool)
-        conv = [i for i in range(k * s) if real[i] and b[k - 1] * abs(np.real(Vp[s * k - 1, i])) < norm_sqrt_eps]
+        conv = [i for i in range(k * s) if b[k - 1] * abs(Vp[s * k - 1, i]) < norm_sqrt_eps]   # :324-328
         brk = len(conv) > nritz                                 # :329
         breaks.append(brk)
         if brk:
             nritz = len(conv)
-            Y = Q[:, : k * s] @ np.real(Vp[:, conv])            # :334-336
+            # columns in eig order; the pair (i, i+1), Im w(i) > 0, as (Re v, Im v)
+            M = np.zeros((k * s, nritz))
+            for q_, i in enumerate(conv):
+                v = Vp[:, i]
+                if np.iscomplexobj(v) and w[i].imag != 0:
+                    v = v.real if w[i].imag > 0 else (-v.imag)  # conj(v) of the pair's first: Im -> second column
+                M[:, q_] = np.real(v)
+            Y = Q[:, : k * s] @ M                               # :334-336
             QR, _, _ = normalize(Y)                             # :339
         nritz_hist.append(nritz)
+        ncplx_hist.append(sum(1 for i in conv if np.iscomplexobj(w) and w[i].imag != 0))
         if diagnostics:
             ritz.append(w)
             rnorm[k - 1, : s * k] = compute_ritz_rnorm(A, Q[:, : s * k], Vp, w)
@@ -813,6 +822,7 @@ def ca_lanczos_selective(A, q, Bk, t, s, basis, diagnostics=True):
                           Bk=Bk, shifts=np.zeros(0), reorth=reorth, ritz_values=ritz)
     res.breaks = breaks
     res.nritz = nritz_hist
+    res.ncomplex = ncplx_hist  # converged Ritz values with a nonzero imaginary part
     res.norm_A = norm_A
     return res
 

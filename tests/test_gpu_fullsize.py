@@ -13,9 +13,15 @@ benchmark sizes, plus size-independent properties where it cannot:
     pair's residual norm recomputed on the host from the device's Q, and the
     size-independent properties (spectrum bounds, last Q block orthonormal);
   * config 2 (lap2d_1000, n = 10^6): the whole t = 15 run against the NumPy
-    oracle (T to 1e-9 * ||A||, identical flags, extreme Ritz values).
+    oracle (T to 1e-9 * ||A||, identical flags, extreme Ritz values);
+  * config 5 at its full size (the G3_circuit stand-in circuit_1259, n =
+    1,585,081, CSR SpMV): the implicitly restarted solve of the bench against
+    ARPACK's top 8 (tests/golden/circuit_1259_top8.npz, made by
+    tests/golden/make_circuit_eigs.py) to 1e-10 relative, Q_conv orthonormal,
+    every residual ||A v - l v|| / |l| below 1e-7.
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -123,3 +129,23 @@ def test_ca_lanczos_config2_vs_oracle(cal, ref):
     w = np.sort(np.linalg.eigvals(out.T).real)
     we = np.sort(np.linalg.eigvals(exp.T).real)
     assert abs(w[-1] - we[-1]) < 1e-10 * 8.0 and abs(w[0] - we[0]) < 1e-10 * 8.0
+
+
+def test_impl_restarted_config5_fullsize(cal):
+    """BASELINE config 5 at n = 1.58 M: impl_restarted_ca_lanczos (m = 64,
+    8 wanted, s = 8 Newton, 'full', tol 1e-8; impl_restarted_ca_lanczos.m:
+    333-426 with the fixes listed in DESIGN.md §8 f3) on the irregular SPD
+    stand-in, r = ones, against the golden ARPACK eigenvalues."""
+    gold = np.load(os.path.join(os.path.dirname(__file__), "golden", "circuit_1259_top8.npz"))
+    A = cal.matrices.circuit_like(1259)
+    assert A.shape[0] == int(gold["n"]) and A.nnz == int(gold["nnz"])
+    eref = gold["eigs"]
+    out = cal.impl_restarted_ca_lanczos(A, np.ones(A.shape[0]), 64, 8, 8, "newton", "full", 1.0e-8)
+    assert out["converged"]
+    ev = out["conv_eigs"]
+    assert np.all(np.diff(ev) <= 0)
+    assert np.max(np.abs(ev - eref) / np.abs(eref)) <= 1e-10, (ev, eref)
+    V = out["Q_conv"]
+    assert np.max(np.abs(V.T @ V - np.eye(8))) < 1e-9
+    res = np.linalg.norm(A @ V - V * ev, axis=0) / np.abs(ev)
+    assert np.max(res) < 1e-7
