@@ -75,6 +75,7 @@ struct SpmvArgs {
     double shift;         // y = A x - shift * x
     double im2;           //     + im2 * xprev
     int mode;             // 0: y = A x, 1: shifted, 2: shifted + im2 term
+    int xcd;              // XCD-contiguous block order (set by launch_spmv)
 };
 
 // Row-pattern storage ("PSR"): row r is pattern pat[r], a sequence of

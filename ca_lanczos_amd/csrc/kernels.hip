@@ -79,10 +79,19 @@ __device__ __forceinline__ double spmv_epilogue(double sum, const SpmvArgs& a, i
     return y;
 }
 
+// XCD-aware block order: the hardware deals consecutive blocks round-robin
+// over the 8 XCDs (each with its own L2); the remap gives each XCD one
+// contiguous run of blocks, so the x lines a row block gathers from its
+// neighbours' rows are found in that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+    const int q = nwg >> 3, r = nwg & 7, x = b & 7, i = b >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
 template <int MODE, int NIT>
 __global__ __launch_bounds__(kSpmvThreads) void k_spmv(SpmvArgs a) {
     __shared__ double prod[kSpmvNnz];
-    const int b = blockIdx.x;
+    const int b = a.xcd ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int tid = threadIdx.x;
     const int r0 = a.blk[b], r1 = a.blk[b + 1];
     const int p0 = a.rowptr[r0], p1 = a.rowptr[r1];
@@ -147,8 +156,14 @@ static hipError_t launch_spmv_mode(const SpmvArgs& a, int nit, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_spmv(const SpmvArgs& a, hipStream_t st) {
-    if (a.nblk <= 0) return hipSuccess;
+hipError_t launch_spmv(const SpmvArgs& a0, hipStream_t st) {
+    if (a0.nblk <= 0) return hipSuccess;
+    static const int xcd = [] {  // CAL_SPMV_XCD=0: hardware block order (A/B)
+        const char* e = std::getenv("CAL_SPMV_XCD");
+        return e ? std::atoi(e) : 1;
+    }();
+    SpmvArgs a = a0;
+    a.xcd = xcd;
     // a.mode carries the per-matrix iteration count in bits 8..15
     const int nit = (a.mode >> 8) & 0xff;
     switch (a.mode & 0xff) {
@@ -167,10 +182,7 @@ hipError_t launch_spmv(const SpmvArgs& a, hipStream_t st) {
 // remapping gives each XCD a contiguous run of rows, so the x lines of the
 // neighbouring planes (col - row = +-N^2) are re-read from that XCD's L2.
 // --------------------------------------------------------------------------
-__device__ __forceinline__ int xcd_remap(int b, int nwg) {
-    const int q = nwg >> 3, r = nwg & 7, x = b & 7, i = b >> 3;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
-}
+// (xcd_remap: defined above k_spmv)
 
 // fixed-order butterfly sum over the 64 lanes of a wave
 __device__ __forceinline__ double wave_sum(double v) {

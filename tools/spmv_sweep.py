@@ -1,6 +1,6 @@
 """SpMV kernel timing on one workload (HBM-resident vectors), one line per run.
 
-  python tools/spmv_sweep.py [--workload lap3d_215] [--format pattern|csr] [--reps 50]
+  python tools/spmv_sweep.py [--workload lap3d_215|circuit_1259] [--format pattern|csr] [--reps 50]
 
 Environment knobs read by the library (e.g. CAL_PAT_ROWS) apply per process.
 """
@@ -25,14 +25,20 @@ def main():
     import ca_lanczos_amd as cal
     from ca_lanczos_amd.matrices import laplacian_rows
     kind, N = a.workload.split("_")
-    dim = {"lap2d": 2, "lap3d": 3}[kind]
     N = int(N)
-    n = N ** dim
-    rp, col, val = laplacian_rows(dim, N, 0, n)
-    nnz = int(rp[-1])
     ctx = cal.Context(device=0, spmv_format=a.format)
-    ctx.set_matrix(sp.csr_matrix((val, col.astype(np.int32), rp), shape=(n, n)))
-    del rp, col, val
+    if kind == "circuit":
+        A = cal.matrices.circuit_like(N)
+        n, nnz = A.shape[0], A.nnz
+        ctx.set_matrix(A)
+        del A
+    else:
+        dim = {"lap2d": 2, "lap3d": 3}[kind]
+        n = N ** dim
+        rp, col, val = laplacian_rows(dim, N, 0, n)
+        nnz = int(rp[-1])
+        ctx.set_matrix(sp.csr_matrix((val, col.astype(np.int32), rp), shape=(n, n)))
+        del rp, col, val
     ctx.bench_spmv(a.reps, a.shift)  # warm (clocks, caches)
     mean, mn = ctx.bench_spmv(a.reps, a.shift)
     fmt = ctx.spmv_format()[0]
