@@ -595,7 +595,24 @@ static int pn_tsqr(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, bool 
     if (!tsqr_ok(m)) return set_error(c, CAL_ERR_UNSUPPORTED, "projectAndNormalize (tsqr): at most 32 columns");
     const Panel W = panel_concat(Qp, X);
     std::vector<double> G1((size_t)wp * m);
-    CAL_TRY(gram_host(c, n, W, X, G1.data()));
+    const int nq = w < 8 ? w : 8;
+    // [Qp | X]'X: the row-parallel tile Gram of the CholQR2 path when the
+    // shapes fit one 16-column tile (+ Qp's ninth column), else k_gram
+    const bool tile = w <= 9 && nq + m <= 16 && Qp.nseg + X.nseg <= kMaxSeg;
+    if (tile) {
+        Panel Tl = panel_slice(W, 0, nq);
+        Tl = panel_concat(Tl, X);
+        const double* E = w == 9 ? panel_slice(Qp, 8, 1).ptr[0] : nullptr;
+        double G16[256], e16[16];
+        CAL_TRY(tilegram_host(c, n, Tl, E, G16, e16));
+        for (int j = 0; j < m; ++j) {
+            for (int i = 0; i < nq; ++i) G1[i + (size_t)j * wp] = G16[i + (nq + j) * 16];
+            if (w == 9) G1[8 + (size_t)j * wp] = e16[nq + j];
+            for (int i = 0; i < m; ++i) G1[w + i + (size_t)j * wp] = G16[(nq + i) + (nq + j) * 16];
+        }
+    } else {
+        CAL_TRY(gram_host(c, n, W, X, G1.data()));
+    }
     std::vector<double> C((size_t)std::max(w, 1) * m, 0.0), before(m);
     double mx = NAN;
     for (int j = 0; j < m; ++j) {
@@ -621,7 +638,15 @@ static int pn_tsqr(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, bool 
     if (reorth) {  // C2 = Qp'Y, Y = W [-C; I]
         std::vector<double> M = coef(C);
         C2.assign((size_t)w * m, 0.0);
-        if (w <= 16 && m <= 16) {
+        if (rowapply_ok(wp, m, true, w) && W.nseg <= kMaxSeg) {
+            // the Gram-only row sweep (pass A's kernel): Qp'Y with Y in registers
+            double G16[256], e16[16];
+            CAL_TRY(rowapply_host(c, n, W, M.data(), m, Qout, 2, w, G16, e16));
+            for (int j = 0; j < m; ++j) {
+                for (int i = 0; i < nq; ++i) C2[i + (size_t)j * w] = G16[i + (nq + j) * 16];
+                if (w == 9) C2[8 + (size_t)j * w] = e16[nq + j];
+            }
+        } else if (w <= 16 && m <= 16) {
             CAL_TRY(apply_host(c, n, W, M.data(), m, nullptr, nullptr, w, C2.data()));
         } else {
             double* dY;

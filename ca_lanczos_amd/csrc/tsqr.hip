@@ -197,8 +197,59 @@ __global__ __launch_bounds__(256) void k_tsqr(TsqrLevelArgs a, TsqrCols P, TsqrQ
     const int64_t base = tile * TR;
     const int64_t mm = (int64_t)m * m;
     double x[RPL][MM];
+    if (SRC == 2) {
+        // formed: Z = P M (+ P(:,0:w2) M2), column k outermost so each M entry
+        // is read from LDS once per tile, not once per row (the row-inner
+        // order re-read all of M for each of the RPL rows and was bound by
+        // the LDS return path); per entry the FMA order over k is unchanged
+        int64_t rc[RPL];
+        bool in[RPL];
 #pragma unroll
-    for (int i = 0; i < RPL; ++i) {
+        for (int i = 0; i < RPL; ++i) {
+            const int64_t r = base + lane + 64 * i;
+            in[i] = r < a.rows;
+            rc[i] = in[i] ? r : 0;
+#pragma unroll
+            for (int c = 0; c < MM; ++c) x[i][c] = 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < WP; ++k) {
+            double p[RPL];
+#pragma unroll
+            for (int i = 0; i < RPL; ++i) p[i] = P.p[k][rc[i]];  // host pads p[k >= wp] (zero rows of M)
+#pragma unroll
+            for (int c = 0; c < MM; ++c) {
+                const double mk = Ms[k * MM + c];
+#pragma unroll
+                for (int i = 0; i < RPL; ++i) x[i][c] = __builtin_fma(p[i], mk, x[i][c]);
+            }
+        }
+        if (a.M2) {
+            // projectAndNormalize.m:63: Z = Y - Qp C2 on the ROUNDED
+            // Y = X - Qp C (one combined coefficient would lose C2 below
+            // u |C|); Qp = the first w2 panel columns (reloaded: cache hits)
+#pragma unroll
+            for (int k = 0; k < WP; ++k) {
+                if (k < a.w2) {
+                    double p[RPL];
+#pragma unroll
+                    for (int i = 0; i < RPL; ++i) p[i] = P.p[k][rc[i]];
+#pragma unroll
+                    for (int c = 0; c < MM; ++c) {
+                        const double mk = Ms[WP * MM + k * MM + c];
+#pragma unroll
+                        for (int i = 0; i < RPL; ++i) x[i][c] = __builtin_fma(p[i], mk, x[i][c]);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < RPL; ++i)
+#pragma unroll
+            for (int c = 0; c < MM; ++c) x[i][c] = in[i] ? x[i][c] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < (SRC == 2 ? 0 : RPL); ++i) {
         const int64_t r = base + lane + 64 * i;
         const bool in = r < a.rows;
         const int64_t rc = in ? r : 0;
@@ -210,36 +261,12 @@ __global__ __launch_bounds__(256) void k_tsqr(TsqrLevelArgs a, TsqrCols P, TsqrQ
                 const double v = src[(int64_t)(c < m ? c : 0) * m];
                 x[i][c] = (in && c < m) ? v : 0.0;
             }
-        } else if (SRC == 1) {
+        } else {
 #pragma unroll
             for (int c = 0; c < MM; ++c) {
                 const double v = P.p[c][rc];  // host pads p[c >= m] with a valid column
                 x[i][c] = (in && c < m) ? v : 0.0;
             }
-        } else {
-#pragma unroll
-            for (int c = 0; c < MM; ++c) x[i][c] = 0.0;
-#pragma unroll
-            for (int k = 0; k < WP; ++k) {
-                const double p = P.p[k][rc];  // host pads p[k >= wp] (zero rows of M)
-#pragma unroll
-                for (int c = 0; c < MM; ++c) x[i][c] = __builtin_fma(p, Ms[k * MM + c], x[i][c]);
-            }
-            if (a.M2) {
-                // projectAndNormalize.m:63: Z = Y - Qp C2 on the ROUNDED
-                // Y = X - Qp C (one combined coefficient would lose C2 below
-                // u |C|); Qp = the first w2 panel columns (reloaded: cache hits)
-#pragma unroll
-                for (int k = 0; k < WP; ++k) {
-                    if (k < a.w2) {
-                        const double p = P.p[k][rc];
-#pragma unroll
-                        for (int c = 0; c < MM; ++c) x[i][c] = __builtin_fma(p, Ms[WP * MM + k * MM + c], x[i][c]);
-                    }
-                }
-            }
-#pragma unroll
-            for (int c = 0; c < MM; ++c) x[i][c] = in ? x[i][c] : 0.0;
         }
     }
     double tau[MM], beta[MM];
@@ -272,34 +299,48 @@ __global__ __launch_bounds__(256) void k_tsqr(TsqrLevelArgs a, TsqrCols P, TsqrQ
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     tile_org2r<MM, RPL>(x, tau, m, lane);
+    // O = Q_tile S, half of the tile's rows at a time with each S entry read
+    // from LDS once per half (per row it was re-read RPL times); per entry
+    // the sum over k is in the same order
+    constexpr int H = RPL >= 2 ? RPL / 2 : 1;
 #pragma unroll
-    for (int i = 0; i < RPL; ++i) {
-        const int64_t r = base + lane + 64 * i;
-        double o[MM];
+    for (int i0 = 0; i0 < RPL; i0 += H) {
+        double o[H][MM];
 #pragma unroll
-        for (int c = 0; c < MM; ++c) o[c] = 0.0;
+        for (int h = 0; h < H; ++h)
+#pragma unroll
+            for (int c = 0; c < MM; ++c) o[h][c] = 0.0;
 #pragma unroll
         for (int k = 0; k < MM; ++k) {
             if (k < m) {
 #pragma unroll
                 for (int c = 0; c < MM; ++c) {
-                    const double u = x[i][k] * S[k + c * MM];
-                    o[c] = o[c] + u;
+                    const double sk = S[k + c * MM];
+#pragma unroll
+                    for (int h = 0; h < H; ++h) {
+                        const double u = x[i0 + h][k] * sk;
+                        o[h][c] = o[h][c] + u;
+                    }
                 }
             }
         }
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+        const int i = i0 + h;
+        const int64_t r = base + lane + 64 * i;
         if (r < a.rows) {
             if (SRC == 0) {
                 const int64_t blk = r / m, rr = r - blk * m;
                 double* dst = a.out + blk * mm + rr;
 #pragma unroll
                 for (int c = 0; c < MM; ++c)
-                    if (c < m) dst[(int64_t)c * m] = o[c];
+                    if (c < m) dst[(int64_t)c * m] = o[h][c];
             } else {
 #pragma unroll
                 for (int c = 0; c < MM; ++c)
-                    if (c < m) Q.p[c][r] = o[c];
+                    if (c < m) Q.p[c][r] = o[h][c];
             }
+        }
         }
     }
 }
