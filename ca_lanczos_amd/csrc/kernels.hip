@@ -875,17 +875,19 @@ __global__ __launch_bounds__(256) void k_gram(Panel A, Panel B, int64_t n, doubl
 // lane -- 512 contiguous bytes per wave instruction instead of 16 column
 // pieces -- and staged in LDS ([row][col], odd leading dimension), then read
 // back in k_gram's operand layout: lane (c16, g) of wave w takes row
-// w*4RUN + g*RUN + m of column 16t + c16 for MFMA m of tile t.  The B tile
-// is read once per row block into registers; A goes through LDS 16 columns
-// at a time, the next chunk's loads in flight during the current MFMAs.
-template <int NTA, int RUN>
+// w*4RUN + g*RUN + m of column 16t + c16 for MFMA m of tile t.  U grid steps
+// (rows rb0 + u*stride, u < U) share one staging round, so one barrier
+// covers U*16*RUN rows; the MFMAs still take the steps in order.  The B tile
+// is read once per round into registers; A goes through LDS 16 columns at a
+// time, the next chunk's loads in flight during the current MFMAs.
+template <int NTA, int RUN, int U>
 __global__ __launch_bounds__(256) void k_gram_lds(Panel A, Panel B, int64_t n, double* __restrict__ partial) {
-    constexpr int R = 16 * RUN;   // rows per block step
+    constexpr int R = 16 * RUN;   // rows per grid step of a block
     constexpr int LD = 17;        // [row][col] leading dimension (odd: conflict-free row-major writes)
-    constexpr int PER = R / 16;   // values per thread per 16-column chunk
+    constexpr int PER = R / 16;   // values per thread per 16-column chunk and step
+    constexpr int BUF = U * R * LD;
     // dynamic LDS: the two staging buffers, later reused for the wave partials
     extern __shared__ __attribute__((aligned(16))) double lds_g[];
-    double* sT[2] = {lds_g, lds_g + R * LD};
     auto red = reinterpret_cast<double (*)[NTA][64][4]>(lds_g);  // [3][NTA][64][4]
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
@@ -898,45 +900,56 @@ __global__ __launch_bounds__(256) void k_gram_lds(Panel A, Panel B, int64_t n, d
     for (int t = 0; t < NTA; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
     const int orow = wave * 4 * RUN + g * RUN;  // this lane's operand rows: orow + m
     const int64_t stride = (int64_t)gridDim.x * R;
-    double v[PER];
+    double v[U][PER];
     auto load = [&](int c, int64_t rb) {
-        const int64_t rr = rb + lrow0;
-        const bool in = rr < n;
 #pragma unroll
-        for (int q = 0; q < PER; ++q) {
-            const int cc = __builtin_amdgcn_readfirstlane((tid + 256 * q) / R) + (c > 0 ? 16 * (c - 1) : 0);
-            const bool on = cc < (c == 0 ? B.total : A.total);
-            const double* pc = c == 0 ? pcol(B, on ? cc : 0) : pcol(A, on ? cc : 0);
-            const double x = pc[in ? rr : 0];
-            v[q] = (on && in) ? x : 0.0;
+        for (int u = 0; u < U; ++u) {
+            const int64_t rr = rb + u * stride + lrow0;
+            const bool in = rr < n;
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                const int cc = __builtin_amdgcn_readfirstlane((tid + 256 * q) / R) + (c > 0 ? 16 * (c - 1) : 0);
+                const bool on = cc < (c == 0 ? B.total : A.total);
+                const double* pc = c == 0 ? pcol(B, on ? cc : 0) : pcol(A, on ? cc : 0);
+                const double x = pc[in ? rr : 0];
+                v[u][q] = (on && in) ? x : 0.0;
+            }
         }
     };
     int64_t rb0 = (int64_t)blockIdx.x * R;
     if (rb0 < n) load(0, rb0);
-    for (; rb0 < n; rb0 += stride) {
-        double bv[RUN];
+    for (; rb0 < n; rb0 += U * stride) {
+        double bv[U][RUN];
 #pragma unroll
         for (int c = 0; c <= NTA; ++c) {
             // buffer c & 1: its last reader was chunk c - 2, done before the
-            // barrier after chunk c - 1's write (and the step-end barrier)
-            double* s = sT[c & 1];
+            // barrier after chunk c - 1's write (and the round-end barrier)
+            double* s = lds_g + (c & 1) * BUF;
 #pragma unroll
-            for (int q = 0; q < PER; ++q) s[lrow0 * LD + (tid + 256 * q) / R] = v[q];
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int q = 0; q < PER; ++q) s[(u * R + lrow0) * LD + (tid + 256 * q) / R] = v[u][q];
             // the next chunk's loads are in flight across the barrier and the MFMAs
             if (c < NTA) load(c + 1, rb0);
-            else if (rb0 + stride < n) load(0, rb0 + stride);
+            else if (rb0 + U * stride < n) load(0, rb0 + U * stride);
             __syncthreads();
-            if (c == 0) {
 #pragma unroll
-                for (int m = 0; m < RUN; ++m) bv[m] = s[(orow + m) * LD + c16];
-            } else {
+            for (int u = 0; u < U; ++u) {
+                if (rb0 + u * stride >= n) break;  // block-uniform: k_gram has no such step
+                const double* su = s + u * R * LD;
+                if (c == 0) {
 #pragma unroll
-                for (int m = 0; m < RUN; ++m) acc[c - 1] = mfma64(s[(orow + m) * LD + c16], bv[m], acc[c - 1]);
+                    for (int m = 0; m < RUN; ++m) bv[u][m] = su[(orow + m) * LD + c16];
+                } else {
+#pragma unroll
+                    for (int m = 0; m < RUN; ++m)
+                        acc[c - 1] = mfma64(su[(orow + m) * LD + c16], bv[u][m], acc[c - 1]);
+                }
             }
         }
-        __syncthreads();  // the next step's chunk 0 rewrites buffer 0
+        __syncthreads();  // the next round's chunk 0 rewrites buffer 0
     }
-    __syncthreads();  // (no step ran) the staging buffers become the partials
+    __syncthreads();  // (no round ran) the staging buffers become the partials
     if (wave > 0) {
 #pragma unroll
         for (int t = 0; t < NTA; ++t)
@@ -978,8 +991,11 @@ GramPlan gram_plan(int wa, int wb, int64_t n) {
 
 template <int NTA, int RUN>
 static void launch_gram_lds(const Panel& A, const Panel& B, int64_t n, int blocks, double* partial, hipStream_t st) {
-    const size_t lds = std::max((size_t)2 * 16 * RUN * 17, (size_t)3 * NTA * 64 * 4) * sizeof(double);
-    hipLaunchKernelGGL((k_gram_lds<NTA, RUN>), dim3(blocks), dim3(256), lds, st, A, B, n, partial);
+    // grid steps per staging round: U = 2 / 4 (fewer barriers, twice / four
+    // times the LDS) measured 5-20 % slower than U = 1 (occupancy)
+    constexpr int U = 1;
+    const size_t lds = std::max((size_t)2 * U * 16 * RUN * 17, (size_t)3 * NTA * 64 * 4) * sizeof(double);
+    hipLaunchKernelGGL((k_gram_lds<NTA, RUN, U>), dim3(blocks), dim3(256), lds, st, A, B, n, partial);
 }
 
 bool gram_lds_on() {  // CAL_GRAM_LDS=0: the direct-load k_gram (A/B; same bits)
