@@ -247,6 +247,8 @@ hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64
                                         int64_t pstride, hipStream_t st);
 int spmv_resid_pair_multi_dev(cal_ctx* c, const double* X, int64_t ldx, const int* col, const double* lam,
                               const int* out, int npr, double* partial, int64_t pstride);
+int spmv_pair_resid_multi_blocks(const PatArgs& a);
+int spmv_resid_pair_multi_blocks(cal_ctx* c);  // its grid (0: no pair path)
 // store-only Y = P M on the matrix cores (one segment each, 16-B aligned,
 // Y not aliasing P; M wp x wy column-major on the device)
 bool apply_mt_ok(int wp, int wy);

@@ -506,11 +506,14 @@ __global__ __launch_bounds__(256) void k_spmv_pair_resid(PatArgs a, const uint16
 
 // k_spmv_pair_resid over many Ritz pairs in one launch: blockIdx.y takes
 // pairs [CPB y, CPB y + CPB) of the list (x = X + col[i] * ldx, l = lam[i]);
-// the pair ids and the table are loaded once per block and reused for every
-// pair.  Per pair the products, the per-lane sums, the wave sums and the
-// block sum are those of k_spmv_pair_resid, so are the bits; the block's
-// two sums go to partial[(2 out[i] + e) * pstride + blockIdx.x].
-template <int MAXLEN, int CPB>
+// the pair table is staged once per block.  Each thread takes PPT row pairs
+// of the block's contiguous run (pair b*256*PPT + j*256 + tid), reads each
+// pair's id and table entries once for all CPB Ritz pairs, and keeps its
+// sums per Ritz pair in registers, so the table staging, the wave sums and
+// the partial writes are paid once per 256*PPT row pairs.  Per row the
+// products and their order are k_spmv_pair's MODE 1 (y = A x - l x); the
+// block's two sums of Ritz pair i go to partial[(2 out[i] + e) * pstride + b].
+template <int MAXLEN, int CPB, int PPT>
 __global__ __launch_bounds__(256) void k_spmv_pair_resid_multi(PatArgs a, const uint16_t* __restrict__ ppat,
                                                               const int* __restrict__ ppoff,
                                                               const double2* __restrict__ ppval,
@@ -525,10 +528,7 @@ __global__ __launch_bounds__(256) void k_spmv_pair_resid_multi(PatArgs a, const 
     __shared__ double ws[CPB][2][4];
     const int tid = threadIdx.x;
     const int64_t npairs = (a.n + 1) >> 1;
-    const int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 256 + tid;
-    const int64_t tcl = t < npairs ? t : npairs - 1;
-    const int id = ppat[tcl];
-    const int64_t r0 = 2 * tcl;
+    const int64_t b0 = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 256 * PPT;
     for (int i = tid; i < a.npent; i += 256) {
         s_pv[i] = ppval[i];
         s_poff[i] = ppoff[i];
@@ -537,67 +537,92 @@ __global__ __launch_bounds__(256) void k_spmv_pair_resid_multi(PatArgs a, const 
     const int i0 = blockIdx.y * CPB;
     const int nq = npairs_ritz - i0 < CPB ? npairs_ritz - i0 : CPB;  // uniform over the block
     const int lane = tid & 63, wave = tid >> 6;
-    const bool two = r0 + 1 < a.n;  // see k_spmv_pair_resid (odd distributed slab)
-    const int base = id != kPairSplit ? id * MAXLEN : 0;
-    // the pair's table entries, read from LDS once for all CPB columns
-    int code[MAXLEN];
-    double2 v[MAXLEN];
+    const double* xq[CPB];
+    double lq[CPB], num[CPB], den[CPB];
 #pragma unroll
-    for (int e = 0; e < MAXLEN; ++e) {
-        code[e] = s_poff[base + e];
-        v[e] = s_pv[base + e];
+    for (int q = 0; q < CPB; ++q) {
+        const int qq = q < nq ? q : 0;
+        xq[q] = X + (int64_t)col[i0 + qq] * ldx;
+        lq[q] = lam[i0 + qq];
+        num[q] = 0.0;
+        den[q] = 0.0;
     }
-    // one column at a time (two columns' loads in flight measured slower:
-    // 2.9 vs 2.2 ms per 64 columns at n = 9.94 M)
-    for (int q = 0; q < nq; ++q) {
-        const double* x = X + (int64_t)col[i0 + q] * ldx;
-        const double l = lam[i0 + q];
-        double2 xc[MAXLEN];
+    for (int j = 0; j < PPT; ++j) {
+        const int64_t t = b0 + (int64_t)j * 256 + tid;
+        if (b0 + (int64_t)j * 256 >= npairs) break;  // uniform over the block
+        const int64_t tcl = t < npairs ? t : npairs - 1;
+        const int id = ppat[tcl];
+        const int64_t r0 = 2 * tcl;
+        const bool two = r0 + 1 < a.n;  // see k_spmv_pair_resid (odd distributed slab)
+        const int base = id != kPairSplit ? id * MAXLEN : 0;
+        int code[MAXLEN];
+        double2 v[MAXLEN];
 #pragma unroll
         for (int e = 0; e < MAXLEN; ++e) {
-            int64_t ad = r0 + a.pslot[e];
-            ad = ad < a.xlo ? a.xlo : (ad > a.xhi - 2 ? a.xhi - 2 : ad);
-            xc[e] = ld16(x + ad);
+            code[e] = s_poff[base + e];
+            v[e] = s_pv[base + e];
         }
-        const double2 xs = ld16(x + (r0 < a.xhi - 2 ? r0 : a.xhi - 2));
-        double nu = 0.0, de = 0.0;
-        if (t < npairs) {
-            if (id != kPairSplit) {
-                double y0 = 0.0, y1 = 0.0;
+        int64_t ad[MAXLEN];
 #pragma unroll
-                for (int e = 0; e < MAXLEN; ++e) {
-                    const double t0 = v[e].x * xc[e].x, t1 = v[e].y * xc[e].y;
-                    double a0 = y0 + t0, a1 = y1 + t1;
-                    asm volatile("" : "+v"(a0), "+v"(a1));
-                    y0 = (code[e] & 1) ? a0 : y0;
-                    y1 = (code[e] & 2) ? a1 : y1;
-                }
-                const double u0 = l * xs.x, u1 = l * xs.y;
-                y0 = y0 - u0;
-                y1 = y1 - u1;
-                nu = y0 * y0 + (two ? y1 * y1 : 0.0);
-                de = u0 * u0 + (two ? u1 * u1 : 0.0);
-            } else {
-                for (int k = 0; k < 2 && r0 + k < a.n; ++k) {
-                    const int64_t rr = r0 + k;
-                    const int2 pi = a.pinfo[a.pat[rr]];
-                    double sum = 0.0;
-                    for (int e = 0; e < pi.y; ++e) {
-                        const double tv = a.pval[pi.x + e] * x[rr + a.pdelta[pi.x + e]];
-                        sum = sum + tv;
+        for (int e = 0; e < MAXLEN; ++e) {
+            const int64_t d = r0 + a.pslot[e];
+            ad[e] = d < a.xlo ? a.xlo : (d > a.xhi - 2 ? a.xhi - 2 : d);
+        }
+        const int64_t rs = r0 < a.xhi - 2 ? r0 : a.xhi - 2;
+#pragma unroll
+        for (int q = 0; q < CPB; ++q) {
+            if (q >= nq) break;
+            const double* x = xq[q];
+            const double l = lq[q];
+            double2 xc[MAXLEN];
+#pragma unroll
+            for (int e = 0; e < MAXLEN; ++e) xc[e] = ld16(x + ad[e]);
+            const double2 xs = ld16(x + rs);
+            if (t < npairs) {
+                if (id != kPairSplit) {
+                    double y0 = 0.0, y1 = 0.0;
+#pragma unroll
+                    for (int e = 0; e < MAXLEN; ++e) {
+                        const double t0 = v[e].x * xc[e].x, t1 = v[e].y * xc[e].y;
+                        double a0 = y0 + t0, a1 = y1 + t1;
+                        asm volatile("" : "+v"(a0), "+v"(a1));
+                        y0 = (code[e] & 1) ? a0 : y0;
+                        y1 = (code[e] & 2) ? a1 : y1;
                     }
-                    const double u = l * x[rr];
-                    const double y = sum - u;
-                    nu = nu + y * y;
-                    de = de + u * u;
+                    const double u0 = l * xs.x, u1 = l * xs.y;
+                    y0 = y0 - u0;
+                    y1 = y1 - u1;
+                    num[q] = num[q] + (y0 * y0 + (two ? y1 * y1 : 0.0));
+                    den[q] = den[q] + (u0 * u0 + (two ? u1 * u1 : 0.0));
+                } else {
+                    double nu = 0.0, de = 0.0;
+                    for (int k = 0; k < 2 && r0 + k < a.n; ++k) {
+                        const int64_t rr = r0 + k;
+                        const int2 pi = a.pinfo[a.pat[rr]];
+                        double sum = 0.0;
+                        for (int e = 0; e < pi.y; ++e) {
+                            const double tv = a.pval[pi.x + e] * x[rr + a.pdelta[pi.x + e]];
+                            sum = sum + tv;
+                        }
+                        const double u = l * x[rr];
+                        const double y = sum - u;
+                        nu = nu + y * y;
+                        de = de + u * u;
+                    }
+                    num[q] = num[q] + nu;
+                    den[q] = den[q] + de;
                 }
             }
         }
-        nu = wave_sum(nu);
-        de = wave_sum(de);
-        if (lane == 0) {
-            ws[q][0][wave] = nu;
-            ws[q][1][wave] = de;
+    }
+#pragma unroll
+    for (int q = 0; q < CPB; ++q) {
+        if (q < nq) {
+            const double nu = wave_sum(num[q]), de = wave_sum(den[q]);
+            if (lane == 0) {
+                ws[q][0][wave] = nu;
+                ws[q][1][wave] = de;
+            }
         }
     }
     __syncthreads();
@@ -703,26 +728,42 @@ hipError_t launch_spmv_pair_resid(const PatArgs& a, double lr, double* partial, 
     return hipGetLastError();
 }
 
+// row pairs per thread of the batched residual kernel (CAL_RESID_PPT = 1, 2,
+// 4 or 8 for A/B) and its grid
+static int resid_ppt() {
+    static const int ppt = [] {
+        const char* e = std::getenv("CAL_RESID_PPT");
+        const int v = e ? std::atoi(e) : 4;
+        return v == 1 || v == 2 || v == 8 ? v : 4;
+    }();
+    return ppt;
+}
+
+int spmv_pair_resid_multi_blocks(const PatArgs& a) {
+    const int nb = spmv_pair_resid_blocks(a);
+    return nb > 0 ? (nb + resid_ppt() - 1) / resid_ppt() : 0;
+}
+
 hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64_t ldx, const int* col,
                                         const double* lam, const int* out, int npr, double* partial,
                                         int64_t pstride, hipStream_t st) {
-    // Ritz pairs per block (CAL_RESID_CPB = 2 / 4 / 8 for A/B): more pairs
-    // share the table reads, fewer keep the blocks in flight on fewer columns
+    // Ritz pairs per block (CAL_RESID_CPB = 2 / 4 / 8 for A/B)
     static const int cpb = [] {
         const char* e = std::getenv("CAL_RESID_CPB");
         const int v = e ? std::atoi(e) : 4;
         return v == 2 || v == 8 ? v : 4;
     }();
-    const int blocks = spmv_pair_resid_blocks(a);
+    const int blocks = spmv_pair_resid_multi_blocks(a);
     if (blocks <= 0 || pstride < blocks) return hipErrorInvalidValue;
     if (npr <= 0) return hipSuccess;
+    if (a.pmaxlen > 8) return hipErrorInvalidValue;
     const size_t lds = (size_t)a.npent * 20 + 16;
-    auto go = [&](auto cpb_c) {
-        constexpr int CPB = decltype(cpb_c)::value;
+    auto go2 = [&](auto cpb_c, auto ppt_c) {
+        constexpr int CPB = decltype(cpb_c)::value, PPT = decltype(ppt_c)::value;
         dim3 g(blocks, (npr + CPB - 1) / CPB), bl(256);
-#define CAL_PRM(ML)                                                                                                \
-    hipLaunchKernelGGL((k_spmv_pair_resid_multi<ML, CPB>), g, bl, lds, st, a, a.ppat, a.ppoff, a.ppval, X, ldx, col, \
-                       lam, out, npr, partial, pstride)
+#define CAL_PRM(ML)                                                                                             \
+    hipLaunchKernelGGL((k_spmv_pair_resid_multi<ML, CPB, PPT>), g, bl, lds, st, a, a.ppat, a.ppoff, a.ppval, X, \
+                       ldx, col, lam, out, npr, partial, pstride)
         switch (a.pmaxlen) {
             case 1: CAL_PRM(1); break;
             case 2: CAL_PRM(2); break;
@@ -735,7 +776,14 @@ hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64
         }
 #undef CAL_PRM
     };
-    if (a.pmaxlen > 8) return hipErrorInvalidValue;
+    auto go = [&](auto cpb_c) {
+        switch (resid_ppt()) {
+            case 1: go2(cpb_c, std::integral_constant<int, 1>{}); break;
+            case 2: go2(cpb_c, std::integral_constant<int, 2>{}); break;
+            case 8: go2(cpb_c, std::integral_constant<int, 8>{}); break;
+            default: go2(cpb_c, std::integral_constant<int, 4>{}); break;
+        }
+    };
     if (cpb == 2) go(std::integral_constant<int, 2>{});
     else if (cpb == 8) go(std::integral_constant<int, 8>{});
     else go(std::integral_constant<int, 4>{});

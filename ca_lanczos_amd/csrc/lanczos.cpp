@@ -424,7 +424,7 @@ static int diag_launch(cal_ctx* c, LanczosState& L, DiagJob& J) {
     int* h_col = reinterpret_cast<int*>(L.h_din + o_col);
     int* h_out = reinterpret_cast<int*>(L.h_din + o_out);
     J.sep.clear();
-    const int nbp = spmv_resid_pair_blocks(c);  // 0: no pair path (row kernel for every pair)
+    const int nbp = spmv_resid_pair_multi_blocks(c);  // 0: no pair path (row kernel for every pair)
     for (int i = 0, q = 0; i < sk; ++i) {
         const RitzPair& p = J.pairs[i];
         if (nbp > 0 && p.ci < 0) {

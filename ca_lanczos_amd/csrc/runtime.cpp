@@ -491,6 +491,13 @@ int spmv_resid_pair_dev(cal_ctx* c, const double* x, double lr, double* partial,
     return 0;
 }
 
+int spmv_resid_pair_multi_blocks(cal_ctx* c) {
+    const DevMatrix& A = c->A;
+    if (!c->has_A || !A.use_pat || !A.use_pair) return 0;
+    const PatArgs p = pat_args(A, A.ext_off, A.n_local, nullptr, nullptr, 1, 0.0, 0.0, nullptr);
+    return spmv_pair_resid_multi_blocks(p);
+}
+
 int spmv_resid_pair_multi_dev(cal_ctx* c, const double* X, int64_t ldx, const int* col, const double* lam,
                               const int* out, int npr, double* partial, int64_t pstride) {
     const DevMatrix& A = c->A;
