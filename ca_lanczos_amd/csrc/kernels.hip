@@ -1396,7 +1396,7 @@ hipError_t launch_apply(const Panel& P, const double* dM, int wp, int wy, const 
 // 120 x 120 in 6.6 ms vs 12.5 ms).  Each output is the k-ascending FMA chain
 // starting from 0, as k_apply_rows computes it (the probe compares bitwise).
 // One segment each; Y must not alias P.  Grid: blockIdx.y = 16*NT-column group.
-template <int NT, int WAVES>
+template <int NT, int WAVES, int KG>
 __global__ __launch_bounds__(64 * WAVES) void k_apply_mt(const double* __restrict__ P, int64_t ldp,
                                                          const double* __restrict__ M, int wp, int wy,
                                                          double* __restrict__ Y, int64_t ldy, int64_t n) {
@@ -1419,27 +1419,47 @@ __global__ __launch_bounds__(64 * WAVES) void k_apply_mt(const double* __restric
         d4 acc[NT][2];
 #pragma unroll
         for (int ty = 0; ty < NT; ++ty) acc[ty][0] = acc[ty][1] = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-        for (int kc = 0; kc < nkc; ++kc) {
-            const int c = 4 * kc + g;
-            const bool con = c < wp;
-            const double* pc = P + (int64_t)(con ? c : 0) * ldp;
-            double b0, b1;
-            if (full) {
-                const d2 x = *reinterpret_cast<const d2*>(pc + rb);
-                b0 = x[0];
-                b1 = x[1];
-            } else {
-                b0 = rb < n ? pc[rb] : 0.0;
-                b1 = rb + 1 < n ? pc[rb + 1] : 0.0;
-            }
-            b0 = con ? b0 : 0.0;
-            b1 = con ? b1 : 0.0;
+        // B operands in groups of KG k-steps, the next group's loads issued
+        // before this group's MFMAs (KG per NT from tools/ritz_apply_probe.hip)
+        auto load_group = [&](int kc0, double (&b)[KG][2]) {
 #pragma unroll
-            for (int ty = 0; ty < NT; ++ty) {
-                const double a = Ms[c * ldm + 16 * ty + c16];
-                acc[ty][0] = mfma64(a, b0, acc[ty][0]);
-                acc[ty][1] = mfma64(a, b1, acc[ty][1]);
+            for (int u = 0; u < KG; ++u) {
+                const int c = 4 * (kc0 + u) + g;
+                const bool con = c < wp;
+                const double* pc = P + (int64_t)(con ? c : 0) * ldp;
+                double b0, b1;
+                if (full) {
+                    const d2 x = *reinterpret_cast<const d2*>(pc + rb);
+                    b0 = x[0];
+                    b1 = x[1];
+                } else {
+                    b0 = rb < n ? pc[rb] : 0.0;
+                    b1 = rb + 1 < n ? pc[rb + 1] : 0.0;
+                }
+                b[u][0] = con ? b0 : 0.0;
+                b[u][1] = con ? b1 : 0.0;
+            }
+        };
+        double bcur[KG][2], bnxt[KG][2];
+        load_group(0, bcur);
+        for (int kc0 = 0; kc0 < nkc; kc0 += KG) {
+            if (kc0 + KG < nkc) load_group(kc0 + KG, bnxt);
+#pragma unroll
+            for (int u = 0; u < KG; ++u) {
+                const int c = 4 * (kc0 + u) + g;  // rows of Ms past wpp are never read: kc0 + u < nkc below
+                if (kc0 + u < nkc) {
+#pragma unroll
+                    for (int ty = 0; ty < NT; ++ty) {
+                        const double a = Ms[c * ldm + 16 * ty + c16];
+                        acc[ty][0] = mfma64(a, bcur[u][0], acc[ty][0]);
+                        acc[ty][1] = mfma64(a, bcur[u][1], acc[ty][1]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < KG; ++u) {
+                bcur[u][0] = bnxt[u][0];
+                bcur[u][1] = bnxt[u][1];
             }
         }
 #pragma unroll
@@ -1463,6 +1483,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_apply_mt(const double* __restric
     }
 }
 
+// k-steps per load group of k_apply_mt by tile count
+constexpr int apply_mt_kg(int nt) { return nt <= 2 ? 2 : 4; }
+
 // 16-column tiles per block: ceil(wy / 16) up to 8 (no idle tiles), fewer
 // until M (wpp x 16 NT doubles) fits the 160 KB of LDS of one CU (0: never)
 static int apply_mt_nt(int wp, int wy) {
@@ -1484,13 +1507,14 @@ hipError_t launch_apply_mt(const double* P, int64_t ldp, const double* dM, int w
     // waves, 2 blocks per CU (1 at 128 outputs); fewer when M does not fit
     auto go = [&](auto nt_c, auto waves_c, int per_cu) {
         constexpr int NT = decltype(nt_c)::value, WAVES = decltype(waves_c)::value;
+        constexpr int KG = apply_mt_kg(NT);
         const size_t lds = (size_t)wpp * 16 * NT * sizeof(double);
         const int fit = (int)((160 * 1024) / lds);
         const int bpc = std::max(1, std::min(per_cu, fit));
         int64_t blocks = (n + 32 * WAVES - 1) / (32 * WAVES);
         if (blocks > 256 * bpc) blocks = 256 * bpc;
         const unsigned groups = (unsigned)((wy + 16 * NT - 1) / (16 * NT));
-        hipLaunchKernelGGL((k_apply_mt<NT, WAVES>), dim3((unsigned)blocks, groups), dim3(64 * WAVES), lds, st, P, ldp,
+        hipLaunchKernelGGL((k_apply_mt<NT, WAVES, KG>), dim3((unsigned)blocks, groups), dim3(64 * WAVES), lds, st, P, ldp,
                            dM, wp, wy, Y, ldy, n);
     };
     using I = std::integral_constant<int, 4>;

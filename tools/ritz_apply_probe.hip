@@ -175,7 +175,38 @@ int main() {
         const double t48 = time([&] { probe::launch_mt<4, 8>(Pbuf, ld, dM, sk, sk, Ybuf, ld, n, 2); });
         const double t24 = time([&] { probe::launch_mt<2, 4>(Pbuf, ld, dM, sk, sk, Ybuf, ld, n, 4); });
         const double d24 = maxdiff(sk);
+        const double tlib = time([&] { cal::launch_apply_mt(Pbuf, ld, dM, sk, sk, Ybuf, ld, n, 0); });
+        const double dlib = maxdiff(sk);
+        // k-step grouping of the library kernel (KG) at this sk's tile count
+        auto kg_time = [&](auto kg_c) {
+            constexpr int KG = decltype(kg_c)::value;
+            auto one = [&](auto nt_c, auto w_c, int per_cu) {
+                constexpr int NT = decltype(nt_c)::value, W = decltype(w_c)::value;
+                const size_t lds = (size_t)((sk + 3) & ~3) * 16 * NT * 8;
+                const int bpc = std::max(1, std::min(per_cu, (int)((160 * 1024) / lds)));
+                int64_t blocks = std::min<int64_t>((n + 32 * W - 1) / (32 * W), 256 * bpc);
+                return time([&] {
+                    hipLaunchKernelGGL((cal::k_apply_mt<NT, W, KG>), dim3((unsigned)blocks, (sk + 16 * NT - 1) / (16 * NT)),
+                                       dim3(64 * W), lds, 0, Pbuf, ld, dM, sk, sk, Ybuf, ld, n);
+                });
+            };
+            using I = std::integral_constant<int, 4>;
+            using E = std::integral_constant<int, 8>;
+            switch (std::min(8, (sk + 15) / 16)) {
+                case 1: return one(std::integral_constant<int, 1>{}, I{}, 4);
+                case 2: return one(std::integral_constant<int, 2>{}, I{}, 4);
+                case 3: return one(std::integral_constant<int, 3>{}, E{}, 2);
+                case 4: return one(std::integral_constant<int, 4>{}, E{}, 2);
+                case 6: return one(std::integral_constant<int, 6>{}, E{}, 2);
+                default: return one(std::integral_constant<int, 8>{}, E{}, 1);
+            }
+        };
+        printf("{\"sk\": %d, \"kg1_us\": %.0f, \"kg2_us\": %.0f, \"kg4_us\": %.0f}\n", sk,
+               kg_time(std::integral_constant<int, 1>{}), kg_time(std::integral_constant<int, 2>{}),
+               kg_time(std::integral_constant<int, 4>{}));
         const double fl = 2.0 * sk * sk * n, by = 2.0 * sk * 8.0 * n;
+        printf("{\"sk\": %d, \"launch_apply_mt_us\": %.0f, \"TF\": %.1f, \"diff_vs_rows\": %.2e}\n", sk, tlib,
+               fl / (tlib * 1e-6) / 1e12, dlib);
         auto rate = [&](double us) { return fl / (us * 1e-6) / 1e12; };
         auto bw = [&](double us) { return by / (us * 1e-6) / 1e9; };
         printf("{\"sk\": %d, \"lib_us\": %.0f, \"lib_TF\": %.1f, \"rocblas_us\": %.0f, \"rocblas_TF\": %.1f, \"rocblas_GBps\": %.0f, "
