@@ -255,3 +255,45 @@ def test_circuit_like_shape(ref):
     d = A.diagonal()
     off = np.asarray(abs(A).sum(axis=1)).ravel() - d
     assert np.all(d > off)                         # strictly diagonally dominant -> SPD
+
+
+def test_selective_locks_complex_pair_by_real_span(ref, monkeypatch):
+    """'selective' locks a converged complex-conjugate Ritz pair as the real
+    span of Q v, Q conj(v) (ca_lanczos.m:321-340 with complex QR columns).
+    Every eig(T) is rewritten so that its two most converged real eigenpairs
+    (smallest |Vp(sk,i)|) come back as one conjugate pair with eigenvectors
+    (v_i +- i v_j)/sqrt 2: the pair is then locked -- both members, as two
+    real columns -- whenever b(k)|Vp(sk,i)| passes for it, and the run stays a
+    valid selective CA-Lanczos (T symmetric to rounding, the same block
+    structure and size as the all-real run)."""
+    import math
+
+    import scipy.sparse as sp
+
+    a = ref.matlab_linspace(1.0, 100.0, 500)
+    A = sp.csr_matrix(sp.diags(a))
+    r = np.ones(500)
+    base = ref.ca_lanczos(A, r, 8, 160, "newton", "selective", diagnostics=False)
+    orig = ref.matlab_eig
+
+    def paired(T):
+        w, V = orig(T)
+        if np.iscomplexobj(w) or len(w) < 2:
+            return w, V
+        i, j = np.argsort(np.abs(V[-1, :]))[:2]
+        wc = w.astype(complex)
+        Vc = V.astype(complex)
+        vi, vj = V[:, i].copy(), V[:, j].copy()
+        wc[i] = complex(0.5 * (w[i] + w[j]), 1.0e-3)
+        wc[j] = np.conj(wc[i])
+        Vc[:, i] = (vi + 1j * vj) / math.sqrt(2.0)
+        Vc[:, j] = (vi - 1j * vj) / math.sqrt(2.0)
+        return wc, Vc
+
+    monkeypatch.setattr(ref, "matlab_eig", paired)
+    out = ref.ca_lanczos(A, r, 8, 160, "newton", "selective", diagnostics=False)
+    assert max(base.nritz) >= 2 and max(out.ncomplex) == 2  # the pair was locked, both members
+    assert all(c in (0, 2) for c in out.ncomplex)
+    assert max(out.nritz) >= 2
+    assert out.T.shape == base.T.shape
+    assert np.max(np.abs(out.T - out.T.T)) <= 1e-8 * 100.0
