@@ -764,7 +764,41 @@ int project_and_normalize_dev(cal_ctx* c, int64_t n, const Panel& Qp, const Pane
         Mz[w + j + (size_t)j * wp] = 1.0;
     }
     std::vector<double> Rtmp((size_t)m * m);
-    if (!dense::chol_upper(m, GZ.data(), m, Rtmp.data(), m)) {
+    const bool chol_ok = dense::chol_upper(m, GZ.data(), m, Rtmp.data(), m);
+    // A wide projection whose reorth test does not fire (projectAndNormalize.m:
+    // 52-58: no second pass; the 'fro' projection of ca_lanczos.m:197 against
+    // all of Q, whose block is already orthonormal): one projection and the
+    // normalize, as the reference does -- Q = [Qp | X] [-C; I] R^-1 with R =
+    // chol(Y'Y) in ONE apply sweep after the Gram sweep, instead of the two-
+    // pass CholQR2 (four wide sweeps).  Taken only when Y is so well
+    // conditioned that one Cholesky pass is orthonormal to rounding: the
+    // column-scaled Gram of Y is diagonally dominant with off-diagonal row
+    // sums < 1/2, so kappa(Y) < sqrt(3) and the loss of orthogonality ~ 3u.
+    if (w > 9 && !reorth && chol_ok && c->normalize_kind != 1) {
+        bool dominant = true;
+        for (int i = 0; i < m && dominant; ++i) {
+            double off = 0.0;
+            const double gii = GZ[i + (size_t)i * m];
+            for (int j = 0; j < m; ++j)
+                if (j != i) off += std::fabs(GZ[i + (size_t)j * m]) / std::sqrt(gii * GZ[j + (size_t)j * m]);
+            dominant = gii > 0.0 && off < 0.5;
+        }
+        if (dominant) {
+            std::vector<double> Ri((size_t)m * m), M1((size_t)wp * m);
+            dense::tri_inv_upper(m, Rtmp.data(), m, Ri.data(), m);
+            dense::matmul(wp, m, m, Mz.data(), wp, Ri.data(), m, M1.data(), wp);
+            CAL_TRY(apply_host(c, n, W, M1.data(), m, &Qout, nullptr, 0, nullptr));
+            std::copy(Rtmp.begin(), Rtmp.end(), R);
+            std::copy(C.begin(), C.end(), Rq);
+            if (res) {
+                res->reorth = false;
+                res->rank = rank_from_R(m, R, 1.0e-8);
+                res->chol_shifted = false;
+            }
+            return 0;
+        }
+    }
+    if (!chol_ok) {
         if (c->normalize_kind != 2 && tsqr_ok(m)) return pn_tsqr(c, n, Qp, X, doreorth, Qout, Rq, R, res);
         // the algebraic Gram lost definiteness (heavy cancellation): Y'Y directly
         CAL_TRY(apply_host(c, n, W, Mz.data(), m, nullptr, GZ.data(), 0, nullptr));
