@@ -5,10 +5,14 @@
 //  * the projected block Y = X - Qp*(Qp'X) (and the second-pass Z) is never
 //    written to HBM: every pass re-forms it on the fly inside k_apply from
 //    [Qp | X] with a small coefficient matrix;
-//  * tsqr's Householder QR is replaced by CholQR2 (two Cholesky-QR passes,
-//    the second in place on the stored block), which gives the same unique
-//    positive-diagonal R up to rounding and O(eps) orthogonality while
-//    kappa(Y) < ~1e7; a failed Cholesky falls back to shifted CholQR3;
+//  * in the CA-Lanczos loop tsqr's Householder QR is CholQR2 (two
+//    Cholesky-QR passes fused with the second projection), which gives the
+//    same unique positive-diagonal R up to rounding and O(eps) orthogonality
+//    while kappa(Y) < ~1e7; a failed Cholesky falls back to the device
+//    Householder TSQR (tsqr.hip / tsqr_tree.cpp, pn_tsqr below), which the
+//    host-pointer calls and normalize = "tsqr" use throughout;
+//  * a wide projection whose reorth test does not fire is one projection and
+//    one normalize, as in the reference: one Gram and one apply sweep;
 //  * the reorthogonalisation test of projectAndNormalize.m:52 is evaluated
 //    on norms taken from the same Gram (before: diag X'X; after: diag of
 //    X'X - C'C = ||Y_i||^2), so the pass count follows the reference.
@@ -908,26 +912,31 @@ int gram_async(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* d_
 
 // One block-MGS pass of project.m over the nb blocks (doreorth = false);
 // region r of d_red / h_red holds block r's Gram; ldc[r] its leading dimension.
+// dSrc (optional): the input block when it is not dX; the first projection
+// reads it and writes dX (no separate copy of X into the work block).
 static int project_blocks_async(cal_ctx* c, int64_t n, int64_t ld, int nb, const std::vector<double*>& dQ,
-                                const int* widths, int m, double* dX, int region0, std::vector<int>& ldc) {
-    Panel X = panel();
-    panel_add(X, dX, ld, m);
+                                const int* widths, int m, double* dX, int region0, std::vector<int>& ldc,
+                                const double* dSrc = nullptr) {
     const PanelOut Xo = panel_out(dX, ld, m);
+    const double* cur = dSrc ? dSrc : dX;  // where X currently is
     ldc.assign(nb, 0);
     for (int i = 0; i < nb; ++i) {
         const int w = widths[i];
         if (w <= 0) continue;
         const size_t off = kAsyncBase + (size_t)(region0 + i) * kAsyncRegion;
-        Panel Qi = panel();
+        Panel Qi = panel(), X = panel();
         panel_add(Qi, dQ[i], ld, w);
+        panel_add(X, cur, ld, m);
         CAL_TRY(gram_async(c, n, Qi, X, c->d_red + off, c->h_red + off, &ldc[i]));  // R{i} = Q{i}'*X
         double* dM = c->d_red + off + 4096;
         CAL_HIP(c, launch_form_projM(c->d_red + off, ldc[i], w, m, dM, c->stream));
         Panel W = panel();
         panel_add(W, dQ[i], ld, w);
-        panel_add(W, dX, ld, m);
+        panel_add(W, cur, ld, m);
         CAL_TRY(apply_dev(c, n, W, dM, m, Xo));  // X = X - Q{i}*R{i}
+        cur = dX;
     }
+    if (cur != dX) CAL_HIP(c, copy_cols(c, dX, cur, ld, n, m));  // no block to project against
     return 0;
 }
 
@@ -962,9 +971,8 @@ int project_and_normalize_blocks_dev(cal_ctx* c, int64_t n, int64_t ld, int nblo
         int ldx = 0;
         const size_t offx = kAsyncBase + (size_t)nblocks * kAsyncRegion;
         CAL_TRY(gram_async(c, n, Xp, Xp, c->d_red + offx, c->h_red + offx, &ldx));  // norms before (:17-22)
-        CAL_HIP(c, copy_cols(c, dY, dX, ld, n, m));
         std::vector<int> ldc;
-        CAL_TRY(project_blocks_async(c, n, ld, nblocks, dQ, widths, m, dY, 0, ldc));  // :25
+        CAL_TRY(project_blocks_async(c, n, ld, nblocks, dQ, widths, m, dY, 0, ldc, dX));  // :25 (Y from X)
         CAL_TRY(normalize_dev(c, n, Yp, Qout, R, 1.0e-8, &rk, &sh));                   // :26 (waits)
         for (int i = 0; i < m; ++i) before[i] = std::sqrt(c->h_red[offx + i + (size_t)i * ldx]);
         read_async_R(c, nblocks, widths, m, 0, ldc, RY);
