@@ -896,14 +896,18 @@ static bool async_ok(int nb, const int* widths, int m) {
 
 // Gram A'B (A <= 128 columns, B <= 16) reduced (and all-reduced) into d_dst
 // (ld *ldc) and copied to h_dst; nothing waits.
-int gram_async(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* d_dst, double* h_dst, int* ldc) {
+int gram_async(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* d_dst, double* h_dst, int* ldc,
+               double* part) {
     if (B.total > 16 || A.total > 128) return set_error(c, CAL_ERR_ARG, "gram_async: A <= 128, B <= 16 columns");
     const GramPlan pl = gram_plan(A.total, B.total, n);
-    CAL_TRY(ensure_partial(c, (size_t)pl.blocks * pl.entries));
+    if (!part) {
+        CAL_TRY(ensure_partial(c, (size_t)pl.blocks * pl.entries));
+        part = c->d_partial;
+    }
     const int t = timer_begin(c, 1);
-    CAL_HIP(c, launch_gram(A, B, n, pl, c->d_partial, c->stream));
+    CAL_HIP(c, launch_gram(A, B, n, pl, part, c->stream));
     timer_end(c, t);
-    CAL_HIP(c, launch_reduce(c->d_partial, pl.blocks, pl.entries, d_dst, c->stream));
+    CAL_HIP(c, launch_reduce(part, pl.blocks, pl.entries, d_dst, c->stream));
     CAL_TRY(allreduce_sum(c, d_dst, pl.entries));
     CAL_HIP(c, hipMemcpyAsync(h_dst, d_dst, pl.entries * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     *ldc = 16 * pl.nta;

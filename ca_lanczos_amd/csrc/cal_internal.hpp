@@ -237,7 +237,9 @@ hipError_t launch_gather(double* dst, const double* src, const int* idx, int64_t
 // fused SpMV + Ritz residual partials for one Ritz pair (diagnostics)
 // Gram A'B (A <= 128 columns, B <= 16) reduced, all-reduced and copied to
 // h_dst (ld *ldc) asynchronously: valid after the stream's next wait
-int gram_async(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* d_dst, double* h_dst, int* ldc);
+// (part: the block partials' scratch, gram_plan blocks x entries doubles; default c->d_partial)
+int gram_async(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* d_dst, double* h_dst, int* ldc,
+               double* part = nullptr);
 int spmv_pair_resid_blocks(const PatArgs& a);
 hipError_t launch_spmv_pair_resid(const PatArgs& a, double lr, double* partial, hipStream_t st);
 // the same for npr real Ritz pairs in one launch: x_i = X + col[i] * ldx,
@@ -304,6 +306,7 @@ struct CalTimerRec {
 struct cal_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t aux_stream = nullptr;  // second stream of the diagnostics (lanczos.cpp diag_launch), lazy
     std::string err;
     cal::DevMatrix A;
     bool has_A = false;

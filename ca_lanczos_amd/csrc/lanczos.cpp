@@ -52,7 +52,8 @@ struct DiagJob {
     std::vector<OeChunk> oe;
     int wa = 0;
     std::vector<int> sep;  // pairs reduced on their own (row kernel)
-    hipEvent_t ev = nullptr;
+    hipEvent_t ev = nullptr;           // the job's results are in pinned memory
+    std::vector<hipEvent_t> evc;       // diag_launch: chunk q of X written; [nch]: the job's start
 };
 
 struct LanczosState {
@@ -91,6 +92,8 @@ struct LanczosState {
     double* d_din = nullptr;   // inputs: Vp (sk x sk), Ritz values, pair columns / slots
     double* h_din = nullptr;   // pinned
     size_t din_cap = 0;
+    double* d_dpart = nullptr;  // block partials of the diagnostics' auxiliary-stream kernels
+    size_t dpart_cap = 0;
     int64_t lpad = 0;  // local origin inside each column (left halo space)
     double* col(int j) { return dQ + (size_t)j * ld + lpad; }
     double* vcolumn(int j, int par = 0) { return dV + ((size_t)par * (s + 1) + j) * ld + lpad; }
@@ -390,33 +393,75 @@ static int grow_pinned(cal_ctx* c, double** d, double** h, size_t* cap, size_t n
     return 0;
 }
 
+static int grow_pinned_dev(cal_ctx* c, double** d, size_t* cap, size_t need) {
+    if (need <= *cap) return 0;
+    if (*d) CAL_HIP(c, hipFree(*d));
+    *d = nullptr;
+    const size_t n = std::max(need, *cap + *cap / 2);
+    CAL_HIP(c, hipMalloc((void**)d, n * sizeof(double)));
+    *cap = n;
+    return 0;
+}
+
+// c->stream pointed at another stream for a scope (every launcher and helper
+// enqueues on c->stream)
+struct StreamScope {
+    cal_ctx* c;
+    hipStream_t saved;
+    StreamScope(cal_ctx* ctx, hipStream_t s) : c(ctx), saved(ctx->stream) { c->stream = s; }
+    ~StreamScope() { c->stream = saved; }
+};
+
+// The GPU work of one job: the orthogonality-error Grams, the Ritz-vector
+// apply (bound by the f64 matrix cores), the residual sums (bound by the
+// gather), one reduction and copy.  Optionally (A/B switches below) on two
+// streams: the apply on the context stream in column chunks, the Grams and
+// each chunk's residuals on an auxiliary stream behind that chunk's apply.
+// The context stream waits for the job's last event, so what follows it (the
+// next step, a reuse of the work columns) is ordered after it.
 static int diag_launch(cal_ctx* c, LanczosState& L, DiagJob& J) {
     const int s = L.s, sk = s * J.k;
     const int64_t n = c->A.n_local, ld = c->A.ld;
+    // CAL_DIAG_AUX=1 (second stream), CAL_DIAG_CHUNKS=2..4 (apply chunks): the
+    // overlap below, measured slower (lap3d_215, 15 iterations: one stream, one
+    // chunk 130.5 outer-it/s; two streams 125.3; two chunks 117-120: the
+    // residual blocks take LDS and CU slots from the 120-KB-LDS apply blocks),
+    // so both are off by default
+    static const int use_aux = [] {
+        const char* e = std::getenv("CAL_DIAG_AUX");
+        return e ? std::atoi(e) : 0;
+    }();
+    static const int chunks_env = [] {
+        const char* e = std::getenv("CAL_DIAG_CHUNKS");
+        return e ? std::atoi(e) : 1;
+    }();
+    if (use_aux && !c->aux_stream) CAL_HIP(c, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
+    const hipStream_t main = c->stream, aux = use_aux ? c->aux_stream : c->stream;
     // compute_orth_err(Q(:,1:sk+1), s): Q(:,1:j-s-1)'Q(:,j-s:j) for j > s+1,
     // else Q'Q - I; Grams in chunks of 128 x 16 columns (gram_async)
     const int jq = sk + 1;
     J.wa = jq > s + 1 ? jq - s - 1 : s + 1;
     const int bcol = jq > s + 1 ? J.wa : 0;
     J.oe.clear();
-    size_t off = (size_t)2 * sk;
+    size_t off = (size_t)2 * sk, oe_part = 0;
     for (int a0 = 0; a0 < J.wa; a0 += 128)
         for (int b0 = 0; b0 < s + 1; b0 += 16) {
             const int na = std::min(128, J.wa - a0), nb = std::min(16, s + 1 - b0);
             const GramPlan pl = gram_plan(na, nb, n);
             J.oe.push_back({a0, na, b0, nb, 16 * pl.nta, off});
             off += (size_t)pl.entries;
+            oe_part = std::max(oe_part, (size_t)pl.blocks * pl.entries);
         }
     CAL_TRY(grow_pinned(c, &L.d_dres, &L.h_dres, &L.dres_cap, off));
-    for (const auto& ch : J.oe) {
-        Panel OA = panel(), OB = panel();
-        panel_add(OA, L.col(ch.a0), ld, ch.na);
-        panel_add(OB, L.col(bcol + ch.b0), ld, ch.nb);
-        int ldc = 0;
-        CAL_TRY(gram_async(c, n, OA, OB, L.d_dres + ch.off, L.h_dres + ch.off, &ldc));
-    }
-    // X = Q(:,1:sk) * Vp (ca_lanczos.m:93) into work columns
-    const int npr = (int)std::count_if(J.pairs.begin(), J.pairs.end(), [](const RitzPair& p) { return p.ci < 0; });
+    // the Ritz vectors in column chunks (two from 48 columns: the second
+    // chunk's apply overlaps the first chunk's residuals)
+    const bool mt = apply_mt_ok(sk, sk);
+    const int nch = mt && sk >= 48 ? std::max(1, std::min(4, chunks_env)) : 1;
+    const int cw = nch == 1 ? sk : ((sk + nch * 16 - 1) / (nch * 16)) * 16;
+    auto chunk_of = [&](int col) { return std::min(nch - 1, col / cw); };
+    // inputs: Vp, then the batched pairs grouped by chunk (Ritz value, column,
+    // output slot), offsets per chunk
+    const int nbp = spmv_resid_pair_multi_blocks(c);  // 0: no pair path (row kernel for every pair)
     const size_t o_lam = (size_t)sk * sk, o_col = o_lam + sk, o_out = o_col + (sk + 1) / 2;
     CAL_TRY(grow_pinned(c, &L.d_din, &L.h_din, &L.din_cap, o_out + (sk + 1) / 2));
     std::copy(J.V.begin(), J.V.end(), L.h_din);
@@ -424,74 +469,111 @@ static int diag_launch(cal_ctx* c, LanczosState& L, DiagJob& J) {
     int* h_col = reinterpret_cast<int*>(L.h_din + o_col);
     int* h_out = reinterpret_cast<int*>(L.h_din + o_out);
     J.sep.clear();
-    const int nbp = spmv_resid_pair_multi_blocks(c);  // 0: no pair path (row kernel for every pair)
-    for (int i = 0, q = 0; i < sk; ++i) {
-        const RitzPair& p = J.pairs[i];
-        if (nbp > 0 && p.ci < 0) {
+    std::vector<int> cnt(nch + 1, 0);  // batched pairs per chunk, then prefix offsets
+    for (int i = 0; i < sk; ++i) {
+        if (nbp > 0 && J.pairs[i].ci < 0) cnt[chunk_of(J.pairs[i].cr) + 1]++;
+        else J.sep.push_back(i);
+    }
+    for (int q = 0; q < nch; ++q) cnt[q + 1] += cnt[q];
+    {
+        std::vector<int> pos(cnt.begin(), cnt.end() - 1);
+        for (int i = 0; i < sk; ++i) {
+            const RitzPair& p = J.pairs[i];
+            if (!(nbp > 0 && p.ci < 0)) continue;
+            const int q = pos[chunk_of(p.cr)]++;
             h_lam[q] = p.lr;
             h_col[q] = p.cr;
             h_out[q] = i;
-            ++q;
-        } else {
-            J.sep.push_back(i);
         }
     }
     CAL_HIP(c, hipMemcpyAsync(L.d_din, L.h_din, (o_out + (sk + 1) / 2) * sizeof(double), hipMemcpyHostToDevice,
-                              c->stream));
+                              main));
     // sized for the last iteration at once (each growth frees and zeroes)
     CAL_TRY(ensure_work(c, std::max(sk, s * L.max_outer), ld));
     double* X = work_col(c, 0) + c->A.lpad;
-    if (apply_mt_ok(sk, sk)) {
-        const int t = timer_begin(c, 2);
-        hipError_t e = launch_apply_mt(L.col(0), ld, L.d_din, sk, sk, X, ld, n, c->stream);
-        timer_end(c, t);
-        if (e != hipSuccess) return hip_fail(c, e, "launch_apply_mt (Ritz vectors)");
-    } else {  // sk > 1280: the generic apply in column chunks
-        Panel Qp = panel();
-        panel_add(Qp, L.col(0), ld, sk);
-        CAL_TRY(apply_dev(c, n, Qp, L.d_din, sk, panel_out(X, ld, sk)));
-    }
-    // ||A x - l x||^2, ||l x||^2 per pair (ca_lanczos.m:94): entry 2i + e
     const int nbr = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (n + 255) / 256));
     const bool batched = nbp > 0;
-    const size_t sep0 = batched ? (size_t)2 * sk * nbp : 0;  // row-kernel partials
-    CAL_TRY(ensure_partial(c, sep0 + (size_t)2 * sk * nbr));
-    if (batched && npr > 0) {
-        for (int i = 0; i < sk; ++i)
-            if (J.pairs[i].ci < 0) CAL_TRY(halo_exchange(c, X + (int64_t)J.pairs[i].cr * ld));
+    const size_t sep0 = batched ? (size_t)2 * sk * nbp : 0;           // row-kernel partials
+    const size_t oe0 = sep0 + (size_t)2 * std::max<size_t>(J.sep.size(), batched ? 0 : sk) * nbr;
+    CAL_TRY(grow_pinned_dev(c, &L.d_dpart, &L.dpart_cap, oe0 + oe_part));
+    if (J.evc.size() < (size_t)nch + 1) {
+        const size_t old = J.evc.size();
+        J.evc.resize(nch + 1, nullptr);
+        for (size_t q = old; q < J.evc.size(); ++q) CAL_HIP(c, hipEventCreateWithFlags(&J.evc[q], hipEventDisableTiming));
+    }
+    // the aux stream starts behind everything on the context stream so far
+    CAL_HIP(c, hipEventRecord(J.evc[nch], main));
+    CAL_HIP(c, hipStreamWaitEvent(aux, J.evc[nch], 0));
+    {
+        StreamScope on_aux(c, aux);
+        for (const auto& ch : J.oe) {
+            Panel OA = panel(), OB = panel();
+            panel_add(OA, L.col(ch.a0), ld, ch.na);
+            panel_add(OB, L.col(bcol + ch.b0), ld, ch.nb);
+            int ldc = 0;
+            CAL_TRY(gram_async(c, n, OA, OB, L.d_dres + ch.off, L.h_dres + ch.off, &ldc, L.d_dpart + oe0));
+        }
+    }
+    for (int q = 0; q < nch; ++q) {
+        const int c0 = q * cw, c1 = q + 1 == nch ? sk : std::min(sk, c0 + cw);
+        // X(:, c0:c1) = Q(:,1:sk) * Vp(:, c0:c1) (ca_lanczos.m:93)
+        if (mt) {
+            const int t = timer_begin(c, 2);
+            hipError_t e = launch_apply_mt(L.col(0), ld, L.d_din + (size_t)c0 * sk, sk, c1 - c0, X + (int64_t)c0 * ld,
+                                           ld, n, main);
+            timer_end(c, t);
+            if (e != hipSuccess) return hip_fail(c, e, "launch_apply_mt (Ritz vectors)");
+        } else {  // sk > 1280: the generic apply in column chunks
+            Panel Qp = panel();
+            panel_add(Qp, L.col(0), ld, sk);
+            CAL_TRY(apply_dev(c, n, Qp, L.d_din, sk, panel_out(X, ld, sk)));
+        }
+        CAL_HIP(c, hipEventRecord(J.evc[q], main));
+        const int npq = cnt[q + 1] - cnt[q];
+        if (npq == 0) continue;
+        CAL_HIP(c, hipStreamWaitEvent(aux, J.evc[q], 0));
+        StreamScope on_aux(c, aux);
+        for (int i = cnt[q]; i < cnt[q + 1]; ++i) CAL_TRY(halo_exchange(c, X + (int64_t)h_col[i] * ld));
+        // ||A x - l x||^2, ||l x||^2 per pair (ca_lanczos.m:94): entry 2i + e
         const int t = timer_begin(c, 3);
-        CAL_TRY(spmv_resid_pair_multi_dev(c, X, ld, reinterpret_cast<const int*>(L.d_din + o_col), L.d_din + o_lam,
-                                          reinterpret_cast<const int*>(L.d_din + o_out), npr, c->d_partial, nbp));
+        CAL_TRY(spmv_resid_pair_multi_dev(c, X, ld, reinterpret_cast<const int*>(L.d_din + o_col) + cnt[q],
+                                          L.d_din + o_lam + cnt[q], reinterpret_cast<const int*>(L.d_din + o_out) + cnt[q],
+                                          npq, L.d_dpart, nbp));
         timer_end(c, t);
     }
-    for (size_t q = 0; q < J.sep.size(); ++q) {
-        const RitzPair& p = J.pairs[J.sep[q]];
-        double* xr = X + (int64_t)p.cr * ld;
-        double* xi = p.ci >= 0 ? X + (int64_t)p.ci * ld : nullptr;
-        CAL_TRY(halo_exchange(c, xr));
-        if (xi) CAL_TRY(halo_exchange(c, xi));
-        SpmvArgs a{};
-        a.rowptr = c->A.rowptr + c->A.ext_off;  // local rows of a stored slab
-        a.col = c->A.col;
-        a.val = c->A.val;
-        a.x = xr;
-        // no pair path: every pair entry-major at stride nbr (one reduction)
-        double* part = c->d_partial + sep0 + (batched ? q : (size_t)J.sep[q]) * 2 * nbr;
-        const int t = timer_begin(c, 3);
-        CAL_HIP(c, launch_spmv_resid(a, xi, p.lr, p.li, n, part, nbr, c->stream));
-        timer_end(c, t);
+    CAL_HIP(c, hipStreamWaitEvent(aux, J.evc[nch - 1], 0));  // every chunk of X written
+    {
+        StreamScope on_aux(c, aux);
+        for (size_t q = 0; q < J.sep.size(); ++q) {
+            const RitzPair& p = J.pairs[J.sep[q]];
+            double* xr = X + (int64_t)p.cr * ld;
+            double* xi = p.ci >= 0 ? X + (int64_t)p.ci * ld : nullptr;
+            CAL_TRY(halo_exchange(c, xr));
+            if (xi) CAL_TRY(halo_exchange(c, xi));
+            SpmvArgs a{};
+            a.rowptr = c->A.rowptr + c->A.ext_off;  // local rows of a stored slab
+            a.col = c->A.col;
+            a.val = c->A.val;
+            a.x = xr;
+            // no pair path: every pair entry-major at stride nbr (one reduction)
+            double* part = L.d_dpart + sep0 + (batched ? q : (size_t)J.sep[q]) * 2 * nbr;
+            const int t = timer_begin(c, 3);
+            CAL_HIP(c, launch_spmv_resid(a, xi, p.lr, p.li, n, part, nbr, c->stream));
+            timer_end(c, t);
+        }
+        if (batched) {
+            if (cnt[nch] > 0) CAL_HIP(c, launch_reduce(L.d_dpart, nbp, 2 * sk, L.d_dres, c->stream));
+            for (size_t q = 0; q < J.sep.size(); ++q)
+                CAL_HIP(c, launch_reduce(L.d_dpart + sep0 + q * 2 * nbr, nbr, 2, L.d_dres + 2 * J.sep[q], c->stream));
+        } else {
+            CAL_HIP(c, launch_reduce(L.d_dpart, nbr, 2 * sk, L.d_dres, c->stream));
+        }
+        CAL_TRY(allreduce_sum(c, L.d_dres, 2 * sk));
+        CAL_HIP(c, hipMemcpyAsync(L.h_dres, L.d_dres, 2 * sk * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        if (!J.ev) CAL_HIP(c, hipEventCreateWithFlags(&J.ev, hipEventDisableTiming));
+        CAL_HIP(c, hipEventRecord(J.ev, c->stream));
     }
-    if (batched) {
-        if (npr > 0) CAL_HIP(c, launch_reduce(c->d_partial, nbp, 2 * sk, L.d_dres, c->stream));
-        for (size_t q = 0; q < J.sep.size(); ++q)
-            CAL_HIP(c, launch_reduce(c->d_partial + sep0 + q * 2 * nbr, nbr, 2, L.d_dres + 2 * J.sep[q], c->stream));
-    } else {
-        CAL_HIP(c, launch_reduce(c->d_partial, nbr, 2 * sk, L.d_dres, c->stream));
-    }
-    CAL_TRY(allreduce_sum(c, L.d_dres, 2 * sk));
-    CAL_HIP(c, hipMemcpyAsync(L.h_dres, L.d_dres, 2 * sk * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    if (!J.ev) CAL_HIP(c, hipEventCreateWithFlags(&J.ev, hipEventDisableTiming));
-    CAL_HIP(c, hipEventRecord(J.ev, c->stream));
+    CAL_HIP(c, hipStreamWaitEvent(main, J.ev, 0));
     return 0;
 }
 
@@ -529,8 +611,11 @@ static int diag_flush(cal_ctx* c, LanczosState& L) {
 }
 
 static void diag_free(LanczosState& L) {
-    if (L.ready.ev) hipEventDestroy(L.ready.ev);
-    if (L.pending.ev) hipEventDestroy(L.pending.ev);
+    for (DiagJob* J : {&L.ready, &L.pending}) {
+        if (J->ev) hipEventDestroy(J->ev);
+        for (hipEvent_t e : J->evc) hipEventDestroy(e);
+    }
+    if (L.d_dpart) hipFree(L.d_dpart);
     if (L.d_dres) hipFree(L.d_dres);
     if (L.h_dres) hipHostFree(L.h_dres);
     if (L.d_din) hipFree(L.d_din);

@@ -704,6 +704,7 @@ void cal_destroy(cal_ctx* c) {
     if (c->d_tsqr) hipFree(c->d_tsqr);
     if (c->d_zbuf) hipFree(c->d_zbuf);
     if (c->h_pub) hipHostFree(c->h_pub);
+    if (c->aux_stream) hipStreamDestroy(c->aux_stream);
     hipStreamDestroy(c->stream);
     delete c;
 }
