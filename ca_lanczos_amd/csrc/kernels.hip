@@ -310,8 +310,8 @@ __device__ __forceinline__ double2 ld16(const double* p) {
 // load is issued before the staging loads so both share one memory round
 // trip.  Split pairs (and the lone last row of an odd n) read the row
 // tables from global memory (rare).
-template <int MODE, int MAXLEN, bool CANON>
-__global__ __launch_bounds__(256) void k_spmv_pair(PatArgs a, const uint16_t* __restrict__ ppat,
+template <int MODE, int MAXLEN, bool CANON, int TB = 256>
+__global__ __launch_bounds__(TB) void k_spmv_pair(PatArgs a, const uint16_t* __restrict__ ppat,
                                                   const int2* __restrict__ ppinfo, const int* __restrict__ ppoff,
                                                   const double2* __restrict__ ppval) {
     extern __shared__ __attribute__((aligned(16))) double lds_pair[];
@@ -320,7 +320,7 @@ __global__ __launch_bounds__(256) void k_spmv_pair(PatArgs a, const uint16_t* __
     int* s_poff = reinterpret_cast<int*>(s_pinfo + (CANON ? 0 : a.nppat));
     const int tid = threadIdx.x;
     const int64_t npairs = (a.n + 1) >> 1;  // compact pairs (both ranges)
-    const int64_t tc = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 256 + tid;
+    const int64_t tc = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * TB + tid;
     const int64_t tcl = tc < npairs ? tc : npairs - 1;
     const int64_t t = tcl + (tcl >= a.gap_at ? a.gap : 0);  // stored pair (skips the gap)
     const int id = ppat[t];
@@ -343,12 +343,12 @@ __global__ __launch_bounds__(256) void k_spmv_pair(PatArgs a, const uint16_t* __
         if (MODE != 0) xs = ld16(a.x + rc);
         if (MODE == 2) xp = ld16(a.xprev + rc);
     }
-    for (int i = tid; i < a.npent; i += 256) {
+    for (int i = tid; i < a.npent; i += TB) {
         s_pv[i] = ppval[i];
         s_poff[i] = ppoff[i];
     }
     if (!CANON)
-        for (int i = tid; i < a.nppat; i += 256) s_pinfo[i] = ppinfo[i];
+        for (int i = tid; i < a.nppat; i += TB) s_pinfo[i] = ppinfo[i];
     __syncthreads();
     if (tc >= npairs) return;
     const int64_t r = 2 * t;
@@ -649,10 +649,28 @@ static hipError_t launch_pat_mode(const PatArgs& a, hipStream_t st) {
     const size_t lds2 = (size_t)a.npent * 20 + (size_t)a.nppat * 8 + 16;
     if (spmv_pat_pair_path(a)) {
         const int64_t npairs = (a.n + 1) / 2;
-        dim3 g((unsigned)((npairs + 255) / 256)), b(256);
-#define CAL_PR(ML)                                                                                           \
-    if (a.pcanon) hipLaunchKernelGGL((k_spmv_pair<MODE, ML, true>), g, b, lds2, st, a, a.ppat, a.ppinfo, a.ppoff, \
-                                     a.ppval);                                                                  \
+        // threads per block: 512 (1024 rows; half the table stagings of 256 threads:
+        // lap3d_215 in the loop 45.2 -> 42.7 us per SpMV, 809 -> 825 outer-it/s);
+        // CAL_PAIR_TB = 256 / 1024 for A/B
+        static const int tb = [] {
+            const char* e = std::getenv("CAL_PAIR_TB");
+            const int v = e ? std::atoi(e) : 512;
+            return v == 256 || v == 1024 ? v : 512;
+        }();
+        dim3 g((unsigned)((npairs + tb - 1) / tb)), b(tb);
+#define CAL_PR(ML)                                                                                                    \
+    if (tb == 512) {                                                                                                   \
+        if (a.pcanon) hipLaunchKernelGGL((k_spmv_pair<MODE, ML, true, 512>), g, b, lds2, st, a, a.ppat, a.ppinfo,     \
+                                         a.ppoff, a.ppval);                                                            \
+        else hipLaunchKernelGGL((k_spmv_pair<MODE, ML, false, 512>), g, b, lds2, st, a, a.ppat, a.ppinfo, a.ppoff,    \
+                                a.ppval);                                                                              \
+    } else if (tb == 1024) {                                                                                           \
+        if (a.pcanon) hipLaunchKernelGGL((k_spmv_pair<MODE, ML, true, 1024>), g, b, lds2, st, a, a.ppat, a.ppinfo,    \
+                                         a.ppoff, a.ppval);                                                            \
+        else hipLaunchKernelGGL((k_spmv_pair<MODE, ML, false, 1024>), g, b, lds2, st, a, a.ppat, a.ppinfo, a.ppoff,   \
+                                a.ppval);                                                                              \
+    } else if (a.pcanon) hipLaunchKernelGGL((k_spmv_pair<MODE, ML, true>), g, b, lds2, st, a, a.ppat, a.ppinfo,       \
+                                            a.ppoff, a.ppval);                                                        \
     else hipLaunchKernelGGL((k_spmv_pair<MODE, ML, false>), g, b, lds2, st, a, a.ppat, a.ppinfo, a.ppoff, a.ppval);
         switch (a.pmaxlen) {
             case 1: CAL_PR(1); break;
