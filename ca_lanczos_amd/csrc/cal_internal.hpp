@@ -287,11 +287,16 @@ struct TsqrLevelArgs {
     const double* S = nullptr;
     const double* M2 = nullptr;  // formed mode: Z = (P M) + P(:, 0:w2) M2 (w2 x m)
     int w2 = 0;
+    // level 0: UP stores each tile's factored registers (reflectors and R,
+    // 64 * RPL * MM doubles per tile, lane-contiguous) and tau / beta (MM
+    // each); DOWN (src 3) reloads them instead of re-forming and re-factoring
+    double* V = nullptr;
+    double* tb = nullptr;
 };
 int tsqr_mm(int m);          // register tile width (8, 16, 32; 0: m > 32)
 int tsqr_tile_rows(int m);   // rows per tile (4096 / tsqr_mm)
 bool tsqr_form_ok(int wp, int m);
-// src: 0 stack, 1 direct columns, 2 formed
+// src: 0 stack, 1 direct columns, 2 formed, 3 (DOWN at level 0) the reflectors UP stored
 hipError_t launch_tsqr(bool down, int src, const TsqrLevelArgs& a, const TsqrCols& P, const TsqrQ& Q,
                        hipStream_t st);
 
@@ -363,6 +368,8 @@ struct cal_ctx {
     bool tier1 = false;  // inside a host-pointer (tier-1) entry point (api.cpp)
     double* d_tsqr = nullptr;  // TSQR tree workspace
     size_t tsqr_cap = 0;
+    double* d_tsqrv = nullptr;  // level-0 reflectors of the TSQR (tsqr_tree.cpp)
+    size_t tsqrv_cap = 0;
     double* d_zbuf = nullptr;  // n x m block of the TSQR paths (blockorth.cpp)
     size_t zbuf_cap = 0;
 };

@@ -703,6 +703,7 @@ void cal_destroy(cal_ctx* c) {
     if (c->orth_event) hipEventDestroy(c->orth_event);
     if (c->d_tsqr) hipFree(c->d_tsqr);
     if (c->d_zbuf) hipFree(c->d_zbuf);
+    if (c->d_tsqrv) hipFree(c->d_tsqrv);
     if (c->h_pub) hipHostFree(c->h_pub);
     if (c->aux_stream) hipStreamDestroy(c->aux_stream);
     hipStreamDestroy(c->stream);

@@ -175,7 +175,8 @@ __device__ __forceinline__ void tile_org2r(double (&a)[RPL][MM], const double (&
     }
 }
 
-// SRC: 0 stack (block layout), 1 direct columns, 2 formed Z = P M (WP columns)
+// SRC: 0 stack (block layout), 1 direct columns, 2 formed Z = P M (WP columns),
+// 3 (DOWN, level 0) the factored tile UP stored in a.V / a.tb
 template <int MM, int SRC, int WP, bool DOWN>
 __global__ __launch_bounds__(256) void k_tsqr(TsqrLevelArgs a, TsqrCols P, TsqrQ Q, int64_t ntiles) {
     constexpr int RPL = 64 / MM, TR = 64 * RPL;
@@ -197,6 +198,19 @@ __global__ __launch_bounds__(256) void k_tsqr(TsqrLevelArgs a, TsqrCols P, TsqrQ
     const int64_t base = tile * TR;
     const int64_t mm = (int64_t)m * m;
     double x[RPL][MM];
+    double tau[MM], beta[MM];
+    double* const vt = a.V ? a.V + tile * (int64_t)(64 * RPL * MM) + lane : nullptr;  // lane-contiguous tile store
+    if (SRC == 3) {
+#pragma unroll
+        for (int i = 0; i < RPL; ++i)
+#pragma unroll
+            for (int c = 0; c < MM; ++c) x[i][c] = vt[(i * MM + c) * 64];
+#pragma unroll
+        for (int c = 0; c < MM; ++c) {
+            tau[c] = a.tb[tile * (2 * MM) + c];
+            beta[c] = a.tb[tile * (2 * MM) + MM + c];
+        }
+    }
     if (SRC == 2) {
         // formed: Z = P M (+ P(:,0:w2) M2), column k outermost so each M entry
         // is read from LDS once per tile, not once per row (the row-inner
@@ -249,7 +263,7 @@ __global__ __launch_bounds__(256) void k_tsqr(TsqrLevelArgs a, TsqrCols P, TsqrQ
             for (int c = 0; c < MM; ++c) x[i][c] = in[i] ? x[i][c] : 0.0;
     }
 #pragma unroll
-    for (int i = 0; i < (SRC == 2 ? 0 : RPL); ++i) {
+    for (int i = 0; i < (SRC >= 2 ? 0 : RPL); ++i) {
         const int64_t r = base + lane + 64 * i;
         const bool in = r < a.rows;
         const int64_t rc = in ? r : 0;
@@ -269,8 +283,22 @@ __global__ __launch_bounds__(256) void k_tsqr(TsqrLevelArgs a, TsqrCols P, TsqrQ
             }
         }
     }
-    double tau[MM], beta[MM];
-    tile_geqr2<MM, RPL>(x, tau, beta, m, lane);
+    if (SRC != 3) tile_geqr2<MM, RPL>(x, tau, beta, m, lane);
+    if (!DOWN && vt) {  // level 0: keep the factored tile for the down pass
+#pragma unroll
+        for (int i = 0; i < RPL; ++i)
+#pragma unroll
+            for (int c = 0; c < MM; ++c) vt[(i * MM + c) * 64] = x[i][c];
+        if (lane < MM) {
+            // lane c writes tau[c], beta[c] (the arrays are wave-uniform)
+#pragma unroll
+            for (int c = 0; c < MM; ++c)
+                if (lane == c) {
+                    a.tb[tile * (2 * MM) + c] = tau[c];
+                    a.tb[tile * (2 * MM) + MM + c] = beta[c];
+                }
+        }
+    }
     if (!DOWN) {
         // R of this tile -> block `tile` of the next level's stack
         if (lane < m) {
@@ -365,7 +393,12 @@ hipError_t launch_tsqr(bool down, int src, const TsqrLevelArgs& a, const TsqrCol
         if (down) hipLaunchKernelGGL((k_tsqr<MMV, SRCV, WPV, true>), g, b, 0, st, a, P, Q, tiles);          \
         else hipLaunchKernelGGL((k_tsqr<MMV, SRCV, WPV, false>), g, b, 0, st, a, P, Q, tiles);              \
     } while (0)
-    if (src == 2) {
+    if (src == 3) {
+        if (!down || !a.V || !a.tb) return hipErrorInvalidValue;
+        if (MM == 8) hipLaunchKernelGGL((k_tsqr<8, 3, 0, true>), g, b, 0, st, a, P, Q, tiles);
+        else if (MM == 16) hipLaunchKernelGGL((k_tsqr<16, 3, 0, true>), g, b, 0, st, a, P, Q, tiles);
+        else hipLaunchKernelGGL((k_tsqr<32, 3, 0, true>), g, b, 0, st, a, P, Q, tiles);
+    } else if (src == 2) {
         if (MM == 8 && a.wp <= 17) CAL_TQ(8, 2, 17);
         else if (MM == 16 && a.wp <= 33) CAL_TQ(16, 2, 33);
         else return hipErrorInvalidValue;

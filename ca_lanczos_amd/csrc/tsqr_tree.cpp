@@ -80,6 +80,18 @@ int tsqr_dev(cal_ctx* c, int64_t n, const Panel& W, const double* dM, int m, con
         while (lv.back().tiles > 1) push(0, lv.back().tiles * m);
     }
     CAL_TRY(ensure_tsqr(c, need));
+    // level 0's factored tiles (4096 doubles each) and tau / beta, kept by the
+    // up pass for the down pass (which then neither re-forms nor re-factors)
+    const int MM = tsqr_mm(m);
+    const size_t vneed = (size_t)lv[0].tiles * (4096 + 2 * (size_t)MM);
+    if (vneed > c->tsqrv_cap) {
+        if (c->d_tsqrv) CAL_HIP(c, hipFree(c->d_tsqrv));
+        c->d_tsqrv = nullptr;
+        CAL_HIP(c, hipMalloc((void**)&c->d_tsqrv, vneed * sizeof(double)));
+        c->tsqrv_cap = vneed;
+    }
+    double* const dV = c->d_tsqrv;
+    double* const dTB = c->d_tsqrv + (size_t)lv[0].tiles * 4096;
     double* p = c->d_tsqr;
     for (size_t l = 0; l < lv.size(); ++l) {
         Level& L = lv[l];
@@ -121,6 +133,10 @@ int tsqr_dev(cal_ctx* c, int64_t n, const Panel& W, const double* dM, int m, con
     }
     auto args = [&](const Level& L, bool down) {
         TsqrLevelArgs a;
+        if (&L == &lv[0]) {
+            a.V = dV;
+            a.tb = dTB;
+        }
         a.rows = L.rows;
         a.m = m;
         a.wp = wp;
@@ -146,7 +162,7 @@ int tsqr_dev(cal_ctx* c, int64_t n, const Panel& W, const double* dM, int m, con
     // down the tree (queued before the host waits for R)
     for (size_t l = lv.size(); l-- > 0;) {
         const int t = timer_begin(c, l == 0 ? 2 : 3);
-        CAL_HIP(c, launch_tsqr(true, lv[l].src, args(lv[l], true), cols, qo, c->stream));
+        CAL_HIP(c, launch_tsqr(true, l == 0 ? 3 : lv[l].src, args(lv[l], true), cols, qo, c->stream));
         timer_end(c, t);
     }
     if (c->pre_wait) {  // e.g. the next step's matrix powers (lanczos_step)
