@@ -449,7 +449,14 @@ def main():
     tsqr_leg = None
     if args.normalize != "tsqr" and not args.no_legs:
         ctx.set_normalize("tsqr")
-        tsqr_leg = timed_leg(ctx, r_full[r0:r1], s, min(K, 10), min(W, 2), args.basis, args.orth, dist)
+        try:  # a secondary leg: a failure is reported in the line, the headline stands
+            tsqr_leg = timed_leg(ctx, r_full[r0:r1], s, min(K, 10), min(W, 2), args.basis, args.orth, dist)
+        except cal.CalError as e:
+            tsqr_leg = {"error": str(e)}
+            try:
+                ctx.lanczos_end()
+            except cal.CalError:
+                pass
         ctx.set_normalize(args.normalize)
     if world == 1 and rank == 0 and ctx.spmv_format()[0] == "pattern":
         # the bench's own SpMV kernel back to back on one x / y pair (the
@@ -551,11 +558,13 @@ def main():
         line["spmv_kernel_back_to_back"] = {"avg_us": pat_spmv[0] * 1e3, "min_us": pat_spmv[1] * 1e3,
                                             "gbps": b_spmv_launch / (pat_spmv[0] * 1e-3) / 1e9,
                                             "bytes_per_launch": b_spmv_launch}
-    if tsqr_leg is not None:
+    if tsqr_leg is not None and "error" not in tsqr_leg:
         # per step: P1 Gram + pass-A projection Gram + TSQR up (leaf sweep
         # "gram") + TSQR down (leaf sweep "apply") + tree levels ("other")
         tsqr_leg["normalize"] = "Householder TSQR (tile QR per wave, stacked-R tree%s)" % (
             ", RCCL allgather of the rank roots" if world > 1 else "")
+        line["tsqr_step"] = tsqr_leg
+    elif tsqr_leg is not None:
         line["tsqr_step"] = tsqr_leg
     if csr_leg is not None:
         csr_leg["spmv_format"] = "csr"
