@@ -703,3 +703,38 @@ def test_normalize_randomize_null_space(cal, ref):
     assert np.max(np.abs(Q[:, :rk] * sg - Qr[:, :rk])) <= 1e-10
     assert np.max(np.abs(R[:rk] * sg[:, None] - Rr[:rk])) <= 1e-10 * nx
     assert np.max(np.abs(Q[:, rk:] - Qr[:, rk:])) <= 1e-10
+
+
+@pytest.mark.parametrize("case", ["spread", "reorth", "ill"])
+def test_project_and_normalize_wide_block_cholqr(cal, ref, case):
+    """One wide block (w = 40 > 9: the generic sweeps) on the CholQR path.
+    'spread': the reorth test does not fire and Y is well conditioned, so the
+    single projection + normalize of projectAndNormalize.m:25-26,52-58 runs as
+    one Gram and one apply sweep; 'reorth': 90 % of X inside span(Qp), the
+    second pass (:63-73); 'ill': X's columns nearly parallel (kappa(Y) ~ 1e6,
+    not diagonally dominant): the two-pass CholQR2.  All three against the
+    oracle (LAPACK QR + the sign fix)."""
+    rng = np.random.RandomState(21)
+    n, w, m = 20000, 40, 8
+    Qp, _ = np.linalg.qr(rng.randn(n, w))
+    if case == "spread":
+        X = 0.1 * Qp @ rng.randn(w, m) + rng.randn(n, m) / np.sqrt(n)
+    elif case == "reorth":
+        X = 0.9 * Qp @ rng.randn(w, m) + 0.1 * rng.randn(n, m) / np.sqrt(n)
+    else:
+        base = rng.randn(n, 1)
+        X = base + 1e-6 * rng.randn(n, m)
+    ctx = cal.default_context()
+    ctx.set_normalize("cholqr2")
+    try:
+        QZ, RZ, re, rank = cal.projectAndNormalize_ex([Qp], X)
+    finally:
+        ctx.set_normalize("auto")
+    QZr, RZr, info = ref.projectAndNormalize_ex([Qp], X)
+    assert re == info.reorth == (case == "reorth")
+    scale = np.max(np.abs(RZr[1]))
+    tol_r = 1e-11 if case != "ill" else 1e-6
+    assert np.max(np.abs(RZ[0] - RZr[0])) <= 1e-12 * max(1.0, np.max(np.abs(RZr[0])))
+    assert np.max(np.abs(RZ[1] - RZr[1])) <= tol_r * scale
+    assert np.max(np.abs(QZ.T @ QZ - np.eye(m))) < 1e-13
+    assert np.max(np.abs(QZ.T @ Qp)) < 1e-13
