@@ -23,6 +23,7 @@
  * NumPy oracle's prologue, ca_lanczos.m:66-72).
  */
 #include <math.h>
+#include <stdio.h>
 #include <omp.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -36,6 +37,7 @@
  * x[1..] = v(2:end) */
 static double house(double* x, size_t len, size_t inc) {
     double xn = 0.0;
+#pragma omp simd reduction(+ : xn)
     for (size_t i = 1; i < len; ++i) xn += x[i * inc] * x[i * inc];
     xn = sqrt(xn);
     if (xn == 0.0) return 0.0;
@@ -60,6 +62,7 @@ static void geqr2(size_t rows, int m, double* A, size_t ld, double* tau) {
         for (int c = j + 1; c < m; ++c) {
             double* cc = A + IDX(j, c, ld);
             double d = cc[0];
+#pragma omp simd reduction(+ : d)
             for (size_t i = 1; i < rows - j; ++i) d += col[i] * cc[i];
             d *= tau[j];
             cc[0] -= d;
@@ -77,6 +80,7 @@ static void apply_q(size_t rows, int m, const double* A, size_t ld, const double
         for (int c = 0; c < ncol; ++c) {
             double* cc = C + IDX(j, c, ldc);
             double d = cc[0];
+#pragma omp simd reduction(+ : d)
             for (size_t i = 1; i < rows - j; ++i) d += v[i] * cc[i];
             d *= tau[j];
             cc[0] -= d;
@@ -86,12 +90,14 @@ static void apply_q(size_t rows, int m, const double* A, size_t ld, const double
 }
 
 /* tsqr.m:7-12: [Q,R] = qr(X,0), d = sign(diag(R)), R = diag(d) R, Q = Q diag(d).
- * X (n x m, ld n) is overwritten by Q; R is m x m (ld m).  Two-level TSQR:
+ * S (n x m, ld n) is the input, X (ld n) receives Q (S == X: in place; else
+ * each tile is copied into X inside the parallel tile loop and S is left
+ * untouched); R is m x m (ld m).  Two-level TSQR:
  * Householder QR of cache-sized row tiles (in parallel), Householder QR of
  * the stacked tile R factors, then each tile's Q applied to its block of the
  * stack's Q. */
 #define TSQR_TILE 2048
-static void tsqr(size_t n, int m, double* X, double* R) {
+static void tsqr(size_t n, int m, const double* S, double* X, double* R) {
     const size_t nt = (n + TSQR_TILE - 1) / TSQR_TILE, PR = nt * (size_t)m;
     double* Rs = calloc(PR * m, sizeof(double));
     double* taus = calloc(nt * m, sizeof(double));
@@ -99,6 +105,8 @@ static void tsqr(size_t n, int m, double* X, double* R) {
     for (size_t t = 0; t < nt; ++t) {
         const size_t r0 = t * TSQR_TILE, rows = (r0 + TSQR_TILE <= n ? TSQR_TILE : n - r0);
         double* Xb = X + r0;
+        if (S != X)
+            for (int j = 0; j < m; ++j) memcpy(Xb + (size_t)j * n, S + r0 + (size_t)j * n, rows * sizeof(double));
         geqr2(rows, m, Xb, n, taus + t * m);
         for (int j = 0; j < m; ++j)
             for (int i = 0; i <= j && (size_t)i < rows; ++i) Rs[IDX(t * m + i, j, PR)] = Xb[IDX(i, j, n)];
@@ -111,6 +119,14 @@ static void tsqr(size_t n, int m, double* X, double* R) {
     double* Qtop = calloc(PR * m, sizeof(double));
     for (int j = 0; j < m; ++j) Qtop[IDX(j, j, PR)] = 1.0;
     apply_q(PR, m, Rs, PR, ttop, Qtop, PR, m);
+    /* sign fix (sign(0) = 0, as MATLAB); Q's columns are scaled by d as the
+     * tiles are written back below */
+    double d[64];
+    for (int j = 0; j < m; ++j) {
+        const double rj = R[IDX(j, j, m)];
+        d[j] = rj > 0.0 ? 1.0 : (rj < 0.0 ? -1.0 : 0.0);
+        for (int c = 0; c < m; ++c) R[IDX(j, c, m)] *= d[j];
+    }
     /* Q tile t = H_t [Qtop block t; 0] */
 #pragma omp parallel
     {
@@ -123,20 +139,14 @@ static void tsqr(size_t n, int m, double* X, double* R) {
             for (int j = 0; j < m; ++j)
                 for (int i = 0; i < m && (size_t)i < rows; ++i) C[IDX(i, j, rows)] = Qtop[IDX(t * m + i, j, PR)];
             apply_q(rows, m, Xb, n, taus + t * m, C, rows, m);
-            for (int j = 0; j < m; ++j) memcpy(Xb + (size_t)j * n, C + (size_t)j * rows, rows * sizeof(double));
+            for (int j = 0; j < m; ++j) {
+                double* xc = Xb + (size_t)j * n;
+                const double* cc = C + (size_t)j * rows;
+                for (size_t i = 0; i < rows; ++i) xc[i] = cc[i] * d[j];
+            }
         }
         free(C);
     }
-    /* sign fix (sign(0) = 0, as MATLAB) */
-    double d[64];
-    for (int j = 0; j < m; ++j) {
-        const double rj = R[IDX(j, j, m)];
-        d[j] = rj > 0.0 ? 1.0 : (rj < 0.0 ? -1.0 : 0.0);
-        for (int c = 0; c < m; ++c) R[IDX(j, c, m)] *= d[j];
-    }
-#pragma omp parallel for schedule(static)
-    for (size_t i = 0; i < n; ++i)
-        for (int j = 0; j < m; ++j) X[IDX(i, j, n)] *= d[j];
     free(Rs);
     free(taus);
     free(ttop);
@@ -160,6 +170,7 @@ static void gemm_tn(size_t n, int w, int m, const double* Qp, const double* X, d
                 for (int a = 0; a < w; ++a) {
                     const double* q = Qp + (size_t)a * n;
                     double sum = 0.0;
+#pragma omp simd reduction(+ : sum)
                     for (size_t i = i0; i < i1; ++i) sum += q[i] * x[i];
                     acc[IDX(a, j, w)] += sum;
                 }
@@ -171,8 +182,8 @@ static void gemm_tn(size_t n, int w, int m, const double* Qp, const double* X, d
     }
 }
 
-/* X -= Qp G, by row blocks and columns */
-static void gemm_sub(size_t n, int w, int m, const double* Qp, const double* G, double* X) {
+/* Y = X - Qp G, by row blocks and columns (Y may be X) */
+static void gemm_sub(size_t n, int w, int m, const double* Qp, const double* G, const double* X, double* Y) {
     const size_t nb = (n + GEMM_BLK - 1) / GEMM_BLK;
 #pragma omp parallel for schedule(static)
     for (size_t b = 0; b < nb; ++b) {
@@ -185,15 +196,16 @@ static void gemm_sub(size_t n, int w, int m, const double* Qp, const double* G, 
                 const double g = G[IDX(a, j, w)];
                 for (size_t i = i0; i < i1; ++i) s[i - i0] += q[i] * g;
             }
-            double* x = X + (size_t)j * n;
-            for (size_t i = i0; i < i1; ++i) x[i] -= s[i - i0];
+            const double* x = X + (size_t)j * n;
+            double* y = Y + (size_t)j * n;
+            for (size_t i = i0; i < i1; ++i) y[i] = x[i] - s[i - i0];
         }
     }
 }
 
 static double col_norm(size_t n, const double* x) {
     double s = 0.0;
-#pragma omp parallel for reduction(+ : s) schedule(static)
+#pragma omp parallel for simd reduction(+ : s) schedule(static)
     for (size_t i = 0; i < n; ++i) s += x[i] * x[i];
     return sqrt(s);
 }
@@ -224,6 +236,10 @@ static void spmv(size_t n, const int64_t* rp, const int32_t* col, const double* 
 /* ca_lanczos_basic, orth 'local', diagnostics off (ca_lanczos.m:150-245).
  * q: normalised start vector; Bk (s+1) x s; T_out (st x st, ld st);
  * reorth_out[t]: 1 where projectAndNormalize took its second pass. */
+/* per-phase wall time, printed to stderr when CAL_OMP_PROFILE is set */
+static double g_ph[8], g_loop;
+#define PH(i, stmt) do { double t0_ = omp_get_wtime(); stmt; g_ph[i] += omp_get_wtime() - t0_; } while (0)
+
 int cal_omp_ca_lanczos_local(int64_t n_, const int64_t* rowptr, const int32_t* col, const double* val,
                              const double* q, const double* Bk, int s, int t, int newton, double* T_out,
                              int* reorth_out) {
@@ -237,18 +253,31 @@ int cal_omp_ca_lanczos_local(int64_t n_, const int64_t* rowptr, const int32_t* c
     double* b = calloc((size_t)t + 1, sizeof(double));
     if (!Q || !V || !Y || !T || !b) return -2;
     const int ldT = st + 1;
+    /* first touch of the n-length buffers on all threads (the pages are
+     * faulted here, in parallel, not inside the first iteration's kernels);
+     * the loop below is what cal_omp_loop_seconds() reports, the analogue of
+     * the GPU bench's resident buffers */
+#pragma omp parallel for schedule(static)
+    for (size_t i = 0; i < n; ++i) {
+        for (int j = 0; j <= st; ++j) Q[IDX(i, j, n)] = 0.0;
+        for (int j = 0; j <= s; ++j) V[IDX(i, j, n)] = 0.0;
+        for (int j = 0; j < s; ++j) Y[IDX(i, j, n)] = 0.0;
+    }
+    const double t_loop = omp_get_wtime();
     memcpy(Q, q, n * sizeof(double));
     for (int k = 1; k <= t; ++k) {
         /* matrix powers (ca_lanczos.m:110-118) */
-        memcpy(V, Q + (size_t)((k - 1) * s) * n, n * sizeof(double));
+        /* V(:,1) = Q(:,(k-1)s+1); only k = 1 reads it back (the QR of all
+         * s+1 columns), so later blocks start the recurrence from Q itself */
+        const double* v0 = Q + (size_t)((k - 1) * s) * n;
+        if (k == 1) PH(2, memcpy(V, v0, n * sizeof(double)));
         for (int i = 0; i < s; ++i)
-            spmv(n, rowptr, col, val, V + (size_t)i * n, V + (size_t)(i + 1) * n, newton ? Bk[IDX(i, i, s1)] : 0.0,
-                 newton);
+            PH(0, spmv(n, rowptr, col, val, i == 0 ? v0 : V + (size_t)i * n, V + (size_t)(i + 1) * n,
+                       newton ? Bk[IDX(i, i, s1)] : 0.0, newton));
         if (k == 1) {
             /* [Q(:,1:s+1),Rk] = normalize(V) ; T = Rk*Bk/Rk(1:s,1:s) (:176-182) */
             double Rk[17 * 17], RB[17 * 16], R11[16 * 16];
-            tsqr(n, s1, V, Rk);
-            memcpy(Q, V, n * (size_t)s1 * sizeof(double));
+            PH(5, tsqr(n, s1, V, Q, Rk));
             for (int j = 0; j < s; ++j)
                 for (int i = 0; i < s1; ++i) {
                     double a = 0.0;
@@ -268,12 +297,11 @@ int cal_omp_ca_lanczos_local(int64_t n_, const int64_t* rowptr, const int32_t* c
         const double* Qp = Q + (size_t)((k - 2) * s) * n;
         double* X = V + n;
         double before[16], after[16], RY[17 * 16], RZ[17 * 16], R[16 * 16];
-        for (int j = 0; j < s; ++j) before[j] = col_norm(n, X + (size_t)j * n);        /* :17-22 */
-        memcpy(Y, X, n * (size_t)s * sizeof(double));
-        gemm_tn(n, s1, s, Qp, Y, RY);                                                 /* project :25 */
-        gemm_sub(n, s1, s, Qp, RY, Y);
-        memcpy(X, Y, n * (size_t)s * sizeof(double));                                  /* keep Y */
-        tsqr(n, s, X, R);                                                              /* normalize :26 */
+        for (int j = 0; j < s; ++j) PH(1, before[j] = col_norm(n, X + (size_t)j * n)); /* :17-22 */
+        double* Qk = Q + (size_t)((k - 1) * s + 1) * n;                               /* :188 */
+        PH(3, gemm_tn(n, s1, s, Qp, X, RY));                                          /* project :25 */
+        PH(4, gemm_sub(n, s1, s, Qp, RY, X, Y));                                      /* Y kept for :63 */
+        PH(5, tsqr(n, s, Y, Qk, R));                                                  /* normalize :26 */
         double worst = -1.0;
         for (int j = 0; j < s; ++j) {
             double a = 0.0;
@@ -285,15 +313,13 @@ int cal_omp_ca_lanczos_local(int64_t n_, const int64_t* rowptr, const int32_t* c
         int reorth = worst > 0.5;                                                      /* :52 */
         const double* Rkk_s = RY;
         if (reorth) {
-            gemm_tn(n, s1, s, Qp, Y, RZ);                                              /* :63 */
-            gemm_sub(n, s1, s, Qp, RZ, Y);
-            tsqr(n, s, Y, R);                                                          /* :64 */
+            PH(3, gemm_tn(n, s1, s, Qp, Y, RZ));                                       /* :63 */
+            PH(4, gemm_sub(n, s1, s, Qp, RZ, Y, Y));
+            PH(5, tsqr(n, s, Y, Qk, R));                                               /* :64 */
             for (int e = 0; e < s1 * s; ++e) RZ[e] += RY[e];                           /* :71-73 */
             Rkk_s = RZ;
-            memcpy(X, Y, n * (size_t)s * sizeof(double));
         }
         reorth_out[k - 1] = reorth;
-        memcpy(Q + (size_t)((k - 1) * s + 1) * n, X, n * (size_t)s * sizeof(double)); /* :188 */
         /* T update (:200-223) */
         double Rk[17 * 17], R11[16 * 16], Rkk11[16 * 16], t1[16 * 16], t3[16 * 16];
         memset(Rk, 0, sizeof(Rk));
@@ -332,8 +358,13 @@ int cal_omp_ca_lanczos_local(int64_t n_, const int64_t* rowptr, const int32_t* c
         T[IDX(m0, m0 - 1, ldT)] = bprev;
         T[IDX(m0 + s, m0 + s - 1, ldT)] = b[k - 1];
     }
+    g_loop = omp_get_wtime() - t_loop;
     for (int j = 0; j < st; ++j)
         for (int i = 0; i < st; ++i) T_out[IDX(i, j, st)] = T[IDX(i, j, ldT)];
+    if (getenv("CAL_OMP_PROFILE"))
+        fprintf(stderr, "cal_omp phases (s): spmv %.3f norms %.3f copies %.3f gram %.3f sub %.3f tsqr %.3f\n",
+                g_ph[0], g_ph[1], g_ph[2], g_ph[3], g_ph[4], g_ph[5]);
+    memset(g_ph, 0, sizeof(g_ph));
     free(Q);
     free(V);
     free(Y);
@@ -343,3 +374,7 @@ int cal_omp_ca_lanczos_local(int64_t n_, const int64_t* rowptr, const int32_t* c
 }
 
 int cal_omp_threads(void) { return omp_get_max_threads(); }
+
+/* wall time of the last cal_omp_ca_lanczos_local's outer loop (allocation and
+ * first touch excluded) */
+double cal_omp_loop_seconds(void) { return g_loop; }

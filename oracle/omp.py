@@ -27,11 +27,18 @@ def lib():
         _lib = ctypes.CDLL(LIB)
         _lib.cal_omp_ca_lanczos_local.restype = ctypes.c_int
         _lib.cal_omp_threads.restype = ctypes.c_int
+        _lib.cal_omp_loop_seconds.restype = ctypes.c_double
     return _lib
 
 
 def threads() -> int:
     return int(lib().cal_omp_threads())
+
+
+def loop_seconds() -> float:
+    """Wall time of the last ca_lanczos_local's outer loop (buffers allocated
+    and first-touched before it, as the GPU bench's are resident)."""
+    return float(lib().cal_omp_loop_seconds())
 
 
 def ca_lanczos_local(A, q, Bk, s, t, newton=True):
