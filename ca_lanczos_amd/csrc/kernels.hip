@@ -769,7 +769,7 @@ hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64
     static const int cpb = [] {
         const char* e = std::getenv("CAL_RESID_CPB");
         const int v = e ? std::atoi(e) : 4;
-        return v == 2 || v == 8 ? v : 4;
+        return v == 1 || v == 2 || v == 8 ? v : 4;
     }();
     const int blocks = spmv_pair_resid_multi_blocks(a);
     if (blocks <= 0 || pstride < blocks) return hipErrorInvalidValue;
@@ -802,7 +802,8 @@ hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64
             default: go2(cpb_c, std::integral_constant<int, 4>{}); break;
         }
     };
-    if (cpb == 2) go(std::integral_constant<int, 2>{});
+    if (cpb == 1) go(std::integral_constant<int, 1>{});
+    else if (cpb == 2) go(std::integral_constant<int, 2>{});
     else if (cpb == 8) go(std::integral_constant<int, 8>{});
     else go(std::integral_constant<int, 4>{});
     return hipGetLastError();
