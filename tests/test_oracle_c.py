@@ -36,3 +36,16 @@ def test_omp_lap3d_and_config1(ref, omp):
     w, we = np.sort(np.linalg.eigvals(T).real), np.sort(np.linalg.eigvals(exp.T).real)
     assert abs(w[-1] - we[-1]) < 1e-8 * 1000 and abs(w[0] - we[0]) < 1e-8 * 1000
     assert abs(w[-1] - 1000.0) < 1e-5 and abs(w[0] - 1.0) < 1e-5
+
+
+def test_omp_multi_tile_tsqr_and_loop_timer(ref, omp):
+    """n = 5041: three TSQR row tiles (2048, 2048, 945 rows), so the stacked-R
+    tree and the ragged last tile of the out-of-place TSQR are exercised; the
+    loop timer reports the outer loop of the last call."""
+    A = ref.laplacian_2d(71)
+    r = ref.matlab_rand(A.shape[0])
+    T, flags = omp.ca_lanczos(A, r, 8, 56, "newton")
+    exp = ref.ca_lanczos(A, r, 8, 56, "newton", "local", diagnostics=False)
+    assert flags == list(exp.reorth)
+    assert np.max(np.abs(T - exp.T)) <= 1e-12 * 8.0
+    assert omp.loop_seconds() > 0.0
