@@ -11,6 +11,7 @@
 
 #include "../../include/calanczos_host.h"
 #include "cal_internal.hpp"
+#include "comm.hpp"
 #include "dense.hpp"
 
 using namespace cal;
@@ -54,6 +55,14 @@ int check_ctx(cal_ctx* c, bool need_A) {
     hipSetDevice(c->device);
     if (need_A && !c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
     return 0;
+}
+
+// `count` draws of MATLAB's rand (genrand_res53: two 32-bit words per double)
+void cal_matlab_rand_stream(std::mt19937& g, int64_t count, double* out) {
+    for (int64_t i = 0; i < count; ++i) {
+        const uint32_t a = g() >> 5, b = g() >> 6;
+        out[i] = (a * 67108864.0 + b) / 9007199254740992.0;
+    }
 }
 
 }  // namespace
@@ -201,8 +210,28 @@ int cal_normalize_opt(cal_ctx* c, int64_t n, int m, const double* X, const char*
         CAL_TRY(apply_host(c, n, Qp, U.data(), m, &Wo, nullptr, 0, nullptr));
         // :43-50: Q(:,null) = rand(nrows, ncols-rank); project against Q(:,1:rank); tsqr
         const int k = m - rk;
+        // MATLAB's rand(nrows, k) fills the GLOBAL column-major matrix: on a
+        // row slab [row0, row0 + n) of n_global rows, column j is the stream
+        // slice j*n_global + row0 ... + n - 1 (each draw takes two 32-bit words)
+        int64_t row0 = 0, nglob = n;
+        if (c->comm && c->comm->nranks > 1) {
+            if (!c->has_A || c->A.n_local != n)
+                return set_error(c, CAL_ERR_ARG,
+                                 "normalize 'randomizeNullSpace' on a distributed context needs the matrix's row slabs");
+            row0 = c->A.row0;
+            nglob = c->A.n_global;
+        }
         std::vector<double> h((size_t)n * k);
-        cal_matlab_rand(n * k, 5489, h.data());
+        {
+            std::mt19937 g(5489);
+            int64_t pos = 0;
+            for (int j = 0; j < k; ++j) {
+                const int64_t start = (int64_t)j * nglob + row0;
+                g.discard((unsigned long long)(2 * (start - pos)));
+                cal_matlab_rand_stream(g, n, h.data() + (size_t)j * n);
+                pos = start + n;
+            }
+        }
         double* dN = dW + (size_t)rk * ld;
         CAL_TRY(upload(c, dN, ld, h.data(), n, k));
         if (rk > 0) {
@@ -230,10 +259,7 @@ int cal_normalize_opt(cal_ctx* c, int64_t n, int m, const double* X, const char*
 int cal_matlab_rand(int64_t count, unsigned seed, double* out) {
     if (count < 0 || (count > 0 && !out)) return CAL_ERR_ARG;
     std::mt19937 g(seed);
-    for (int64_t i = 0; i < count; ++i) {
-        const uint32_t a = g() >> 5, b = g() >> 6;
-        out[i] = (a * 67108864.0 + b) / 9007199254740992.0;
-    }
+    cal_matlab_rand_stream(g, count, out);
     return 0;
 }
 

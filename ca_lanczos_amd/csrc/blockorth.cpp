@@ -778,7 +778,11 @@ int project_and_normalize_dev(cal_ctx* c, int64_t n, const Panel& Qp, const Pane
     // conditioned that one Cholesky pass is orthonormal to rounding: the
     // column-scaled Gram of Y is diagonally dominant with off-diagonal row
     // sums < 1/2, so kappa(Y) < sqrt(3) and the loss of orthogonality ~ 3u.
-    if (w > 9 && !reorth && chol_ok && c->normalize_kind != 1) {
+    // The 0.5 norm-loss test guards it whatever doreorth says: R = chol(X'X -
+    // C'C) from the algebraic Gram cancels when most of X lies in span(Qp)
+    // (orthogonality ~ u ||X||^2 / ||Y||^2), and with doreorth = false the
+    // reorth flag is always off, so it cannot stand in for that test.
+    if (w > 9 && !(nan_max(rel) > 0.5) && chol_ok && c->normalize_kind != 1) {
         bool dominant = true;
         for (int i = 0; i < m && dominant; ++i) {
             double off = 0.0;

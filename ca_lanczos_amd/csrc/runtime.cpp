@@ -780,15 +780,36 @@ int cal_set_matrix_csr(cal_ctx* c, int64_t n, const int64_t* rowptr, const int32
 }
 
 int cal_set_matrix_csc(cal_ctx* c, int64_t n, const int64_t* jc, const int64_t* ir, const double* pr) {
-    // A is symmetric (ca_lanczos.m:8), so its CSC arrays are its CSR arrays.
+    // MATLAB's CSC (mwIndex jc/ir) transposed into CSR by a counting sort over
+    // the rows, so the device holds A, not A', whatever its symmetry: SpMV.m:8
+    // is a general A*v.  Walking the columns in order leaves every CSR row with
+    // ascending column indices, which is MATLAB's own accumulation order for
+    // y(i) in sparse mtimes (column by column), so y is bit-identical to A*v.
+    // For a symmetric A the result equals the CSC arrays read as CSR.
     if (!c || n < 0 || !jc) return set_error(c, CAL_ERR_ARG, "cal_set_matrix_csc: bad arguments");
+    if (n >= ((int64_t)1 << 31)) return set_error(c, CAL_ERR_UNSUPPORTED, "n and nnz must be < 2^31 per rank");
+    if (jc[0] != 0) return set_error(c, CAL_ERR_ARG, "column pointers must start at 0");
+    for (int64_t j = 0; j < n; ++j)
+        if (jc[j + 1] < jc[j]) return set_error(c, CAL_ERR_ARG, "column pointers must be non-decreasing");
     const int64_t nnz = jc[n];
-    std::vector<int32_t> col32(nnz);
+    if (nnz >= ((int64_t)1 << 31)) return set_error(c, CAL_ERR_UNSUPPORTED, "n and nnz must be < 2^31 per rank");
+    if (nnz > 0 && (!ir || !pr)) return set_error(c, CAL_ERR_ARG, "cal_set_matrix_csc: bad arguments");
+    std::vector<int64_t> rowptr(n + 1, 0);
     for (int64_t p = 0; p < nnz; ++p) {
         if (ir[p] < 0 || ir[p] >= n) return set_error(c, CAL_ERR_ARG, "row index out of range");
-        col32[p] = (int32_t)ir[p];
+        rowptr[ir[p] + 1]++;
     }
-    return cal_set_matrix_csr(c, n, jc, col32.data(), pr);
+    for (int64_t i = 0; i < n; ++i) rowptr[i + 1] += rowptr[i];
+    std::vector<int64_t> next(rowptr.begin(), rowptr.end() - 1);
+    std::vector<int32_t> col32(nnz);
+    std::vector<double> val(nnz);
+    for (int64_t j = 0; j < n; ++j)
+        for (int64_t p = jc[j]; p < jc[j + 1]; ++p) {
+            const int64_t q = next[ir[p]]++;
+            col32[q] = (int32_t)j;
+            val[q] = pr[p];
+        }
+    return cal_set_matrix_csr(c, n, rowptr.data(), col32.data(), val.data());
 }
 
 int cal_set_spmv_format(cal_ctx* c, const char* fmt) {

@@ -26,12 +26,13 @@ int cal_leja(int n, const double* x_re, const double* x_im, double* y_re, double
  *                                   newton_basis_matrix.m:13-60 */
 int cal_newton_basis_matrix(int s, const double* lam_re, const double* lam_im, int modifiedp, double* B);
 
-/* [V,D] = eig(T) for the Ritz analysis (ca_lanczos.m:229): symmetric solver
- * when T is exactly symmetric, general (Hessenberg QR) otherwise.  V is n x n
- * column-major; complex pairs are stored as (real, imag) column pairs. */
 /* MATLAB rand of a fresh session with rng(seed,'twister'): MT19937
  * genrand_res53, `count` values in column-major order. */
 int cal_matlab_rand(int64_t count, unsigned seed, double* out);
+
+/* [V,D] = eig(T) for the Ritz analysis (ca_lanczos.m:229): symmetric solver
+ * when T is exactly symmetric, general (Hessenberg QR) otherwise.  V is n x n
+ * column-major; complex pairs are stored as (real, imag) column pairs. */
 int cal_eig(int n, const double* T, int ldt, double* wr, double* wi, double* V);
 
 /* Eigenvalues of the symmetric tridiagonal T = diag(alpha) + diag(beta,+-1),

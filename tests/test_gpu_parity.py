@@ -684,6 +684,33 @@ def test_set_matrix_csc_matlab_layout(cal, ref):
     c2.close()
 
 
+def test_set_matrix_csc_nonsymmetric(cal, ref):
+    """SpMV.m:8 is a general A*v: a NONSYMMETRIC A through the MATLAB-layout
+    CSC entry (cal_set_matrix_csc, what SpMV.mexa64 binds) must give A @ v,
+    not A' @ v, bit for bit (CSR rows in ascending column order = MATLAB's
+    column-by-column accumulation).  Covers empty rows and columns, a dense
+    row and a dense column."""
+    import scipy.sparse as sp
+    rng = np.random.RandomState(11)
+    n = 3000
+    B = sp.random(n, n, density=0.002, random_state=rng, format="lil")
+    B[5, :] = rng.randn(n)          # a dense row
+    B[:, 7] = rng.randn(n, 1)       # a dense column
+    B[11, :] = 0.0                  # an empty row
+    B[:, 13] = 0.0                  # an empty column
+    A = B.tocsr()
+    A.eliminate_zeros()
+    A.sort_indices()
+    assert abs(A - A.T).max() > 0
+    c1 = cal.Context().set_matrix_csc(A.tocsc())
+    v = ref.matlab_rand(n, seed=5) - 0.5
+    y = c1.spmv(v)
+    assert np.array_equal(y, ref.SpMV(A, v))
+    assert np.max(np.abs(y - A @ v)) <= 1e-12 * np.max(np.abs(A @ v))
+    assert np.max(np.abs(y - A.T @ v)) > 1e-3
+    c1.close()
+
+
 def test_normalize_randomize_null_space(cal, ref):
     """normalize(X,'randomizeNullSpace') (normalize.m:28-31,38-51) on a rank-5
     block of 8 columns: same rank; R = S W' and Q(:,1:rank) = Q U match the
@@ -703,6 +730,30 @@ def test_normalize_randomize_null_space(cal, ref):
     assert np.max(np.abs(Q[:, :rk] * sg - Qr[:, :rk])) <= 1e-10
     assert np.max(np.abs(R[:rk] * sg[:, None] - Rr[:rk])) <= 1e-10 * nx
     assert np.max(np.abs(Q[:, rk:] - Qr[:, rk:])) <= 1e-10
+
+
+def test_project_and_normalize_wide_block_no_reorth_in_span(cal, ref):
+    """doreorth = false with 99 % of X inside span(Qp) (w = 40 > 9,
+    'cholqr2').  The reference does one projection + normalize
+    (projectAndNormalize.m:25-26, no second pass).  The single-sweep wide path
+    (R = chol(X'X - C'C) from the algebraic Gram) would cancel here, so it must
+    not be taken: the result stays orthonormal to 1e-13 and orthogonal to Qp
+    to the level one projection reaches (the oracle's own Qp'QZ, x10)."""
+    rng = np.random.RandomState(23)
+    n, w, m = 20000, 40, 8
+    Qp, _ = np.linalg.qr(rng.randn(n, w))
+    X = 0.99 * Qp @ rng.randn(w, m) + 0.01 * rng.randn(n, m) / np.sqrt(n)
+    ctx = cal.default_context()
+    ctx.set_normalize("cholqr2")
+    try:
+        QZ, RZ, re, rank = cal.projectAndNormalize_ex([Qp], X, doreorth=False)
+    finally:
+        ctx.set_normalize("auto")
+    QZr, RZr, info = ref.projectAndNormalize_ex([Qp], X, doreorth=False)
+    assert re is False or re == 0
+    assert np.max(np.abs(QZ.T @ QZ - np.eye(m))) < 1e-13
+    assert np.max(np.abs(QZ.T @ Qp)) <= 10 * np.max(np.abs(QZr.T @ Qp)) + 1e-13
+    assert np.max(np.abs(RZ[0] - RZr[0])) <= 1e-12 * max(1.0, np.max(np.abs(RZr[0])))
 
 
 @pytest.mark.parametrize("case", ["spread", "reorth", "ill"])

@@ -33,3 +33,59 @@ def test_shims_call_declared_entry_points():
             src = open(os.path.join(MEX, f)).read()
             used = {u for u in re.findall(r"\b(cal_[a-z0-9_]+)\s*\(", src) if not u.startswith("cal_mex_")}
             assert used <= declared, (f, used - declared)
+
+
+_CACHE_HARNESS = r"""
+#include <stdio.h>
+#include <stdlib.h>
+#include <stdarg.h>
+#include "cal_mex_common.h"
+/* stand-ins: an mxArray is a sparse CSC triple; the ABI calls only count */
+struct mxArray_tag { mwSize n; mwIndex* jc; mwIndex* ir; double* pr; };
+static int uploads = 0;
+int cal_create(int dev, cal_ctx** c) { (void)dev; *c = (cal_ctx*)1; return 0; }
+void cal_destroy(cal_ctx* c) { (void)c; }
+const char* cal_last_error(const cal_ctx* c) { (void)c; return ""; }
+int cal_set_matrix_csc(cal_ctx* c, int64_t n, const int64_t* jc, const int64_t* ir, const double* pr) {
+    (void)c; (void)n; (void)jc; (void)ir; (void)pr; return ++uploads, 0; }
+void mexErrMsgIdAndTxt(const char* id, const char* fmt, ...) { (void)fmt; fprintf(stderr, "%s\n", id); exit(3); }
+void mexWarnMsgIdAndTxt(const char* id, const char* fmt, ...) { (void)id; (void)fmt; }
+int mexAtExit(void (*fn)(void)) { (void)fn; return 0; }
+int mxIsSparse(const mxArray* a) { (void)a; return 1; }
+int mxIsComplex(const mxArray* a) { (void)a; return 0; }
+mwSize mxGetM(const mxArray* a) { return a->n; }
+mwSize mxGetN(const mxArray* a) { return a->n; }
+mwIndex* mxGetJc(const mxArray* a) { return a->jc; }
+mwIndex* mxGetIr(const mxArray* a) { return a->ir; }
+double* mxGetPr(const mxArray* a) { return a->pr; }
+int main(void) {
+    mwIndex jc[4] = {0, 1, 2, 3}, ir[3] = {0, 1, 2};
+    double pr[3] = {1.0, 2.0, 3.0};
+    mxArray A = {3, jc, ir, pr};
+    cal_mex_ctx(&A);            /* first call: upload */
+    cal_mex_ctx(&A);            /* same matrix: cached */
+    pr[1] = 5.0;                /* in-place A(2,2)=5: same pointers and nnz */
+    cal_mex_ctx(&A);
+    ir[0] = 2; ir[2] = 0;       /* same values, other pattern */
+    cal_mex_ctx(&A);
+    cal_mex_ctx(&A);
+    printf("%d\n", uploads);
+    return 0;
+}
+"""
+
+
+def test_mex_matrix_cache_sees_in_place_edits(tmp_path):
+    """the MEX context reuses the device copy of A only
+    when pointers, nnz AND the content digest of jc/ir/pr match, so an
+    in-place A(i,j)=v (same pointers, same nnz) re-uploads.  The harness
+    stubs the MEX API and the one ABI call and counts uploads.  CPU only."""
+    src = tmp_path / "cache.c"
+    src.write_text(_CACHE_HARNESS)
+    exe = tmp_path / "cache"
+    p = subprocess.run(["gcc", "-O2", "-std=c99", "-Wall", "-Werror", "-Wno-unused-function", "-I" + MEX,
+                        "-I" + os.path.join(MEX, "syntax"), "-I" + os.path.join(ROOT, "include"), str(src),
+                        "-o", str(exe)], capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout
+    assert out.strip() == "3"

@@ -1,0 +1,13 @@
+# Round-3 baseline on a fresh box: gpu tests, smoke, default bench line (with CPU baseline).
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=$GRAFT_REPO_ROOT/gpurun_out/${TAG:-base}
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -4 $O/pytest.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
+timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
+rc=$?; echo "bench rc=$rc"; cut -c1-300 $O/bench.json
+exit $rc
