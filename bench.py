@@ -158,11 +158,40 @@ def _blas_threads():
         return 1
 
 
+def usable_cpus():
+    """The CPUs this process may actually run on: the affinity mask, capped by
+    the cgroup CPU quota (v2 cpu.max, v1 cfs_quota_us / cfs_period_us), with
+    OMP_NUM_THREADS as found in the environment (reported, not trusted)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        try:
+            q = float(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            period = float(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / period
+        except (OSError, ValueError):
+            pass
+    usable = aff if quota is None else max(1, min(aff, int(math.floor(quota + 1e-9))))
+    return {"affinity_cpus": aff, "cgroup_quota_cpus": quota, "usable": usable,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
 def cpu_baseline(wl, s, iters, basis="newton"):
-    """The C/OpenMP restatement (oracle/c/ca_lanczos_omp.c, all host cores)
-    timed on this host: Newton prologue excluded, `iters` outer iterations of
-    ca_lanczos_basic 'local' (k = 1..iters, diagnostics off) on the same
-    matrix and start vector (SURVEY §8d CPU baseline (2))."""
+    """The C/OpenMP restatement (oracle/c/ca_lanczos_omp.c) timed on this host
+    with one thread per usable CPU (affinity and cgroup quota, usable_cpus();
+    SURVEY §8d "OMP_NUM_THREADS = nproc"): Newton prologue excluded, `iters`
+    outer iterations of ca_lanczos_basic 'local' (k = 1..iters, diagnostics
+    off) on the same matrix and start vector (SURVEY §8d CPU baseline (2)).
+    When more than 16 CPUs are usable, 16 threads (the box's per-GPU CPU
+    share) are timed too and reported beside it."""
     from oracle import ca_lanczos_ref as ref
     from oracle import omp
     A = wl.full()
@@ -170,16 +199,26 @@ def cpu_baseline(wl, s, iters, basis="newton"):
     q = r / math.sqrt(r @ r)
     Bk, _, _ = ref.newton_change_of_basis(A, q, s)
     omp.lib()
-    t0 = time.perf_counter()
-    omp.ca_lanczos_local(A, q, Bk, s, iters, basis == "newton")
-    dt_call = time.perf_counter() - t0
-    dt = omp.loop_seconds()
-    th = omp.threads()
-    return {"value": iters / dt, "unit": "outer-iters/s", "cores": th, "kind": "port",
-            "sample": "oracle/c/ca_lanczos_omp.c (C/OpenMP, %d threads): %d outer iterations (k=1..%d, s=%d, "
-                      "Newton, 'local', Householder TSQR normalize, diagnostics off) on the same %s matrix; "
-                      "outer loop %.1f s (buffers allocated and first-touched before it, as the GPU's are "
-                      "resident; whole call %.1f s)" % (th, iters, iters, s, wl.name, dt, dt_call)}
+    cpus = usable_cpus()
+
+    def timed(th):
+        omp.set_threads(th)
+        t0 = time.perf_counter()
+        omp.ca_lanczos_local(A, q, Bk, s, iters, basis == "newton")
+        return omp.loop_seconds(), time.perf_counter() - t0, omp.threads()
+
+    dt, dt_call, th = timed(cpus["usable"])
+    out = {"value": iters / dt, "unit": "outer-iters/s", "cores": th, "kind": "port",
+           "sample": "oracle/c/ca_lanczos_omp.c (C/OpenMP, %d threads = the usable CPUs): %d outer iterations "
+                     "(k=1..%d, s=%d, Newton, 'local', Householder TSQR normalize, diagnostics off) on the same "
+                     "%s matrix; outer loop %.1f s (buffers allocated and first-touched in parallel before it, as "
+                     "the GPU's are resident; whole call %.1f s)" % (th, iters, iters, s, wl.name, dt, dt_call),
+           "cpus": cpus}
+    if cpus["usable"] > 16:
+        dt16, _, th16 = timed(16)
+        out["value_16_threads"] = iters / dt16
+        out["sample"] += "; with 16 threads: %.1f s" % dt16
+    return out
 
 
 def cpu_baseline_numpy(wl, s, iters, basis="newton"):

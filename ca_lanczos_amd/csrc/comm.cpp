@@ -164,27 +164,30 @@ int halo_exchange_deep(cal_ctx* c, double* x, int d, hipStream_t hs_st) {
         CAL_NCCL(c, ncclGroupEnd());
         return 0;
     }
+    // host-staged: the copies run on hs_st (the compute stream, or the
+    // communicator's stream when the exchange overlaps the interior powers;
+    // then this runs on the comm thread, runtime.cpp powers_dev)
     CAL_TRY(ensure_stage(c, (size_t)(stot + rtot)));
     double* hs = m->h_stage;
     double* hr = m->h_stage + stot;
     int64_t so = 0;
     for (const Piece& p : pieces) {
         if (p.s_cnt > 0)
-            CAL_HIP(c, hipMemcpyAsync(hs + so, x + p.s_off, p.s_cnt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+            CAL_HIP(c, hipMemcpyAsync(hs + so, x + p.s_off, p.s_cnt * sizeof(double), hipMemcpyDeviceToHost, hs_st));
         so += p.s_cnt;
     }
-    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    CAL_HIP(c, hipStreamSynchronize(hs_st));
     so = 0;
     int64_t ro = 0;
     for (const Piece& p : pieces) {
         if (m->ex(m->user, p.peer, hs + so, p.s_cnt, hr + ro, p.r_cnt) != 0)
             return set_error(c, CAL_ERR_COMM, "exchange callback failed");
         if (p.r_cnt > 0)
-            CAL_HIP(c, hipMemcpyAsync(x + p.r_off, hr + ro, p.r_cnt * sizeof(double), hipMemcpyHostToDevice, c->stream));
+            CAL_HIP(c, hipMemcpyAsync(x + p.r_off, hr + ro, p.r_cnt * sizeof(double), hipMemcpyHostToDevice, hs_st));
         so += p.s_cnt;
         ro += p.r_cnt;
     }
-    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    CAL_HIP(c, hipStreamSynchronize(hs_st));
     return 0;
 }
 
@@ -244,6 +247,21 @@ int cal_comm_unique_id(void* id128) {
     return 0;
 }
 
+// the halo stream (high priority: the exchange's copies / RCCL kernels are
+// dispatched between the interior matrix-powers blocks) and its two events
+static int comm_make_halo_stream(cal_ctx* c, Comm* m) {
+    int lo = 0, hi = 0;
+    hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (hipStreamCreateWithPriority(&m->stream, hipStreamNonBlocking, hi) != hipSuccess ||
+        hipEventCreateWithFlags(&m->ev_q, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&m->ev_halo, hipEventDisableTiming) != hipSuccess) {
+        c->comm = m;
+        comm_destroy(c);
+        return set_error(c, CAL_ERR_HIP, "halo stream / events");
+    }
+    return 0;
+}
+
 int cal_comm_init_rccl(cal_ctx* c, int nranks, int rank, const void* id128) {
     if (!c || nranks < 1 || rank < 0 || rank >= nranks || !id128) return set_error(c, CAL_ERR_ARG, "bad comm args");
     hipSetDevice(c->device);
@@ -259,17 +277,7 @@ int cal_comm_init_rccl(cal_ctx* c, int nranks, int rank, const void* id128) {
         delete m;
         return nccl_fail(c, r, "ncclCommInitRank");
     }
-    // the halo stream (high priority: its RCCL kernel is dispatched between
-    // the interior matrix-powers blocks) and its two events
-    int lo = 0, hi = 0;
-    hipDeviceGetStreamPriorityRange(&lo, &hi);
-    if (hipStreamCreateWithPriority(&m->stream, hipStreamNonBlocking, hi) != hipSuccess ||
-        hipEventCreateWithFlags(&m->ev_q, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&m->ev_halo, hipEventDisableTiming) != hipSuccess) {
-        c->comm = m;
-        comm_destroy(c);
-        return set_error(c, CAL_ERR_HIP, "halo stream / events");
-    }
+    CAL_TRY(comm_make_halo_stream(c, m));
     c->comm = m;
     return 0;
 }
@@ -278,6 +286,7 @@ int cal_comm_init_host(cal_ctx* c, int nranks, int rank, cal_allreduce_fn allred
                        void* user) {
     if (!c || nranks < 1 || rank < 0 || rank >= nranks || !allreduce || !exchange)
         return set_error(c, CAL_ERR_ARG, "bad comm args");
+    hipSetDevice(c->device);
     comm_destroy(c);
     Comm* m = new Comm();
     m->nranks = nranks;
@@ -286,6 +295,9 @@ int cal_comm_init_host(cal_ctx* c, int nranks, int rank, cal_allreduce_fn allred
     m->ar = allreduce;
     m->ex = exchange;
     m->user = user;
+    // the same stream / event pair as RCCL: the split matrix-powers schedule
+    // runs the host-staged exchange on it from a comm thread (powers_dev)
+    CAL_TRY(comm_make_halo_stream(c, m));
     c->comm = m;
     return 0;
 }

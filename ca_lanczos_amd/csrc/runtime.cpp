@@ -1,5 +1,6 @@
 // runtime.cpp -- context lifecycle, device buffers, matrix upload, timers.
 #include <algorithm>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -617,26 +618,52 @@ int powers_dev(cal_ctx* c, int s, const double* q, double* const* Y, const doubl
     auto ilo = [&](int j) { return dep_lo ? A.row0 + (int64_t)j * bl : glo(j); };
     auto ihi = [&](int j) { return dep_hi ? row1 - (int64_t)j * br : ghi(j); };
     Comm* m = c->comm;
-    const bool rccl = mpk && m && m->kind == 1 && m->stream && m->ev_q && m->ev_halo;
+    const bool comm_stream = mpk && m && m->stream && m->ev_q && m->ev_halo;
+    const bool rccl = comm_stream && m->kind == 1;
     const int ov = mpk_overlap_env();
     const bool split = (fake > 0 || (mpk && (ov == 1 || (ov < 0 && rccl)))) && (dep_lo || dep_hi) &&
                        ilo(s) + 4 < ihi(s);
-    c->powers_schedule = split ? (rccl ? 2 : 3) : 1;
+    c->powers_schedule = split ? (rccl ? 2 : (comm_stream ? 4 : 3)) : 1;
     if (!split) {
         CAL_TRY(halo_exchange_deep(c, const_cast<double*>(q), s, c->stream));
         for (int j = 1; j <= s; ++j) CAL_TRY(launch(j, stored_range(A, glo(j), ghi(j)), PowRange{0, 0}));
         return 0;
     }
-    if (rccl) {  // exchange on the communicator's stream, behind q
+    // The exchange runs on the communicator's stream behind an event recorded
+    // when q is ready; the compute stream waits for ev_halo only before the
+    // boundary pieces.  RCCL enqueues its send/recv kernels there directly.
+    // The host-staged twin (schedule 4) keeps the same event graph: a comm
+    // thread waits for ev_q through the stream, stages q's pieces to the host,
+    // runs the exchange callbacks, copies the ghost rows back on the same
+    // stream and records ev_halo, while this thread enqueues the interior
+    // powers; the wait on ev_halo is enqueued after the join (an event must be
+    // recorded before a stream can wait for it).
+    std::thread comm_thread;
+    int comm_status = 0;
+    if (comm_stream) {
         CAL_HIP(c, hipEventRecord(m->ev_q, c->stream));
         CAL_HIP(c, hipStreamWaitEvent(m->stream, m->ev_q, 0));
-        CAL_TRY(halo_exchange_deep(c, const_cast<double*>(q), s, m->stream));
-        CAL_HIP(c, hipEventRecord(m->ev_halo, m->stream));
+        if (rccl) {
+            CAL_TRY(halo_exchange_deep(c, const_cast<double*>(q), s, m->stream));
+            CAL_HIP(c, hipEventRecord(m->ev_halo, m->stream));
+        } else {
+            comm_thread = std::thread([c, m, q, s, &comm_status]() {
+                hipSetDevice(c->device);
+                comm_status = halo_exchange_deep(c, const_cast<double*>(q), s, m->stream);
+                if (comm_status == 0 && hipEventRecord(m->ev_halo, m->stream) != hipSuccess)
+                    comm_status = set_error(c, CAL_ERR_HIP, "halo event record");
+            });
+        }
     } else if (mpk) {
         CAL_TRY(halo_exchange_deep(c, const_cast<double*>(q), s, c->stream));
     }
-    for (int j = 1; j <= s; ++j) CAL_TRY(launch(j, stored_range(A, ilo(j), ihi(j)), PowRange{0, 0}));
-    if (rccl) CAL_HIP(c, hipStreamWaitEvent(c->stream, m->ev_halo, 0));
+    int interior_status = 0;
+    for (int j = 1; j <= s && interior_status == 0; ++j)
+        interior_status = launch(j, stored_range(A, ilo(j), ihi(j)), PowRange{0, 0});
+    if (comm_thread.joinable()) comm_thread.join();
+    CAL_TRY(interior_status);
+    CAL_TRY(comm_status);
+    if (comm_stream) CAL_HIP(c, hipStreamWaitEvent(c->stream, m->ev_halo, 0));
     for (int j = 1; j <= s; ++j) {
         const PowRange lo = dep_lo ? stored_range(A, glo(j), ilo(j)) : PowRange{0, 0};
         const PowRange hi = dep_hi ? stored_range(A, ihi(j), ghi(j)) : PowRange{0, 0};

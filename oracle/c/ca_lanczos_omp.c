@@ -375,6 +375,14 @@ int cal_omp_ca_lanczos_local(int64_t n_, const int64_t* rowptr, const int32_t* c
 
 int cal_omp_threads(void) { return omp_get_max_threads(); }
 
+/* the thread count of the following calls (bench.py sets it from the usable
+ * CPUs: affinity and the cgroup quota) */
+int cal_omp_set_threads(int n) {
+    if (n < 1) return -1;
+    omp_set_num_threads(n);
+    return 0;
+}
+
 /* wall time of the last cal_omp_ca_lanczos_local's outer loop (allocation and
  * first touch excluded) */
 double cal_omp_loop_seconds(void) { return g_loop; }

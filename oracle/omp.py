@@ -27,12 +27,19 @@ def lib():
         _lib = ctypes.CDLL(LIB)
         _lib.cal_omp_ca_lanczos_local.restype = ctypes.c_int
         _lib.cal_omp_threads.restype = ctypes.c_int
+        _lib.cal_omp_set_threads.restype = ctypes.c_int
+        _lib.cal_omp_set_threads.argtypes = [ctypes.c_int]
         _lib.cal_omp_loop_seconds.restype = ctypes.c_double
     return _lib
 
 
 def threads() -> int:
     return int(lib().cal_omp_threads())
+
+
+def set_threads(n: int) -> None:
+    if lib().cal_omp_set_threads(int(n)) != 0:
+        raise ValueError("thread count must be >= 1")
 
 
 def loop_seconds() -> float:

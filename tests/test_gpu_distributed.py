@@ -95,8 +95,12 @@ def test_two_ranks_one_gpu_match_single(cal, ref, case):
         assert flags == list(single.reorth)
         assert brk == (single.info.get("n_orth_breaks"), single.info.get("n_ritz_locked"))
         assert np.max(np.abs(T - single.T)) <= 1e-9 * normA
-        big = single.ritz_rnorm[:, 0] > 1e-10
-        assert np.all(np.abs(np.log(rn[big, 0] / single.ritz_rnorm[big, 0])) < np.log(1.5))
+        # every Ritz pair's residual norm above 1e-10: 1e-8 relative (the
+        # config-4 bar); the two runs differ only in the Gram summation order
+        big = single.ritz_rnorm > 1e-10
+        dev = np.abs(rn[big] / single.ritz_rnorm[big] - 1.0)
+        print("case %s rank %d: max rel rn deviation %.2e over %d pairs" % (case, rank, dev.max(), dev.size))
+        assert np.all(dev <= 1e-8)
     assert np.array_equal(res[0][3], res[1][3])
 
 

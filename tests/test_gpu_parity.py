@@ -231,14 +231,19 @@ def test_project_and_normalize_two_blocks(cal, ref):
 
 
 # ---------------------------------------------------------------- a10 - a14
-def _compare_lanczos(out, exp, normA, check_rn=True):
+def _compare_lanczos(out, exp, normA, check_rn=True, t_blocks=None):
+    """T is compared within 1e-9 ||A|| on its leading t_blocks x t_blocks
+    blocks of s (None: the whole T).  A test limits t_blocks only where the
+    ORACLE's own T moves by more than 1e-12 ||A|| under a 1e-15 relative
+    perturbation of r ('local' orth after orthogonality is lost: ghost Ritz
+    values make later blocks chaotic); the measured spread is in its
+    docstring.  No test compares less than the first 2 blocks."""
     assert out.T.shape == exp.T.shape
     assert list(out.reorth) == list(exp.reorth)
     if len(exp.shifts):
         assert np.max(np.abs(out.shifts - exp.shifts)) <= 1e-9 * normA
-    # first block of T (k <= 2)
     s = exp.Bk.shape[1]
-    m = min(2 * s, exp.T.shape[0])
+    m = exp.T.shape[0] if t_blocks is None else min(max(2, t_blocks) * s, exp.T.shape[0])
     assert np.max(np.abs(out.T[:m, :m] - exp.T[:m, :m])) <= 1e-9 * normA
     # converged Ritz values of the final T
     w = np.sort(np.linalg.eigvals(out.T).real)
@@ -262,13 +267,16 @@ def test_ca_lanczos_config1_monomial(cal, ref):
     _compare_lanczos(out, exp, 1000.0)
 
 
-@pytest.mark.parametrize("N,dim,it", [(32, 2, 80), (12, 3, 80)])
-def test_ca_lanczos_newton_local(cal, ref, N, dim, it):
+@pytest.mark.parametrize("N,dim,it,t_blocks", [(32, 2, 80, None), (12, 3, 80, 8)])
+def test_ca_lanczos_newton_local(cal, ref, N, dim, it, t_blocks):
+    """lap2d 32^2: the whole 80 x 80 T (oracle spread 2e-15 ||A||).  lap3d
+    12^3: the leading 8 of 10 blocks (oracle spread per block 5e-15 up to
+    block 8, then 2e-11 and 2e-6 ||A||)."""
     A = cal.matrices.laplacian_2d(N) if dim == 2 else cal.matrices.laplacian_3d(N)
     r = ref.matlab_rand(A.shape[0])
     out = cal.ca_lanczos_ex(A, r, 8, it, "newton", "local")
     exp = ref.ca_lanczos(A, r, 8, it, "newton", "local")
-    _compare_lanczos(out, exp, 4.0 * dim)
+    _compare_lanczos(out, exp, 4.0 * dim, t_blocks=t_blocks)
 
 
 def test_ca_lanczos_newton_full(cal, ref):
@@ -514,7 +522,12 @@ def test_ca_lanczos_block_sizes(cal, ref, s, basis):
     device-coefficient fast path for the generic sweeps; s + 1 > 16 takes the
     Householder TSQR normalize (32-column tiles); s = 1 is plain Lanczos with
     one-column blocks.  s = 4, 8, 12, 16 with 120 steps is the reference's
-    own harness (test_ca_lanczos.m:29-41).  Same bars as the s = 4 / 8 cases."""
+    own harness (test_ca_lanczos.m:29-41).  Same bars as the s = 4 / 8 cases;
+    T on the whole matrix for s <= 9 (oracle spread <= 6e-13 ||A||), on the
+    leading blocks where the oracle's own spread stays <= 3e-12 ||A|| for
+    s >= 12 (measured per block: s = 12 up to block 6, then 1e-10, 2e-3;
+    s = 15, 16 up to 5, then 5e-8 / 2e-3; s = 20 up to 4... 3e-12 at 4,
+    then 0.2; s = 24 up to 2, then 7e-12, 1e-2)."""
     N = 20
     A = cal.matrices.laplacian_2d(N)
     r = ref.matlab_rand(N * N)
@@ -523,7 +536,7 @@ def test_ca_lanczos_block_sizes(cal, ref, s, basis):
     it = min(120, 8 * s) if s >= 12 else s * 5
     out = cal.ca_lanczos_ex(A, r, s, it, basis, "local")
     exp = ref.ca_lanczos(A, r, s, it, basis, "local")
-    _compare_lanczos(out, exp, 8.0)
+    _compare_lanczos(out, exp, 8.0, t_blocks={12: 6, 15: 5, 16: 5, 20: 4, 24: 2}.get(s))
 
 
 @pytest.mark.parametrize("s,basis", [(2, "monomial"), (4, "monomial"), (4, "newton")])
