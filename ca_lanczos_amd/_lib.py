@@ -42,7 +42,7 @@ class LanczosInfo(ctypes.Structure):
         ("t", c_int), ("s", c_int), ("n_reorth", c_int), ("n_rank_deficient", c_int),
         ("breakdown", c_int), ("shifts", c_double * 64), ("shifts_im", c_double * 64),
         ("prologue_ms", c_double), ("loop_ms", c_double), ("diag_ms", c_double),
-        ("n_orth_breaks", c_int), ("n_ritz_locked", c_int), ("norm_A", c_double),
+        ("n_orth_breaks", c_int), ("n_ritz_locked", c_int), ("norm_A", c_double), ("n_ritz_complex", c_int),
     ]
 
 

@@ -505,7 +505,8 @@ def ca_lanczos_ex(A, r, s, iter, basis, orth="local", diagnostics=True, return_Q
         info=dict(t=k, n_reorth=info.n_reorth, n_rank_deficient=info.n_rank_deficient,
                   breakdown=info.breakdown, prologue_ms=info.prologue_ms, loop_ms=info.loop_ms,
                   diag_ms=info.diag_ms, status=st, n_orth_breaks=info.n_orth_breaks,
-                  n_ritz_locked=info.n_ritz_locked, norm_A=info.norm_A))
+                  n_ritz_locked=info.n_ritz_locked, norm_A=info.norm_A,
+                  n_ritz_complex=info.n_ritz_complex))
 
 
 def ca_lanczos(A, r, s, iter, basis, orth="local"):

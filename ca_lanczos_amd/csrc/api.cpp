@@ -57,14 +57,6 @@ int check_ctx(cal_ctx* c, bool need_A) {
     return 0;
 }
 
-// `count` draws of MATLAB's rand (genrand_res53: two 32-bit words per double)
-void cal_matlab_rand_stream(std::mt19937& g, int64_t count, double* out) {
-    for (int64_t i = 0; i < count; ++i) {
-        const uint32_t a = g() >> 5, b = g() >> 6;
-        out[i] = (a * 67108864.0 + b) / 9007199254740992.0;
-    }
-}
-
 }  // namespace
 
 extern "C" {
@@ -228,7 +220,7 @@ int cal_normalize_opt(cal_ctx* c, int64_t n, int m, const double* X, const char*
             for (int j = 0; j < k; ++j) {
                 const int64_t start = (int64_t)j * nglob + row0;
                 g.discard((unsigned long long)(2 * (start - pos)));
-                cal_matlab_rand_stream(g, n, h.data() + (size_t)j * n);
+                dense::matlab_rand(g, n, h.data() + (size_t)j * n);
                 pos = start + n;
             }
         }
@@ -253,14 +245,6 @@ int cal_normalize_opt(cal_ctx* c, int64_t n, int m, const double* X, const char*
     }
     CAL_TRY(download(c, Q, dQ, ld, n, m));
     return rk < m ? CAL_WARN_RANK_DEFICIENT : 0;
-}
-
-// MATLAB rand (MT19937 genrand_res53) of a fresh stream seeded `seed`
-int cal_matlab_rand(int64_t count, unsigned seed, double* out) {
-    if (count < 0 || (count > 0 && !out)) return CAL_ERR_ARG;
-    std::mt19937 g(seed);
-    cal_matlab_rand_stream(g, count, out);
-    return 0;
 }
 
 int cal_cholqr(cal_ctx* c, int64_t n, int m, const double* X, double* Q, double* R) {

@@ -10,6 +10,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <cstdint>
 #include <functional>
@@ -17,6 +18,14 @@
 #include <vector>
 
 #include "../../include/calanczos.h"
+
+// rocprofv3 --marker-trace range (host time) for the scope of one object
+struct RoctxRange {
+    explicit RoctxRange(const char* msg) { roctxRangePushA(msg); }
+    ~RoctxRange() { roctxRangePop(); }
+    RoctxRange(const RoctxRange&) = delete;
+    RoctxRange& operator=(const RoctxRange&) = delete;
+};
 
 namespace cal {
 

@@ -765,5 +765,12 @@ void hess_qrstep(int m, double* H, int ldh, double* W, int ldw, double mu) {
     for (int i = 0; i < m; ++i) h(i, i) += mu;
 }
 
+void matlab_rand(std::mt19937& g, int64_t count, double* out) {
+    for (int64_t i = 0; i < count; ++i) {
+        const uint32_t a = g() >> 5, b = g() >> 6;
+        out[i] = (a * 67108864.0 + b) / 9007199254740992.0;
+    }
+}
+
 }  // namespace dense
 }  // namespace cal

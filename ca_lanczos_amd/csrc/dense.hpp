@@ -3,6 +3,8 @@
 // All matrices are column-major: A(i,j) = A[i + j*ld].
 #pragma once
 
+#include <cstdint>
+#include <random>
 #include <vector>
 
 namespace cal {
@@ -37,6 +39,9 @@ void eig_symmetric(int n, const double* A, int lda, double* w, double* V, int ld
 // One explicit shifted QR step on an upper-Hessenberg H: H <- Q'HQ,
 // W <- WQ with H - mu I = QR (Givens rotations; qrstep of the implicit restart).
 void hess_qrstep(int m, double* H, int ldh, double* W, int ldw, double mu);
+// `count` draws of MATLAB's rand from the MT19937 stream g (genrand_res53:
+// two 32-bit words per double)
+void matlab_rand(std::mt19937& g, int64_t count, double* out);
 
 }  // namespace dense
 }  // namespace cal

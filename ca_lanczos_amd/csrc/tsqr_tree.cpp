@@ -15,6 +15,7 @@
 
 #include "cal_internal.hpp"
 #include "comm.hpp"
+#include "tsqr_plan.hpp"
 
 namespace cal {
 
@@ -28,15 +29,6 @@ bool use_tsqr(const cal_ctx* c, int m, bool tier1) {
 }
 
 namespace {
-
-struct Level {
-    int src;             // 0 stack, 1 direct, 2 formed
-    int64_t rows, tiles;
-    const double* in;    // stack input (src 0)
-    double* up;          // UP output: tiles blocks of m x m
-    double* down;        // DOWN output (src 0): rows of the input shape; null at level 0
-    const double* S;     // DOWN: parent blocks; null at the root
-};
 
 int ensure_tsqr(cal_ctx* c, size_t doubles) {
     if (doubles <= c->tsqr_cap) return 0;
@@ -59,27 +51,12 @@ int tsqr_dev(cal_ctx* c, int64_t n, const Panel& W, const double* dM, int m, con
     if (Qout.total != m) return set_error(c, CAL_ERR_ARG, "tsqr: output shape");
     const int64_t TR = tsqr_tile_rows(m), mm = (int64_t)m * m;
     const int P = c->comm ? c->comm->nranks : 1, me = c->comm ? c->comm->rank : 0;
-    // level structure and workspace: local levels, then (P > 1) global levels
-    std::vector<Level> lv;
-    size_t need = 0;
-    auto push = [&](int src, int64_t rows) {
-        Level L{};
-        L.src = src;
-        L.rows = rows;
-        L.tiles = (rows + TR - 1) / TR;
-        lv.push_back(L);
-        need += (size_t)L.tiles * mm;                      // UP output
-        if (src == 0) need += (size_t)rows / m * mm;        // DOWN output (input shape)
-    };
-    push(form ? 2 : 1, std::max<int64_t>(n, 1));
-    while (lv.back().tiles > 1) push(0, lv.back().tiles * m);
-    const size_t nlocal = lv.size();
-    if (P > 1) {
-        push(0, (int64_t)P * m);  // the gathered local roots (allgather's output = this level's input)
-        need += (size_t)P * mm;
-        while (lv.back().tiles > 1) push(0, lv.back().tiles * m);
-    }
-    CAL_TRY(ensure_tsqr(c, need));
+    // level structure and workspace layout (tsqr_plan.cpp): local levels, then
+    // (P > 1) the global levels over the all-gathered local roots
+    const TsqrPlan plan = tsqr_plan(n, m, TR, form, P, me);
+    const std::vector<TsqrLevelPlan>& lv = plan.lv;
+    const size_t nlocal = plan.nlocal;
+    CAL_TRY(ensure_tsqr(c, plan.need));
     // level 0's factored tiles (4096 doubles each) and tau / beta, kept by the
     // up pass for the down pass (which then neither re-forms nor re-factors)
     const int MM = tsqr_mm(m);
@@ -92,26 +69,8 @@ int tsqr_dev(cal_ctx* c, int64_t n, const Panel& W, const double* dM, int m, con
     }
     double* const dV = c->d_tsqrv;
     double* const dTB = c->d_tsqrv + (size_t)lv[0].tiles * 4096;
-    double* p = c->d_tsqr;
-    for (size_t l = 0; l < lv.size(); ++l) {
-        Level& L = lv[l];
-        if (P > 1 && l == nlocal) {  // gathered stack
-            L.in = p;
-            p += (size_t)P * mm;
-        }
-        L.up = p;
-        p += (size_t)L.tiles * mm;
-        if (L.src == 0) {
-            L.down = p;
-            p += (size_t)L.rows / m * mm;
-        }
-        if (l + 1 < lv.size() && !(P > 1 && l + 1 == nlocal)) lv[l + 1].in = L.up;
-    }
-    // DOWN inputs: level l's S = level l+1's DOWN output; the local root's S =
-    // this rank's block of the global level 0's DOWN output
-    for (size_t l = 0; l + 1 < lv.size(); ++l) lv[l].S = lv[l + 1].down;
-    if (P > 1) lv[nlocal - 1].S = lv[nlocal].down + (size_t)me * mm;
-    lv.back().S = nullptr;
+    double* const ws = c->d_tsqr;
+    auto at = [&](int64_t off) -> double* { return off < 0 ? nullptr : ws + off; };
 
     TsqrCols cols{};
     for (int k = 0; k < kTsqrMaxCols; ++k) {
@@ -131,9 +90,10 @@ int tsqr_dev(cal_ctx* c, int64_t n, const Panel& W, const double* dM, int m, con
             base += Qout.ncol[sg];
         }
     }
-    auto args = [&](const Level& L, bool down) {
+    auto args = [&](size_t l, bool down) {
+        const TsqrLevelPlan& L = lv[l];
         TsqrLevelArgs a;
-        if (&L == &lv[0]) {
+        if (l == 0) {
             a.V = dV;
             a.tb = dTB;
         }
@@ -141,28 +101,28 @@ int tsqr_dev(cal_ctx* c, int64_t n, const Panel& W, const double* dM, int m, con
         a.m = m;
         a.wp = wp;
         a.M = dM;
-        a.in = L.in;
-        a.out = down ? L.down : L.up;
-        a.S = L.S;
+        a.in = at(L.in);
+        a.out = at(down ? L.down : L.up);
+        a.S = at(L.S);
         a.M2 = dM2;
         a.w2 = w2;
         return a;
     };
     // up the tree
     for (size_t l = 0; l < lv.size(); ++l) {
-        if (P > 1 && l == nlocal) CAL_TRY(allgather(c, lv[nlocal - 1].up, const_cast<double*>(lv[nlocal].in), mm));
+        if (P > 1 && l == nlocal) CAL_TRY(allgather(c, at(lv[nlocal - 1].up), at(lv[nlocal].in), mm));
         const int t = timer_begin(c, l == 0 ? 1 : 3);
-        CAL_HIP(c, launch_tsqr(false, lv[l].src, args(lv[l], false), cols, qo, c->stream));
+        CAL_HIP(c, launch_tsqr(false, lv[l].src, args(l, false), cols, qo, c->stream));
         timer_end(c, t);
     }
     CAL_TRY(ensure_red(c, mm));
-    CAL_HIP(c, hipMemcpyAsync(c->h_red, lv.back().up, mm * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    CAL_HIP(c, hipMemcpyAsync(c->h_red, at(lv.back().up), mm * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     if (!c->orth_event) CAL_HIP(c, hipEventCreateWithFlags(&c->orth_event, hipEventDisableTiming));
     CAL_HIP(c, hipEventRecord(c->orth_event, c->stream));
     // down the tree (queued before the host waits for R)
     for (size_t l = lv.size(); l-- > 0;) {
         const int t = timer_begin(c, l == 0 ? 2 : 3);
-        CAL_HIP(c, launch_tsqr(true, l == 0 ? 3 : lv[l].src, args(lv[l], true), cols, qo, c->stream));
+        CAL_HIP(c, launch_tsqr(true, l == 0 ? 3 : lv[l].src, args(l, true), cols, qo, c->stream));
         timer_end(c, t);
     }
     if (c->pre_wait) {  // e.g. the next step's matrix powers (lanczos_step)

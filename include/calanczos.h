@@ -167,6 +167,7 @@ typedef struct cal_lanczos_info {
     int n_orth_breaks;  /* periodic: full reorthogonalisations; selective: QR rebuilds */
     int n_ritz_locked;  /* selective: converged Ritz vectors in QR               */
     double norm_A;      /* normest(A) (periodic / selective)                    */
+    int n_ritz_complex; /* selective: of n_ritz_locked, members of complex pairs */
 } cal_lanczos_info;
 
 /* [T,Q,rn,oe] = ca_lanczos(A,r,s,iter,basis,orth).           ca_lanczos.m:24-86

@@ -802,3 +802,101 @@ def test_project_and_normalize_wide_block_cholqr(cal, ref, case):
     assert np.max(np.abs(RZ[1] - RZr[1])) <= tol_r * scale
     assert np.max(np.abs(QZ.T @ QZ - np.eye(m))) < 1e-13
     assert np.max(np.abs(QZ.T @ Qp)) < 1e-13
+
+
+def _matlab_extreme(w):
+    """min/max of eig(T) as MATLAB takes them: by modulus once any value is
+    complex (test_ca_lanczos.m:81-82,87-88 print abs(se - min(eig(T))))."""
+    w = np.asarray(w)
+    if np.iscomplexobj(w) and np.any(w.imag != 0):
+        return w[np.argmin(np.abs(w))], w[np.argmax(np.abs(w))]
+    return np.min(w.real), np.max(w.real)
+
+
+@pytest.mark.parametrize("s", [4, 8, 12, 16])
+def test_ca_lanczos_reference_harness(cal, ref, s):
+    """The reference's own known-answer harness: test_convergence_diagonal_
+    matrices.m:9-21 -> test_ca_lanczos.m:32-41 (N = 500, A = diag(linspace(1,
+    100,500)), r = ones, 480 steps, 'periodic', Newton, s = 4, 8, 12, 16).
+    The metric the harness prints (test_ca_lanczos.m:79-98): the relative
+    error of the smallest and largest eigenvalue of T against the known 1 and
+    100 -- below 1e-12 here and within 1e-12 of the oracle's.  Against the
+    oracle: the same periodic break count and reorth flags (both stable under
+    1e-15 relative perturbations of r in the oracle itself), and T within
+    1e-9 ||A|| on the whole 480 x 480 matrix for s = 4, 8 and on the leading
+    blocks where the oracle's own spread stays below 1e-12 ||A|| for s = 12
+    (27 of 40 blocks) and s = 16 (15 of 30)."""
+    import scipy.sparse as sp
+    a = ref.matlab_linspace(1.0, 100.0, 500)
+    A = sp.csr_matrix(sp.diags(a))
+    r = np.ones(500)
+    exp = ref.ca_lanczos(A, r, s, 480, "newton", "periodic", diagnostics=False)
+    out = cal.ca_lanczos_ex(A, r, s, 480, "newton", "periodic", diagnostics=False)
+    assert out.T.shape == exp.T.shape == (480, 480)
+    assert out.info["n_orth_breaks"] == sum(exp.breaks)
+    assert list(out.reorth) == list(exp.reorth)
+    m = {12: 27, 16: 15}.get(s, 480 // s) * s
+    assert np.max(np.abs(out.T[:m, :m] - exp.T[:m, :m])) <= 1e-9 * 100.0
+    lo, hi = _matlab_extreme(np.linalg.eigvals(out.T))
+    elo, ehi = _matlab_extreme(np.linalg.eigvals(exp.T))
+    err = (abs(1.0 - lo) / 1.0, abs(100.0 - hi) / 100.0)
+    eerr = (abs(1.0 - elo) / 1.0, abs(100.0 - ehi) / 100.0)
+    print("s=%d: error in smallest %.3e (oracle %.3e), largest %.3e (oracle %.3e)" % (s, err[0], eerr[0], err[1], eerr[1]))
+    assert max(err) < 1e-12 and max(eerr) < 1e-12
+    assert abs(err[0] - eerr[0]) < 1e-12 and abs(err[1] - eerr[1]) < 1e-12
+
+
+def test_ca_lanczos_selective_complex_pair(cal, ref, monkeypatch):
+    """'selective' locking of a converged complex-conjugate Ritz pair
+    (ca_lanczos.m:317-336: QR(:,nritz) = Q*Vp(:,i) is complex and is
+    normalize'd).  No input reachable here produces one, so both sides get the
+    same test-only perturbation of eig(T) inside the selective update: the two
+    most converged eigenpairs become one conjugate pair 0.5 (w_i + w_j) +-
+    1e-3 i with unit vectors (v_i +- i v_j)/sqrt 2 (the oracle through a
+    monkeypatched matlab_eig -- the Newton prologue's eig left alone -- the
+    device through CAL_TEST_EIG_PAIR).  The device locks the pair as the
+    real span Q Re(v), Q Im(v) of the reference's complex columns.  Bars: the
+    pair is locked (2 complex members at the last rebuild, as in the oracle),
+    the same rebuild count, locked count and reorth flags, T within 1e-8
+    ||A||."""
+    import math
+
+    import scipy.sparse as sp
+    a = ref.matlab_linspace(1.0, 100.0, 500)
+    A = sp.csr_matrix(sp.diags(a))
+    r = np.ones(500)
+    orig, orig_ncb = ref.matlab_eig, ref.newton_change_of_basis
+    active = {"on": True}
+
+    def paired(T):
+        w, V = orig(T)
+        if not active["on"] or np.iscomplexobj(w) or len(w) < 2:
+            return w, V
+        i, j = np.argsort(np.abs(V[-1, :]), kind="stable")[:2]
+        wc, Vc = w.astype(complex), V.astype(complex)
+        vi, vj = V[:, i] / np.linalg.norm(V[:, i]), V[:, j] / np.linalg.norm(V[:, j])
+        wc[i] = complex(0.5 * (w[i] + w[j]), 1.0e-3)
+        wc[j] = np.conj(wc[i])
+        Vc[:, i] = (vi + 1j * vj) / math.sqrt(2.0)
+        Vc[:, j] = (vi - 1j * vj) / math.sqrt(2.0)
+        return wc, Vc
+
+    def ncb(*args, **kw):
+        active["on"] = False
+        try:
+            return orig_ncb(*args, **kw)
+        finally:
+            active["on"] = True
+
+    monkeypatch.setattr(ref, "matlab_eig", paired)
+    monkeypatch.setattr(ref, "newton_change_of_basis", ncb)
+    exp = ref.ca_lanczos(A, r, 8, 160, "newton", "selective", diagnostics=False)
+    monkeypatch.setenv("CAL_TEST_EIG_PAIR", "1")
+    out = cal.ca_lanczos_ex(A, r, 8, 160, "newton", "selective", diagnostics=False)
+    last = max(i for i, b in enumerate(exp.breaks) if b)
+    assert exp.ncomplex[last] == 2
+    assert out.info["n_ritz_complex"] == 2
+    assert out.info["n_orth_breaks"] == sum(exp.breaks)
+    assert out.info["n_ritz_locked"] == exp.nritz[-1]
+    assert list(out.reorth) == list(exp.reorth)
+    assert np.max(np.abs(out.T - exp.T)) <= 1e-8 * 100.0

@@ -297,3 +297,21 @@ def test_selective_locks_complex_pair_by_real_span(ref, monkeypatch):
     assert max(out.nritz) >= 2
     assert out.T.shape == base.T.shape
     assert np.max(np.abs(out.T - out.T.T)) <= 1e-8 * 100.0
+
+
+def test_reference_harness_known_answer(ref):
+    """test_convergence_diagonal_matrices.m:9-21 -> test_ca_lanczos.m:32-41 on
+    the oracle: diag(linspace(1,100,500)), r = ones, 480 steps, 'periodic',
+    Newton, s = 4, 8, 12, 16.  The harness prints the relative error of the
+    extreme eigenvalues of T against the known 1 and 100 (:79-98): below
+    1e-12 for every s, with T 480 x 480 and real spectrum."""
+    import scipy.sparse as sp
+    a = ref.matlab_linspace(1.0, 100.0, 500)
+    A = sp.csr_matrix(sp.diags(a))
+    for s in (4, 8, 12, 16):
+        out = ref.ca_lanczos(A, np.ones(500), s, 480, "newton", "periodic", diagnostics=False)
+        assert out.T.shape == (480, 480)
+        w = np.linalg.eigvals(out.T)
+        assert np.all(w.imag == 0)
+        assert abs(1.0 - w.real.min()) < 1e-12 and abs(100.0 - w.real.max()) / 100.0 < 1e-12
+        assert 0 < sum(out.breaks) < 480 // s
