@@ -491,7 +491,11 @@ def main():
     if args.normalize != "tsqr" and not args.no_legs:
         ctx.set_normalize("tsqr")
         try:  # a secondary leg: a failure is reported in the line, the headline stands
+            f0 = ctx.tsqr_fold_stats()
             tsqr_leg = timed_leg(ctx, r_full[r0:r1], s, min(K, 10), min(W, 2), args.basis, args.orth, dist)
+            f1 = ctx.tsqr_fold_stats()
+            tsqr_leg["fold"] = {"blocks": f1["runs"] - f0["runs"], "declined": f1["declined"] - f0["declined"],
+                                "last_loss_estimate": f1["last_est"]}
         except cal.CalError as e:
             tsqr_leg = {"error": str(e)}
             try:

@@ -80,6 +80,13 @@ class Context:
         check(self.h, lib.cal_mpk_schedule(self.h, ctypes.byref(v)))
         return v.value
 
+    def tsqr_fold_stats(self):
+        """Fused-TSQR projectAndNormalize counters (cal_tsqr_fold_stats):
+        blocks run, blocks declined (explicit-Z path), last estimate."""
+        r, d, e = ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_double()
+        check(self.h, lib.cal_tsqr_fold_stats(self.h, ctypes.byref(r), ctypes.byref(d), ctypes.byref(e)))
+        return dict(runs=r.value, declined=d.value, last_est=e.value)
+
     def set_orth_coef(self, where: str):
         """Run the block-orthogonalisation s x s algebra on the "device"
         (default) or on the "host" (same bits; for testing)."""

@@ -18,10 +18,12 @@
 //    X'X - C'C = ||Y_i||^2), so the pass count follows the reference.
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <vector>
 
 #include "cal_internal.hpp"
+#include "comm.hpp"
 #include "dense.hpp"
 
 namespace cal {
@@ -587,6 +589,202 @@ static int ensure_zbuf(cal_ctx* c, int64_t n, int m, double** p, int64_t* ld) {
     return 0;
 }
 
+// ---- projectAndNormalize with the fused TSQR (tsqr_fold.hip) ---------------
+// One CA block (m <= 8 columns against w <= 9) with no host round trip:
+// P1 Gram -> k_fold_coef0 (C, reorth flag) -> k_fold_up (Y formed, tile QR,
+// in-launch tree, Qp'Y on the matrix cores) -> the Gram reduced -> [several
+// ranks: root all-gather + the global levels] -> k_fold_coef1 (R, RY, S, K;
+// published) -> the tree walked down -> k_fold_down (Q = Q_Y S - Qp K).  The
+// host waits once, for the published R.  Returns 2 when the shape does not
+// apply, 1 when the fold declined after running (||W|| too large, or a
+// non-finite value): the caller then takes the explicit-Z path.
+static bool fold_enabled() {
+    static const int on = [] {
+        const char* e = std::getenv("CAL_TSQR_FOLD");
+        return e ? std::atoi(e) : 1;
+    }();
+    return on != 0;
+}
+
+static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, bool doreorth, const PanelOut& Qout,
+                        double* Rq, double* R, PNResult* res) {
+    const int w = Qp.total, m = X.total, nq = w < 8 ? w : 8;
+    const int P = c->comm ? c->comm->nranks : 1;
+    if (!fold_enabled() || !fold_shape_ok(n, m, w) || Qp.nseg + X.nseg > kMaxSeg || Qout.total != m ||
+        Qout.nseg > kMaxSeg || (int64_t)P * m > 512)
+        return 2;
+    const int me = c->comm ? c->comm->rank : 0;
+    const int64_t n0 = fold_tiles(n), nblk = fold_blocks(n), n1 = fold_l1_tiles(n), n2 = fold_l2_tiles(n);
+    const int64_t mm = (int64_t)m * m;
+    // workspace (doubles): level-0 tiles, then the small levels and scalars
+    const size_t t0 = fold_l0_tile_doubles(), tu = fold_tile_doubles();
+    size_t off = 0;
+    auto take = [&](size_t cnt) {
+        const size_t o = off;
+        off += (cnt + 7) & ~size_t(7);
+        return o;
+    };
+    const size_t oV0 = take(n0 * t0), otb0 = take(n0 * 16), oR0 = take(n0 * 64), oS0 = take(n0 * 64);
+    const size_t oV1 = take(n1 * tu), otb1 = take(n1 * 16), oR1 = take(n1 * 64), oS1 = take(n1 * 64);
+    const size_t oV2 = take(n2 * tu), otb2 = take(n2 * 16), oR2 = take(n2 * 64), oS2 = take(n2 * 64);
+    const size_t oV3 = take(tu), otb3 = take(16);
+    const size_t oRr = take(64), oRrm = take(64), oSb = take(64), oSm = take(64), oK = take(72), oC = take(88);
+    const size_t oOut = take(520), oT1 = take(272), oT2 = take(272);
+    const size_t oG = take((size_t)P * mm), oGup = take(mm), oGdn = take((size_t)P * mm);
+    if (off > c->fold_cap) {
+        if (c->d_fold) CAL_HIP(c, hipFree(c->d_fold));
+        c->d_fold = nullptr;
+        CAL_HIP(c, hipMalloc((void**)&c->d_fold, off * sizeof(double)));
+        c->fold_cap = off;
+    }
+    if ((size_t)n2 + 1 > c->fold_cnt_cap) {
+        if (c->d_fold_cnt) CAL_HIP(c, hipFree(c->d_fold_cnt));
+        c->d_fold_cnt = nullptr;
+        const size_t cap = std::max<size_t>(n2 + 1, 128);
+        CAL_HIP(c, hipMalloc((void**)&c->d_fold_cnt, cap * sizeof(unsigned)));
+        CAL_HIP(c, hipMemsetAsync(c->d_fold_cnt, 0, cap * sizeof(unsigned), c->stream));
+        c->fold_cnt_cap = cap;
+    }
+    double* const F = c->d_fold;
+    double* const d_out = F + oOut;
+    FoldArgs fa;
+    fa.n = n;
+    fa.m = m;
+    fa.w = w;
+    fa.nblk = (int)nblk;
+    fa.n0 = (int)n0;
+    fa.n1 = (int)n1;
+    fa.n2 = (int)n2;
+    fa.C = F + oC;
+    fa.flags = d_out + 512;
+    fa.K = F + oK;
+    fa.V0 = F + oV0;
+    fa.tb0 = F + otb0;
+    fa.R0 = F + oR0;
+    fa.S0 = F + oS0;
+    fa.V1 = F + oV1;
+    fa.tb1 = F + otb1;
+    fa.R1 = F + oR1;
+    fa.S1 = F + oS1;
+    fa.V2 = F + oV2;
+    fa.tb2 = F + otb2;
+    fa.R2 = F + oR2;
+    fa.S2 = F + oS2;
+    fa.V3 = F + oV3;
+    fa.tb3 = F + otb3;
+    fa.Rroot = F + oRr;
+    fa.Rroot_m = F + oRrm;
+    fa.cnt = c->d_fold_cnt;
+    const Panel W = panel_concat(Qp, X);
+    // P1: [Qp(0:nq) | X]' X (+ Qp column 8), the CholQR2 path's row Gram
+    int64_t gblocks = std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, kRowGramBlocks));
+    CAL_TRY(ensure_partial(c, std::max<size_t>((size_t)gblocks * 272, (size_t)nblk * 272)));
+    fa.partial = c->d_partial;
+    {
+        ColList ct{};
+        const Panel T = panel_concat(panel_slice(W, 0, nq), X);
+        const int nt = T.total;
+        for (int cc = 0; cc < 16; ++cc) ct.p[cc] = panel_slice(T, cc < nt ? cc : nt - 1, 1).ptr[0];
+        ct.p[16] = w == 9 ? panel_slice(Qp, 8, 1).ptr[0] : ct.p[0];
+        const int t = timer_begin(c, 1);
+        CAL_HIP(c, launch_rowgram(ct, nt, w == 9, n, (int)gblocks, c->d_partial, c->stream));
+        timer_end(c, t);
+    }
+    CAL_HIP(c, launch_reduce(c->d_partial, (int)gblocks, 272, F + oT1, c->stream));
+    CAL_TRY(allreduce_sum(c, F + oT1, 272));
+    CAL_HIP(c, launch_fold_coef0(F + oT1, F + oC, d_out, w, m, doreorth ? 1 : 0, c->stream));
+    // up: Y, the tile QRs and the tree to the local root, Qp'Y
+    ColList cu{};
+    const double* x0 = panel_slice(X, 0, 1).ptr[0];
+    for (int k = 0; k < 9; ++k) cu.p[k] = k < w ? panel_slice(Qp, k, 1).ptr[0] : x0;
+    for (int j = 0; j < 8; ++j) cu.p[9 + j] = j < m ? panel_slice(X, j, 1).ptr[0] : x0;
+    {
+        const int t = timer_begin(c, 1);
+        CAL_HIP(c, launch_fold_up(cu, fa, c->stream));
+        timer_end(c, t);
+    }
+    {
+        const int t = timer_begin(c, 3);
+        CAL_HIP(c, launch_fold_tree(fa, c->stream));
+        timer_end(c, t);
+    }
+    CAL_HIP(c, launch_fold_reduce(c->d_partial, (int)nblk, F + oT2, c->stream));
+    CAL_TRY(allreduce_sum(c, F + oT2, 272));
+    // the root over the ranks: all-gather the local roots, factor the stack
+    // (the tree kernel's stack level, redundantly on every rank)
+    const double* Rtop = fa.Rroot;
+    int ldr = 8;
+    TsqrLevelArgs ga;
+    TsqrCols gcols{};
+    TsqrQ gq{};
+    if (P > 1) {
+        CAL_TRY(allgather(c, fa.Rroot_m, F + oG, mm));
+        ga.rows = (int64_t)P * m;
+        ga.m = m;
+        ga.wp = m;
+        ga.in = F + oG;
+        ga.out = F + oGup;
+        const int t = timer_begin(c, 3);
+        CAL_HIP(c, launch_tsqr(false, 0, ga, gcols, gq, c->stream));
+        timer_end(c, t);
+        Rtop = F + oGup;
+        ldr = m;
+    }
+    CAL_TRY(ensure_pub(c));
+    const unsigned long long seq = ++c->pub_seq;
+    double* h_out = c->h_pub;
+    unsigned long long* h_seq = reinterpret_cast<unsigned long long*>(c->h_pub + 516);
+    unsigned long long* d_seq = reinterpret_cast<unsigned long long*>(c->d_pub + 516);
+    CAL_HIP(c, launch_fold_coef1(F + oT2, Rtop, ldr, F + oC, d_out, F + oSb, F + oSm, F + oK, w, m,
+                                 (double)global_rows(c, n) * (P > 1 && !c->has_A ? P : 1), c->d_pub, d_seq, seq,
+                                 c->stream));
+    // down: [the global levels,] the group and block levels, level 0
+    const double* Stop = F + oSb;
+    int lds = 8;
+    if (P > 1) {
+        ga.S = F + oSm;
+        ga.out = F + oGdn;
+        const int t = timer_begin(c, 3);
+        CAL_HIP(c, launch_tsqr(true, 0, ga, gcols, gq, c->stream));
+        timer_end(c, t);
+        Stop = F + oGdn + (size_t)me * mm;
+        lds = m;
+    }
+    {
+        const int t = timer_begin(c, 3);
+        CAL_HIP(c, launch_fold_down_tree(fa, Stop, lds, c->stream));
+        timer_end(c, t);
+    }
+    OutList qo{};
+    for (int j = 0; j < 16; ++j) qo.p[j] = panel_out_slice(Qout, j < m ? j : 0, 1).ptr[0];
+    {
+        const int t = timer_begin(c, 2);
+        CAL_HIP(c, launch_fold_down(cu, qo, fa, c->stream));
+        timer_end(c, t);
+    }
+    if (c->pre_wait) {  // e.g. the next step's matrix powers (lanczos_step)
+        auto hook = std::move(c->pre_wait);
+        c->pre_wait = nullptr;
+        CAL_TRY(hook());
+    }
+    CAL_TRY(wait_published(c, h_seq, seq));
+    c->fold_runs++;
+    c->fold_last_est = h_out[515];
+    if (h_out[513] != 0.0) {
+        c->fold_declined++;
+        return 1;
+    }
+    std::copy(h_out, h_out + (size_t)mm, R);
+    std::copy(h_out + 256, h_out + 256 + (size_t)w * m, Rq);
+    const bool reorth = h_out[514] != 0.0;
+    if (res) {
+        res->reorth = reorth;
+        res->rank = rank_from_R(m, R, 1.0e-8);
+        res->chol_shifted = false;
+    }
+    return 0;
+}
+
 // projectAndNormalize.m:3-90 against one block with the Householder TSQR
 // normalize (tsqr.m): C = Qp'X and X'X from one Gram sweep; the reorth test
 // of :45-52 on the algebraic norms ||Y_i||^2 = diag(X'X - C'C); on reorth the
@@ -597,6 +795,12 @@ static int pn_tsqr(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, bool 
                    double* Rq, double* R, PNResult* res) {
     const int w = Qp.total, m = X.total, wp = w + m;
     if (!tsqr_ok(m)) return set_error(c, CAL_ERR_UNSUPPORTED, "projectAndNormalize (tsqr): at most 32 columns");
+    if (w > 0) {
+        const int st = pn_tsqr_fold(c, n, Qp, X, doreorth, Qout, Rq, R, res);
+        CAL_TRY(st);
+        if (st == 0) return 0;
+        if (st == 1) c->orth_redone = true;  // declined after running: the explicit-Z path below
+    }
     const Panel W = panel_concat(Qp, X);
     std::vector<double> G1((size_t)wp * m);
     const int nq = w < 8 ? w : 8;

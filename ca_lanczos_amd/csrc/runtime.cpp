@@ -731,6 +731,8 @@ void cal_destroy(cal_ctx* c) {
     if (c->d_tsqr) hipFree(c->d_tsqr);
     if (c->d_zbuf) hipFree(c->d_zbuf);
     if (c->d_tsqrv) hipFree(c->d_tsqrv);
+    if (c->d_fold) hipFree(c->d_fold);
+    if (c->d_fold_cnt) hipFree(c->d_fold_cnt);
     if (c->h_pub) hipHostFree(c->h_pub);
     if (c->aux_stream) hipStreamDestroy(c->aux_stream);
     hipStreamDestroy(c->stream);
@@ -904,6 +906,14 @@ int cal_set_normalize(cal_ctx* c, const char* kind) {
 int cal_get_normalize(cal_ctx* c, int* kind) {
     if (!c || !kind) return CAL_ERR_ARG;
     *kind = c->normalize_kind;
+    return 0;
+}
+
+int cal_tsqr_fold_stats(cal_ctx* c, long long* runs, long long* declined, double* last_est) {
+    if (!c) return CAL_ERR_ARG;
+    if (runs) *runs = c->fold_runs;
+    if (declined) *declined = c->fold_declined;
+    if (last_est) *last_est = c->fold_last_est;
     return 0;
 }
 

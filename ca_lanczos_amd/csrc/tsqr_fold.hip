@@ -1,0 +1,699 @@
+// tsqr_fold.hip -- projectAndNormalize with the Householder TSQR normalize
+// (projectAndNormalize.m:3-90, normalize.m:14, tsqr.m:7-12) for one CA block
+// (m <= 8 new columns against a previous block Qp of w <= 9 columns), fused
+// into few launches with no host round trip:
+//
+//   P1      [Qp | X]'X on the row Gram sweep (blockorth.cpp) -> k_fold_coef0:
+//           C = Qp'X, the norms-before/after test of :45-52 (reorth flag).
+//   up      k_fold_up: Y = X - Qp C formed per row (project.m:30), the
+//           register-tile Householder QR of Y (256-row tiles, one per wave),
+//           and -- from the same registers -- the Gram [Qp | Y]'[Qp | Y] on
+//           the matrix cores, i.e. the second projection's C2 = Qp'Y (:63).
+//   tree    k_fold_tree: the stacked tile R factors, 64 per 512-row tile,
+//           level by level to the local root in one launch (the last block
+//           of a group takes the next level: an atomic arrival count; no
+//           block ever waits on another).
+//   coef1   k_fold_coef1: Y = Q_Y R_Y from the tree.  With the second
+//           projection Z = Y - Qp C2, Z'Z = Y'Y - C2'C2, so with W = C2 R_Y^-1:
+//           R_Z = U R_Y, U = chol(I - W'W), and Q_Z = Q_Y U^-1 - Qp W U^-1.
+//           The root's S block becomes diag(sign) U^-1 (tsqr.m:9-12's sign fix
+//           folded in) and K = W U^-1 is the down pass's correction.
+//           I - W'W is perfectly conditioned when the first projection did
+//           its job (||W|| << 1): the explicit-Z path (blockorth.cpp pn_tsqr)
+//           is taken instead when ||W||_F > 1/2.  R = R_Z, RY = C + C2
+//           (:71-73), the flag, published to pinned host memory.
+//   down    k_fold_down_top / _l1: the tree walked down (explicit Q factors of
+//           the stored tiles times the parent's S); k_fold_down: level 0,
+//           Q = Q_tile S - Qp K, one store.
+//
+// HBM traffic per block (n rows): P1 (w+m)·8n, up (w+m)·8n + m·8n (the
+// factored tiles), down m·8n (tiles) + w·8n (Qp, only when the second
+// projection runs) + m·8n (Q).  Everything above level 0 is n/64 rows.
+#include "cal_internal.hpp"
+#include "tsqr_tile.hpp"
+
+namespace cal {
+
+namespace {
+
+using namespace tsqr_tile;
+typedef double fd4 __attribute__((ext_vector_type(4)));
+typedef double fd2 __attribute__((ext_vector_type(2)));
+
+constexpr int FM = 8;             // register tile width (m <= 8)
+constexpr int L0RPL = 4;          // rows per lane of a level-0 tile
+constexpr int FTR0 = 64 * L0RPL;  // 256 rows per level-0 tile
+constexpr int FRPL = 8;           // rows per lane of an upper-level tile
+constexpr int FTR = 64 * FRPL;    // 512 rows: 64 R factors of the level below
+constexpr int FTPB = 4;           // tiles (waves) per block
+constexpr int FG = FTR / FM;      // tiles per upper-level tile (64 R factors of m = 8 rows)
+constexpr int FTLD = 17;        // padded LDS row of the Gram transpose
+// timing-probe switches (tools/fold_probe.hip; never set in the library)
+#ifndef FOLD_PROBE
+#define FOLD_PROBE 0
+#endif
+constexpr int kProbe = FOLD_PROBE;  // bit 1: no Gram, 2: no tile QR, 3: no tile store, 4: tree level 1 only
+#ifndef FOLD_UP_WPE
+#define FOLD_UP_WPE 3  // k_fold_up waves per SIMD (VGPR budget 512 / WPE)
+#endif
+constexpr int kFoldXmax = 80;   // st: C at [0, 72), max_j ||X_j|| at 80
+constexpr double kFoldTol = 1e-14;  // largest accepted loss-of-orthogonality estimate
+
+__device__ __forceinline__ fd4 fmfma(double a, double b, fd4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void fwsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// factored register tile <-> lane-contiguous storage (64 doubles per lane slot)
+template <int RPL>
+__device__ __forceinline__ void fstore_tile(double* V, int lane, const double (&x)[RPL][FM]) {
+    double* vt = V + lane;
+#pragma unroll
+    for (int i = 0; i < RPL; ++i)
+#pragma unroll
+        for (int c = 0; c < FM; ++c) vt[(i * FM + c) * 64] = x[i][c];
+}
+template <int RPL>
+__device__ __forceinline__ void fload_tile(const double* V, int lane, double (&x)[RPL][FM]) {
+    const double* vt = V + lane;
+#pragma unroll
+    for (int i = 0; i < RPL; ++i)
+#pragma unroll
+        for (int c = 0; c < FM; ++c) x[i][c] = vt[(i * FM + c) * 64];
+}
+__device__ __forceinline__ void fstore_tb(double* tb, int lane, const double (&tau)[FM], const double (&beta)[FM]) {
+#pragma unroll
+    for (int c = 0; c < FM; ++c)
+        if (lane == c) {
+            tb[c] = tau[c];
+            tb[FM + c] = beta[c];
+        }
+}
+__device__ __forceinline__ void fload_tau(const double* tb, double (&tau)[FM]) {
+#pragma unroll
+    for (int c = 0; c < FM; ++c) tau[c] = tb[c];
+}
+// R of a factored tile (row j in lane j, slot 0) -> an 8 x 8 column-major
+// block (zeros below the diagonal and outside m x m); lanes 0..7 write
+__device__ __forceinline__ void fput_R(double* Rb, int lane, int m, const double (&x0)[FM]) {
+    if (lane < FM) {
+#pragma unroll
+        for (int c = 0; c < FM; ++c) Rb[c * FM + lane] = (lane < m && c >= lane && c < m) ? x0[c] : 0.0;
+    }
+}
+// rows [r0, r0 + 64 RPL) of a stack of R blocks into a register tile: block
+// b holds stack rows 8b .. 8b+7 (its 8 x 8 column-major R; rows >= m are
+// zero, which leaves the R of the stack unchanged), zero past `rows`
+template <int RPL>
+__device__ __forceinline__ void fload_stack(const double* Rs, int64_t r0, int64_t rows, int lane,
+                                            double (&x)[RPL][FM]) {
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+        const int64_t r = r0 + lane + 64 * i;
+        const bool in = r < rows;
+        const double* src = Rs + (in ? (r >> 3) * 64 + (r & 7) : 0);
+#pragma unroll
+        for (int c = 0; c < FM; ++c) {
+            const double v = src[c * FM];
+            x[i][c] = in ? v : 0.0;
+        }
+    }
+}
+// O = Q S for the register rows (S 8 x 8 column-major in LDS, k < m ascending)
+__device__ __forceinline__ void fmul_S(const double (&q)[FM], const double* S, int m, double (&o)[FM]) {
+#pragma unroll
+    for (int c = 0; c < FM; ++c) o[c] = 0.0;
+#pragma unroll
+    for (int k = 0; k < FM; ++k) {
+        if (k < m) {
+            // row k of S read right before use (see k_fold_up's C rows)
+#pragma unroll
+            for (int c = 0; c < FM; ++c) asm volatile("" : "+v"(o[c]));
+#pragma unroll
+            for (int c = 0; c < FM; ++c) {
+                const double u = q[k] * S[k + c * FM];
+                o[c] = o[c] + u;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+// P: column pointers, slots 0..8 the previous block Qp (slots >= w padded
+// with a valid column: their coefficients are zero), slots 9..16 X (slots
+// >= 9 + m padded).  One 256-row tile per wave, 4 independent waves per
+// block (no block-level step: a serial tail would hold the block's slots).
+// Registers are kept under 168 (3 waves per SIMD) so that 12 waves per CU
+// keep their next chunk's 17 column loads in flight.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FOLD_UP_WPE))) void k_fold_up(ColList P, FoldArgs a) {
+    __shared__ double Cs[9 * FM];
+    __shared__ double tl[FTPB][64 * FTLD];  // per-wave Gram transpose; then the block's partials
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int c16 = lane & 15, g = lane >> 4;
+    const int m = a.m, w = a.w, nq = w < 8 ? w : 8;
+    const int64_t n = a.n;
+    const int b = blockIdx.x;
+    for (int e = tid; e < 9 * FM; e += 256) {
+        const int k = e / FM, cc = e % FM;
+        Cs[e] = (k < w && cc < m) ? a.C[k + cc * w] : 0.0;
+    }
+    __syncthreads();
+    const int64_t ntiles = (n + FTR0 - 1) / FTR0;
+    const int64_t tile = (int64_t)b * FTPB + wave;
+    fd4 acc = fd4{0.0, 0.0, 0.0, 0.0};
+    fd4 acc2 = fd4{0.0, 0.0, 0.0, 0.0};
+    if (tile < ntiles) {
+        const int64_t base = tile * FTR0;
+        double x[L0RPL][FM];
+        double tau[FM], beta[FM];
+        double p[17];
+        auto load = [&](int i) {
+            const int64_t r = base + lane + 64 * i;
+            const int64_t rr = r < n ? r : n - 1;  // a valid row; masked below
+#pragma unroll
+            for (int k = 0; k < 17; ++k) p[k] = P.p[k][rr];
+        };
+        load(0);
+#pragma unroll
+        for (int i = 0; i < L0RPL; ++i) {
+            // keep chunk i's loads and LDS traffic inside its iteration (the
+            // scheduler would otherwise hoist every chunk's loads and spill)
+            asm volatile("" ::: "memory");
+            const bool in = base + lane + 64 * i < n;
+            // Y = X - Qp C (project.m:30): the product first, k ascending
+            double t[FM];
+#pragma unroll
+            for (int cc = 0; cc < FM; ++cc) t[cc] = 0.0;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                // one C row per k, read right before use: the pin takes the
+                // accumulators as operands, so row k's FMAs retire before row
+                // k+1's broadcasts issue (otherwise all 72 C values are held)
+#pragma unroll
+                for (int cc = 0; cc < FM; ++cc) asm volatile("" : "+v"(t[cc]));
+#pragma unroll
+                for (int cc = 0; cc < FM; cc += 2) {
+                    const fd2 v = *reinterpret_cast<const fd2*>(&Cs[k * FM + cc]);
+                    t[cc] = __builtin_fma(p[k], v[0], t[cc]);
+                    t[cc + 1] = __builtin_fma(p[k], v[1], t[cc + 1]);
+                }
+            }
+#pragma unroll
+            for (int cc = 0; cc < FM; ++cc) x[i][cc] = (in && cc < m) ? p[9 + cc] - t[cc] : 0.0;
+            // [Qp(0:8) | Y] (+ Qp column 8) through LDS onto the matrix cores
+            double* trow = tl[wave] + lane * FTLD;
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc) trow[cc] = (in && cc < nq) ? p[cc] : 0.0;
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc) trow[8 + cc] = x[i][cc];
+            trow[16] = (in && w > 8) ? p[8] : 0.0;
+            if (i + 1 < L0RPL) load(i + 1);  // the next chunk's loads fly during the Gram
+            fwsync();
+            if (!(kProbe & 2)) {
+#pragma unroll
+                for (int kk = 0; kk < 16; ++kk) {
+                    // tile'tile, and Qp(:,8)'tile as a second MFMA whose A rows
+                    // all hold the extra column (every output row is the same sum)
+                    const int row = 4 * kk + g;
+                    const double av = tl[wave][row * FTLD + c16];
+                    const double ev = tl[wave][row * FTLD + 16];
+                    acc = fmfma(av, av, acc);
+                    acc2 = fmfma(ev, av, acc2);
+                }
+            }
+            fwsync();
+        }
+        if (!(kProbe & 4)) tile_geqr2<FM, L0RPL>(x, tau, beta, m, lane);
+        if (!(kProbe & 8)) fstore_tile<L0RPL>(a.V0 + tile * (64 * L0RPL * FM), lane, x);
+        fstore_tb(a.tb0 + tile * (2 * FM), lane, tau, beta);
+        fput_R(a.R0 + tile * 64, lane, m, x[0]);
+    }
+    __syncthreads();  // the transposes are done (tl is reused below)
+    // the block's Gram partial (entry-major, as k_rowapply's)
+    double* red = &tl[0][0];
+    if (wave > 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[((wave - 1) * 64 + lane) * 5 + r] = acc[r];
+        red[((wave - 1) * 64 + lane) * 5 + 4] = acc2[0];
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const int64_t nb = a.nblk;
+        double* out = a.partial + b;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            double v = acc[r];
+            v = v + red[(0 * 64 + lane) * 5 + r];
+            v = v + red[(1 * 64 + lane) * 5 + r];
+            v = v + red[(2 * 64 + lane) * 5 + r];
+            out[(int64_t)(c16 * 16 + g + 4 * r) * nb] = v;
+        }
+        double e = acc2[0];
+        e = e + red[(0 * 64 + lane) * 5 + 4];
+        e = e + red[(1 * 64 + lane) * 5 + 4];
+        e = e + red[(2 * 64 + lane) * 5 + 4];
+        if (g == 0) out[(int64_t)(256 + c16) * nb] = e;
+    }
+}
+
+// The tree above level 0 (one launch; its blocks never wait on each other):
+// level 1, one 512-row tile (64 tile R factors) per wave; the last block of
+// each 16-block group factors the group's 64 level-1 R factors (level 2);
+// the last level-2 tile's block factors the level-2 stack (the local root,
+// <= 512 rows).  Arrivals are counted with device-scope atomics after an
+// agent-scope release fence -- in this small launch only (in k_fold_up every
+// block's fence would write its XCD's L2 back: 2.8 ms measured).
+__global__ __launch_bounds__(256) void k_fold_tree(FoldArgs a) {
+    __shared__ int sflag;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = a.m;
+    const int t1 = blockIdx.x * FTPB + wave;  // level-1 tile
+    if (t1 < a.n1) {
+        const int64_t rows = (int64_t)((a.n0 - t1 * FG) < FG ? (a.n0 - t1 * FG) : FG) * FM;
+        double x[FRPL][FM], tau[FM], beta[FM];
+        fload_stack<FRPL>(a.R0 + (int64_t)t1 * FG * 64, 0, rows, lane, x);
+        tile_geqr2<FM, FRPL>(x, tau, beta, m, lane);
+        fstore_tile<FRPL>(a.V1 + (int64_t)t1 * (64 * FRPL * FM), lane, x);
+        fstore_tb(a.tb1 + (int64_t)t1 * (2 * FM), lane, tau, beta);
+        fput_R(a.R1 + (int64_t)t1 * 64, lane, m, x[0]);
+    }
+    if (kProbe & 16) return;
+    constexpr int BPG = FG / FTPB;  // blocks per level-2 tile
+    const int t2 = blockIdx.x / BPG;
+    const int gblocks = ((int)gridDim.x - t2 * BPG) < BPG ? ((int)gridDim.x - t2 * BPG) : BPG;
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned old = atomicAdd(&a.cnt[t2], 1u);
+        sflag = old == (unsigned)(gblocks - 1);
+    }
+    __syncthreads();
+    if (!sflag) return;
+    __threadfence();
+    if (wave == 0) {
+        if (lane == 0) a.cnt[t2] = 0u;  // ready for the next call
+        const int64_t rows = (int64_t)((a.n1 - t2 * FG) < FG ? (a.n1 - t2 * FG) : FG) * FM;
+        double x[FRPL][FM], tau[FM], beta[FM];
+        fload_stack<FRPL>(a.R1 + (int64_t)t2 * FG * 64, 0, rows, lane, x);
+        tile_geqr2<FM, FRPL>(x, tau, beta, m, lane);
+        fstore_tile<FRPL>(a.V2 + (int64_t)t2 * (64 * FRPL * FM), lane, x);
+        fstore_tb(a.tb2 + (int64_t)t2 * (2 * FM), lane, tau, beta);
+        fput_R(a.R2 + (int64_t)t2 * 64, lane, m, x[0]);
+    }
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned old = atomicAdd(&a.cnt[a.n2], 1u);
+        sflag = old == (unsigned)(a.n2 - 1);
+    }
+    __syncthreads();
+    if (!sflag) return;
+    __threadfence();
+    if (wave == 0) {
+        if (lane == 0) a.cnt[a.n2] = 0u;
+        double x[FRPL][FM], tau[FM], beta[FM];
+        fload_stack<FRPL>(a.R2, 0, (int64_t)a.n2 * FM, lane, x);
+        tile_geqr2<FM, FRPL>(x, tau, beta, m, lane);
+        fstore_tile<FRPL>(a.V3, lane, x);
+        fstore_tb(a.tb3, lane, tau, beta);
+        fput_R(a.Rroot, lane, m, x[0]);
+        // the same R with leading dimension m (the stack layout of tsqr.hip,
+        // for the all-gather of the local roots over several ranks)
+        if (lane < m)
+            for (int cc = 0; cc < m; ++cc) a.Rroot_m[lane + cc * m] = cc >= lane ? x[0][cc] : 0.0;
+    }
+}
+
+// ---- the s x s algebra --------------------------------------------------
+// Phase 0 (after the P1 Gram tile [Qp(0:nq) | X]'[...] + Qp column 8):
+// C = Qp'X -> st (w x m, ld w); the reorth test of projectAndNormalize.m:
+// 17-22,45-52 on the algebraic norms ||Y_j||^2 = X_j'X_j - C_j'C_j -> out[514].
+__global__ __launch_bounds__(64) void k_fold_coef0(const double* __restrict__ tile, double* __restrict__ st,
+                                                  double* __restrict__ out, int w, int m, int doreorth) {
+    __shared__ double rel[FM], nrm[FM];
+    const int tid = threadIdx.x, nq = w < 8 ? w : 8;
+    for (int e = tid; e < w * m; e += 64) {
+        const int i = e % w, j = e / w;
+        st[e] = i < 8 ? tile[i + (nq + j) * 16] : tile[256 + nq + j];
+    }
+    if (tid < m) {
+        const int j = tid;
+        double cc = 0.0;
+        for (int k = 0; k < w; ++k) {
+            const double v = k < 8 ? tile[k + (nq + j) * 16] : tile[256 + nq + j];
+            cc = cc + v * v;
+        }
+        const double xx = tile[(nq + j) + (nq + j) * 16];
+        const double before = sqrt(xx);
+        const double after = sqrt(fmax(xx - cc, 0.0));
+        rel[j] = fabs(before - after) / before;
+        nrm[j] = before;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double mx = NAN, xmax = 0.0;
+        for (int j = 0; j < m; ++j) {
+            const double r = rel[j];
+            if (!isnan(r) && (isnan(mx) || r > mx)) mx = r;
+            xmax = fmax(xmax, nrm[j]);
+        }
+        st[kFoldXmax] = xmax;
+        out[512] = 0.0;
+        out[513] = 0.0;
+        out[514] = (w > 0 && doreorth && mx > 0.5) ? 1.0 : 0.0;
+    }
+}
+
+// Phase 1 (after the tree, the Gram tile reduced, and on several ranks the
+// global levels): Rtop the root R (ld ldr, raw signs), G the Gram tile
+// [Qp(0:8) | Y]'[...] (+ Qp column 8).  Writes S_top (8 x 8, ld 8; and ld m
+// to Sm), K (9 x 8, ld 9), out (R, RY, flags) and publishes out.  One wave;
+// the 8 x 8 matrices in LDS (column-major, ld 8), entry (r, c) computed by
+// lane r + 8c, triangular inverses by one lane per column.
+__device__ __forceinline__ void finv_col(const double* T, double* Ti, int j, int m) {
+    // column j of T^-1 (T upper, m x m): back substitution, i descending
+    double col[FM];
+#pragma unroll
+    for (int i = FM - 1; i >= 0; --i) {
+        double s = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = i + 1; k < FM; ++k) s = (k <= j) ? s - T[i + k * FM] * col[k] : s;
+        col[i] = (i <= j && j < m) ? s / T[i + i * FM] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) Ti[i + j * FM] = col[i];
+}
+
+__global__ __launch_bounds__(64) void k_fold_coef1(const double* __restrict__ G, const double* __restrict__ Rtop,
+                                                  int ldr, const double* __restrict__ st, double* __restrict__ out,
+                                                  double* __restrict__ Sbuf, double* __restrict__ Sm,
+                                                  double* __restrict__ Kbuf, int w, int m, double nglob,
+                                                  double* __restrict__ hout,
+                                                  unsigned long long* __restrict__ hseq, unsigned long long seq) {
+    __shared__ double RY[64], Ri[64], Ws[9 * FM], U[64], Ui[64], D[FM], red[64];
+    __shared__ int fail;
+    const int lane = threadIdx.x, r = lane & 7, c = lane >> 3;
+    const bool reorth = out[514] != 0.0;
+    const bool in = r < m && c < m;
+    if (lane < FM) {
+        const double rii = lane < m ? Rtop[lane + lane * ldr] : 0.0;
+        D[lane] = rii > 0.0 ? 1.0 : (rii < 0.0 ? -1.0 : 0.0);  // sign(0) = 0 (tsqr.m:9-10)
+    }
+    if (lane == 0) fail = 0;
+    U[lane] = (r == c && r < m) ? 1.0 : 0.0;
+    Ui[lane] = U[lane];
+    __syncthreads();
+    RY[lane] = (in && r <= c) ? D[r] * Rtop[r + c * ldr] : 0.0;  // R_Y = D R
+    __syncthreads();
+    double est = 0.0;
+    if (reorth) {
+        if (lane < FM) finv_col(RY, Ri, lane, m);  // R_Y^-1 (Inf / NaN at a zero pivot)
+        __syncthreads();
+        // W = C2 R_Y^-1 (w x m), C2 = Qp'Y from the Gram tile
+        for (int e = lane; e < 9 * FM; e += 64) {
+            const int i = e % 9, cc = e / 9;
+            double v = 0.0;
+            if (i < w && cc < m)
+                for (int k = 0; k <= cc; ++k) {
+                    const double c2 = i < 8 ? G[i + (8 + k) * 16] : G[256 + 8 + k];
+                    v = v + c2 * Ri[k + cc * FM];
+                }
+            Ws[i + cc * 9] = v;
+        }
+        __syncthreads();
+        // A = I - W'W (entry per lane); ||W||_F^2, ||R_Y^-1||_F^2
+        double a = (r == c && r < m) ? 1.0 : 0.0;
+        if (in)
+            for (int k = 0; k < w; ++k) a = a - Ws[k + r * 9] * Ws[k + c * 9];
+        double nw = Ws[lane] * Ws[lane] + (lane < 8 ? Ws[64 + lane] * Ws[64 + lane] : 0.0);
+        double nri = Ri[lane] * Ri[lane];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            nw = nw + __shfl_xor(nw, o, 64);
+            nri = nri + __shfl_xor(nri, o, 64);
+        }
+        // the fold's loss of orthogonality ~ 2 ||W|| ||E||, E = Qp'Q_Y - W
+        // (the rounding of C2 and of Y's factorization through R_Y^-1):
+        // ||E|| <~ u sqrt(n) max||X_j|| ||R_Y^-1||; decline (explicit Z)
+        // unless that is below kFoldTol and ||W||_F <= 1/2
+        est = 2.0 * sqrt(nw) * 0x1p-53 * sqrt(nglob) * st[kFoldXmax] * sqrt(nri);
+        red[lane] = a;
+        __syncthreads();
+        if (lane == 0) {
+            // U = chol(A) (upper), serially (host dense::chol_upper's order)
+            int bad = !(nw <= 0.25) || !(est <= kFoldTol);  // also NaN / Inf
+            for (int j = 0; j < m && !bad; ++j) {
+                double sj = red[j + j * FM];
+                for (int k = 0; k < j; ++k) sj = sj - U[k + j * FM] * U[k + j * FM];
+                if (!(sj > 0.0) || !isfinite(sj)) {
+                    bad = 1;
+                    break;
+                }
+                const double ujj = sqrt(sj);
+                U[j + j * FM] = ujj;
+                for (int i = j + 1; i < m; ++i) {
+                    double t = red[j + i * FM];
+                    for (int k = 0; k < j; ++k) t = t - U[k + j * FM] * U[k + i * FM];
+                    U[j + i * FM] = t / ujj;
+                }
+            }
+            fail = bad;
+        }
+        __syncthreads();
+        if (!fail && lane < FM) finv_col(U, Ui, lane, m);
+        __syncthreads();
+    }
+    if (lane == 0) {
+        out[513] = fail ? 1.0 : 0.0;
+        out[515] = est;
+    }
+    if (!fail) {
+        // S_top = D U^-1, R_Z = U R_Y
+        const double sv = D[r] * Ui[lane];
+        Sbuf[lane] = sv;
+        if (in) Sm[r + c * m] = sv;
+        double rz = 0.0;
+        for (int k = r; k <= c; ++k) rz = rz + U[r + k * FM] * RY[k + c * FM];
+        if (in) out[r + c * m] = r <= c ? rz : 0.0;
+        // K = W U^-1 (9 x 8, ld 9)
+        for (int e = lane; e < 9 * FM; e += 64) {
+            const int i = e % 9, cc = e / 9;
+            double kv = 0.0;
+            if (reorth)
+                for (int k = 0; k <= cc; ++k) kv = kv + Ws[i + k * 9] * Ui[k + cc * FM];
+            Kbuf[e] = kv;
+        }
+        // RY = C + C2 (projectAndNormalize.m:71-73)
+        for (int e = lane; e < w * m; e += 64) {
+            const int i = e % w, j = e / w;
+            const double c2 = reorth ? (i < 8 ? G[i + (8 + j) * 16] : G[256 + 8 + j]) : 0.0;
+            out[256 + e] = st[e] + c2;
+        }
+    }
+    __syncthreads();
+    if (hout) {
+        for (int e = lane; e < 516; e += 64) hout[e] = out[e];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (lane == 0) {
+            __threadfence_system();
+            __hip_atomic_store(hseq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+// Fixed-order reduction of the up launch's Gram partials (entry-major,
+// nparts per entry): one 1024-thread block per entry; same sum on every run.
+__global__ __launch_bounds__(1024) void k_fold_reduce(const double* __restrict__ part, int nparts,
+                                                     double* __restrict__ outv) {
+    __shared__ double ws[16];
+    const int64_t e = blockIdx.x;
+    const double* p = part + e * nparts;
+    double s = 0.0;
+    for (int i = threadIdx.x; i < nparts; i += 1024) s = s + p[i];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s = s + __shfl_xor(s, o, 64);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) ws[wave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int k = 0; k < 16; ++k) t = t + ws[k];
+        outv[e] = t;
+    }
+}
+
+// ---- down the tree ---------------------------------------------------------
+// Stack row r of a level's input is row r & 7 of R block r >> 3 (rows >= m
+// are zero rows: their Q rows are zero, so the S rows written there are zero).
+// The root's Q factor times S_top (ld lds) -> the level-2 tiles' S blocks.
+__global__ __launch_bounds__(64) void k_fold_down_root(FoldArgs a, const double* __restrict__ Stop, int lds) {
+    __shared__ double Ss[64];
+    const int lane = threadIdx.x, m = a.m;
+    {
+        const int k = lane & 7, cc = lane >> 3;
+        Ss[lane] = (k < m && cc < m) ? Stop[k + cc * lds] : 0.0;
+    }
+    double x[FRPL][FM], tau[FM];
+    fload_tile<FRPL>(a.V3, lane, x);
+    fload_tau(a.tb3, tau);
+    fwsync();
+    tile_org2r<FM, FRPL>(x, tau, m, lane);
+    const int64_t rows = (int64_t)a.n2 * FM;
+#pragma unroll
+    for (int i = 0; i < FRPL; ++i) {
+        const int64_t r = lane + 64 * i;
+        double o[FM];
+        fmul_S(x[i], Ss, m, o);
+        if (r < rows) {
+#pragma unroll
+            for (int cc = 0; cc < FM; ++cc) a.S2[(r >> 3) * 64 + (r & 7) + cc * FM] = o[cc];
+        }
+    }
+}
+
+// One upper level down: one wave per tile of the level (Vl / tbl, S blocks
+// Sl), its Q factor times its S -> the S blocks of the level below (Sb,
+// nb blocks in all).
+__global__ __launch_bounds__(256) void k_fold_down_level(const double* __restrict__ Vl, const double* __restrict__ tbl,
+                                                         const double* __restrict__ Sl, int ntl,
+                                                         double* __restrict__ Sb, int nb, int m) {
+    __shared__ double Ss[FTPB][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int t = blockIdx.x * FTPB + wave;
+    if (t >= ntl) return;  // whole waves; no block-wide sync below
+    Ss[wave][lane] = Sl[(int64_t)t * 64 + lane];
+    double x[FRPL][FM], tau[FM];
+    fload_tile<FRPL>(Vl + (int64_t)t * (64 * FRPL * FM), lane, x);
+    fload_tau(tbl + (int64_t)t * (2 * FM), tau);
+    fwsync();
+    tile_org2r<FM, FRPL>(x, tau, m, lane);
+    const int64_t rows = (int64_t)((nb - t * FG) < FG ? (nb - t * FG) : FG) * FM;
+#pragma unroll
+    for (int i = 0; i < FRPL; ++i) {
+        const int64_t r = lane + 64 * i;
+        double o[FM];
+        fmul_S(x[i], Ss[wave], m, o);
+        if (r < rows) {
+            const int64_t blk = (int64_t)t * FG + (r >> 3);
+#pragma unroll
+            for (int cc = 0; cc < FM; ++cc) Sb[blk * 64 + (r & 7) + cc * FM] = o[cc];
+        }
+    }
+}
+
+// Level 0: Q = Q_tile S - Qp K, one store.  Q: output columns (slots >= m
+// unused); P as in k_fold_up (Qp in slots 0..8).  Independent waves.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_fold_down(ColList P, OutList Q,
+                                                                                           FoldArgs a) {
+    __shared__ double Ss[FTPB][64];
+    __shared__ double Ks[9 * FM];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = a.m, w = a.w;
+    const int64_t n = a.n;
+    const int64_t ntiles = (n + FTR0 - 1) / FTR0;
+    const int64_t tile = (int64_t)blockIdx.x * FTPB + wave;
+    for (int e = tid; e < 9 * FM; e += 256) {
+        const int k = e % 9, cc = e / 9;
+        Ks[e] = (k < w && cc < m) ? a.K[e] : 0.0;
+    }
+    const bool corr = a.flags[2] != 0.0;
+    __syncthreads();
+    if (tile >= ntiles) return;
+    double x[L0RPL][FM], tau[FM];
+    fload_tile<L0RPL>(a.V0 + tile * (64 * L0RPL * FM), lane, x);
+    fload_tau(a.tb0 + tile * (2 * FM), tau);
+    Ss[wave][lane] = a.S0[tile * 64 + lane];
+    fwsync();
+    tile_org2r<FM, L0RPL>(x, tau, m, lane);
+    const int64_t base = tile * FTR0;
+    double q[9];
+    auto loadq = [&](int i) {
+        const int64_t r = base + lane + 64 * i;
+        const int64_t rr = r < n ? r : n - 1;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) q[k] = P.p[k][rr];
+    };
+    if (corr) loadq(0);
+#pragma unroll
+    for (int i = 0; i < L0RPL; ++i) {
+        asm volatile("" ::: "memory");
+        double o[FM];
+        fmul_S(x[i], Ss[wave], m, o);
+        if (corr) {
+            double t[FM];
+#pragma unroll
+            for (int cc = 0; cc < FM; ++cc) t[cc] = 0.0;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+#pragma unroll
+                for (int cc = 0; cc < FM; ++cc) asm volatile("" : "+v"(t[cc]));
+#pragma unroll
+                for (int cc = 0; cc < FM; ++cc) t[cc] = __builtin_fma(q[k], Ks[k + cc * 9], t[cc]);
+            }
+            if (i + 1 < L0RPL) loadq(i + 1);
+#pragma unroll
+            for (int cc = 0; cc < FM; ++cc) o[cc] = o[cc] - t[cc];
+        }
+        const int64_t r = base + lane + 64 * i;
+        if (r < n) {
+#pragma unroll
+            for (int cc = 0; cc < FM; ++cc)
+                if (cc < m) Q.p[cc][r] = o[cc];
+        }
+    }
+}
+
+int fold_tiles(int64_t n) { return (int)((n + FTR0 - 1) / FTR0); }
+int fold_blocks(int64_t n) { return (fold_tiles(n) + FTPB - 1) / FTPB; }
+int fold_l1_tiles(int64_t n) { return (fold_tiles(n) + FG - 1) / FG; }
+int fold_l2_tiles(int64_t n) { return (fold_l1_tiles(n) + FG - 1) / FG; }
+bool fold_shape_ok(int64_t n, int m, int w) {
+    if (n < 1 || m < 1 || m > FM || w < 1 || w > 9) return false;
+    return fold_l2_tiles(n) <= FG;  // the root stack fits one 512-row tile (n <= 67M rows)
+}
+size_t fold_l0_tile_doubles() { return (size_t)64 * L0RPL * FM; }
+size_t fold_tile_doubles() { return (size_t)64 * FRPL * FM; }
+
+hipError_t launch_fold_up(const ColList& P, const FoldArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(k_fold_up, dim3(a.nblk), dim3(256), 0, st, P, a);
+    return hipGetLastError();
+}
+hipError_t launch_fold_tree(const FoldArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(k_fold_tree, dim3((a.n1 + FTPB - 1) / FTPB), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_fold_reduce(const double* partial, int nparts, double* outv, hipStream_t st) {
+    hipLaunchKernelGGL(k_fold_reduce, dim3(272), dim3(1024), 0, st, partial, nparts, outv);
+    return hipGetLastError();
+}
+hipError_t launch_fold_coef0(const double* tile, double* stc, double* out, int w, int m, int doreorth,
+                             hipStream_t st) {
+    hipLaunchKernelGGL(k_fold_coef0, dim3(1), dim3(64), 0, st, tile, stc, out, w, m, doreorth);
+    return hipGetLastError();
+}
+hipError_t launch_fold_coef1(const double* G, const double* Rtop, int ldr, const double* stc, double* out,
+                             double* Sbuf, double* Sm, double* Kbuf, int w, int m, double nglob, double* hout,
+                             unsigned long long* hseq, unsigned long long seq, hipStream_t st) {
+    hipLaunchKernelGGL(k_fold_coef1, dim3(1), dim3(64), 0, st, G, Rtop, ldr, stc, out, Sbuf, Sm, Kbuf, w, m, nglob,
+                       hout, hseq, seq);
+    return hipGetLastError();
+}
+hipError_t launch_fold_down_tree(const FoldArgs& a, const double* Stop, int lds, hipStream_t st) {
+    hipLaunchKernelGGL(k_fold_down_root, dim3(1), dim3(64), 0, st, a, Stop, lds);
+    hipLaunchKernelGGL(k_fold_down_level, dim3((a.n2 + FTPB - 1) / FTPB), dim3(256), 0, st, a.V2, a.tb2, a.S2, a.n2,
+                       a.S1, a.n1, a.m);
+    hipLaunchKernelGGL(k_fold_down_level, dim3((a.n1 + FTPB - 1) / FTPB), dim3(256), 0, st, a.V1, a.tb1, a.S1, a.n1,
+                       a.S0, a.n0, a.m);
+    return hipGetLastError();
+}
+hipError_t launch_fold_down(const ColList& P, const OutList& Q, const FoldArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(k_fold_down, dim3(a.nblk), dim3(256), 0, st, P, Q, a);
+    return hipGetLastError();
+}
+
+}  // namespace cal

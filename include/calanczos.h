@@ -110,6 +110,12 @@ int cal_set_orth_coef(cal_ctx* ctx, const char* where);
  * Householder TSQR.  get: 0 auto, 1 tsqr, 2 cholqr2. */
 int cal_set_normalize(cal_ctx* ctx, const char* kind);
 int cal_get_normalize(cal_ctx* ctx, int* kind);
+/* Counters of the fused TSQR projectAndNormalize (Householder TSQR of Y with
+ * the second projection folded into the R factor; blockorth.cpp
+ * pn_tsqr_fold): blocks run, blocks declined (the explicit-Z TSQR path was
+ * taken because the fold's loss-of-orthogonality estimate exceeded 1e-14),
+ * and the last block's estimate.  Any pointer may be null. */
+int cal_tsqr_fold_stats(cal_ctx* ctx, long long* runs, long long* declined, double* last_est);
 /* Device-resident SpMV timing: `reps` launches of y = (A - shift I) x on
  * HBM-resident vectors (x = ones), HIP events around each launch on the
  * context stream; returns the mean and the minimum kernel time. */

@@ -1,0 +1,126 @@
+// Probe: the fused-TSQR kernels (ca_lanczos_amd/csrc/tsqr_fold.hip) at the
+// bench's shape (n = 215^3 rows, Qp 9 columns, X 8 columns), timed with HIP
+// events, with FOLD_PROBE switching parts of k_fold_up off (see kProbe).
+// Not part of the library.  Build (one binary per switch value):
+//   hipcc -O3 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -Iinclude \
+//     -mllvm -pragma-unroll-threshold=4000000 -DFOLD_PROBE=<bits> tools/fold_probe.hip -o tools/fold_probe_<bits>
+#include "../ca_lanczos_amd/csrc/tsqr_fold.hip"
+
+#include <cstdio>
+#include <vector>
+
+#define CK(x)                                                                      \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) {                                                    \
+            printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__);           \
+            return 1;                                                              \
+        }                                                                          \
+    } while (0)
+
+__global__ void k_fill(double* p, int64_t cnt, unsigned long long seed, double scale) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * 256) {
+        unsigned long long z = (unsigned long long)i * 0x9E3779B97F4A7C15ull + seed;
+        z ^= z >> 31;
+        z *= 0xBF58476D1CE4E5B9ull;
+        z ^= z >> 29;
+        p[i] = scale * ((double)(z >> 11) * 0x1p-53 - 0.5);
+    }
+}
+
+int main(int argc, char** argv) {
+    using namespace cal;
+    const int64_t n = 9938375;
+    const int m = 8, w = 9, reps = 10;
+    const int64_t ld = (n + 63) / 64 * 64;
+    double *P, *Q, *F;
+    CK(hipMalloc((void**)&P, (size_t)17 * ld * sizeof(double)));
+    CK(hipMalloc((void**)&Q, (size_t)8 * ld * sizeof(double)));
+    const int64_t n0 = fold_tiles(n), nblk = fold_blocks(n), n1 = fold_l1_tiles(n), n2 = fold_l2_tiles(n);
+    size_t off = 0;
+    auto take = [&](size_t cnt) {
+        const size_t o = off;
+        off += (cnt + 7) & ~size_t(7);
+        return o;
+    };
+    const size_t t0 = fold_l0_tile_doubles(), tu = fold_tile_doubles();
+    const size_t oV0 = take(n0 * t0), otb0 = take(n0 * 16), oR0 = take(n0 * 64), oS0 = take(n0 * 64);
+    const size_t oV1 = take(n1 * tu), otb1 = take(n1 * 16), oR1 = take(n1 * 64), oS1 = take(n1 * 64);
+    const size_t oV2 = take(n2 * tu), otb2 = take(n2 * 16), oR2 = take(n2 * 64), oS2 = take(n2 * 64);
+    const size_t oV3 = take(tu), otb3 = take(16);
+    const size_t oRr = take(64), oRrm = take(64), oK = take(72), oC = take(88), oOut = take(520),
+                 oPart = take((size_t)272 * nblk);
+    CK(hipMalloc((void**)&F, off * sizeof(double)));
+    unsigned* cnt;
+    CK(hipMalloc((void**)&cnt, 128 * sizeof(unsigned)));
+    CK(hipMemset(cnt, 0, 128 * sizeof(unsigned)));
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, P, (int64_t)17 * ld, 1ull, 1.0);
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, F, (int64_t)off, 7ull, 0.2);
+    CK(hipDeviceSynchronize());
+    std::vector<double> flags(520, 0.0);
+    flags[514] = 1.0;
+    CK(hipMemcpy(F + oOut, flags.data(), 520 * sizeof(double), hipMemcpyHostToDevice));
+    FoldArgs fa;
+    fa.n = n;
+    fa.m = m;
+    fa.w = w;
+    fa.nblk = (int)nblk;
+    fa.n0 = (int)n0;
+    fa.n1 = (int)n1;
+    fa.n2 = (int)n2;
+    fa.C = F + oC;
+    fa.flags = F + oOut + 512;
+    fa.K = F + oK;
+    fa.V0 = F + oV0;
+    fa.tb0 = F + otb0;
+    fa.R0 = F + oR0;
+    fa.S0 = F + oS0;
+    fa.V1 = F + oV1;
+    fa.tb1 = F + otb1;
+    fa.R1 = F + oR1;
+    fa.S1 = F + oS1;
+    fa.V2 = F + oV2;
+    fa.tb2 = F + otb2;
+    fa.R2 = F + oR2;
+    fa.S2 = F + oS2;
+    fa.V3 = F + oV3;
+    fa.tb3 = F + otb3;
+    fa.Rroot = F + oRr;
+    fa.Rroot_m = F + oRrm;
+    fa.partial = F + oPart;
+    fa.cnt = cnt;
+    ColList cu{};
+    for (int k = 0; k < 17; ++k) cu.p[k] = P + (size_t)k * ld;
+    OutList qo{};
+    for (int j = 0; j < 16; ++j) qo.p[j] = Q + (size_t)(j < 8 ? j : 0) * ld;
+    hipStream_t st;
+    CK(hipStreamCreate(&st));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    auto timeit = [&](const char* name, double bytes, auto&& launch) -> int {
+        for (int i = 0; i < 2; ++i) CK(launch());
+        float tot = 0.0f, mn = 1e30f;
+        for (int i = 0; i < reps; ++i) {
+            CK(hipEventRecord(a, st));
+            CK(launch());
+            CK(hipEventRecord(b, st));
+            CK(hipEventSynchronize(b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            tot += ms;
+            mn = ms < mn ? ms : mn;
+        }
+        const double avg = tot / reps;
+        printf("probe=%d wpe=%d %-10s avg %8.1f us  min %8.1f us  %6.2f TB/s (algorithmic %.3f GB)\n", FOLD_PROBE, FOLD_UP_WPE, name,
+               avg * 1e3, mn * 1e3, bytes / (avg * 1e-3) / 1e12, bytes / 1e9);
+        return 0;
+    };
+    const double b_up = 25.0 * 8.0 * n, b_down = 25.0 * 8.0 * n;
+    if (timeit("up", b_up, [&] { return launch_fold_up(cu, fa, st); })) return 1;
+    if (timeit("tree", 0.0, [&] { return launch_fold_tree(fa, st); })) return 1;
+    if (timeit("down_tree", 0.0, [&] { return launch_fold_down_tree(fa, F + oRr, 8, st); })) return 1;
+    if (timeit("down", b_down, [&] { return launch_fold_down(cu, qo, fa, st); })) return 1;
+    CK(hipDeviceSynchronize());
+    return 0;
+}
