@@ -591,9 +591,9 @@ static int ensure_zbuf(cal_ctx* c, int64_t n, int m, double** p, int64_t* ld) {
 
 // ---- projectAndNormalize with the fused TSQR (tsqr_fold.hip) ---------------
 // One CA block (m <= 8 columns against w <= 9) with no host round trip:
-// P1 Gram -> k_fold_coef0 (C, reorth flag) -> k_fold_up (Y formed, tile QR,
-// in-launch tree, Qp'Y on the matrix cores) -> the Gram reduced -> [several
-// ranks: root all-gather + the global levels] -> k_fold_coef1 (R, RY, S, K;
+// P1 Gram (C = Qp'X) -> k_fold_up (Y formed, tile QR, Qp'Y on the matrix
+// cores) -> the tree up -> the Gram reduced -> [several ranks: root
+// all-gather + the global levels] -> k_fold_coef1 (reorth flag, R, RY, S, K;
 // published) -> the tree walked down -> k_fold_down (Q = Q_Y S - Qp K).  The
 // host waits once, for the published R.  Returns 2 when the shape does not
 // apply, 1 when the fold declined after running (||W|| too large, or a
@@ -602,6 +602,16 @@ static bool fold_enabled() {
     static const int on = [] {
         const char* e = std::getenv("CAL_TSQR_FOLD");
         return e ? std::atoi(e) : 1;
+    }();
+    return on != 0;
+}
+
+// CAL_TSQR_REFORM=1: the down pass re-forms and refactors each level-0 tile
+// instead of reloading the factored tile the up pass stored
+static bool fold_reform() {
+    static const int on = [] {
+        const char* e = std::getenv("CAL_TSQR_REFORM");
+        return e ? std::atoi(e) : 0;
     }();
     return on != 0;
 }
@@ -628,7 +638,7 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
     const size_t oV1 = take(n1 * tu), otb1 = take(n1 * 16), oR1 = take(n1 * 64), oS1 = take(n1 * 64);
     const size_t oV2 = take(n2 * tu), otb2 = take(n2 * 16), oR2 = take(n2 * 64), oS2 = take(n2 * 64);
     const size_t oV3 = take(tu), otb3 = take(16);
-    const size_t oRr = take(64), oRrm = take(64), oSb = take(64), oSm = take(64), oK = take(72), oC = take(88);
+    const size_t oRr = take(64), oRrm = take(64), oSb = take(64), oSm = take(64), oK = take(72);
     const size_t oOut = take(520), oT1 = take(272), oT2 = take(272);
     const size_t oG = take((size_t)P * mm), oGup = take(mm), oGdn = take((size_t)P * mm);
     if (off > c->fold_cap) {
@@ -636,14 +646,6 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
         c->d_fold = nullptr;
         CAL_HIP(c, hipMalloc((void**)&c->d_fold, off * sizeof(double)));
         c->fold_cap = off;
-    }
-    if ((size_t)n2 + 1 > c->fold_cnt_cap) {
-        if (c->d_fold_cnt) CAL_HIP(c, hipFree(c->d_fold_cnt));
-        c->d_fold_cnt = nullptr;
-        const size_t cap = std::max<size_t>(n2 + 1, 128);
-        CAL_HIP(c, hipMalloc((void**)&c->d_fold_cnt, cap * sizeof(unsigned)));
-        CAL_HIP(c, hipMemsetAsync(c->d_fold_cnt, 0, cap * sizeof(unsigned), c->stream));
-        c->fold_cnt_cap = cap;
     }
     double* const F = c->d_fold;
     double* const d_out = F + oOut;
@@ -655,10 +657,10 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
     fa.n0 = (int)n0;
     fa.n1 = (int)n1;
     fa.n2 = (int)n2;
-    fa.C = F + oC;
+    fa.C = F + oT1;
     fa.flags = d_out + 512;
     fa.K = F + oK;
-    fa.V0 = F + oV0;
+    fa.V0 = fold_reform() ? nullptr : F + oV0;
     fa.tb0 = F + otb0;
     fa.R0 = F + oR0;
     fa.S0 = F + oS0;
@@ -674,7 +676,6 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
     fa.tb3 = F + otb3;
     fa.Rroot = F + oRr;
     fa.Rroot_m = F + oRrm;
-    fa.cnt = c->d_fold_cnt;
     const Panel W = panel_concat(Qp, X);
     // P1: [Qp(0:nq) | X]' X (+ Qp column 8), the CholQR2 path's row Gram
     int64_t gblocks = std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, kRowGramBlocks));
@@ -692,7 +693,6 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
     }
     CAL_HIP(c, launch_reduce(c->d_partial, (int)gblocks, 272, F + oT1, c->stream));
     CAL_TRY(allreduce_sum(c, F + oT1, 272));
-    CAL_HIP(c, launch_fold_coef0(F + oT1, F + oC, d_out, w, m, doreorth ? 1 : 0, c->stream));
     // up: Y, the tile QRs and the tree to the local root, Qp'Y
     ColList cu{};
     const double* x0 = panel_slice(X, 0, 1).ptr[0];
@@ -735,9 +735,9 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
     double* h_out = c->h_pub;
     unsigned long long* h_seq = reinterpret_cast<unsigned long long*>(c->h_pub + 516);
     unsigned long long* d_seq = reinterpret_cast<unsigned long long*>(c->d_pub + 516);
-    CAL_HIP(c, launch_fold_coef1(F + oT2, Rtop, ldr, F + oC, d_out, F + oSb, F + oSm, F + oK, w, m,
-                                 (double)global_rows(c, n) * (P > 1 && !c->has_A ? P : 1), c->d_pub, d_seq, seq,
-                                 c->stream));
+    CAL_HIP(c, launch_fold_coef1(F + oT1, F + oT2, Rtop, ldr, d_out, F + oSb, F + oSm, F + oK, w, m,
+                                 doreorth ? 1 : 0, (double)global_rows(c, n) * (P > 1 && !c->has_A ? P : 1),
+                                 c->d_pub, d_seq, seq, c->stream));
     // down: [the global levels,] the group and block levels, level 0
     const double* Stop = F + oSb;
     int lds = 8;

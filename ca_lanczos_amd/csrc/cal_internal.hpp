@@ -315,13 +315,12 @@ hipError_t launch_tsqr(bool down, int src, const TsqrLevelArgs& a, const TsqrCol
 // 256 rows: factored tiles V0 / tau-beta tb0, R factors R0, S blocks S0),
 // level 1 (n1 tiles of 64 level-0 R factors: V1 / tb1 / R1 / S1), level 2
 // (n2 tiles: V2 / tb2 / R2 / S2) and the root (V3 / tb3; Rroot, and Rroot_m with
-// ld m); the coefficients C (w x m), K (9 x 8), the flags (out[512..515]),
-// the Gram partials (272 x nblk, entry-major) and the tree launch's arrival
-// counters (n2 + 1, self-resetting).
+// ld m); the P1 tile C, K (9 x 8), the flags (out[512..515]) and the Gram
+// partials (272 x nblk, entry-major).
 struct FoldArgs {
     int64_t n = 0;
     int m = 0, w = 0, nblk = 0, n0 = 0, n1 = 0, n2 = 0;
-    const double* C = nullptr;
+    const double* C = nullptr;  // the reduced P1 tile (272 doubles): C = Qp'X is read from it
     const double* flags = nullptr;
     const double* K = nullptr;
     double *V0 = nullptr, *tb0 = nullptr, *R0 = nullptr, *S0 = nullptr;
@@ -329,7 +328,6 @@ struct FoldArgs {
     double *V2 = nullptr, *tb2 = nullptr, *R2 = nullptr, *S2 = nullptr;
     double *V3 = nullptr, *tb3 = nullptr, *Rroot = nullptr, *Rroot_m = nullptr;
     double* partial = nullptr;
-    unsigned* cnt = nullptr;
 };
 int fold_tiles(int64_t n);     // level-0 tiles
 int fold_blocks(int64_t n);    // k_fold_up / k_fold_down blocks
@@ -338,14 +336,15 @@ int fold_l2_tiles(int64_t n);
 bool fold_shape_ok(int64_t n, int m, int w);
 size_t fold_l0_tile_doubles();  // one level-0 tile
 size_t fold_tile_doubles();     // one upper-level tile
-hipError_t launch_fold_coef0(const double* tile, double* stc, double* out, int w, int m, int doreorth,
-                             hipStream_t st);
 hipError_t launch_fold_up(const ColList& P, const FoldArgs& a, hipStream_t st);
-hipError_t launch_fold_tree(const FoldArgs& a, hipStream_t st);
+hipError_t launch_fold_tree(const FoldArgs& a, hipStream_t st);  // levels 1, 2 and the root
 hipError_t launch_fold_reduce(const double* partial, int nparts, double* out, hipStream_t st);  // 272 entries
-hipError_t launch_fold_coef1(const double* G, const double* Rtop, int ldr, const double* stc, double* out,
-                             double* Sbuf, double* Sm, double* Kbuf, int w, int m, double nglob, double* hout,
-                             unsigned long long* hseq, unsigned long long seq, hipStream_t st);
+// k_fold_coef1: T1 the reduced P1 tile, G the up launch's Gram tile, Rtop the
+// root R (ld ldr); writes out (R, RY, flags), S_top (Sbuf ld 8, Sm ld m), K
+// and publishes R / RY / flags to hout, then seq to *hseq
+hipError_t launch_fold_coef1(const double* T1, const double* G, const double* Rtop, int ldr, double* out,
+                             double* Sbuf, double* Sm, double* Kbuf, int w, int m, int doreorth, double nglob,
+                             double* hout, unsigned long long* hseq, unsigned long long seq, hipStream_t st);
 hipError_t launch_fold_down_tree(const FoldArgs& a, const double* Stop, int lds, hipStream_t st);
 hipError_t launch_fold_down(const ColList& P, const OutList& Q, const FoldArgs& a, hipStream_t st);
 
@@ -423,8 +422,6 @@ struct cal_ctx {
     size_t zbuf_cap = 0;
     double* d_fold = nullptr;  // fused TSQR workspace (blockorth.cpp pn_tsqr_fold)
     size_t fold_cap = 0;
-    unsigned* d_fold_cnt = nullptr;  // its arrival counters
-    size_t fold_cnt_cap = 0;
     long fold_runs = 0, fold_declined = 0;  // fused-TSQR blocks run / declined (explicit-Z path taken)
     double fold_last_est = 0.0;             // the last block's loss-of-orthogonality estimate
 };

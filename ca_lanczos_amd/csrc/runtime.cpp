@@ -732,7 +732,6 @@ void cal_destroy(cal_ctx* c) {
     if (c->d_zbuf) hipFree(c->d_zbuf);
     if (c->d_tsqrv) hipFree(c->d_tsqrv);
     if (c->d_fold) hipFree(c->d_fold);
-    if (c->d_fold_cnt) hipFree(c->d_fold_cnt);
     if (c->h_pub) hipHostFree(c->h_pub);
     if (c->aux_stream) hipStreamDestroy(c->aux_stream);
     hipStreamDestroy(c->stream);

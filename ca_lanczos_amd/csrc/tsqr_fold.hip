@@ -3,16 +3,15 @@
 // (m <= 8 new columns against a previous block Qp of w <= 9 columns), fused
 // into few launches with no host round trip:
 //
-//   P1      [Qp | X]'X on the row Gram sweep (blockorth.cpp) -> k_fold_coef0:
-//           C = Qp'X, the norms-before/after test of :45-52 (reorth flag).
+//   P1      [Qp | X]'X on the row Gram sweep (blockorth.cpp): C = Qp'X (read
+//           by k_fold_up straight from the reduced tile) and the norms of
+//           the reorth test of :45-52 (evaluated in k_fold_coef1).
 //   up      k_fold_up: Y = X - Qp C formed per row (project.m:30), the
 //           register-tile Householder QR of Y (256-row tiles, one per wave),
 //           and -- from the same registers -- the Gram [Qp | Y]'[Qp | Y] on
 //           the matrix cores, i.e. the second projection's C2 = Qp'Y (:63).
 //   tree    k_fold_tree: the stacked tile R factors, 64 per 512-row tile,
-//           level by level to the local root in one launch (the last block
-//           of a group takes the next level: an atomic arrival count; no
-//           block ever waits on another).
+//           level by level to the local root (one block per tile).
 //   coef1   k_fold_coef1: Y = Q_Y R_Y from the tree.  With the second
 //           projection Z = Y - Qp C2, Z'Z = Y'Y - C2'C2, so with W = C2 R_Y^-1:
 //           R_Z = U R_Y, U = chol(I - W'W), and Q_Z = Q_Y U^-1 - Qp W U^-1.
@@ -22,7 +21,7 @@
 //           its job (||W|| << 1): the explicit-Z path (blockorth.cpp pn_tsqr)
 //           is taken instead when ||W||_F > 1/2.  R = R_Z, RY = C + C2
 //           (:71-73), the flag, published to pinned host memory.
-//   down    k_fold_down_top / _l1: the tree walked down (explicit Q factors of
+//   down    k_fold_down_root / _level: the tree walked down (explicit Q factors of
 //           the stored tiles times the parent's S); k_fold_down: level 0,
 //           Q = Q_tile S - Qp K, one store.
 //
@@ -56,7 +55,6 @@ constexpr int kProbe = FOLD_PROBE;  // bit 1: no Gram, 2: no tile QR, 3: no tile
 #ifndef FOLD_UP_WPE
 #define FOLD_UP_WPE 3  // k_fold_up waves per SIMD (VGPR budget 512 / WPE)
 #endif
-constexpr int kFoldXmax = 80;   // st: C at [0, 72), max_j ||X_j|| at 80
 constexpr double kFoldTol = 1e-14;  // largest accepted loss-of-orthogonality estimate
 
 __device__ __forceinline__ fd4 fmfma(double a, double b, fd4 c) {
@@ -145,6 +143,77 @@ __device__ __forceinline__ void fmul_S(const double (&q)[FM], const double* S, i
 
 }  // namespace
 
+// Level-0 tile formation (256 rows, chunk i = rows base + lane + 64 i):
+// Y = X - Qp C (project.m:30; the product first, k ascending) into the
+// register tile x; with GRAM also [Qp(0:8) | Y] (+ Qp column 8) through the
+// wave's LDS rows tlw onto the matrix cores (acc: the 16 x 16 Gram, acc2:
+// Qp(:,8)'[...]).  k_fold_up and k_fold_down_reform run the same code on the
+// same inputs, so the tile QR that follows gives the same reflectors in both.
+template <bool GRAM>
+__device__ __forceinline__ void fform(const ColList P, const double* Cs, double* tlw, int64_t base, int64_t n,
+                                      int lane, int m, int w, double (&x)[L0RPL][FM], fd4& acc, fd4& acc2) {
+    const int c16 = lane & 15, g = lane >> 4, nq = w < 8 ? w : 8;
+    double p[17];
+    auto load = [&](int i) {
+        const int64_t r = base + lane + 64 * i;
+        const int64_t rr = r < n ? r : n - 1;  // a valid row; masked below
+#pragma unroll
+        for (int k = 0; k < 17; ++k) p[k] = P.p[k][rr];
+    };
+    load(0);
+#pragma unroll
+    for (int i = 0; i < L0RPL; ++i) {
+        // keep chunk i's loads and LDS traffic inside its iteration (the
+        // scheduler would otherwise hoist every chunk's loads and spill)
+        asm volatile("" ::: "memory");
+        const bool in = base + lane + 64 * i < n;
+        double t[FM];
+#pragma unroll
+        for (int cc = 0; cc < FM; ++cc) t[cc] = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            // one C row per k, read right before use: the pin takes the
+            // accumulators as operands, so row k's FMAs retire before row
+            // k+1's broadcasts issue (otherwise all 72 C values are held)
+#pragma unroll
+            for (int cc = 0; cc < FM; ++cc) asm volatile("" : "+v"(t[cc]));
+#pragma unroll
+            for (int cc = 0; cc < FM; cc += 2) {
+                const fd2 v = *reinterpret_cast<const fd2*>(&Cs[k * FM + cc]);
+                t[cc] = __builtin_fma(p[k], v[0], t[cc]);
+                t[cc + 1] = __builtin_fma(p[k], v[1], t[cc + 1]);
+            }
+        }
+#pragma unroll
+        for (int cc = 0; cc < FM; ++cc) x[i][cc] = (in && cc < m) ? p[9 + cc] - t[cc] : 0.0;
+        if (GRAM) {
+            double* trow = tlw + lane * FTLD;
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc) trow[cc] = (in && cc < nq) ? p[cc] : 0.0;
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc) trow[8 + cc] = x[i][cc];
+            trow[16] = (in && w > 8) ? p[8] : 0.0;
+        }
+        if (i + 1 < L0RPL) load(i + 1);  // the next chunk's loads fly during the Gram
+        if (GRAM) {
+            fwsync();
+            if (!(kProbe & 2)) {
+#pragma unroll
+                for (int kk = 0; kk < 16; ++kk) {
+                    // tile'tile, and Qp(:,8)'tile as a second MFMA whose A rows
+                    // all hold the extra column (every output row is the same sum)
+                    const int row = 4 * kk + g;
+                    const double av = tlw[row * FTLD + c16];
+                    const double ev = tlw[row * FTLD + 16];
+                    acc = fmfma(av, av, acc);
+                    acc2 = fmfma(ev, av, acc2);
+                }
+            }
+            fwsync();
+        }
+    }
+}
+
 // P: column pointers, slots 0..8 the previous block Qp (slots >= w padded
 // with a valid column: their coefficients are zero), slots 9..16 X (slots
 // >= 9 + m padded).  One 256-row tile per wave, 4 independent waves per
@@ -156,12 +225,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FOLD_UP_WPE
     __shared__ double tl[FTPB][64 * FTLD];  // per-wave Gram transpose; then the block's partials
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int c16 = lane & 15, g = lane >> 4;
-    const int m = a.m, w = a.w, nq = w < 8 ? w : 8;
+    const int m = a.m, w = a.w;
     const int64_t n = a.n;
     const int b = blockIdx.x;
-    for (int e = tid; e < 9 * FM; e += 256) {
-        const int k = e / FM, cc = e % FM;
-        Cs[e] = (k < w && cc < m) ? a.C[k + cc * w] : 0.0;
+    {  // C = Qp'X straight from the reduced P1 tile [Qp(0:nq) | X]'[...] (+ Qp column 8)
+        const int nq = w < 8 ? w : 8;
+        for (int e = tid; e < 9 * FM; e += 256) {
+            const int k = e / FM, cc = e % FM;
+            Cs[e] = (k < w && cc < m) ? (k < 8 ? a.C[k + (nq + cc) * 16] : a.C[256 + nq + cc]) : 0.0;
+        }
     }
     __syncthreads();
     const int64_t ntiles = (n + FTR0 - 1) / FTR0;
@@ -172,66 +244,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FOLD_UP_WPE
         const int64_t base = tile * FTR0;
         double x[L0RPL][FM];
         double tau[FM], beta[FM];
-        double p[17];
-        auto load = [&](int i) {
-            const int64_t r = base + lane + 64 * i;
-            const int64_t rr = r < n ? r : n - 1;  // a valid row; masked below
-#pragma unroll
-            for (int k = 0; k < 17; ++k) p[k] = P.p[k][rr];
-        };
-        load(0);
-#pragma unroll
-        for (int i = 0; i < L0RPL; ++i) {
-            // keep chunk i's loads and LDS traffic inside its iteration (the
-            // scheduler would otherwise hoist every chunk's loads and spill)
-            asm volatile("" ::: "memory");
-            const bool in = base + lane + 64 * i < n;
-            // Y = X - Qp C (project.m:30): the product first, k ascending
-            double t[FM];
-#pragma unroll
-            for (int cc = 0; cc < FM; ++cc) t[cc] = 0.0;
-#pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                // one C row per k, read right before use: the pin takes the
-                // accumulators as operands, so row k's FMAs retire before row
-                // k+1's broadcasts issue (otherwise all 72 C values are held)
-#pragma unroll
-                for (int cc = 0; cc < FM; ++cc) asm volatile("" : "+v"(t[cc]));
-#pragma unroll
-                for (int cc = 0; cc < FM; cc += 2) {
-                    const fd2 v = *reinterpret_cast<const fd2*>(&Cs[k * FM + cc]);
-                    t[cc] = __builtin_fma(p[k], v[0], t[cc]);
-                    t[cc + 1] = __builtin_fma(p[k], v[1], t[cc + 1]);
-                }
-            }
-#pragma unroll
-            for (int cc = 0; cc < FM; ++cc) x[i][cc] = (in && cc < m) ? p[9 + cc] - t[cc] : 0.0;
-            // [Qp(0:8) | Y] (+ Qp column 8) through LDS onto the matrix cores
-            double* trow = tl[wave] + lane * FTLD;
-#pragma unroll
-            for (int cc = 0; cc < 8; ++cc) trow[cc] = (in && cc < nq) ? p[cc] : 0.0;
-#pragma unroll
-            for (int cc = 0; cc < 8; ++cc) trow[8 + cc] = x[i][cc];
-            trow[16] = (in && w > 8) ? p[8] : 0.0;
-            if (i + 1 < L0RPL) load(i + 1);  // the next chunk's loads fly during the Gram
-            fwsync();
-            if (!(kProbe & 2)) {
-#pragma unroll
-                for (int kk = 0; kk < 16; ++kk) {
-                    // tile'tile, and Qp(:,8)'tile as a second MFMA whose A rows
-                    // all hold the extra column (every output row is the same sum)
-                    const int row = 4 * kk + g;
-                    const double av = tl[wave][row * FTLD + c16];
-                    const double ev = tl[wave][row * FTLD + 16];
-                    acc = fmfma(av, av, acc);
-                    acc2 = fmfma(ev, av, acc2);
-                }
-            }
-            fwsync();
-        }
+        fform<true>(P, Cs, tl[wave], base, n, lane, m, w, x, acc, acc2);
         if (!(kProbe & 4)) tile_geqr2<FM, L0RPL>(x, tau, beta, m, lane);
-        if (!(kProbe & 8)) fstore_tile<L0RPL>(a.V0 + tile * (64 * L0RPL * FM), lane, x);
-        fstore_tb(a.tb0 + tile * (2 * FM), lane, tau, beta);
+        if (a.V0 && !(kProbe & 8)) {  // stored for the down pass (V0 null: it re-forms the tile)
+            fstore_tile<L0RPL>(a.V0 + tile * (64 * L0RPL * FM), lane, x);
+            fstore_tb(a.tb0 + tile * (2 * FM), lane, tau, beta);
+        }
         fput_R(a.R0 + tile * 64, lane, m, x[0]);
     }
     __syncthreads();  // the transposes are done (tl is reused below)
@@ -262,113 +280,50 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FOLD_UP_WPE
     }
 }
 
-// The tree above level 0 (one launch; its blocks never wait on each other):
-// level 1, one 512-row tile (64 tile R factors) per wave; the last block of
-// each 16-block group factors the group's 64 level-1 R factors (level 2);
-// the last level-2 tile's block factors the level-2 stack (the local root,
-// <= 512 rows).  Arrivals are counted with device-scope atomics after an
-// agent-scope release fence -- in this small launch only (in k_fold_up every
-// block's fence would write its XCD's L2 back: 2.8 ms measured).
-__global__ __launch_bounds__(256) void k_fold_tree(FoldArgs a) {
-    __shared__ int sflag;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = a.m;
-    const int t1 = blockIdx.x * FTPB + wave;  // level-1 tile
-    if (t1 < a.n1) {
-        const int64_t rows = (int64_t)((a.n0 - t1 * FG) < FG ? (a.n0 - t1 * FG) : FG) * FM;
-        double x[FRPL][FM], tau[FM], beta[FM];
-        fload_stack<FRPL>(a.R0 + (int64_t)t1 * FG * 64, 0, rows, lane, x);
-        tile_geqr2<FM, FRPL>(x, tau, beta, m, lane);
-        fstore_tile<FRPL>(a.V1 + (int64_t)t1 * (64 * FRPL * FM), lane, x);
-        fstore_tb(a.tb1 + (int64_t)t1 * (2 * FM), lane, tau, beta);
-        fput_R(a.R1 + (int64_t)t1 * 64, lane, m, x[0]);
-    }
-    if (kProbe & 16) return;
-    constexpr int BPG = FG / FTPB;  // blocks per level-2 tile
-    const int t2 = blockIdx.x / BPG;
-    const int gblocks = ((int)gridDim.x - t2 * BPG) < BPG ? ((int)gridDim.x - t2 * BPG) : BPG;
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) {
-        const unsigned old = atomicAdd(&a.cnt[t2], 1u);
-        sflag = old == (unsigned)(gblocks - 1);
-    }
-    __syncthreads();
-    if (!sflag) return;
-    __threadfence();
+// The tree above level 0: one 512-row tile (64 R factors of the level
+// below) per block, spread over its 4 waves (128 rows each) with the
+// block-cooperative tile QR -- these launches are latency-bound, one tile's
+// QR deep, and one wave alone takes ~18 us for it.  k_fold_tree: level 1 (n1
+// blocks), level 2 (n2 blocks), the root (one block, the level-2 R factors,
+// <= 512 rows).  Kernel boundaries order the levels (a device-scope release
+// in every block of a launch writes each XCD's L2 back: 2.8 ms measured when
+// k_fold_up did that).
+constexpr int BRPL = FRPL / FTPB;  // rows per lane of one wave's share of a 512-row tile
+__device__ __forceinline__ void fold_level_up(const double* Rin, int64_t rows, double* V, double* tb, double* Rout,
+                                              double* Rout_m, int m, int lane, int wave, double* xlds) {
+    double x[BRPL][FM], tau[FM], beta[FM];
+    fload_stack<BRPL>(Rin, (int64_t)wave * 64 * BRPL, rows, lane, x);
+    tile_geqr2_blk<FM, BRPL, FTPB>(x, tau, beta, m, lane, wave, xlds);
+    fstore_tile<BRPL>(V + (int64_t)wave * BRPL * FM * 64, lane, x);
     if (wave == 0) {
-        if (lane == 0) a.cnt[t2] = 0u;  // ready for the next call
-        const int64_t rows = (int64_t)((a.n1 - t2 * FG) < FG ? (a.n1 - t2 * FG) : FG) * FM;
-        double x[FRPL][FM], tau[FM], beta[FM];
-        fload_stack<FRPL>(a.R1 + (int64_t)t2 * FG * 64, 0, rows, lane, x);
-        tile_geqr2<FM, FRPL>(x, tau, beta, m, lane);
-        fstore_tile<FRPL>(a.V2 + (int64_t)t2 * (64 * FRPL * FM), lane, x);
-        fstore_tb(a.tb2 + (int64_t)t2 * (2 * FM), lane, tau, beta);
-        fput_R(a.R2 + (int64_t)t2 * 64, lane, m, x[0]);
-    }
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) {
-        const unsigned old = atomicAdd(&a.cnt[a.n2], 1u);
-        sflag = old == (unsigned)(a.n2 - 1);
-    }
-    __syncthreads();
-    if (!sflag) return;
-    __threadfence();
-    if (wave == 0) {
-        if (lane == 0) a.cnt[a.n2] = 0u;
-        double x[FRPL][FM], tau[FM], beta[FM];
-        fload_stack<FRPL>(a.R2, 0, (int64_t)a.n2 * FM, lane, x);
-        tile_geqr2<FM, FRPL>(x, tau, beta, m, lane);
-        fstore_tile<FRPL>(a.V3, lane, x);
-        fstore_tb(a.tb3, lane, tau, beta);
-        fput_R(a.Rroot, lane, m, x[0]);
+        fstore_tb(tb, lane, tau, beta);
+        fput_R(Rout, lane, m, x[0]);
         // the same R with leading dimension m (the stack layout of tsqr.hip,
         // for the all-gather of the local roots over several ranks)
-        if (lane < m)
-            for (int cc = 0; cc < m; ++cc) a.Rroot_m[lane + cc * m] = cc >= lane ? x[0][cc] : 0.0;
+        if (Rout_m && lane < m)
+            for (int cc = 0; cc < m; ++cc) Rout_m[lane + cc * m] = cc >= lane ? x[0][cc] : 0.0;
+    }
+}
+
+// level: 1 (R0 -> V1 / R1), 2 (R1 -> V2 / R2), 3 (the root: R2 -> V3 / Rroot)
+__global__ __launch_bounds__(256) void k_fold_tree(FoldArgs a, int level) {
+    __shared__ double xlds[2 * FTPB * 2 * FM];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = a.m;
+    const int t = blockIdx.x;
+    if (level == 1) {
+        const int64_t rows = (int64_t)((a.n0 - t * FG) < FG ? (a.n0 - t * FG) : FG) * FM;
+        fold_level_up(a.R0 + (int64_t)t * FG * 64, rows, a.V1 + (int64_t)t * (64 * FRPL * FM),
+                      a.tb1 + (int64_t)t * (2 * FM), a.R1 + (int64_t)t * 64, nullptr, m, lane, wave, xlds);
+    } else if (level == 2) {
+        const int64_t rows = (int64_t)((a.n1 - t * FG) < FG ? (a.n1 - t * FG) : FG) * FM;
+        fold_level_up(a.R1 + (int64_t)t * FG * 64, rows, a.V2 + (int64_t)t * (64 * FRPL * FM),
+                      a.tb2 + (int64_t)t * (2 * FM), a.R2 + (int64_t)t * 64, nullptr, m, lane, wave, xlds);
+    } else {
+        fold_level_up(a.R2, (int64_t)a.n2 * FM, a.V3, a.tb3, a.Rroot, a.Rroot_m, m, lane, wave, xlds);
     }
 }
 
 // ---- the s x s algebra --------------------------------------------------
-// Phase 0 (after the P1 Gram tile [Qp(0:nq) | X]'[...] + Qp column 8):
-// C = Qp'X -> st (w x m, ld w); the reorth test of projectAndNormalize.m:
-// 17-22,45-52 on the algebraic norms ||Y_j||^2 = X_j'X_j - C_j'C_j -> out[514].
-__global__ __launch_bounds__(64) void k_fold_coef0(const double* __restrict__ tile, double* __restrict__ st,
-                                                  double* __restrict__ out, int w, int m, int doreorth) {
-    __shared__ double rel[FM], nrm[FM];
-    const int tid = threadIdx.x, nq = w < 8 ? w : 8;
-    for (int e = tid; e < w * m; e += 64) {
-        const int i = e % w, j = e / w;
-        st[e] = i < 8 ? tile[i + (nq + j) * 16] : tile[256 + nq + j];
-    }
-    if (tid < m) {
-        const int j = tid;
-        double cc = 0.0;
-        for (int k = 0; k < w; ++k) {
-            const double v = k < 8 ? tile[k + (nq + j) * 16] : tile[256 + nq + j];
-            cc = cc + v * v;
-        }
-        const double xx = tile[(nq + j) + (nq + j) * 16];
-        const double before = sqrt(xx);
-        const double after = sqrt(fmax(xx - cc, 0.0));
-        rel[j] = fabs(before - after) / before;
-        nrm[j] = before;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        double mx = NAN, xmax = 0.0;
-        for (int j = 0; j < m; ++j) {
-            const double r = rel[j];
-            if (!isnan(r) && (isnan(mx) || r > mx)) mx = r;
-            xmax = fmax(xmax, nrm[j]);
-        }
-        st[kFoldXmax] = xmax;
-        out[512] = 0.0;
-        out[513] = 0.0;
-        out[514] = (w > 0 && doreorth && mx > 0.5) ? 1.0 : 0.0;
-    }
-}
-
 // Phase 1 (after the tree, the Gram tile reduced, and on several ranks the
 // global levels): Rtop the root R (ld ldr, raw signs), G the Gram tile
 // [Qp(0:8) | Y]'[...] (+ Qp column 8).  Writes S_top (8 x 8, ld 8; and ld m
@@ -389,16 +344,47 @@ __device__ __forceinline__ void finv_col(const double* T, double* Ti, int j, int
     for (int i = 0; i < FM; ++i) Ti[i + j * FM] = col[i];
 }
 
-__global__ __launch_bounds__(64) void k_fold_coef1(const double* __restrict__ G, const double* __restrict__ Rtop,
-                                                  int ldr, const double* __restrict__ st, double* __restrict__ out,
+__global__ __launch_bounds__(64) void k_fold_coef1(const double* __restrict__ T1, const double* __restrict__ G,
+                                                  const double* __restrict__ Rtop, int ldr, double* __restrict__ out,
                                                   double* __restrict__ Sbuf, double* __restrict__ Sm,
-                                                  double* __restrict__ Kbuf, int w, int m, double nglob,
+                                                  double* __restrict__ Kbuf, int w, int m, int doreorth, double nglob,
                                                   double* __restrict__ hout,
                                                   unsigned long long* __restrict__ hseq, unsigned long long seq) {
-    __shared__ double RY[64], Ri[64], Ws[9 * FM], U[64], Ui[64], D[FM], red[64];
-    __shared__ int fail;
-    const int lane = threadIdx.x, r = lane & 7, c = lane >> 3;
-    const bool reorth = out[514] != 0.0;
+    __shared__ double RY[64], Ri[64], Ws[9 * FM], U[64], Ui[64], D[FM], red[64], rel[FM], nrm[FM];
+    __shared__ int fail, reo;
+    const int lane = threadIdx.x, r = lane & 7, c = lane >> 3, nq = w < 8 ? w : 8;
+    // from the P1 tile T1: C = Qp'X, and the reorth test of
+    // projectAndNormalize.m:17-22,45-52 on the algebraic norms
+    // ||Y_j||^2 = X_j'X_j - C_j'C_j
+    auto cq = [&](int i, int j) { return i < 8 ? T1[i + (nq + j) * 16] : T1[256 + nq + j]; };
+    if (lane < m) {
+        const int j = lane;
+        double cc = 0.0;
+        for (int k = 0; k < w; ++k) {
+            const double v = cq(k, j);
+            cc = cc + v * v;
+        }
+        const double xx = T1[(nq + j) + (nq + j) * 16];
+        const double before = sqrt(xx);
+        const double after = sqrt(fmax(xx - cc, 0.0));
+        rel[j] = fabs(before - after) / before;
+        nrm[j] = before;
+    }
+    __syncthreads();
+    double xmax = 0.0;
+    if (lane == 0) {
+        double mx = NAN;
+        for (int j = 0; j < m; ++j) {
+            const double rj = rel[j];
+            if (!isnan(rj) && (isnan(mx) || rj > mx)) mx = rj;
+        }
+        reo = (w > 0 && doreorth && mx > 0.5) ? 1 : 0;
+        out[512] = 0.0;
+        out[514] = reo ? 1.0 : 0.0;
+    }
+    for (int j = 0; j < m; ++j) xmax = fmax(xmax, nrm[j]);
+    __syncthreads();
+    const bool reorth = reo != 0;
     const bool in = r < m && c < m;
     if (lane < FM) {
         const double rii = lane < m ? Rtop[lane + lane * ldr] : 0.0;
@@ -441,7 +427,7 @@ __global__ __launch_bounds__(64) void k_fold_coef1(const double* __restrict__ G,
         // (the rounding of C2 and of Y's factorization through R_Y^-1):
         // ||E|| <~ u sqrt(n) max||X_j|| ||R_Y^-1||; decline (explicit Z)
         // unless that is below kFoldTol and ||W||_F <= 1/2
-        est = 2.0 * sqrt(nw) * 0x1p-53 * sqrt(nglob) * st[kFoldXmax] * sqrt(nri);
+        est = 2.0 * sqrt(nw) * 0x1p-53 * sqrt(nglob) * xmax * sqrt(nri);
         red[lane] = a;
         __syncthreads();
         if (lane == 0) {
@@ -492,12 +478,14 @@ __global__ __launch_bounds__(64) void k_fold_coef1(const double* __restrict__ G,
         for (int e = lane; e < w * m; e += 64) {
             const int i = e % w, j = e / w;
             const double c2 = reorth ? (i < 8 ? G[i + (8 + j) * 16] : G[256 + 8 + j]) : 0.0;
-            out[256 + e] = st[e] + c2;
+            out[256 + e] = cq(i, j) + c2;
         }
     }
     __syncthreads();
     if (hout) {
-        for (int e = lane; e < 516; e += 64) hout[e] = out[e];
+        for (int e = lane; e < m * m; e += 64) hout[e] = out[e];
+        for (int e = lane; e < w * m; e += 64) hout[256 + e] = out[256 + e];
+        if (lane < 4) hout[512 + lane] = out[512 + lane];
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (lane == 0) {
@@ -531,60 +519,54 @@ __global__ __launch_bounds__(1024) void k_fold_reduce(const double* __restrict__
 // ---- down the tree ---------------------------------------------------------
 // Stack row r of a level's input is row r & 7 of R block r >> 3 (rows >= m
 // are zero rows: their Q rows are zero, so the S rows written there are zero).
-// The root's Q factor times S_top (ld lds) -> the level-2 tiles' S blocks.
-__global__ __launch_bounds__(64) void k_fold_down_root(FoldArgs a, const double* __restrict__ Stop, int lds) {
-    __shared__ double Ss[64];
-    const int lane = threadIdx.x, m = a.m;
-    {
-        const int k = lane & 7, cc = lane >> 3;
-        Ss[lane] = (k < m && cc < m) ? Stop[k + cc * lds] : 0.0;
-    }
-    double x[FRPL][FM], tau[FM];
-    fload_tile<FRPL>(a.V3, lane, x);
-    fload_tau(a.tb3, tau);
-    fwsync();
-    tile_org2r<FM, FRPL>(x, tau, m, lane);
-    const int64_t rows = (int64_t)a.n2 * FM;
+// One upper-level tile down, one block: its Q factor (from the stored
+// reflectors) times its S block (Ss, LDS) -> the S blocks of the level below
+// (rows r < rows of the tile: block blk0 + (r >> 3) of Sb, row r & 7).
+__device__ __forceinline__ void fold_level_down(const double* V, const double* tb, const double* Ss, int64_t rows,
+                                                double* Sb, int64_t blk0, int m, int lane, int wave, double* xlds) {
+    double x[BRPL][FM], tau[FM];
+    fload_tile<BRPL>(V + (int64_t)wave * BRPL * FM * 64, lane, x);
+    fload_tau(tb, tau);
+    tile_org2r_blk<FM, BRPL, FTPB>(x, tau, m, lane, wave, xlds);
 #pragma unroll
-    for (int i = 0; i < FRPL; ++i) {
-        const int64_t r = lane + 64 * i;
+    for (int i = 0; i < BRPL; ++i) {
+        const int64_t r = (int64_t)wave * 64 * BRPL + lane + 64 * i;
         double o[FM];
         fmul_S(x[i], Ss, m, o);
         if (r < rows) {
 #pragma unroll
-            for (int cc = 0; cc < FM; ++cc) a.S2[(r >> 3) * 64 + (r & 7) + cc * FM] = o[cc];
+            for (int cc = 0; cc < FM; ++cc) Sb[(blk0 + (r >> 3)) * 64 + (r & 7) + cc * FM] = o[cc];
         }
     }
 }
 
-// One upper level down: one wave per tile of the level (Vl / tbl, S blocks
-// Sl), its Q factor times its S -> the S blocks of the level below (Sb,
-// nb blocks in all).
-__global__ __launch_bounds__(256) void k_fold_down_level(const double* __restrict__ Vl, const double* __restrict__ tbl,
-                                                         const double* __restrict__ Sl, int ntl,
-                                                         double* __restrict__ Sb, int nb, int m) {
-    __shared__ double Ss[FTPB][64];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int t = blockIdx.x * FTPB + wave;
-    if (t >= ntl) return;  // whole waves; no block-wide sync below
-    Ss[wave][lane] = Sl[(int64_t)t * 64 + lane];
-    double x[FRPL][FM], tau[FM];
-    fload_tile<FRPL>(Vl + (int64_t)t * (64 * FRPL * FM), lane, x);
-    fload_tau(tbl + (int64_t)t * (2 * FM), tau);
-    fwsync();
-    tile_org2r<FM, FRPL>(x, tau, m, lane);
-    const int64_t rows = (int64_t)((nb - t * FG) < FG ? (nb - t * FG) : FG) * FM;
-#pragma unroll
-    for (int i = 0; i < FRPL; ++i) {
-        const int64_t r = lane + 64 * i;
-        double o[FM];
-        fmul_S(x[i], Ss[wave], m, o);
-        if (r < rows) {
-            const int64_t blk = (int64_t)t * FG + (r >> 3);
-#pragma unroll
-            for (int cc = 0; cc < FM; ++cc) Sb[blk * 64 + (r & 7) + cc * FM] = o[cc];
-        }
+// The root: its Q factor times S_top (ld lds) -> the level-2 tiles' S blocks.
+__global__ __launch_bounds__(256) void k_fold_down_root(FoldArgs a, const double* __restrict__ Stop, int lds) {
+    __shared__ double Ss[64];
+    __shared__ double xlds[2 * FTPB * 2 * FM];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = a.m;
+    if (tid < 64) {
+        const int k = tid & 7, cc = tid >> 3;
+        Ss[tid] = (k < m && cc < m) ? Stop[k + cc * lds] : 0.0;
     }
+    __syncthreads();
+    fold_level_down(a.V3, a.tb3, Ss, (int64_t)a.n2 * FM, a.S2, 0, m, lane, wave, xlds);
+}
+
+// One upper level down: one block per tile of the level (Vl / tbl, S blocks
+// Sl) -> the S blocks of the level below (Sb, nb blocks in all).
+__global__ __launch_bounds__(256) void k_fold_down_level(const double* __restrict__ Vl, const double* __restrict__ tbl,
+                                                         const double* __restrict__ Sl, double* __restrict__ Sb, int nb,
+                                                         int m) {
+    __shared__ double Ss[64];
+    __shared__ double xlds[2 * FTPB * 2 * FM];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int t = blockIdx.x;
+    if (tid < 64) Ss[tid] = Sl[(int64_t)t * 64 + tid];
+    __syncthreads();
+    const int64_t rows = (int64_t)((nb - t * FG) < FG ? (nb - t * FG) : FG) * FM;
+    fold_level_down(Vl + (int64_t)t * (64 * FRPL * FM), tbl + (int64_t)t * (2 * FM), Ss, rows, Sb, (int64_t)t * FG, m,
+                    lane, wave, xlds);
 }
 
 // Level 0: Q = Q_tile S - Qp K, one store.  Q: output columns (slots >= m
@@ -648,6 +630,76 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     }
 }
 
+// Level 0 without stored tiles: re-form Y and refactor it (the up pass's
+// code on the same inputs: the same reflectors), then Q = Q_tile S - Qp K;
+// Qp is read again for the correction (the rows this wave just formed from,
+// mostly served by the caches).  Reads (w + m) 8n, writes m 8n.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FOLD_UP_WPE))) void k_fold_down_reform(
+    ColList P, OutList Q, FoldArgs a) {
+    __shared__ double Cs[9 * FM];
+    __shared__ double Ss[FTPB][64];
+    __shared__ double Ks[9 * FM];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = a.m, w = a.w;
+    const int64_t n = a.n;
+    const int64_t ntiles = (n + FTR0 - 1) / FTR0;
+    const int64_t tile = (int64_t)blockIdx.x * FTPB + wave;
+    {
+        const int nq = w < 8 ? w : 8;
+        for (int e = tid; e < 9 * FM; e += 256) {
+            const int k = e / FM, cc = e % FM;
+            Cs[e] = (k < w && cc < m) ? (k < 8 ? a.C[k + (nq + cc) * 16] : a.C[256 + nq + cc]) : 0.0;
+            const int k2 = e % 9, c2 = e / 9;
+            Ks[e] = (k2 < w && c2 < m) ? a.K[e] : 0.0;
+        }
+    }
+    const bool corr = a.flags[2] != 0.0;
+    __syncthreads();
+    if (tile >= ntiles) return;
+    Ss[wave][lane] = a.S0[tile * 64 + lane];
+    const int64_t base = tile * FTR0;
+    double x[L0RPL][FM], tau[FM], beta[FM];
+    fd4 d0 = fd4{0.0, 0.0, 0.0, 0.0}, d1 = d0;
+    fform<false>(P, Cs, nullptr, base, n, lane, m, w, x, d0, d1);
+    tile_geqr2<FM, L0RPL>(x, tau, beta, m, lane);
+    tile_org2r<FM, L0RPL>(x, tau, m, lane);
+    fwsync();
+    double q[9];
+    auto loadq = [&](int i) {
+        const int64_t r = base + lane + 64 * i;
+        const int64_t rr = r < n ? r : n - 1;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) q[k] = P.p[k][rr];
+    };
+    if (corr) loadq(0);
+#pragma unroll
+    for (int i = 0; i < L0RPL; ++i) {
+        asm volatile("" ::: "memory");
+        double o[FM];
+        fmul_S(x[i], Ss[wave], m, o);
+        if (corr) {
+            double t[FM];
+#pragma unroll
+            for (int cc = 0; cc < FM; ++cc) t[cc] = 0.0;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+#pragma unroll
+                for (int cc = 0; cc < FM; ++cc) asm volatile("" : "+v"(t[cc]));
+#pragma unroll
+                for (int cc = 0; cc < FM; ++cc) t[cc] = __builtin_fma(q[k], Ks[k + cc * 9], t[cc]);
+            }
+            if (i + 1 < L0RPL) loadq(i + 1);
+#pragma unroll
+            for (int cc = 0; cc < FM; ++cc) o[cc] = o[cc] - t[cc];
+        }
+        const int64_t r = base + lane + 64 * i;
+        if (r < n) {
+#pragma unroll
+            for (int cc = 0; cc < FM; ++cc)
+                if (cc < m) Q.p[cc][r] = o[cc];
+        }
+    }
+}
+
 int fold_tiles(int64_t n) { return (int)((n + FTR0 - 1) / FTR0); }
 int fold_blocks(int64_t n) { return (fold_tiles(n) + FTPB - 1) / FTPB; }
 int fold_l1_tiles(int64_t n) { return (fold_tiles(n) + FG - 1) / FG; }
@@ -664,35 +716,31 @@ hipError_t launch_fold_up(const ColList& P, const FoldArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_fold_tree(const FoldArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(k_fold_tree, dim3((a.n1 + FTPB - 1) / FTPB), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_fold_tree, dim3(a.n1), dim3(256), 0, st, a, 1);
+    hipLaunchKernelGGL(k_fold_tree, dim3(a.n2), dim3(256), 0, st, a, 2);
+    hipLaunchKernelGGL(k_fold_tree, dim3(1), dim3(256), 0, st, a, 3);
     return hipGetLastError();
 }
 hipError_t launch_fold_reduce(const double* partial, int nparts, double* outv, hipStream_t st) {
     hipLaunchKernelGGL(k_fold_reduce, dim3(272), dim3(1024), 0, st, partial, nparts, outv);
     return hipGetLastError();
 }
-hipError_t launch_fold_coef0(const double* tile, double* stc, double* out, int w, int m, int doreorth,
-                             hipStream_t st) {
-    hipLaunchKernelGGL(k_fold_coef0, dim3(1), dim3(64), 0, st, tile, stc, out, w, m, doreorth);
-    return hipGetLastError();
-}
-hipError_t launch_fold_coef1(const double* G, const double* Rtop, int ldr, const double* stc, double* out,
-                             double* Sbuf, double* Sm, double* Kbuf, int w, int m, double nglob, double* hout,
-                             unsigned long long* hseq, unsigned long long seq, hipStream_t st) {
-    hipLaunchKernelGGL(k_fold_coef1, dim3(1), dim3(64), 0, st, G, Rtop, ldr, stc, out, Sbuf, Sm, Kbuf, w, m, nglob,
-                       hout, hseq, seq);
+hipError_t launch_fold_coef1(const double* T1, const double* G, const double* Rtop, int ldr, double* out,
+                             double* Sbuf, double* Sm, double* Kbuf, int w, int m, int doreorth, double nglob,
+                             double* hout, unsigned long long* hseq, unsigned long long seq, hipStream_t st) {
+    hipLaunchKernelGGL(k_fold_coef1, dim3(1), dim3(64), 0, st, T1, G, Rtop, ldr, out, Sbuf, Sm, Kbuf, w, m, doreorth,
+                       nglob, hout, hseq, seq);
     return hipGetLastError();
 }
 hipError_t launch_fold_down_tree(const FoldArgs& a, const double* Stop, int lds, hipStream_t st) {
-    hipLaunchKernelGGL(k_fold_down_root, dim3(1), dim3(64), 0, st, a, Stop, lds);
-    hipLaunchKernelGGL(k_fold_down_level, dim3((a.n2 + FTPB - 1) / FTPB), dim3(256), 0, st, a.V2, a.tb2, a.S2, a.n2,
-                       a.S1, a.n1, a.m);
-    hipLaunchKernelGGL(k_fold_down_level, dim3((a.n1 + FTPB - 1) / FTPB), dim3(256), 0, st, a.V1, a.tb1, a.S1, a.n1,
-                       a.S0, a.n0, a.m);
+    hipLaunchKernelGGL(k_fold_down_root, dim3(1), dim3(256), 0, st, a, Stop, lds);
+    hipLaunchKernelGGL(k_fold_down_level, dim3(a.n2), dim3(256), 0, st, a.V2, a.tb2, a.S2, a.S1, a.n1, a.m);
+    hipLaunchKernelGGL(k_fold_down_level, dim3(a.n1), dim3(256), 0, st, a.V1, a.tb1, a.S1, a.S0, a.n0, a.m);
     return hipGetLastError();
 }
 hipError_t launch_fold_down(const ColList& P, const OutList& Q, const FoldArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(k_fold_down, dim3(a.nblk), dim3(256), 0, st, P, Q, a);
+    if (a.V0) hipLaunchKernelGGL(k_fold_down, dim3(a.nblk), dim3(256), 0, st, P, Q, a);
+    else hipLaunchKernelGGL(k_fold_down_reform, dim3(a.nblk), dim3(256), 0, st, P, Q, a);
     return hipGetLastError();
 }
 

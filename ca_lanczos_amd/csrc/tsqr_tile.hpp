@@ -157,5 +157,160 @@ __device__ __forceinline__ void tile_org2r(double (&a)[RPL][MM], const double (&
     }
 }
 
+// ---- block-cooperative variants: one tile spread over the NW waves of a
+// block (wave w holds tile rows w * 64 * RPLW + lane + 64 i), for the short
+// launches of the tree above level 0 whose wall time is one tile's latency.
+// Per reflector: wave partial sums (DPP butterfly), then the NW partials and
+// the pivot row through LDS (xlds: 2 * NW * 2 * MM doubles, double-buffered
+// by column parity) summed in wave order -- every wave computes the same
+// tau / beta / w_c.  Called by all NW waves of the block (barriers inside).
+template <int MM, int RPLW, int NW>
+__device__ __forceinline__ void tile_geqr2_blk(double (&a)[RPLW][MM], double (&tau)[MM], double (&beta)[MM], int m,
+                                               int lane, int wave, double* xlds) {
+#pragma unroll
+    for (int j = 0; j < MM; ++j) {
+        tau[j] = 0.0;
+        beta[j] = 0.0;
+        if (j < m) {
+            double d[MM];
+#pragma unroll
+            for (int c = j; c < MM; ++c) d[c] = 0.0;
+#pragma unroll
+            for (int i = 0; i < RPLW; ++i) {
+                const bool below = wave * 64 * RPLW + lane + 64 * i > j;
+                const double x = below ? a[i][j] : 0.0;
+#pragma unroll
+                for (int c = j; c < MM; ++c) {
+                    const double t = x * a[i][c];
+                    d[c] = d[c] + t;
+                }
+            }
+#pragma unroll
+            for (int c = j; c < MM; ++c)
+                if (c < m) d[c] = wave_allsum(d[c]);
+            double pv[MM];  // the pivot row (wave 0, lane j, slot 0)
+#pragma unroll
+            for (int c = j; c < MM; ++c) pv[c] = readlane_f64(a[0][c], j);
+            double* buf = xlds + (j & 1) * (NW * 2 * MM);
+            if (lane == 0) {
+#pragma unroll
+                for (int c = j; c < MM; ++c) {
+                    buf[wave * 2 * MM + c] = d[c];
+                    if (wave == 0) buf[MM + c] = pv[c];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int c = j; c < MM; ++c) {
+                double sum = buf[c];
+#pragma unroll
+                for (int w = 1; w < NW; ++w) sum = sum + buf[w * 2 * MM + c];
+                d[c] = sum;
+                pv[c] = buf[MM + c];
+            }
+            const double alpha = pv[j];
+            double t = 0.0, b = alpha, scal = 0.0;
+            if (d[j] != 0.0) {  // dlarfg: xnorm == 0 -> H = I
+                const double aa = alpha * alpha;
+                const double nrm = sqrt(aa + d[j]);
+                b = alpha >= 0.0 ? -nrm : nrm;
+                t = (b - alpha) / b;
+                scal = 1.0 / (alpha - b);
+            }
+            tau[j] = t;
+            beta[j] = b;
+#pragma unroll
+            for (int c = j + 1; c < MM; ++c) {
+                if (c < m) {
+                    const double u = scal * d[c];
+                    const double w = pv[c] + u;
+                    d[c] = t * w;
+                } else {
+                    d[c] = 0.0;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < RPLW; ++i) {
+                const int row = wave * 64 * RPLW + lane + 64 * i;
+                if (row > j) {
+                    const double v = scal * a[i][j];
+                    a[i][j] = v;
+#pragma unroll
+                    for (int c = j + 1; c < MM; ++c) {
+                        const double u = d[c] * v;
+                        a[i][c] = a[i][c] - u;
+                    }
+                } else if (row == j) {
+                    a[i][j] = b;
+#pragma unroll
+                    for (int c = j + 1; c < MM; ++c) a[i][c] = a[i][c] - d[c];
+                }
+            }
+        }
+    }
+}
+
+template <int MM, int RPLW, int NW>
+__device__ __forceinline__ void tile_org2r_blk(double (&a)[RPLW][MM], const double (&tau)[MM], int m, int lane,
+                                               int wave, double* xlds) {
+#pragma unroll
+    for (int jj = 0; jj < MM; ++jj) {
+        const int j = MM - 1 - jj;
+        if (j < m) {
+            const double t = tau[j];
+            if (j < m - 1) {
+                double d[MM];
+#pragma unroll
+                for (int c = j + 1; c < MM; ++c) d[c] = 0.0;
+#pragma unroll
+                for (int i = 0; i < RPLW; ++i) {
+                    const int row = wave * 64 * RPLW + lane + 64 * i;
+                    const double v = row > j ? a[i][j] : (row == j ? 1.0 : 0.0);
+#pragma unroll
+                    for (int c = j + 1; c < MM; ++c) {
+                        const double u = v * a[i][c];
+                        d[c] = d[c] + u;
+                    }
+                }
+#pragma unroll
+                for (int c = j + 1; c < MM; ++c)
+                    if (c < m) d[c] = wave_allsum(d[c]);
+                double* buf = xlds + (j & 1) * (NW * 2 * MM);
+                if (lane == 0) {
+#pragma unroll
+                    for (int c = j + 1; c < MM; ++c) buf[wave * 2 * MM + c] = d[c];
+                }
+                __syncthreads();
+#pragma unroll
+                for (int c = j + 1; c < MM; ++c) {
+                    double sum = buf[c];
+#pragma unroll
+                    for (int w = 1; w < NW; ++w) sum = sum + buf[w * 2 * MM + c];
+                    d[c] = c < m ? t * sum : 0.0;
+                }
+#pragma unroll
+                for (int i = 0; i < RPLW; ++i) {
+                    const int row = wave * 64 * RPLW + lane + 64 * i;
+                    if (row >= j) {
+                        const double v = row > j ? a[i][j] : 1.0;
+#pragma unroll
+                        for (int c = j + 1; c < MM; ++c) {
+                            const double u = d[c] * v;
+                            a[i][c] = a[i][c] - u;
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < RPLW; ++i) {
+                const int row = wave * 64 * RPLW + lane + 64 * i;
+                const double v = a[i][j];
+                const double mt = -t;
+                a[i][j] = row > j ? mt * v : (row == j ? 1.0 - t : 0.0);
+            }
+        }
+    }
+}
+
 }  // namespace tsqr_tile
 }  // namespace cal

@@ -215,6 +215,33 @@ def test_project_and_normalize_one_block(cal, ref, frac):
     assert np.max(np.abs(QZ.T @ Qp)) < 1e-13
 
 
+@pytest.mark.parametrize("n,w,m,frac", [(70001, 9, 8, 0.9), (1200001, 9, 8, 0.9), (1200001, 5, 4, 0.9),
+                                        (300001, 9, 8, 0.1), (1200001, 3, 2, 0.1)])
+def test_project_and_normalize_fused_tsqr_tree(cal, ref, n, w, m, frac):
+    """The fused TSQR projectAndNormalize (blockorth.cpp pn_tsqr_fold,
+    tsqr_fold.hip) with several tiles on every tree level: 70001 rows = 274
+    level-0 tiles, 5 level-1 tiles; 1.2 M rows = 4688 / 74 / 2 level tiles
+    under the root; m < 8 pads the stacked R factors.  Against the oracle's
+    projectAndNormalize (explicit Z, Householder QR): RZ to 1e-11 (C) and
+    1e-12 ||X|| (R), QZ orthonormal to 1e-13 and to Qp like the oracle's, the
+    reorth flag identical; the fold ran and was not declined."""
+    rng = np.random.RandomState(n % 1000 + m)
+    Qp, _ = np.linalg.qr(rng.randn(n, w))
+    X = frac * Qp @ rng.randn(w, m) + (1 - frac) * rng.randn(n, m) / np.sqrt(n) * 3
+    ctx = cal.default_context()
+    f0 = ctx.tsqr_fold_stats()
+    QZ, RZ, re, rank = cal.projectAndNormalize_ex([Qp], X)
+    f1 = ctx.tsqr_fold_stats()
+    assert f1["runs"] == f0["runs"] + 1 and f1["declined"] == f0["declined"]
+    QZr, RZr, info = ref.projectAndNormalize_ex([Qp], X)
+    assert re == info.reorth
+    assert np.max(np.abs(RZ[0] - RZr[0])) < 1e-11
+    assert np.max(np.abs(RZ[1] - RZr[1])) <= 1e-12 * np.linalg.norm(X, 2)
+    assert np.linalg.norm(QZ.T @ QZ - np.eye(m), 2) <= 1e-13
+    assert np.max(np.abs(QZ.T @ Qp)) <= 10 * np.max(np.abs(QZr.T @ Qp)) + 1e-13
+    assert np.max(np.abs(QZ - QZr)) < 1e-10
+
+
 def test_project_and_normalize_two_blocks(cal, ref):
     rng = np.random.RandomState(12)
     n = 2000

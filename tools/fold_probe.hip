@@ -68,7 +68,7 @@ int main(int argc, char** argv) {
     fa.n0 = (int)n0;
     fa.n1 = (int)n1;
     fa.n2 = (int)n2;
-    fa.C = F + oC;
+    fa.C = F + oOut;  // any 272 doubles stand in for the P1 tile
     fa.flags = F + oOut + 512;
     fa.K = F + oK;
     fa.V0 = F + oV0;
@@ -88,7 +88,6 @@ int main(int argc, char** argv) {
     fa.Rroot = F + oRr;
     fa.Rroot_m = F + oRrm;
     fa.partial = F + oPart;
-    fa.cnt = cnt;
     ColList cu{};
     for (int k = 0; k < 17; ++k) cu.p[k] = P + (size_t)k * ld;
     OutList qo{};
@@ -121,6 +120,10 @@ int main(int argc, char** argv) {
     if (timeit("tree", 0.0, [&] { return launch_fold_tree(fa, st); })) return 1;
     if (timeit("down_tree", 0.0, [&] { return launch_fold_down_tree(fa, F + oRr, 8, st); })) return 1;
     if (timeit("down", b_down, [&] { return launch_fold_down(cu, qo, fa, st); })) return 1;
+    FoldArgs fr = fa;
+    fr.V0 = nullptr;  // re-forming down pass, up without the tile store
+    if (timeit("up_nost", 17.0 * 8.0 * n, [&] { return launch_fold_up(cu, fr, st); })) return 1;
+    if (timeit("down_ref", b_down, [&] { return launch_fold_down(cu, qo, fr, st); })) return 1;
     CK(hipDeviceSynchronize());
     return 0;
 }
