@@ -634,6 +634,142 @@ __global__ __launch_bounds__(256) void k_spmv_pair_resid_multi(PatArgs a, const 
     }
 }
 
+// Persistent variant of k_spmv_pair_resid_multi (CAL_RESID_PERS=1; measured
+// slower, off by default: diagnostics-on lap3d_215 117-120 outer-it/s at 1, 2
+// or 4 pairs per pass against 137 for the 2-D grid, profiles/r03/diag/): the
+// kernel is bound by its gather requests, not by the re-read bytes.
+// gridDim.x = 8 nbx blocks; XCD x (blockIdx.x & 7 on a 1-D grid) owns
+// one contiguous range of 256-row-pair chunks and its nbx blocks stride
+// through it, CPB Ritz pairs at a time (pair groups the outer loop).  At any
+// moment an XCD's blocks then work on a window of ~nbx * 512 rows, so a row's
+// +-N^2 (plane) neighbours are read while that XCD's L2 still holds them; the
+// 2-D grid spread each XCD's in-flight rows over ~11 planes times 4 pairs and
+// fetched 2.65x the algorithmic bytes.  The pair table is staged once per
+// block.  Same products and per-row order as the single-pair kernel.
+template <int MAXLEN, int CPB>
+__global__ __launch_bounds__(256) void k_spmv_pair_resid_pers(PatArgs a, const uint16_t* __restrict__ ppat,
+                                                             const int* __restrict__ ppoff,
+                                                             const double2* __restrict__ ppval,
+                                                             const double* __restrict__ X, int64_t ldx,
+                                                             const int* __restrict__ col,
+                                                             const double* __restrict__ lam,
+                                                             const int* __restrict__ out, int npairs_ritz,
+                                                             double* __restrict__ partial, int64_t pstride) {
+    extern __shared__ __attribute__((aligned(16))) double lds_pair[];
+    double2* s_pv = reinterpret_cast<double2*>(lds_pair);
+    int* s_poff = reinterpret_cast<int*>(s_pv + a.npent);
+    __shared__ double ws[CPB][2][4];
+    const int tid = threadIdx.x;
+    const int64_t npairs = (a.n + 1) >> 1;
+    for (int i = tid; i < a.npent; i += 256) {
+        s_pv[i] = ppval[i];
+        s_poff[i] = ppoff[i];
+    }
+    __syncthreads();
+    const int xcd = blockIdx.x & 7, jb = blockIdx.x >> 3, nbx = gridDim.x >> 3;
+    const int64_t nch = (npairs + 255) / 256;
+    const int64_t lo = xcd * nch / 8, hi = (xcd + 1) * nch / 8;
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int i0 = 0; i0 < npairs_ritz; i0 += CPB) {
+        const int nq = npairs_ritz - i0 < CPB ? npairs_ritz - i0 : CPB;  // uniform over the block
+        const double* xq[CPB];
+        double lq[CPB], num[CPB], den[CPB];
+#pragma unroll
+        for (int q = 0; q < CPB; ++q) {
+            const int qq = q < nq ? q : 0;
+            xq[q] = X + (int64_t)col[i0 + qq] * ldx;
+            lq[q] = lam[i0 + qq];
+            num[q] = 0.0;
+            den[q] = 0.0;
+        }
+        for (int64_t ch = lo + jb; ch < hi; ch += nbx) {
+            const int64_t t = ch * 256 + tid;
+            const int64_t tcl = t < npairs ? t : npairs - 1;
+            const int id = ppat[tcl];
+            const int64_t r0 = 2 * tcl;
+            const bool two = r0 + 1 < a.n;  // see k_spmv_pair_resid (odd distributed slab)
+            const int base = id != kPairSplit ? id * MAXLEN : 0;
+            int code[MAXLEN];
+            double2 v[MAXLEN];
+#pragma unroll
+            for (int e = 0; e < MAXLEN; ++e) {
+                code[e] = s_poff[base + e];
+                v[e] = s_pv[base + e];
+            }
+            int64_t ad[MAXLEN];
+#pragma unroll
+            for (int e = 0; e < MAXLEN; ++e) {
+                const int64_t d = r0 + a.pslot[e];
+                ad[e] = d < a.xlo ? a.xlo : (d > a.xhi - 2 ? a.xhi - 2 : d);
+            }
+            const int64_t rs = r0 < a.xhi - 2 ? r0 : a.xhi - 2;
+#pragma unroll
+            for (int q = 0; q < CPB; ++q) {
+                if (q >= nq) break;
+                const double* x = xq[q];
+                const double l = lq[q];
+                double2 xc[MAXLEN];
+#pragma unroll
+                for (int e = 0; e < MAXLEN; ++e) xc[e] = ld16(x + ad[e]);
+                const double2 xs = ld16(x + rs);
+                if (t < npairs) {
+                    if (id != kPairSplit) {
+                        double y0 = 0.0, y1 = 0.0;
+#pragma unroll
+                        for (int e = 0; e < MAXLEN; ++e) {
+                            const double t0 = v[e].x * xc[e].x, t1 = v[e].y * xc[e].y;
+                            double a0 = y0 + t0, a1 = y1 + t1;
+                            asm volatile("" : "+v"(a0), "+v"(a1));
+                            y0 = (code[e] & 1) ? a0 : y0;
+                            y1 = (code[e] & 2) ? a1 : y1;
+                        }
+                        const double u0 = l * xs.x, u1 = l * xs.y;
+                        y0 = y0 - u0;
+                        y1 = y1 - u1;
+                        num[q] = num[q] + (y0 * y0 + (two ? y1 * y1 : 0.0));
+                        den[q] = den[q] + (u0 * u0 + (two ? u1 * u1 : 0.0));
+                    } else {
+                        double nu = 0.0, de = 0.0;
+                        for (int k = 0; k < 2 && r0 + k < a.n; ++k) {
+                            const int64_t rr = r0 + k;
+                            const int2 pi = a.pinfo[a.pat[rr]];
+                            double sum = 0.0;
+                            for (int e = 0; e < pi.y; ++e) {
+                                const double tv = a.pval[pi.x + e] * x[rr + a.pdelta[pi.x + e]];
+                                sum = sum + tv;
+                            }
+                            const double u = l * x[rr];
+                            const double y = sum - u;
+                            nu = nu + y * y;
+                            de = de + u * u;
+                        }
+                        num[q] = num[q] + nu;
+                        den[q] = den[q] + de;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < CPB; ++q) {
+            if (q < nq) {
+                const double nu = wave_sum(num[q]), de = wave_sum(den[q]);
+                if (lane == 0) {
+                    ws[q][0][wave] = nu;
+                    ws[q][1][wave] = de;
+                }
+            }
+        }
+        __syncthreads();
+        if (tid < 2 * CPB) {
+            const int q = tid >> 1, e = tid & 1;
+            if (q < nq)
+                partial[(2 * (int64_t)out[i0 + q] + e) * pstride + blockIdx.x] =
+                    ((ws[q][e][0] + ws[q][e][1]) + ws[q][e][2]) + ws[q][e][3];
+        }
+        __syncthreads();  // ws is rewritten by the next pair group
+    }
+}
+
 constexpr size_t kPatLdsMax = 64 * 1024;
 
 // the pair kernel needs 16-B aligned columns, rows <= 8 entries and an LDS-sized pair table
@@ -757,9 +893,32 @@ static int resid_ppt() {
     return ppt;
 }
 
+// the persistent residual kernel (CAL_RESID_PERS=1, A/B only; default the
+// 2-D grid) and its pairs per pass (CAL_RESID_PCPB = 1, 2 or 4)
+static int resid_pers() {
+    static const int v = [] {
+        const char* e = std::getenv("CAL_RESID_PERS");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+static int resid_pcpb() {
+    static const int v = [] {
+        const char* e = std::getenv("CAL_RESID_PCPB");
+        const int x = e ? std::atoi(e) : 2;
+        return x == 1 || x == 4 ? x : 2;
+    }();
+    return v;
+}
+
 int spmv_pair_resid_multi_blocks(const PatArgs& a) {
     const int nb = spmv_pair_resid_blocks(a);
-    return nb > 0 ? (nb + resid_ppt() - 1) / resid_ppt() : 0;
+    if (nb <= 0) return 0;
+    if (resid_pers()) {  // 8 XCDs x up to 256 blocks (8 per CU), a multiple of 8
+        const int per = std::max(1, std::min(256, (nb + 7) / 8));
+        return 8 * per;
+    }
+    return (nb + resid_ppt() - 1) / resid_ppt();
 }
 
 hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64_t ldx, const int* col,
@@ -776,6 +935,29 @@ hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64
     if (npr <= 0) return hipSuccess;
     if (a.pmaxlen > 8) return hipErrorInvalidValue;
     const size_t lds = (size_t)a.npent * 20 + 16;
+    if (resid_pers()) {
+        auto gop = [&](auto cpb_c) {
+            constexpr int CPB = decltype(cpb_c)::value;
+#define CAL_PRP(ML)                                                                                           \
+    hipLaunchKernelGGL((k_spmv_pair_resid_pers<ML, CPB>), dim3(blocks), dim3(256), lds, st, a, a.ppat, a.ppoff, \
+                       a.ppval, X, ldx, col, lam, out, npr, partial, pstride)
+            switch (a.pmaxlen) {
+                case 1: CAL_PRP(1); break;
+                case 2: CAL_PRP(2); break;
+                case 3: CAL_PRP(3); break;
+                case 4: CAL_PRP(4); break;
+                case 5: CAL_PRP(5); break;
+                case 6: CAL_PRP(6); break;
+                case 7: CAL_PRP(7); break;
+                default: CAL_PRP(8); break;
+            }
+#undef CAL_PRP
+        };
+        if (resid_pcpb() == 1) gop(std::integral_constant<int, 1>{});
+        else if (resid_pcpb() == 4) gop(std::integral_constant<int, 4>{});
+        else gop(std::integral_constant<int, 2>{});
+        return hipGetLastError();
+    }
     auto go2 = [&](auto cpb_c, auto ppt_c) {
         constexpr int CPB = decltype(cpb_c)::value, PPT = decltype(ppt_c)::value;
         dim3 g(blocks, (npr + CPB - 1) / CPB), bl(256);
@@ -1432,37 +1614,43 @@ __global__ __launch_bounds__(64 * WAVES) void k_apply_mt(const double* __restric
     const int c16 = lane & 15, g = lane >> 4;
     const int nkc = wpp / 4;
     const int64_t stride = (int64_t)gridDim.x * WAVES * 32;
-    for (int64_t r0 = ((int64_t)blockIdx.x * WAVES + wave) * 32; r0 < n; r0 += stride) {
+    // B operands in groups of KG k-steps, the next group's loads issued before
+    // this group's MFMAs (KG per NT from tools/ritz_apply_probe.hip); the last
+    // group of a row tile issues the NEXT row tile's first group, so its load
+    // latency hides behind this tile's last MFMAs and stores
+    auto load_group = [&](int64_t rt, int kc0, double (&b)[KG][2]) {
+        const bool fl = rt + 32 <= n;
+        const int64_t rbt = rt + 2 * c16;
+#pragma unroll
+        for (int u = 0; u < KG; ++u) {
+            const int c = 4 * (kc0 + u) + g;
+            const bool con = c < wp;
+            const double* pc = P + (int64_t)(con ? c : 0) * ldp;
+            double b0, b1;
+            if (fl) {
+                const d2 x = *reinterpret_cast<const d2*>(pc + rbt);
+                b0 = x[0];
+                b1 = x[1];
+            } else {
+                b0 = rbt < n ? pc[rbt] : 0.0;
+                b1 = rbt + 1 < n ? pc[rbt + 1] : 0.0;
+            }
+            b[u][0] = con ? b0 : 0.0;
+            b[u][1] = con ? b1 : 0.0;
+        }
+    };
+    double bcur[KG][2], bnxt[KG][2];
+    const int64_t rstart = ((int64_t)blockIdx.x * WAVES + wave) * 32;
+    if (rstart < n) load_group(rstart, 0, bcur);
+    for (int64_t r0 = rstart; r0 < n; r0 += stride) {
         const bool full = r0 + 32 <= n;
         const int64_t rb = r0 + 2 * c16;
         d4 acc[NT][2];
 #pragma unroll
         for (int ty = 0; ty < NT; ++ty) acc[ty][0] = acc[ty][1] = d4{0.0, 0.0, 0.0, 0.0};
-        // B operands in groups of KG k-steps, the next group's loads issued
-        // before this group's MFMAs (KG per NT from tools/ritz_apply_probe.hip)
-        auto load_group = [&](int kc0, double (&b)[KG][2]) {
-#pragma unroll
-            for (int u = 0; u < KG; ++u) {
-                const int c = 4 * (kc0 + u) + g;
-                const bool con = c < wp;
-                const double* pc = P + (int64_t)(con ? c : 0) * ldp;
-                double b0, b1;
-                if (full) {
-                    const d2 x = *reinterpret_cast<const d2*>(pc + rb);
-                    b0 = x[0];
-                    b1 = x[1];
-                } else {
-                    b0 = rb < n ? pc[rb] : 0.0;
-                    b1 = rb + 1 < n ? pc[rb + 1] : 0.0;
-                }
-                b[u][0] = con ? b0 : 0.0;
-                b[u][1] = con ? b1 : 0.0;
-            }
-        };
-        double bcur[KG][2], bnxt[KG][2];
-        load_group(0, bcur);
         for (int kc0 = 0; kc0 < nkc; kc0 += KG) {
-            if (kc0 + KG < nkc) load_group(kc0 + KG, bnxt);
+            if (kc0 + KG < nkc) load_group(r0, kc0 + KG, bnxt);
+            else if (r0 + stride < n) load_group(r0 + stride, 0, bnxt);
 #pragma unroll
             for (int u = 0; u < KG; ++u) {
                 const int c = 4 * (kc0 + u) + g;  // rows of Ms past wpp are never read: kc0 + u < nkc below
