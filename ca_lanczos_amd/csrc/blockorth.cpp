@@ -624,9 +624,11 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
         Qout.nseg > kMaxSeg || (int64_t)P * m > 512)
         return 2;
     const int me = c->comm ? c->comm->rank : 0;
-    const int64_t n0 = fold_tiles(n), nblk = fold_blocks(n), n1 = fold_l1_tiles(n), n2 = fold_l2_tiles(n);
+    const int64_t n0 = fold_tiles(n), nblk = fold_blocks(n);
+    const std::vector<int> nu = fold_levels(n);
+    const int nlev = (int)nu.size();
     const int64_t mm = (int64_t)m * m;
-    // workspace (doubles): level-0 tiles, then the small levels and scalars
+    // workspace (doubles): level-0 tiles, the upper levels, scalars
     const size_t t0 = fold_l0_tile_doubles(), tu = fold_tile_doubles();
     size_t off = 0;
     auto take = [&](size_t cnt) {
@@ -635,10 +637,14 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
         return o;
     };
     const size_t oV0 = take(n0 * t0), otb0 = take(n0 * 16), oR0 = take(n0 * 64), oS0 = take(n0 * 64);
-    const size_t oV1 = take(n1 * tu), otb1 = take(n1 * 16), oR1 = take(n1 * 64), oS1 = take(n1 * 64);
-    const size_t oV2 = take(n2 * tu), otb2 = take(n2 * 16), oR2 = take(n2 * 64), oS2 = take(n2 * 64);
-    const size_t oV3 = take(tu), otb3 = take(16);
-    const size_t oRr = take(64), oRrm = take(64), oSb = take(64), oSm = take(64), oK = take(72);
+    size_t oVu[3], otbu[3], oRu[3], oSu[3];
+    for (int L = 0; L < nlev; ++L) {
+        oVu[L] = take((size_t)nu[L] * tu);
+        otbu[L] = take((size_t)nu[L] * 16);
+        oRu[L] = take((size_t)nu[L] * 64);
+        oSu[L] = take((size_t)nu[L] * 64);
+    }
+    const size_t oRrm = take(64), oSb = take(64), oSm = take(64), oK = take(72);
     const size_t oOut = take(520), oT1 = take(272), oT2 = take(272);
     const size_t oG = take((size_t)P * mm), oGup = take(mm), oGdn = take((size_t)P * mm);
     if (off > c->fold_cap) {
@@ -655,8 +661,7 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
     fa.w = w;
     fa.nblk = (int)nblk;
     fa.n0 = (int)n0;
-    fa.n1 = (int)n1;
-    fa.n2 = (int)n2;
+    fa.nlev = nlev;
     fa.C = F + oT1;
     fa.flags = d_out + 512;
     fa.K = F + oK;
@@ -664,17 +669,13 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
     fa.tb0 = F + otb0;
     fa.R0 = F + oR0;
     fa.S0 = F + oS0;
-    fa.V1 = F + oV1;
-    fa.tb1 = F + otb1;
-    fa.R1 = F + oR1;
-    fa.S1 = F + oS1;
-    fa.V2 = F + oV2;
-    fa.tb2 = F + otb2;
-    fa.R2 = F + oR2;
-    fa.S2 = F + oS2;
-    fa.V3 = F + oV3;
-    fa.tb3 = F + otb3;
-    fa.Rroot = F + oRr;
+    for (int L = 0; L < nlev; ++L) {
+        fa.nu[L] = nu[L];
+        fa.Vu[L] = F + oVu[L];
+        fa.tbu[L] = F + otbu[L];
+        fa.Ru[L] = F + oRu[L];
+        fa.Su[L] = F + oSu[L];
+    }
     fa.Rroot_m = F + oRrm;
     const Panel W = panel_concat(Qp, X);
     // P1: [Qp(0:nq) | X]' X (+ Qp column 8), the CholQR2 path's row Gram
@@ -709,10 +710,10 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
         timer_end(c, t);
     }
     CAL_HIP(c, launch_fold_reduce(c->d_partial, (int)nblk, F + oT2, c->stream));
-    CAL_TRY(allreduce_sum(c, F + oT2, 272));
+    CAL_TRY(allreduce_sum(c, F + oT2, 72));
     // the root over the ranks: all-gather the local roots, factor the stack
     // (the tree kernel's stack level, redundantly on every rank)
-    const double* Rtop = fa.Rroot;
+    const double* Rtop = fa.Ru[nlev - 1];  // the root level's one R
     int ldr = 8;
     TsqrLevelArgs ga;
     TsqrCols gcols{};

@@ -312,33 +312,35 @@ hipError_t launch_tsqr(bool down, int src, const TsqrLevelArgs& a, const TsqrCol
 
 // ---- projectAndNormalize with the fused TSQR (tsqr_fold.hip) ----------------
 // Workspace of one fused block (8-wide register tiles): level 0 (n0 tiles of
-// 256 rows: factored tiles V0 / tau-beta tb0, R factors R0, S blocks S0),
-// level 1 (n1 tiles of 64 level-0 R factors: V1 / tb1 / R1 / S1), level 2
-// (n2 tiles: V2 / tb2 / R2 / S2) and the root (V3 / tb3; Rroot, and Rroot_m with
-// ld m); the P1 tile C, K (9 x 8), the flags (out[512..515]) and the Gram
-// partials (272 x nblk, entry-major).
+// 256 rows: factored tiles V0 / tau-beta tb0, R factors R0, S blocks S0), the
+// upper levels L = 1 .. nlev (nu[L-1] tiles of 64 R factors of the level
+// below: Vu / tbu / Ru / Su; level nlev is the root, one tile; Rroot_m its R
+// with ld m), the P1 tile C, K (9 x 8), the flags (out[512..515]) and the
+// C2 = Qp'Y partials (72 x nblk, entry-major).
 struct FoldArgs {
     int64_t n = 0;
-    int m = 0, w = 0, nblk = 0, n0 = 0, n1 = 0, n2 = 0;
+    int m = 0, w = 0, nblk = 0, n0 = 0, nlev = 0;
+    int nu[3] = {0, 0, 0};
     const double* C = nullptr;  // the reduced P1 tile (272 doubles): C = Qp'X is read from it
     const double* flags = nullptr;
     const double* K = nullptr;
     double *V0 = nullptr, *tb0 = nullptr, *R0 = nullptr, *S0 = nullptr;
-    double *V1 = nullptr, *tb1 = nullptr, *R1 = nullptr, *S1 = nullptr;
-    double *V2 = nullptr, *tb2 = nullptr, *R2 = nullptr, *S2 = nullptr;
-    double *V3 = nullptr, *tb3 = nullptr, *Rroot = nullptr, *Rroot_m = nullptr;
+    double* Vu[3] = {nullptr, nullptr, nullptr};
+    double* tbu[3] = {nullptr, nullptr, nullptr};
+    double* Ru[3] = {nullptr, nullptr, nullptr};
+    double* Su[3] = {nullptr, nullptr, nullptr};
+    double* Rroot_m = nullptr;
     double* partial = nullptr;
 };
-int fold_tiles(int64_t n);     // level-0 tiles
-int fold_blocks(int64_t n);    // k_fold_up / k_fold_down blocks
-int fold_l1_tiles(int64_t n);
-int fold_l2_tiles(int64_t n);
+int fold_tiles(int64_t n);                 // level-0 tiles
+int fold_blocks(int64_t n);                // k_fold_up / k_fold_down blocks
+std::vector<int> fold_levels(int64_t n);   // tiles of the upper levels (the last: the root)
 bool fold_shape_ok(int64_t n, int m, int w);
 size_t fold_l0_tile_doubles();  // one level-0 tile
-size_t fold_tile_doubles();     // one upper-level tile
+size_t fold_tile_doubles();     // one upper-level tile (512 x 8)
 hipError_t launch_fold_up(const ColList& P, const FoldArgs& a, hipStream_t st);
 hipError_t launch_fold_tree(const FoldArgs& a, hipStream_t st);  // levels 1, 2 and the root
-hipError_t launch_fold_reduce(const double* partial, int nparts, double* out, hipStream_t st);  // 272 entries
+hipError_t launch_fold_reduce(const double* partial, int nparts, double* out, hipStream_t st);  // the 72 C2 entries
 // k_fold_coef1: T1 the reduced P1 tile, G the up launch's Gram tile, Rtop the
 // root R (ld ldr); writes out (R, RY, flags), S_top (Sbuf ld 8, Sm ld m), K
 // and publishes R / RY / flags to hout, then seq to *hseq

@@ -10,7 +10,7 @@
 //           register-tile Householder QR of Y (256-row tiles, one per wave),
 //           and -- from the same registers -- the Gram [Qp | Y]'[Qp | Y] on
 //           the matrix cores, i.e. the second projection's C2 = Qp'Y (:63).
-//   tree    k_fold_tree: the stacked tile R factors, 64 per 512-row tile,
+//   tree    k_fold_tree: the stacked tile R factors, 256 per 2048-row tile,
 //           level by level to the local root (one block per tile).
 //   coef1   k_fold_coef1: Y = Q_Y R_Y from the tree.  With the second
 //           projection Z = Y - Qp C2, Z'Z = Y'Y - C2'C2, so with W = C2 R_Y^-1:
@@ -21,7 +21,7 @@
 //           its job (||W|| << 1): the explicit-Z path (blockorth.cpp pn_tsqr)
 //           is taken instead when ||W||_F > 1/2.  R = R_Z, RY = C + C2
 //           (:71-73), the flag, published to pinned host memory.
-//   down    k_fold_down_root / _level: the tree walked down (explicit Q factors of
+//   down    k_fold_down_level: the tree walked down (explicit Q factors of
 //           the stored tiles times the parent's S); k_fold_down: level 0,
 //           Q = Q_tile S - Qp K, one store.
 //
@@ -30,6 +30,8 @@
 // projection runs) + m·8n (Q).  Everything above level 0 is n/64 rows.
 #include "cal_internal.hpp"
 #include "tsqr_tile.hpp"
+
+#include <vector>
 
 namespace cal {
 
@@ -42,10 +44,11 @@ typedef double fd2 __attribute__((ext_vector_type(2)));
 constexpr int FM = 8;             // register tile width (m <= 8)
 constexpr int L0RPL = 4;          // rows per lane of a level-0 tile
 constexpr int FTR0 = 64 * L0RPL;  // 256 rows per level-0 tile
-constexpr int FRPL = 8;           // rows per lane of an upper-level tile
-constexpr int FTR = 64 * FRPL;    // 512 rows: 64 R factors of the level below
-constexpr int FTPB = 4;           // tiles (waves) per block
-constexpr int FG = FTR / FM;      // tiles per upper-level tile (64 R factors of m = 8 rows)
+constexpr int FTPB = 4;           // level-0 tiles (waves) per block
+constexpr int UW = 4;             // waves of an upper-level block (one tile per block)
+constexpr int URPL = 2;           // rows per lane of each wave's share of an upper tile
+constexpr int FTR = 64 * URPL * UW;  // 512 rows per upper tile
+constexpr int FG = FTR / FM;      // R factors (of the level below) per upper tile: 64
 constexpr int FTLD = 17;        // padded LDS row of the Gram transpose
 // timing-probe switches (tools/fold_probe.hip; never set in the library)
 #ifndef FOLD_PROBE
@@ -145,14 +148,16 @@ __device__ __forceinline__ void fmul_S(const double (&q)[FM], const double* S, i
 
 // Level-0 tile formation (256 rows, chunk i = rows base + lane + 64 i):
 // Y = X - Qp C (project.m:30; the product first, k ascending) into the
-// register tile x; with GRAM also [Qp(0:8) | Y] (+ Qp column 8) through the
-// wave's LDS rows tlw onto the matrix cores (acc: the 16 x 16 Gram, acc2:
-// Qp(:,8)'[...]).  k_fold_up and k_fold_down_reform run the same code on the
+// register tile x; with GRAM also the rows [Qp(0:9) | Y] through the wave's
+// LDS rows tlw onto the matrix cores: one v_mfma_f64_16x16x4f64 per 4 rows
+// with A = the rows' first 16 columns, B = the 16 columns from column 9 on,
+// so acc(i, j) accumulates C2(i, j) = Qp(:,i)'Y(:,j) for i < 9, j < 8 (the
+// other outputs are unused; tlw has FTLD + 16 spare doubles for B's tail).  k_fold_up and k_fold_down_reform run the same code on the
 // same inputs, so the tile QR that follows gives the same reflectors in both.
 template <bool GRAM>
 __device__ __forceinline__ void fform(const ColList P, const double* Cs, double* tlw, int64_t base, int64_t n,
-                                      int lane, int m, int w, double (&x)[L0RPL][FM], fd4& acc, fd4& acc2) {
-    const int c16 = lane & 15, g = lane >> 4, nq = w < 8 ? w : 8;
+                                      int lane, int m, int w, double (&x)[L0RPL][FM], fd4& acc) {
+    const int c16 = lane & 15, g = lane >> 4;
     double p[17];
     auto load = [&](int i) {
         const int64_t r = base + lane + 64 * i;
@@ -189,10 +194,9 @@ __device__ __forceinline__ void fform(const ColList P, const double* Cs, double*
         if (GRAM) {
             double* trow = tlw + lane * FTLD;
 #pragma unroll
-            for (int cc = 0; cc < 8; ++cc) trow[cc] = (in && cc < nq) ? p[cc] : 0.0;
+            for (int cc = 0; cc < 9; ++cc) trow[cc] = (in && cc < w) ? p[cc] : 0.0;
 #pragma unroll
-            for (int cc = 0; cc < 8; ++cc) trow[8 + cc] = x[i][cc];
-            trow[16] = (in && w > 8) ? p[8] : 0.0;
+            for (int cc = 0; cc < 8; ++cc) trow[9 + cc] = x[i][cc];
         }
         if (i + 1 < L0RPL) load(i + 1);  // the next chunk's loads fly during the Gram
         if (GRAM) {
@@ -200,13 +204,10 @@ __device__ __forceinline__ void fform(const ColList P, const double* Cs, double*
             if (!(kProbe & 2)) {
 #pragma unroll
                 for (int kk = 0; kk < 16; ++kk) {
-                    // tile'tile, and Qp(:,8)'tile as a second MFMA whose A rows
-                    // all hold the extra column (every output row is the same sum)
                     const int row = 4 * kk + g;
                     const double av = tlw[row * FTLD + c16];
-                    const double ev = tlw[row * FTLD + 16];
-                    acc = fmfma(av, av, acc);
-                    acc2 = fmfma(ev, av, acc2);
+                    const double bv = tlw[row * FTLD + 9 + c16];
+                    acc = fmfma(av, bv, acc);
                 }
             }
             fwsync();
@@ -222,7 +223,7 @@ __device__ __forceinline__ void fform(const ColList P, const double* Cs, double*
 // keep their next chunk's 17 column loads in flight.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FOLD_UP_WPE))) void k_fold_up(ColList P, FoldArgs a) {
     __shared__ double Cs[9 * FM];
-    __shared__ double tl[FTPB][64 * FTLD];  // per-wave Gram transpose; then the block's partials
+    __shared__ double tl[FTPB][64 * FTLD + 16];  // per-wave Gram transpose; then the block's partials
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int c16 = lane & 15, g = lane >> 4;
     const int m = a.m, w = a.w;
@@ -239,12 +240,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FOLD_UP_WPE
     const int64_t ntiles = (n + FTR0 - 1) / FTR0;
     const int64_t tile = (int64_t)b * FTPB + wave;
     fd4 acc = fd4{0.0, 0.0, 0.0, 0.0};
-    fd4 acc2 = fd4{0.0, 0.0, 0.0, 0.0};
     if (tile < ntiles) {
         const int64_t base = tile * FTR0;
         double x[L0RPL][FM];
         double tau[FM], beta[FM];
-        fform<true>(P, Cs, tl[wave], base, n, lane, m, w, x, acc, acc2);
+        fform<true>(P, Cs, tl[wave], base, n, lane, m, w, x, acc);
         if (!(kProbe & 4)) tile_geqr2<FM, L0RPL>(x, tau, beta, m, lane);
         if (a.V0 && !(kProbe & 8)) {  // stored for the down pass (V0 null: it re-forms the tile)
             fstore_tile<L0RPL>(a.V0 + tile * (64 * L0RPL * FM), lane, x);
@@ -253,80 +253,62 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FOLD_UP_WPE
         fput_R(a.R0 + tile * 64, lane, m, x[0]);
     }
     __syncthreads();  // the transposes are done (tl is reused below)
-    // the block's Gram partial (entry-major, as k_rowapply's)
+    // the block's C2 partial: entry i + 9 j (i < 9, j < 8), entry-major
     double* red = &tl[0][0];
     if (wave > 0) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) red[((wave - 1) * 64 + lane) * 5 + r] = acc[r];
-        red[((wave - 1) * 64 + lane) * 5 + 4] = acc2[0];
+        for (int r = 0; r < 4; ++r) red[((wave - 1) * 64 + lane) * 4 + r] = acc[r];
     }
     __syncthreads();
     if (wave == 0) {
         const int64_t nb = a.nblk;
         double* out = a.partial + b;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < 3; ++r) {
             double v = acc[r];
-            v = v + red[(0 * 64 + lane) * 5 + r];
-            v = v + red[(1 * 64 + lane) * 5 + r];
-            v = v + red[(2 * 64 + lane) * 5 + r];
-            out[(int64_t)(c16 * 16 + g + 4 * r) * nb] = v;
+            v = v + red[(0 * 64 + lane) * 4 + r];
+            v = v + red[(1 * 64 + lane) * 4 + r];
+            v = v + red[(2 * 64 + lane) * 4 + r];
+            const int i = g + 4 * r, j = c16;  // acc[r] of lane l holds D(g + 4r, c16)
+            if (i < 9 && j < 8) out[(int64_t)(i + 9 * j) * nb] = v;
         }
-        double e = acc2[0];
-        e = e + red[(0 * 64 + lane) * 5 + 4];
-        e = e + red[(1 * 64 + lane) * 5 + 4];
-        e = e + red[(2 * 64 + lane) * 5 + 4];
-        if (g == 0) out[(int64_t)(256 + c16) * nb] = e;
     }
 }
 
-// The tree above level 0: one 512-row tile (64 R factors of the level
-// below) per block, spread over its 4 waves (128 rows each) with the
+// The tree above level 0: one 512-row tile (64 R factors of the level below,
+// 8 rows each) per block, spread over its 4 waves (128 rows each) with the
 // block-cooperative tile QR -- these launches are latency-bound, one tile's
-// QR deep, and one wave alone takes ~18 us for it.  k_fold_tree: level 1 (n1
-// blocks), level 2 (n2 blocks), the root (one block, the level-2 R factors,
-// <= 512 rows).  Kernel boundaries order the levels (a device-scope release
-// in every block of a launch writes each XCD's L2 back: 2.8 ms measured when
-// k_fold_up did that).
-constexpr int BRPL = FRPL / FTPB;  // rows per lane of one wave's share of a 512-row tile
-__device__ __forceinline__ void fold_level_up(const double* Rin, int64_t rows, double* V, double* tb, double* Rout,
-                                              double* Rout_m, int m, int lane, int wave, double* xlds) {
-    double x[BRPL][FM], tau[FM], beta[FM];
-    fload_stack<BRPL>(Rin, (int64_t)wave * 64 * BRPL, rows, lane, x);
-    tile_geqr2_blk<FM, BRPL, FTPB>(x, tau, beta, m, lane, wave, xlds);
-    fstore_tile<BRPL>(V + (int64_t)wave * BRPL * FM * 64, lane, x);
-    if (wave == 0) {
-        fstore_tb(tb, lane, tau, beta);
-        fput_R(Rout, lane, m, x[0]);
-        // the same R with leading dimension m (the stack layout of tsqr.hip,
-        // for the all-gather of the local roots over several ranks)
-        if (Rout_m && lane < m)
-            for (int cc = 0; cc < m; ++cc) Rout_m[lane + cc * m] = cc >= lane ? x[0][cc] : 0.0;
-    }
-}
-
-// level: 1 (R0 -> V1 / R1), 2 (R1 -> V2 / R2), 3 (the root: R2 -> V3 / Rroot)
-__global__ __launch_bounds__(256) void k_fold_tree(FoldArgs a, int level) {
-    __shared__ double xlds[2 * FTPB * 2 * FM];
+// QR deep: ~18 us for one wave alone, ~8 us over 4 waves (2048-row tiles over
+// 8 or 16 waves, one level fewer, measured 2x and 9x slower per level: the
+// per-reflector LDS exchange grows with the waves).  Level L = 1 .. nlev, the
+// last one the root (one tile): three levels up to 67 M rows.
+// Kernel boundaries order the levels (a device-scope release in every block
+// of a launch writes each XCD's L2 back: 2.8 ms measured when k_fold_up did).
+__global__ __launch_bounds__(64 * UW) void k_fold_tree(FoldArgs a, int L) {
+    __shared__ double xlds[2 * UW * 2 * FM];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = a.m;
     const int t = blockIdx.x;
-    if (level == 1) {
-        const int64_t rows = (int64_t)((a.n0 - t * FG) < FG ? (a.n0 - t * FG) : FG) * FM;
-        fold_level_up(a.R0 + (int64_t)t * FG * 64, rows, a.V1 + (int64_t)t * (64 * FRPL * FM),
-                      a.tb1 + (int64_t)t * (2 * FM), a.R1 + (int64_t)t * 64, nullptr, m, lane, wave, xlds);
-    } else if (level == 2) {
-        const int64_t rows = (int64_t)((a.n1 - t * FG) < FG ? (a.n1 - t * FG) : FG) * FM;
-        fold_level_up(a.R1 + (int64_t)t * FG * 64, rows, a.V2 + (int64_t)t * (64 * FRPL * FM),
-                      a.tb2 + (int64_t)t * (2 * FM), a.R2 + (int64_t)t * 64, nullptr, m, lane, wave, xlds);
-    } else {
-        fold_level_up(a.R2, (int64_t)a.n2 * FM, a.V3, a.tb3, a.Rroot, a.Rroot_m, m, lane, wave, xlds);
+    const double* Rin = L == 1 ? a.R0 : a.Ru[L - 2];
+    const int nin = L == 1 ? a.n0 : a.nu[L - 2];
+    const int64_t rows = (int64_t)((nin - t * FG) < FG ? (nin - t * FG) : FG) * FM;
+    double x[URPL][FM], tau[FM], beta[FM];
+    fload_stack<URPL>(Rin + (int64_t)t * FG * 64, (int64_t)wave * 64 * URPL, rows, lane, x);
+    tile_geqr2_blk<FM, URPL, UW>(x, tau, beta, m, lane, wave, xlds);
+    fstore_tile<URPL>(a.Vu[L - 1] + (int64_t)t * (64 * URPL * UW * FM) + (int64_t)wave * URPL * FM * 64, lane, x);
+    if (wave == 0) {
+        fstore_tb(a.tbu[L - 1] + (int64_t)t * (2 * FM), lane, tau, beta);
+        fput_R(a.Ru[L - 1] + (int64_t)t * 64, lane, m, x[0]);
+        // the root's R with leading dimension m as well (the stack layout of
+        // tsqr.hip, for the all-gather of the local roots over several ranks)
+        if (L == a.nlev && lane < m)
+            for (int cc = 0; cc < m; ++cc) a.Rroot_m[lane + cc * m] = cc >= lane ? x[0][cc] : 0.0;
     }
 }
 
 // ---- the s x s algebra --------------------------------------------------
 // Phase 1 (after the tree, the Gram tile reduced, and on several ranks the
-// global levels): Rtop the root R (ld ldr, raw signs), G the Gram tile
-// [Qp(0:8) | Y]'[...] (+ Qp column 8).  Writes S_top (8 x 8, ld 8; and ld m
+// global levels): Rtop the root R (ld ldr, raw signs), G the up launch's
+// reduced C2 = Qp'Y (9 x 8, ld 9).  Writes S_top (8 x 8, ld 8; and ld m
 // to Sm), K (9 x 8, ld 9), out (R, RY, flags) and publishes out.  One wave;
 // the 8 x 8 matrices in LDS (column-major, ld 8), entry (r, c) computed by
 // lane r + 8c, triangular inverses by one lane per column.
@@ -350,65 +332,61 @@ __global__ __launch_bounds__(64) void k_fold_coef1(const double* __restrict__ T1
                                                   double* __restrict__ Kbuf, int w, int m, int doreorth, double nglob,
                                                   double* __restrict__ hout,
                                                   unsigned long long* __restrict__ hseq, unsigned long long seq) {
-    __shared__ double RY[64], Ri[64], Ws[9 * FM], U[64], Ui[64], D[FM], red[64], rel[FM], nrm[FM];
+    __shared__ double Cs[9 * FM], C2s[9 * FM], RT[64], XX[FM];
+    __shared__ double RY[64], Ri[64], Ws[9 * FM], U[64], Ui[64], D[FM];
     __shared__ int fail, reo;
     const int lane = threadIdx.x, r = lane & 7, c = lane >> 3, nq = w < 8 ? w : 8;
-    // from the P1 tile T1: C = Qp'X, and the reorth test of
-    // projectAndNormalize.m:17-22,45-52 on the algebraic norms
-    // ||Y_j||^2 = X_j'X_j - C_j'C_j
-    auto cq = [&](int i, int j) { return i < 8 ? T1[i + (nq + j) * 16] : T1[256 + nq + j]; };
-    if (lane < m) {
-        const int j = lane;
-        double cc = 0.0;
-        for (int k = 0; k < w; ++k) {
-            const double v = cq(k, j);
-            cc = cc + v * v;
-        }
-        const double xx = T1[(nq + j) + (nq + j) * 16];
-        const double before = sqrt(xx);
-        const double after = sqrt(fmax(xx - cc, 0.0));
-        rel[j] = fabs(before - after) / before;
-        nrm[j] = before;
+    const bool in = r < m && c < m;
+    // stage every input once (one round of global loads): C = Qp'X and the
+    // diagonal X'X from the P1 tile T1, C2 = Qp'Y from the Gram tile G, the
+    // root R (ld ldr, raw signs)
+    for (int e = lane; e < 9 * FM; e += 64) {
+        const int i = e % 9, j = e / 9;
+        const bool ok = i < w && j < m;
+        Cs[e] = ok ? (i < 8 ? T1[i + (nq + j) * 16] : T1[256 + nq + j]) : 0.0;
+        C2s[e] = ok ? G[e] : 0.0;  // the up launch's reduced Qp'Y (entry i + 9 j)
     }
+    RT[lane] = in ? Rtop[r + c * ldr] : 0.0;
+    if (lane < FM) XX[lane] = lane < m ? T1[(nq + lane) + (nq + lane) * 16] : 0.0;
     __syncthreads();
-    double xmax = 0.0;
+    // the reorth test of projectAndNormalize.m:17-22,45-52 on the algebraic
+    // norms ||Y_j||^2 = X_j'X_j - C_j'C_j (NaN-ignoring max in column order)
     if (lane == 0) {
         double mx = NAN;
         for (int j = 0; j < m; ++j) {
-            const double rj = rel[j];
+            double cc = 0.0;
+            for (int k = 0; k < w; ++k) cc = cc + Cs[k + j * 9] * Cs[k + j * 9];
+            const double before = sqrt(XX[j]);
+            const double after = sqrt(fmax(XX[j] - cc, 0.0));
+            const double rj = fabs(before - after) / before;
             if (!isnan(rj) && (isnan(mx) || rj > mx)) mx = rj;
         }
         reo = (w > 0 && doreorth && mx > 0.5) ? 1 : 0;
+        fail = 0;
         out[512] = 0.0;
         out[514] = reo ? 1.0 : 0.0;
     }
-    for (int j = 0; j < m; ++j) xmax = fmax(xmax, nrm[j]);
-    __syncthreads();
-    const bool reorth = reo != 0;
-    const bool in = r < m && c < m;
     if (lane < FM) {
-        const double rii = lane < m ? Rtop[lane + lane * ldr] : 0.0;
+        const double rii = RT[lane * 9];
         D[lane] = rii > 0.0 ? 1.0 : (rii < 0.0 ? -1.0 : 0.0);  // sign(0) = 0 (tsqr.m:9-10)
     }
-    if (lane == 0) fail = 0;
     U[lane] = (r == c && r < m) ? 1.0 : 0.0;
     Ui[lane] = U[lane];
     __syncthreads();
-    RY[lane] = (in && r <= c) ? D[r] * Rtop[r + c * ldr] : 0.0;  // R_Y = D R
+    double xmax = 0.0;
+    for (int j = 0; j < m; ++j) xmax = fmax(xmax, sqrt(XX[j]));
+    const bool reorth = reo != 0;
+    RY[lane] = (in && r <= c) ? D[r] * RT[lane] : 0.0;  // R_Y = D R
     __syncthreads();
     double est = 0.0;
     if (reorth) {
         if (lane < FM) finv_col(RY, Ri, lane, m);  // R_Y^-1 (Inf / NaN at a zero pivot)
         __syncthreads();
-        // W = C2 R_Y^-1 (w x m), C2 = Qp'Y from the Gram tile
+        // W = C2 R_Y^-1 (w x m)
         for (int e = lane; e < 9 * FM; e += 64) {
             const int i = e % 9, cc = e / 9;
             double v = 0.0;
-            if (i < w && cc < m)
-                for (int k = 0; k <= cc; ++k) {
-                    const double c2 = i < 8 ? G[i + (8 + k) * 16] : G[256 + 8 + k];
-                    v = v + c2 * Ri[k + cc * FM];
-                }
+            for (int k = 0; k <= cc; ++k) v = v + C2s[i + k * 9] * Ri[k + cc * FM];
             Ws[i + cc * 9] = v;
         }
         __syncthreads();
@@ -428,28 +406,23 @@ __global__ __launch_bounds__(64) void k_fold_coef1(const double* __restrict__ T1
         // ||E|| <~ u sqrt(n) max||X_j|| ||R_Y^-1||; decline (explicit Z)
         // unless that is below kFoldTol and ||W||_F <= 1/2
         est = 2.0 * sqrt(nw) * 0x1p-53 * sqrt(nglob) * xmax * sqrt(nri);
-        red[lane] = a;
-        __syncthreads();
-        if (lane == 0) {
-            // U = chol(A) (upper), serially (host dense::chol_upper's order)
-            int bad = !(nw <= 0.25) || !(est <= kFoldTol);  // also NaN / Inf
-            for (int j = 0; j < m && !bad; ++j) {
-                double sj = red[j + j * FM];
-                for (int k = 0; k < j; ++k) sj = sj - U[k + j * FM] * U[k + j * FM];
-                if (!(sj > 0.0) || !isfinite(sj)) {
-                    bad = 1;
-                    break;
-                }
-                const double ujj = sqrt(sj);
-                U[j + j * FM] = ujj;
-                for (int i = j + 1; i < m; ++i) {
-                    double t = red[j + i * FM];
-                    for (int k = 0; k < j; ++k) t = t - U[k + j * FM] * U[k + i * FM];
-                    U[j + i * FM] = t / ujj;
-                }
+        int bad = !(nw <= 0.25) || !(est <= kFoldTol);  // also NaN / Inf
+        // U = chol(A), upper, in registers: lane (r, c), pivot rows by
+        // shuffles (dense::chol_upper's operations and order)
+        double uv = 0.0;
+        for (int j = 0; j < m && !bad; ++j) {
+            const double sj = __shfl(a, j + 8 * j, 64);
+            if (!(sj > 0.0) || !isfinite(sj)) {
+                bad = 1;
+                break;
             }
-            fail = bad;
+            const double ujj = sqrt(sj);
+            if (r == j) uv = c == j ? ujj : (c > j && c < m ? a / ujj : 0.0);
+            const double ujr = __shfl(uv, j + 8 * r, 64), ujc = __shfl(uv, j + 8 * c, 64);
+            if (r > j && c >= r) a = a - ujr * ujc;
         }
+        if (!bad) U[lane] = (in && r <= c) ? uv : 0.0;
+        if (lane == 0) fail = bad;
         __syncthreads();
         if (!fail && lane < FM) finv_col(U, Ui, lane, m);
         __syncthreads();
@@ -477,8 +450,7 @@ __global__ __launch_bounds__(64) void k_fold_coef1(const double* __restrict__ T1
         // RY = C + C2 (projectAndNormalize.m:71-73)
         for (int e = lane; e < w * m; e += 64) {
             const int i = e % w, j = e / w;
-            const double c2 = reorth ? (i < 8 ? G[i + (8 + j) * 16] : G[256 + 8 + j]) : 0.0;
-            out[256 + e] = cq(i, j) + c2;
+            out[256 + e] = Cs[i + j * 9] + (reorth ? C2s[i + j * 9] : 0.0);
         }
     }
     __syncthreads();
@@ -524,13 +496,13 @@ __global__ __launch_bounds__(1024) void k_fold_reduce(const double* __restrict__
 // (rows r < rows of the tile: block blk0 + (r >> 3) of Sb, row r & 7).
 __device__ __forceinline__ void fold_level_down(const double* V, const double* tb, const double* Ss, int64_t rows,
                                                 double* Sb, int64_t blk0, int m, int lane, int wave, double* xlds) {
-    double x[BRPL][FM], tau[FM];
-    fload_tile<BRPL>(V + (int64_t)wave * BRPL * FM * 64, lane, x);
+    double x[URPL][FM], tau[FM];
+    fload_tile<URPL>(V + (int64_t)wave * URPL * FM * 64, lane, x);
     fload_tau(tb, tau);
-    tile_org2r_blk<FM, BRPL, FTPB>(x, tau, m, lane, wave, xlds);
+    tile_org2r_blk<FM, URPL, UW>(x, tau, m, lane, wave, xlds);
 #pragma unroll
-    for (int i = 0; i < BRPL; ++i) {
-        const int64_t r = (int64_t)wave * 64 * BRPL + lane + 64 * i;
+    for (int i = 0; i < URPL; ++i) {
+        const int64_t r = (int64_t)wave * 64 * URPL + lane + 64 * i;
         double o[FM];
         fmul_S(x[i], Ss, m, o);
         if (r < rows) {
@@ -540,33 +512,28 @@ __device__ __forceinline__ void fold_level_down(const double* V, const double* t
     }
 }
 
-// The root: its Q factor times S_top (ld lds) -> the level-2 tiles' S blocks.
-__global__ __launch_bounds__(256) void k_fold_down_root(FoldArgs a, const double* __restrict__ Stop, int lds) {
+// Level L down (L = nlev: the root, whose S is S_top, ld lds; below it the
+// level's own S blocks), one block per tile -> the S blocks of level L - 1.
+__global__ __launch_bounds__(64 * UW) void k_fold_down_level(FoldArgs a, int L, const double* __restrict__ Stop,
+                                                             int lds) {
     __shared__ double Ss[64];
-    __shared__ double xlds[2 * FTPB * 2 * FM];
+    __shared__ double xlds[2 * UW * 2 * FM];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = a.m;
+    const int t = blockIdx.x;
     if (tid < 64) {
-        const int k = tid & 7, cc = tid >> 3;
-        Ss[tid] = (k < m && cc < m) ? Stop[k + cc * lds] : 0.0;
+        if (L == a.nlev) {
+            const int k = tid & 7, cc = tid >> 3;
+            Ss[tid] = (k < m && cc < m) ? Stop[k + cc * lds] : 0.0;
+        } else {
+            Ss[tid] = a.Su[L - 1][(int64_t)t * 64 + tid];
+        }
     }
     __syncthreads();
-    fold_level_down(a.V3, a.tb3, Ss, (int64_t)a.n2 * FM, a.S2, 0, m, lane, wave, xlds);
-}
-
-// One upper level down: one block per tile of the level (Vl / tbl, S blocks
-// Sl) -> the S blocks of the level below (Sb, nb blocks in all).
-__global__ __launch_bounds__(256) void k_fold_down_level(const double* __restrict__ Vl, const double* __restrict__ tbl,
-                                                         const double* __restrict__ Sl, double* __restrict__ Sb, int nb,
-                                                         int m) {
-    __shared__ double Ss[64];
-    __shared__ double xlds[2 * FTPB * 2 * FM];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int t = blockIdx.x;
-    if (tid < 64) Ss[tid] = Sl[(int64_t)t * 64 + tid];
-    __syncthreads();
+    const int nb = L == 1 ? a.n0 : a.nu[L - 2];
+    double* Sb = L == 1 ? a.S0 : a.Su[L - 2];
     const int64_t rows = (int64_t)((nb - t * FG) < FG ? (nb - t * FG) : FG) * FM;
-    fold_level_down(Vl + (int64_t)t * (64 * FRPL * FM), tbl + (int64_t)t * (2 * FM), Ss, rows, Sb, (int64_t)t * FG, m,
-                    lane, wave, xlds);
+    fold_level_down(a.Vu[L - 1] + (int64_t)t * (64 * URPL * UW * FM), a.tbu[L - 1] + (int64_t)t * (2 * FM), Ss, rows,
+                    Sb, (int64_t)t * FG, m, lane, wave, xlds);
 }
 
 // Level 0: Q = Q_tile S - Qp K, one store.  Q: output columns (slots >= m
@@ -658,8 +625,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FOLD_UP_WPE
     Ss[wave][lane] = a.S0[tile * 64 + lane];
     const int64_t base = tile * FTR0;
     double x[L0RPL][FM], tau[FM], beta[FM];
-    fd4 d0 = fd4{0.0, 0.0, 0.0, 0.0}, d1 = d0;
-    fform<false>(P, Cs, nullptr, base, n, lane, m, w, x, d0, d1);
+    fd4 d0 = fd4{0.0, 0.0, 0.0, 0.0};
+    fform<false>(P, Cs, nullptr, base, n, lane, m, w, x, d0);
     tile_geqr2<FM, L0RPL>(x, tau, beta, m, lane);
     tile_org2r<FM, L0RPL>(x, tau, m, lane);
     fwsync();
@@ -702,27 +669,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FOLD_UP_WPE
 
 int fold_tiles(int64_t n) { return (int)((n + FTR0 - 1) / FTR0); }
 int fold_blocks(int64_t n) { return (fold_tiles(n) + FTPB - 1) / FTPB; }
-int fold_l1_tiles(int64_t n) { return (fold_tiles(n) + FG - 1) / FG; }
-int fold_l2_tiles(int64_t n) { return (fold_l1_tiles(n) + FG - 1) / FG; }
+// tiles of the upper levels 1, 2, ... (the last one has one tile: the root)
+std::vector<int> fold_levels(int64_t n) {
+    std::vector<int> nu;
+    int64_t cnt = fold_tiles(n);
+    do {
+        cnt = (cnt + FG - 1) / FG;
+        nu.push_back((int)cnt);
+    } while (cnt > 1);
+    return nu;
+}
 bool fold_shape_ok(int64_t n, int m, int w) {
     if (n < 1 || m < 1 || m > FM || w < 1 || w > 9) return false;
-    return fold_l2_tiles(n) <= FG;  // the root stack fits one 512-row tile (n <= 67M rows)
+    return fold_levels(n).size() <= 3;  // up to 64^3 level-0 tiles
 }
 size_t fold_l0_tile_doubles() { return (size_t)64 * L0RPL * FM; }
-size_t fold_tile_doubles() { return (size_t)64 * FRPL * FM; }
+size_t fold_tile_doubles() { return (size_t)64 * URPL * UW * FM; }
 
 hipError_t launch_fold_up(const ColList& P, const FoldArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_fold_up, dim3(a.nblk), dim3(256), 0, st, P, a);
     return hipGetLastError();
 }
 hipError_t launch_fold_tree(const FoldArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(k_fold_tree, dim3(a.n1), dim3(256), 0, st, a, 1);
-    hipLaunchKernelGGL(k_fold_tree, dim3(a.n2), dim3(256), 0, st, a, 2);
-    hipLaunchKernelGGL(k_fold_tree, dim3(1), dim3(256), 0, st, a, 3);
+    for (int L = 1; L <= a.nlev; ++L)
+        hipLaunchKernelGGL(k_fold_tree, dim3(a.nu[L - 1]), dim3(64 * UW), 0, st, a, L);
     return hipGetLastError();
 }
 hipError_t launch_fold_reduce(const double* partial, int nparts, double* outv, hipStream_t st) {
-    hipLaunchKernelGGL(k_fold_reduce, dim3(272), dim3(1024), 0, st, partial, nparts, outv);
+    hipLaunchKernelGGL(k_fold_reduce, dim3(72), dim3(1024), 0, st, partial, nparts, outv);
     return hipGetLastError();
 }
 hipError_t launch_fold_coef1(const double* T1, const double* G, const double* Rtop, int ldr, double* out,
@@ -733,9 +707,8 @@ hipError_t launch_fold_coef1(const double* T1, const double* G, const double* Rt
     return hipGetLastError();
 }
 hipError_t launch_fold_down_tree(const FoldArgs& a, const double* Stop, int lds, hipStream_t st) {
-    hipLaunchKernelGGL(k_fold_down_root, dim3(1), dim3(256), 0, st, a, Stop, lds);
-    hipLaunchKernelGGL(k_fold_down_level, dim3(a.n2), dim3(256), 0, st, a.V2, a.tb2, a.S2, a.S1, a.n1, a.m);
-    hipLaunchKernelGGL(k_fold_down_level, dim3(a.n1), dim3(256), 0, st, a.V1, a.tb1, a.S1, a.S0, a.n0, a.m);
+    for (int L = a.nlev; L >= 1; --L)
+        hipLaunchKernelGGL(k_fold_down_level, dim3(a.nu[L - 1]), dim3(64 * UW), 0, st, a, L, Stop, lds);
     return hipGetLastError();
 }
 hipError_t launch_fold_down(const ColList& P, const OutList& Q, const FoldArgs& a, hipStream_t st) {

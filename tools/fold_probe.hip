@@ -36,7 +36,8 @@ int main(int argc, char** argv) {
     double *P, *Q, *F;
     CK(hipMalloc((void**)&P, (size_t)17 * ld * sizeof(double)));
     CK(hipMalloc((void**)&Q, (size_t)8 * ld * sizeof(double)));
-    const int64_t n0 = fold_tiles(n), nblk = fold_blocks(n), n1 = fold_l1_tiles(n), n2 = fold_l2_tiles(n);
+    const int64_t n0 = fold_tiles(n), nblk = fold_blocks(n);
+    const std::vector<int> nu = fold_levels(n);
     size_t off = 0;
     auto take = [&](size_t cnt) {
         const size_t o = off;
@@ -45,15 +46,15 @@ int main(int argc, char** argv) {
     };
     const size_t t0 = fold_l0_tile_doubles(), tu = fold_tile_doubles();
     const size_t oV0 = take(n0 * t0), otb0 = take(n0 * 16), oR0 = take(n0 * 64), oS0 = take(n0 * 64);
-    const size_t oV1 = take(n1 * tu), otb1 = take(n1 * 16), oR1 = take(n1 * 64), oS1 = take(n1 * 64);
-    const size_t oV2 = take(n2 * tu), otb2 = take(n2 * 16), oR2 = take(n2 * 64), oS2 = take(n2 * 64);
-    const size_t oV3 = take(tu), otb3 = take(16);
-    const size_t oRr = take(64), oRrm = take(64), oK = take(72), oC = take(88), oOut = take(520),
-                 oPart = take((size_t)272 * nblk);
+    size_t oVu[3], otbu[3], oRu[3], oSu[3];
+    for (size_t L = 0; L < nu.size(); ++L) {
+        oVu[L] = take((size_t)nu[L] * tu);
+        otbu[L] = take((size_t)nu[L] * 16);
+        oRu[L] = take((size_t)nu[L] * 64);
+        oSu[L] = take((size_t)nu[L] * 64);
+    }
+    const size_t oRrm = take(64), oK = take(72), oOut = take(520), oPart = take((size_t)272 * nblk);
     CK(hipMalloc((void**)&F, off * sizeof(double)));
-    unsigned* cnt;
-    CK(hipMalloc((void**)&cnt, 128 * sizeof(unsigned)));
-    CK(hipMemset(cnt, 0, 128 * sizeof(unsigned)));
     hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, P, (int64_t)17 * ld, 1ull, 1.0);
     hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, F, (int64_t)off, 7ull, 0.2);
     CK(hipDeviceSynchronize());
@@ -66,8 +67,7 @@ int main(int argc, char** argv) {
     fa.w = w;
     fa.nblk = (int)nblk;
     fa.n0 = (int)n0;
-    fa.n1 = (int)n1;
-    fa.n2 = (int)n2;
+    fa.nlev = (int)nu.size();
     fa.C = F + oOut;  // any 272 doubles stand in for the P1 tile
     fa.flags = F + oOut + 512;
     fa.K = F + oK;
@@ -75,17 +75,13 @@ int main(int argc, char** argv) {
     fa.tb0 = F + otb0;
     fa.R0 = F + oR0;
     fa.S0 = F + oS0;
-    fa.V1 = F + oV1;
-    fa.tb1 = F + otb1;
-    fa.R1 = F + oR1;
-    fa.S1 = F + oS1;
-    fa.V2 = F + oV2;
-    fa.tb2 = F + otb2;
-    fa.R2 = F + oR2;
-    fa.S2 = F + oS2;
-    fa.V3 = F + oV3;
-    fa.tb3 = F + otb3;
-    fa.Rroot = F + oRr;
+    for (size_t L = 0; L < nu.size(); ++L) {
+        fa.nu[L] = nu[L];
+        fa.Vu[L] = F + oVu[L];
+        fa.tbu[L] = F + otbu[L];
+        fa.Ru[L] = F + oRu[L];
+        fa.Su[L] = F + oSu[L];
+    }
     fa.Rroot_m = F + oRrm;
     fa.partial = F + oPart;
     ColList cu{};
@@ -118,7 +114,7 @@ int main(int argc, char** argv) {
     const double b_up = 25.0 * 8.0 * n, b_down = 25.0 * 8.0 * n;
     if (timeit("up", b_up, [&] { return launch_fold_up(cu, fa, st); })) return 1;
     if (timeit("tree", 0.0, [&] { return launch_fold_tree(fa, st); })) return 1;
-    if (timeit("down_tree", 0.0, [&] { return launch_fold_down_tree(fa, F + oRr, 8, st); })) return 1;
+    if (timeit("down_tree", 0.0, [&] { return launch_fold_down_tree(fa, F + oRrm, 8, st); })) return 1;
     if (timeit("down", b_down, [&] { return launch_fold_down(cu, qo, fa, st); })) return 1;
     FoldArgs fr = fa;
     fr.V0 = nullptr;  // re-forming down pass, up without the tile store
