@@ -56,7 +56,7 @@ constexpr int FTLD = 17;        // padded LDS row of the Gram transpose
 #endif
 constexpr int kProbe = FOLD_PROBE;  // bit 1: no Gram, 2: no tile QR, 3: no tile store, 4: tree level 1 only
 #ifndef FOLD_UP_WPE
-#define FOLD_UP_WPE 3  // k_fold_up waves per SIMD (VGPR budget 512 / WPE)
+#define FOLD_UP_WPE 4  // k_fold_up waves per SIMD (VGPR budget 512 / WPE)
 #endif
 constexpr double kFoldTol = 1e-14;  // largest accepted loss-of-orthogonality estimate
 
