@@ -112,6 +112,7 @@ struct PatArgs {
     int nppat, npent, pmaxlen;
     int pcanon;            // every pair pattern has exactly pmaxlen entries (canonical slots)
     int pslot[8];          // canonical slot offsets (the matrix's distinct col - row, ascending)
+    int pmid = -1;         // pmaxlen / 2 when slots pmid - 1, pmid, pmid + 1 are the offsets -1, 0, +1
     int64_t xlo, xhi;      // addressable range of a vector column around its origin
     // two-range launch (pair kernel): compact pair index t >= gap_at maps to
     // stored pair t + gap, i.e. rows [0, 2 gap_at) and [2 (gap_at + gap),

@@ -306,6 +306,60 @@ __device__ __forceinline__ double2 ld16(const double* p) {
     return v;
 }
 
+// Lane-shared slot loads (PatArgs::pmid = MAXLEN / 2: slots pmid -+ 1 are the
+// offsets -+1).  When the 64 lanes of a wave hold 64 consecutive row pairs,
+// slot -1 (x[r0 - 1], x[r0]) and slot +1 (x[r0 + 1], x[r0 + 2]) are the
+// neighbouring lanes' centre loads x[r0 .. r0 + 1], moved over by one DPP
+// wave shift per half, and the wave's two outer rows come from one broadcast
+// load each: 5 of the 7 slots of a 7-point stencil are vector loads, and the
+// centre also serves the shift term.  The values are the loaded ones, so the
+// sums are bit-identical.  Other waves (a launch's tail, a two-range launch's
+// gap) load every slot.
+template <int CTRL>
+__device__ __forceinline__ double dpp_wave_shift(double v, double edge) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned long long o = (unsigned long long)__double_as_longlong(edge);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)o, (int)(unsigned)b, CTRL, 0xf, 0xf, false);
+    const unsigned hi =
+        (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)(o >> 32), (int)(unsigned)(b >> 32), CTRL, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+constexpr int kDppWaveShl1 = 0x130;  // lane i <- lane i + 1 (lane 63 keeps `edge`)
+constexpr int kDppWaveShr1 = 0x138;  // lane i <- lane i - 1 (lane 0 keeps `edge`)
+
+// wave-uniform: the lanes' stored pair indices t are consecutive; b0 = lane 0's
+template <int MAXLEN>
+__device__ __forceinline__ bool pair_lane_run(const PatArgs& a, int64_t t, int64_t& b0) {
+    if (!(MAXLEN >= 3 && (MAXLEN & 1)) || a.pmid != MAXLEN / 2) return false;
+    const int64_t base = t - (int64_t)(threadIdx.x & 63);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)base);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((unsigned long long)base >> 32));
+    b0 = (int64_t)(((unsigned long long)hi << 32) | lo);
+    return __builtin_amdgcn_ballot_w64(base == b0) == ~0ull;
+}
+
+template <int MAXLEN>
+__device__ __forceinline__ void pair_slot_loads(const PatArgs& a, const double* x, int64_t r0, bool run, int64_t b0,
+                                                double2 (&xc)[MAXLEN]) {
+    constexpr int Z = MAXLEN / 2;
+#pragma unroll
+    for (int e = 0; e < MAXLEN; ++e) {
+        if (MAXLEN >= 3 && (MAXLEN & 1) && run && (e == Z - 1 || e == Z + 1)) continue;
+        int64_t ad = r0 + a.pslot[e];
+        ad = ad < a.xlo ? a.xlo : (ad > a.xhi - 2 ? a.xhi - 2 : ad);
+        xc[e] = ld16(x + ad);
+    }
+    if constexpr (MAXLEN >= 3 && (MAXLEN & 1)) {
+        if (!run) return;
+        int64_t el = 2 * b0 - 1, er = 2 * b0 + 128;  // x[lane 0's r0 - 1], x[lane 63's r0 + 2]
+        el = el < a.xlo ? a.xlo : (el > a.xhi - 1 ? a.xhi - 1 : el);
+        er = er < a.xlo ? a.xlo : (er > a.xhi - 1 ? a.xhi - 1 : er);
+        const double xl = x[el], xr = x[er];
+        xc[Z - 1] = make_double2(dpp_wave_shift<kDppWaveShr1>(xc[Z].y, xl), xc[Z].x);
+        xc[Z + 1] = make_double2(xc[Z].y, dpp_wave_shift<kDppWaveShl1>(xc[Z].x, xr));
+    }
+}
+
 // The pair table (a few KB) is staged in LDS per block; the block's id
 // load is issued before the staging loads so both share one memory round
 // trip.  Split pairs (and the lone last row of an odd n) read the row
@@ -331,16 +385,18 @@ __global__ __launch_bounds__(TB) void k_spmv_pair(PatArgs a, const uint16_t* __r
     double2 xs = make_double2(0.0, 0.0), xp = make_double2(0.0, 0.0);  // shift terms
     {
         const int64_t r0 = 2 * t;
-        if (CANON) {
-#pragma unroll
-            for (int e = 0; e < MAXLEN; ++e) {
-                int64_t ad = r0 + a.pslot[e];
-                ad = ad < a.xlo ? a.xlo : (ad > a.xhi - 2 ? a.xhi - 2 : ad);
-                xc[e] = ld16(a.x + ad);
-            }
+        bool mid = false;
+        if constexpr (CANON) {
+            int64_t b0 = 0;
+            const bool run = pair_lane_run<MAXLEN>(a, t, b0);
+            pair_slot_loads<MAXLEN>(a, a.x, r0, run, b0, xc);
+            mid = MAXLEN >= 3 && (MAXLEN & 1) && a.pmid == MAXLEN / 2;
         }
         const int64_t rc = r0 < a.xhi - 2 ? r0 : a.xhi - 2;
-        if (MODE != 0) xs = ld16(a.x + rc);
+        if constexpr (MODE != 0) {
+            if constexpr (CANON) xs = mid ? xc[MAXLEN / 2] : ld16(a.x + rc);  // the centre slot is x[rc]
+            else xs = ld16(a.x + rc);
+        }
         if (MODE == 2) xp = ld16(a.xprev + rc);
     }
     for (int i = tid; i < a.npent; i += TB) {
@@ -438,13 +494,11 @@ __global__ __launch_bounds__(256) void k_spmv_pair_resid(PatArgs a, const uint16
     const int id = ppat[tcl];
     const int64_t r0 = 2 * tcl;
     double2 xc[MAXLEN];
-#pragma unroll
-    for (int e = 0; e < MAXLEN; ++e) {
-        int64_t ad = r0 + a.pslot[e];
-        ad = ad < a.xlo ? a.xlo : (ad > a.xhi - 2 ? a.xhi - 2 : ad);
-        xc[e] = ld16(a.x + ad);
-    }
-    const double2 xs = ld16(a.x + (r0 < a.xhi - 2 ? r0 : a.xhi - 2));
+    int64_t b0 = 0;
+    const bool run = pair_lane_run<MAXLEN>(a, tcl, b0);
+    pair_slot_loads<MAXLEN>(a, a.x, r0, run, b0, xc);
+    const bool mid = MAXLEN >= 3 && (MAXLEN & 1) && a.pmid == MAXLEN / 2;
+    const double2 xs = mid ? xc[MAXLEN / 2] : ld16(a.x + (r0 < a.xhi - 2 ? r0 : a.xhi - 2));
     for (int i = tid; i < a.npent; i += 256) {
         s_pv[i] = ppval[i];
         s_poff[i] = ppoff[i];
@@ -562,22 +616,18 @@ __global__ __launch_bounds__(256) void k_spmv_pair_resid_multi(PatArgs a, const 
             code[e] = s_poff[base + e];
             v[e] = s_pv[base + e];
         }
-        int64_t ad[MAXLEN];
-#pragma unroll
-        for (int e = 0; e < MAXLEN; ++e) {
-            const int64_t d = r0 + a.pslot[e];
-            ad[e] = d < a.xlo ? a.xlo : (d > a.xhi - 2 ? a.xhi - 2 : d);
-        }
         const int64_t rs = r0 < a.xhi - 2 ? r0 : a.xhi - 2;
+        int64_t b0 = 0;
+        const bool run = pair_lane_run<MAXLEN>(a, tcl, b0);
+        const bool mid = MAXLEN >= 3 && (MAXLEN & 1) && a.pmid == MAXLEN / 2;
 #pragma unroll
         for (int q = 0; q < CPB; ++q) {
             if (q >= nq) break;
             const double* x = xq[q];
             const double l = lq[q];
             double2 xc[MAXLEN];
-#pragma unroll
-            for (int e = 0; e < MAXLEN; ++e) xc[e] = ld16(x + ad[e]);
-            const double2 xs = ld16(x + rs);
+            pair_slot_loads<MAXLEN>(a, x, r0, run, b0, xc);
+            const double2 xs = mid ? xc[MAXLEN / 2] : ld16(x + rs);
             if (t < npairs) {
                 if (id != kPairSplit) {
                     double y0 = 0.0, y1 = 0.0;

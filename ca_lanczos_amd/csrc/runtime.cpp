@@ -453,6 +453,18 @@ static PatArgs pat_args(const DevMatrix& A, int64_t o, int64_t len, const double
     p.pmaxlen = A.pmaxlen;
     p.pcanon = A.pcanon ? 1 : 0;
     for (int k = 0; k < 8; ++k) p.pslot[k] = A.pslot[k];
+    {
+        // the +-1 slots from the neighbouring lanes (k_spmv_pair*); CAL_LANE_SLOTS=0 loads them
+        static const bool lane_slots = [] {
+            const char* e = std::getenv("CAL_LANE_SLOTS");
+            return !e || std::atoi(e) != 0;
+        }();
+        const int z = A.pmaxlen / 2;
+        p.pmid = (lane_slots && A.pcanon && (A.pmaxlen & 1) && A.pmaxlen >= 3 && A.pslot[z] == 0 &&
+                  A.pslot[z - 1] == -1 && A.pslot[z + 1] == 1)
+                     ? z
+                     : -1;
+    }
     p.xlo = -(A.lpad + d);
     p.xhi = A.ld - (A.lpad + d);
     return p;
