@@ -203,6 +203,13 @@ bool apply_rows_ok(int wp, int wy);
 hipError_t launch_apply(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y, bool store,
                         int wq, int64_t n, const ApplyPlan& pl, double* partial, hipStream_t st);
 hipError_t launch_reduce(const double* partial, int nparts, int64_t nent, double* out, hipStream_t st);
+// one-pass block-upper Gram of w <= 128 columns of one buffer (k_gram_wide):
+// gram_wide_entries(w) entries of gram_wide_blocks(n) block partials each
+// (entry-major); entry e is G(i, j) with (i, j) from gram_wide_entry
+hipError_t launch_gram_wide(const double* Q, int64_t ld, int w, int64_t n, double* partial, hipStream_t st);
+int gram_wide_entries(int w);
+int gram_wide_blocks(int64_t n);
+void gram_wide_entry(int w, int e, int* i, int* j);
 // hot-shape kernels (s <= 8): tile Gram (<= 16 columns + 1 extra) and the
 // row-parallel apply with the fused LDS-transposed tile Gram.  Partials:
 // 272 entries (16x16 tile Gram, then 16 extra-column products).

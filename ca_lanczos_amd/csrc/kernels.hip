@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
 
 #include "cal_internal.hpp"
 
@@ -1295,6 +1296,149 @@ static void launch_gram_lds(const Panel& A, const Panel& B, int64_t n, int block
     constexpr int U = 1;
     const size_t lds = std::max((size_t)2 * U * 16 * RUN * 17, (size_t)3 * NTA * 64 * 4) * sizeof(double);
     hipLaunchKernelGGL((k_gram_lds<NTA, RUN, U>), dim3(blocks), dim3(256), lds, st, A, B, n, partial);
+}
+
+// One-pass Gram of the w <= 16 NT columns of Q (column c at Q + c ld), the
+// 16 x 16 tile pairs ta <= tb only (the block-upper part of Q'Q): the
+// orthogonality errors of every deferred iteration of a run from one sweep
+// over Q (compute_orth_err, ca_lanczos.m:99-107; lanczos.cpp: oe_flush),
+// where the per-iteration Grams re-read Q(:,1:s(k-1)) every iteration.
+// Per grid step a block stages R = 32 rows of all columns in LDS ([row][col],
+// odd leading dimension; half a wave loads 32 rows of one column), double
+// buffered, the next step's loads in flight across the barrier and the
+// MFMAs.  Wave v owns the pairs p = v + 4i of the upper pairs in row order
+// (compile-time per wave: the operand reads are fixed LDS offsets) and feeds
+// v_mfma_f64_16x16x4f64 from the staged rows, 4 rows per MFMA.  The pairs of
+// one wave are its own, so there is no block reduction: lane l of the wave
+// owning pair p writes register r of it to entry (p * 64 + l) * 4 + r of
+// the block's partials (entry-major, e * nblocks + block).
+__host__ __device__ constexpr int gw_pair_a(int nt, int p) {
+    int ta = 0;
+    while (p >= nt - ta) {
+        p -= nt - ta;
+        ++ta;
+    }
+    return ta;
+}
+__host__ __device__ constexpr int gw_pair_b(int nt, int p) {
+    int ta = 0;
+    while (p >= nt - ta) {
+        p -= nt - ta;
+        ++ta;
+    }
+    return ta + p;
+}
+
+// pair P = WV + 4 I of the wave, register I (constant-evaluated indices)
+template <int NT, int P, int I, int PW>
+__device__ __forceinline__ void gram_wide_mfma(const double* __restrict__ row, d4 (&acc)[PW]) {
+    if constexpr (P < NT * (NT + 1) / 2) {
+        constexpr int ta = gw_pair_a(NT, P), tb = gw_pair_b(NT, P);
+        acc[I] = mfma64(row[16 * ta], row[16 * tb], acc[I]);
+    }
+}
+
+template <int NT, int WV, int PW, int R, int LDW, int... I>
+__device__ __forceinline__ void gram_wide_step(const double* __restrict__ s, d4 (&acc)[PW], int g, int c16,
+                                               std::integer_sequence<int, I...>) {
+#pragma unroll
+    for (int q = 0; q < R / 4; ++q) {
+        const double* row = s + (4 * q + g) * LDW + c16;
+        (gram_wide_mfma<NT, WV + 4 * I, I, PW>(row, acc), ...);
+    }
+}
+
+template <int NT>
+__global__ __launch_bounds__(256) void k_gram_wide(const double* __restrict__ Q, int64_t ld, int w, int64_t n,
+                                                  double* __restrict__ partial) {
+    constexpr int R = 32, LDW = 16 * NT + 1, NP = NT * (NT + 1) / 2, PW = (NP + 3) / 4;
+    constexpr int PER = R * 16 * NT / 256;  // staged values per thread and step
+    extern __shared__ __attribute__((aligned(16))) double lds_gw[];  // [2][R][LDW]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, c16 = lane & 15, g = lane >> 4;
+    const int lrow = tid & (R - 1), lcol = tid / R;  // loader: column lcol + (256 / R) q, row lrow
+    d4 acc[PW];
+#pragma unroll
+    for (int i = 0; i < PW; ++i) acc[i] = d4{0.0, 0.0, 0.0, 0.0};
+    const int64_t stride = (int64_t)gridDim.x * R;
+    // columns past w are clamped to column 0 (only entries no caller reads
+    // see them); rows past n are zeroed at the LDS write, so nothing waits
+    // on the loads before the barrier and the MFMAs
+    double v[PER];
+    bool vin = false;
+    auto load = [&](int64_t rb) {
+        const int64_t rr = rb + lrow;
+        vin = rr < n;
+        const int64_t ro = vin ? rr : 0;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int c = lcol + (256 / R) * q;
+            v[q] = Q[(int64_t)(c < w ? c : 0) * ld + ro];
+        }
+    };
+    int64_t rb = (int64_t)blockIdx.x * R;
+    if (rb < n) load(rb);
+    for (int buf = 0; rb < n; rb += stride, buf ^= 1) {
+        double* sb = lds_gw + buf * (R * LDW);
+#pragma unroll
+        for (int q = 0; q < PER; ++q) sb[lrow * LDW + lcol + (256 / R) * q] = vin ? v[q] : 0.0;
+        if (rb + stride < n) load(rb + stride);
+        __syncthreads();
+        constexpr auto seq = std::make_integer_sequence<int, PW>{};
+        switch (wave) {  // wave-uniform: each wave's pairs at fixed offsets
+            case 0: gram_wide_step<NT, 0, PW, R, LDW>(sb, acc, g, c16, seq); break;
+            case 1: gram_wide_step<NT, 1, PW, R, LDW>(sb, acc, g, c16, seq); break;
+            case 2: gram_wide_step<NT, 2, PW, R, LDW>(sb, acc, g, c16, seq); break;
+            default: gram_wide_step<NT, 3, PW, R, LDW>(sb, acc, g, c16, seq); break;
+        }
+        // buffer buf is rewritten two steps on, after the next step's barrier,
+        // which every wave passes only once its MFMAs on buf have issued
+    }
+    const int64_t nb = gridDim.x;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+        const int p = wave + 4 * i;
+        if (p < NP)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) partial[((int64_t)(p * 64 + lane) * 4 + r) * nb + blockIdx.x] = acc[i][r];
+    }
+}
+
+int gram_wide_entries(int w) {
+    const int nt = (w + 15) / 16;
+    return nt * (nt + 1) / 2 * 256;
+}
+
+int gram_wide_blocks(int64_t n) {
+    const int64_t b = (n + 31) / 32;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(512, b));
+}
+
+void gram_wide_entry(int w, int e, int* i, int* j) {
+    const int nt = (w + 15) / 16;
+    const int p = e / 256, lane = (e / 4) % 64, r = e % 4;
+    *i = 16 * gw_pair_a(nt, p) + (lane >> 4) + 4 * r;
+    *j = 16 * gw_pair_b(nt, p) + (lane & 15);
+}
+
+hipError_t launch_gram_wide(const double* Q, int64_t ld, int w, int64_t n, double* partial, hipStream_t st) {
+    if (w < 1 || w > 128) return hipErrorInvalidValue;
+    const int nt = (w + 15) / 16, blocks = gram_wide_blocks(n);
+    const size_t lds = (size_t)2 * 32 * (16 * nt + 1) * sizeof(double);
+#define CAL_GW(NT)                                                                                          \
+    case NT: hipLaunchKernelGGL(k_gram_wide<NT>, dim3(blocks), dim3(256), lds, st, Q, ld, w, n, partial); break
+    switch (nt) {
+        CAL_GW(1);
+        CAL_GW(2);
+        CAL_GW(3);
+        CAL_GW(4);
+        CAL_GW(5);
+        CAL_GW(6);
+        CAL_GW(7);
+        CAL_GW(8);
+        default: return hipErrorInvalidValue;
+    }
+#undef CAL_GW
+    return hipGetLastError();
 }
 
 bool gram_lds_on() {  // CAL_GRAM_LDS=0: the direct-load k_gram (A/B; same bits)

@@ -16,6 +16,7 @@
 #include <cmath>
 #include <complex>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -95,6 +96,13 @@ struct LanczosState {
     size_t din_cap = 0;
     double* d_dpart = nullptr;  // block partials of the diagnostics' auxiliary-stream kernels
     size_t dpart_cap = 0;
+    // orthogonality errors deferred to the flush ('local' / 'full': Q(:,1:sk+1)
+    // is final once written): the iterations still to do, one wide Gram then
+    bool oe_defer = false;
+    std::vector<int> oe_pend;
+    double* d_oe = nullptr;  // the wide Gram's entries
+    double* h_oe = nullptr;  // pinned
+    size_t oe_cap = 0;
     int64_t lpad = 0;  // local origin inside each column (left halo space)
     double* col(int j) { return dQ + (size_t)j * ld + lpad; }
     double* vcolumn(int j, int par = 0) { return dV + ((size_t)par * (s + 1) + j) * ld + lpad; }
@@ -446,7 +454,7 @@ static int diag_launch(cal_ctx* c, LanczosState& L, DiagJob& J) {
     const int bcol = jq > s + 1 ? J.wa : 0;
     J.oe.clear();
     size_t off = (size_t)2 * sk, oe_part = 0;
-    for (int a0 = 0; a0 < J.wa; a0 += 128)
+    for (int a0 = 0; a0 < (L.oe_defer ? 0 : J.wa); a0 += 128)
         for (int b0 = 0; b0 < s + 1; b0 += 16) {
             const int na = std::min(128, J.wa - a0), nb = std::min(16, s + 1 - b0);
             const GramPlan pl = gram_plan(na, nb, n);
@@ -596,8 +604,59 @@ static int diag_collect(cal_ctx* c, LanczosState& L, DiagJob& J) {
     if ((int)L.rn.size() < k) L.rn.resize(k);
     if ((int)L.oe.size() < k) L.oe.resize(k, 0.0);
     L.rn[k - 1] = rn;
-    L.oe[k - 1] = oe;
+    if (L.oe_defer) L.oe_pend.push_back(k);
+    else L.oe[k - 1] = oe;
     J.k = 0;
+    return 0;
+}
+
+// The deferred orthogonality errors (compute_orth_err, ca_lanczos.m:99-107)
+// of every pending iteration k from one Gram of Q(:,1:sK+1), K the last of
+// them: k_gram_wide reads Q once (the per-iteration Grams re-read
+// Q(:,1:s(k-1)) every iteration: 77 GB over 15 iterations at n = 9.94 M).
+// Entry (i, j), i < j, is the same dot product the per-iteration Gram
+// forms (another summation order, i.e. the same value to rounding).
+static int oe_flush(cal_ctx* c, LanczosState& L) {
+    if (L.oe_pend.empty()) return 0;
+    const int s = L.s;
+    const int K = *std::max_element(L.oe_pend.begin(), L.oe_pend.end());
+    const int w = s * K + 1;
+    const int64_t n = c->A.n_local;
+    const int nent = gram_wide_entries(w), nb = gram_wide_blocks(n);
+    CAL_TRY(grow_pinned_dev(c, &L.d_dpart, &L.dpart_cap, (size_t)nent * nb));
+    CAL_TRY(grow_pinned(c, &L.d_oe, &L.h_oe, &L.oe_cap, (size_t)nent));
+    CAL_HIP(c, launch_gram_wide(L.col(0), L.ld, w, n, L.d_dpart, c->stream));
+    CAL_HIP(c, launch_reduce(L.d_dpart, nb, nent, L.d_oe, c->stream));
+    CAL_TRY(allreduce_sum(c, L.d_oe, nent));
+    CAL_HIP(c, hipMemcpyAsync(L.h_oe, L.d_oe, (size_t)nent * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    std::vector<double> G((size_t)w * w, 0.0);  // upper tile pairs; diagonal tiles both triangles
+    std::vector<char> have((size_t)w * w, 0);
+    for (int e = 0; e < nent; ++e) {
+        int i, j;
+        gram_wide_entry(w, e, &i, &j);
+        if (i < w && j < w) {
+            G[i + (size_t)j * w] = L.h_oe[e];
+            have[i + (size_t)j * w] = 1;
+        }
+    }
+    for (const int k : L.oe_pend) {
+        const int jq = s * k + 1;  // Q(:,1:jq)
+        double oe = 0.0;
+        if (jq > s + 1) {  // max |Q(:,1:jq-s-1)' Q(:,jq-s:jq)|
+            for (int j = jq - s - 1; j < jq; ++j)
+                for (int i = 0; i < jq - s - 1; ++i) oe = std::max(oe, std::fabs(G[i + (size_t)j * w]));
+        } else {  // max |Q(:,1:jq)'Q(:,1:jq) - I|
+            for (int j = 0; j < jq; ++j)
+                for (int i = 0; i < jq; ++i) {
+                    const size_t e = have[i + (size_t)j * w] ? i + (size_t)j * w : j + (size_t)i * w;
+                    oe = std::max(oe, std::fabs(G[e] - (i == j ? 1.0 : 0.0)));
+                }
+        }
+        if ((int)L.oe.size() < k) L.oe.resize(k, 0.0);
+        L.oe[k - 1] = oe;
+    }
+    L.oe_pend.clear();
     return 0;
 }
 
@@ -609,7 +668,7 @@ static int diag_flush(cal_ctx* c, LanczosState& L) {
         CAL_TRY(diag_launch(c, L, L.pending));
         CAL_TRY(diag_collect(c, L, L.pending));
     }
-    return 0;
+    return oe_flush(c, L);
 }
 
 static void diag_free(LanczosState& L) {
@@ -622,6 +681,8 @@ static void diag_free(LanczosState& L) {
     if (L.h_dres) hipHostFree(L.h_dres);
     if (L.d_din) hipFree(L.d_din);
     if (L.h_din) hipHostFree(L.h_din);
+    if (L.d_oe) hipFree(L.d_oe);
+    if (L.h_oe) hipHostFree(L.h_oe);
 }
 
 // ---- T extension (ca_lanczos.m:176-223) -----------------------------------
@@ -1061,6 +1122,13 @@ int cal_lanczos_begin(cal_ctx* c, const double* r, int s, int max_outer, const c
     CAL_HIP(c, hipMemsetAsync(L->dV, 0, (size_t)2 * (s + 1) * L->ld * sizeof(double), c->stream));
     L->Tld = s * max_outer + 1;
     L->T.assign((size_t)L->Tld * L->Tld, 0.0);
+    {
+        // CAL_OE_DEFER=0: the orthogonality error's Grams every iteration (read
+        // per run: the parity test compares both)
+        const char* e = std::getenv("CAL_OE_DEFER");
+        const bool defer = !e || std::atoi(e) != 0;
+        L->oe_defer = defer && L->mode <= 1 && (int64_t)s * max_outer + 1 <= 128;
+    }
     const double t0 = now_ms();
     // q = r/sqrt(r'*r) (ca_lanczos.m:55)
     CAL_HIP(c, hipMemcpyAsync(L->vcolumn(0), r, L->n * sizeof(double), hipMemcpyHostToDevice, c->stream));
@@ -1100,7 +1168,7 @@ int cal_lanczos_get(cal_ctx* c, double* T, int ldt, double* rn, double* oe, int*
     LanczosState& L = *c->lz;
     const int k = L.k, sk = L.s * L.k;
     if (T && ldt < sk) return set_error(c, CAL_ERR_ARG, "cal_lanczos_get: ldt < s*k");
-    if (L.pending.k || L.ready.k) {  // diagnostics still deferred (a run stopped early)
+    if (L.pending.k || L.ready.k || !L.oe_pend.empty()) {  // diagnostics still deferred
         hipSetDevice(c->device);
         CAL_TRY(diag_flush(c, L));
     }

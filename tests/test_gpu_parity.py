@@ -315,6 +315,32 @@ def test_ca_lanczos_newton_full(cal, ref):
     assert np.max(out.orth_err) < 1e-12
 
 
+@pytest.mark.parametrize("N,orth", [(24, "local"), (64, "full"), (40, "local")])
+def test_orth_err_deferred_wide_gram(cal, ref, monkeypatch, N, orth):
+    """compute_orth_err (ca_lanczos.m:99-107) of every iteration from one
+    block-upper Gram of Q(:,1:sk+1) at the flush (k_gram_wide, lanczos.cpp
+    oe_flush; 'local' / 'full' only, Q's columns are final once written)
+    against the per-iteration Grams (CAL_OE_DEFER=0) on the same run: the
+    same dot products in another summation order.  s = 8, 15 outer
+    iterations (121 columns, the bench's shape), 13.8 k / 262 k / 64 k rows;
+    the 40^3 case is also run with 14 iterations to a flush with fewer
+    columns than the pinned shape."""
+    A = cal.matrices.laplacian_3d(N)
+    r = ref.matlab_rand(A.shape[0])
+    its = [120, 112] if N == 40 else [120]
+    for it in its:
+        monkeypatch.delenv("CAL_OE_DEFER", raising=False)
+        a = cal.ca_lanczos_ex(A, r, 8, it, "newton", orth)
+        monkeypatch.setenv("CAL_OE_DEFER", "0")
+        b = cal.ca_lanczos_ex(A, r, 8, it, "newton", orth)
+        assert np.array_equal(a.T, b.T) and np.array_equal(a.ritz_rnorm, b.ritz_rnorm)
+        assert a.orth_err.shape == b.orth_err.shape == (it // 8,)
+        assert np.all(b.orth_err > 0)
+        assert np.all(np.abs(a.orth_err - b.orth_err) <= 1e-15 + 1e-9 * b.orth_err), (a.orth_err, b.orth_err)
+    if orth == "full":
+        assert np.max(a.orth_err) < 1e-12
+
+
 def test_ca_lanczos_bad_args(cal):
     A = cal.matrices.laplacian_2d(8)
     with pytest.raises(ValueError):
