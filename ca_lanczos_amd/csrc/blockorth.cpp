@@ -704,54 +704,70 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
         CAL_HIP(c, launch_fold_up(cu, fa, c->stream));
         timer_end(c, t);
     }
+    // one rank: the root level, the algebra and the root's way down merged
+    // (k_fold_root; CAL_FOLD_ROOT=0: the three launches)
+    static const bool merged_root = [] {
+        const char* e = std::getenv("CAL_FOLD_ROOT");
+        return !e || std::atoi(e) != 0;
+    }();
+    const bool merged = P == 1 && merged_root;
+    // (the C2 reduction on a side stream beside the tree levels, and the
+    // publish beside the way down, measured 656-661 -> 626-633 outer-it/s:
+    // the cross-stream waits cost more than the two short kernels)
     {
         const int t = timer_begin(c, 3);
-        CAL_HIP(c, launch_fold_tree(fa, c->stream));
+        CAL_HIP(c, launch_fold_tree(fa, c->stream, merged ? nlev - 1 : nlev));
         timer_end(c, t);
     }
     CAL_HIP(c, launch_fold_reduce(c->d_partial, (int)nblk, F + oT2, c->stream));
     CAL_TRY(allreduce_sum(c, F + oT2, 72));
-    // the root over the ranks: all-gather the local roots, factor the stack
-    // (the tree kernel's stack level, redundantly on every rank)
-    const double* Rtop = fa.Ru[nlev - 1];  // the root level's one R
-    int ldr = 8;
-    TsqrLevelArgs ga;
-    TsqrCols gcols{};
-    TsqrQ gq{};
-    if (P > 1) {
-        CAL_TRY(allgather(c, fa.Rroot_m, F + oG, mm));
-        ga.rows = (int64_t)P * m;
-        ga.m = m;
-        ga.wp = m;
-        ga.in = F + oG;
-        ga.out = F + oGup;
-        const int t = timer_begin(c, 3);
-        CAL_HIP(c, launch_tsqr(false, 0, ga, gcols, gq, c->stream));
-        timer_end(c, t);
-        Rtop = F + oGup;
-        ldr = m;
-    }
     CAL_TRY(ensure_pub(c));
     const unsigned long long seq = ++c->pub_seq;
     double* h_out = c->h_pub;
     unsigned long long* h_seq = reinterpret_cast<unsigned long long*>(c->h_pub + 516);
     unsigned long long* d_seq = reinterpret_cast<unsigned long long*>(c->d_pub + 516);
-    CAL_HIP(c, launch_fold_coef1(F + oT1, F + oT2, Rtop, ldr, d_out, F + oSb, F + oSm, F + oK, w, m,
-                                 doreorth ? 1 : 0, (double)global_rows(c, n) * (P > 1 && !c->has_A ? P : 1),
-                                 c->d_pub, d_seq, seq, c->stream));
-    // down: [the global levels,] the group and block levels, level 0
-    const double* Stop = F + oSb;
-    int lds = 8;
-    if (P > 1) {
-        ga.S = F + oSm;
-        ga.out = F + oGdn;
+    const double nglob = (double)global_rows(c, n) * (P > 1 && !c->has_A ? P : 1);
+    if (merged) {
         const int t = timer_begin(c, 3);
-        CAL_HIP(c, launch_tsqr(true, 0, ga, gcols, gq, c->stream));
+        CAL_HIP(c, launch_fold_root(fa, F + oT1, F + oT2, d_out, F + oSb, F + oSm, F + oK, w, doreorth ? 1 : 0,
+                                    nglob, c->d_pub, d_seq, seq, c->stream));
+        CAL_HIP(c, launch_fold_down_tree(fa, nullptr, 8, c->stream, nlev - 1));
         timer_end(c, t);
-        Stop = F + oGdn + (size_t)me * mm;
-        lds = m;
-    }
-    {
+    } else {
+        // the root over the ranks: all-gather the local roots, factor the stack
+        // (the tree kernel's stack level, redundantly on every rank)
+        const double* Rtop = fa.Ru[nlev - 1];  // the root level's one R
+        int ldr = 8;
+        TsqrLevelArgs ga;
+        TsqrCols gcols{};
+        TsqrQ gq{};
+        if (P > 1) {
+            CAL_TRY(allgather(c, fa.Rroot_m, F + oG, mm));
+            ga.rows = (int64_t)P * m;
+            ga.m = m;
+            ga.wp = m;
+            ga.in = F + oG;
+            ga.out = F + oGup;
+            const int t = timer_begin(c, 3);
+            CAL_HIP(c, launch_tsqr(false, 0, ga, gcols, gq, c->stream));
+            timer_end(c, t);
+            Rtop = F + oGup;
+            ldr = m;
+        }
+        CAL_HIP(c, launch_fold_coef1(F + oT1, F + oT2, Rtop, ldr, d_out, F + oSb, F + oSm, F + oK, w, m,
+                                     doreorth ? 1 : 0, nglob, c->d_pub, d_seq, seq, c->stream));
+        // down: [the global levels,] the group and block levels, level 0
+        const double* Stop = F + oSb;
+        int lds = 8;
+        if (P > 1) {
+            ga.S = F + oSm;
+            ga.out = F + oGdn;
+            const int t = timer_begin(c, 3);
+            CAL_HIP(c, launch_tsqr(true, 0, ga, gcols, gq, c->stream));
+            timer_end(c, t);
+            Stop = F + oGdn + (size_t)me * mm;
+            lds = m;
+        }
         const int t = timer_begin(c, 3);
         CAL_HIP(c, launch_fold_down_tree(fa, Stop, lds, c->stream));
         timer_end(c, t);

@@ -347,7 +347,8 @@ bool fold_shape_ok(int64_t n, int m, int w);
 size_t fold_l0_tile_doubles();  // one level-0 tile
 size_t fold_tile_doubles();     // one upper-level tile (512 x 8)
 hipError_t launch_fold_up(const ColList& P, const FoldArgs& a, hipStream_t st);
-hipError_t launch_fold_tree(const FoldArgs& a, hipStream_t st);  // levels 1, 2 and the root
+// levels 1 .. upto (-1: up to the root)
+hipError_t launch_fold_tree(const FoldArgs& a, hipStream_t st, int upto = -1);
 hipError_t launch_fold_reduce(const double* partial, int nparts, double* out, hipStream_t st);  // the 72 C2 entries
 // k_fold_coef1: T1 the reduced P1 tile, G the up launch's Gram tile, Rtop the
 // root R (ld ldr); writes out (R, RY, flags), S_top (Sbuf ld 8, Sm ld m), K
@@ -355,8 +356,15 @@ hipError_t launch_fold_reduce(const double* partial, int nparts, double* out, hi
 hipError_t launch_fold_coef1(const double* T1, const double* G, const double* Rtop, int ldr, double* out,
                              double* Sbuf, double* Sm, double* Kbuf, int w, int m, int doreorth, double nglob,
                              double* hout, unsigned long long* hseq, unsigned long long seq, hipStream_t st);
-hipError_t launch_fold_down_tree(const FoldArgs& a, const double* Stop, int lds, hipStream_t st);
+// one rank: the root level, k_fold_coef1's algebra and the root's way down in
+// one block (the root's R is its own, ld 8); S blocks of level nlev - 1 out
+hipError_t launch_fold_root(const FoldArgs& a, const double* T1, const double* G, double* out, double* Sbuf,
+                            double* Sm, double* Kbuf, int w, int doreorth, double nglob, double* hout,
+                            unsigned long long* hseq, unsigned long long seq, hipStream_t st);
+// levels from .. 1 (-1: from the root, whose S is Stop, ld lds)
+hipError_t launch_fold_down_tree(const FoldArgs& a, const double* Stop, int lds, hipStream_t st, int from = -1);
 hipError_t launch_fold_down(const ColList& P, const OutList& Q, const FoldArgs& a, hipStream_t st);
+
 
 }  // namespace cal
 

@@ -746,6 +746,7 @@ void cal_destroy(cal_ctx* c) {
     if (c->d_fold) hipFree(c->d_fold);
     if (c->h_pub) hipHostFree(c->h_pub);
     if (c->aux_stream) hipStreamDestroy(c->aux_stream);
+
     hipStreamDestroy(c->stream);
     delete c;
 }

@@ -326,45 +326,65 @@ __device__ __forceinline__ void finv_col(const double* T, double* Ti, int j, int
     for (int i = 0; i < FM; ++i) Ti[i + j * FM] = col[i];
 }
 
-__global__ __launch_bounds__(64) void k_fold_coef1(const double* __restrict__ T1, const double* __restrict__ G,
-                                                  const double* __restrict__ Rtop, int ldr, double* __restrict__ out,
-                                                  double* __restrict__ Sbuf, double* __restrict__ Sm,
-                                                  double* __restrict__ Kbuf, int w, int m, int doreorth, double nglob,
-                                                  double* __restrict__ hout,
-                                                  unsigned long long* __restrict__ hseq, unsigned long long seq) {
-    __shared__ double Cs[9 * FM], C2s[9 * FM], RT[64], XX[FM];
+// The body, one wave (lane 0..63; its LDS hand-offs stay inside the wave).
+// Sl: S_top also into this LDS array (the merged root kernel), or null.
+__device__ __forceinline__ void fold_coef1_body(const double* T1, const double* G, const double* Rtop, int ldr,
+                                                double* __restrict__ out, double* __restrict__ Sbuf,
+                                                double* __restrict__ Sm, double* __restrict__ Kbuf, int w, int m,
+                                                int doreorth, double nglob, double* Sl, int lane) {
+    __shared__ double Cs[9 * FM], C2s[9 * FM], RT[64], XX[64];
     __shared__ double RY[64], Ri[64], Ws[9 * FM], U[64], Ui[64], D[FM];
     __shared__ int fail, reo;
-    const int lane = threadIdx.x, r = lane & 7, c = lane >> 3, nq = w < 8 ? w : 8;
+    const int r = lane & 7, c = lane >> 3, nq = w < 8 ? w : 8;
     const bool in = r < m && c < m;
     // stage every input once (one round of global loads): C = Qp'X and the
     // diagonal X'X from the P1 tile T1, C2 = Qp'Y from the Gram tile G, the
     // root R (ld ldr, raw signs)
-    for (int e = lane; e < 9 * FM; e += 64) {
-        const int i = e % 9, j = e / 9;
-        const bool ok = i < w && j < m;
-        Cs[e] = ok ? (i < 8 ? T1[i + (nq + j) * 16] : T1[256 + nq + j]) : 0.0;
-        C2s[e] = ok ? G[e] : 0.0;  // the up launch's reduced Qp'Y (entry i + 9 j)
+    // (every load issued before the first wait: one memory round trip; the
+    // addresses are valid for every lane, the selects come after)
+    const int e1 = lane + 64 < 9 * FM ? lane + 64 : lane;
+    auto t1_at = [&](int e) {
+        const int i = e % 9, j = e / 9, jj = nq + (j < FM ? j : 0);
+        return T1[i < 8 ? i + jj * 16 : 256 + jj];
+    };
+    const double ta = t1_at(lane), tb = t1_at(e1), ga = G[lane], gb = G[e1];
+    const double rtv = Rtop[(r < m ? r : 0) + (c < m ? c : 0) * ldr];
+    const double xxv = T1[(nq + (lane < m ? lane : 0)) * 17];
+    __builtin_amdgcn_sched_barrier(0);  // all six loads issue before any use waits
+    {
+        const int i = lane % 9, j = lane / 9, i1 = e1 % 9, j1 = e1 / 9;
+        const bool ok = i < w && j < m, ok1 = i1 < w && j1 < m;
+        Cs[lane] = ok ? ta : 0.0;
+        C2s[lane] = ok ? ga : 0.0;  // the up launch's reduced Qp'Y (entry i + 9 j)
+        Cs[e1] = ok1 ? tb : 0.0;    // (lanes >= 8: e1 = lane, the same value again)
+        C2s[e1] = ok1 ? gb : 0.0;
     }
-    RT[lane] = in ? Rtop[r + c * ldr] : 0.0;
-    if (lane < FM) XX[lane] = lane < m ? T1[(nq + lane) + (nq + lane) * 16] : 0.0;
-    __syncthreads();
+    RT[lane] = in ? rtv : 0.0;
+    XX[lane] = lane < m ? xxv : 0.0;
+    fwsync();
     // the reorth test of projectAndNormalize.m:17-22,45-52 on the algebraic
-    // norms ||Y_j||^2 = X_j'X_j - C_j'C_j (NaN-ignoring max in column order)
-    if (lane == 0) {
-        double mx = NAN;
-        for (int j = 0; j < m; ++j) {
+    // norms ||Y_j||^2 = X_j'X_j - C_j'C_j: column j on lane j, then the
+    // NaN-ignoring max over the columns (order-free)
+    {
+        double rj = NAN;
+        if (lane < m) {
             double cc = 0.0;
-            for (int k = 0; k < w; ++k) cc = cc + Cs[k + j * 9] * Cs[k + j * 9];
-            const double before = sqrt(XX[j]);
-            const double after = sqrt(fmax(XX[j] - cc, 0.0));
-            const double rj = fabs(before - after) / before;
-            if (!isnan(rj) && (isnan(mx) || rj > mx)) mx = rj;
+            for (int k = 0; k < w; ++k) cc = cc + Cs[k + lane * 9] * Cs[k + lane * 9];
+            const double before = sqrt(XX[lane]);
+            const double after = sqrt(fmax(XX[lane] - cc, 0.0));
+            rj = fabs(before - after) / before;
         }
-        reo = (w > 0 && doreorth && mx > 0.5) ? 1 : 0;
-        fail = 0;
-        out[512] = 0.0;
-        out[514] = reo ? 1.0 : 0.0;
+#pragma unroll
+        for (int o = 4; o >= 1; o >>= 1) {
+            const double q = __shfl_xor(rj, o, 64);
+            rj = isnan(rj) ? q : (isnan(q) ? rj : fmax(rj, q));
+        }
+        if (lane == 0) {
+            reo = (w > 0 && doreorth && rj > 0.5) ? 1 : 0;
+            fail = 0;
+            out[512] = 0.0;
+            out[514] = reo ? 1.0 : 0.0;
+        }
     }
     if (lane < FM) {
         const double rii = RT[lane * 9];
@@ -372,16 +392,16 @@ __global__ __launch_bounds__(64) void k_fold_coef1(const double* __restrict__ T1
     }
     U[lane] = (r == c && r < m) ? 1.0 : 0.0;
     Ui[lane] = U[lane];
-    __syncthreads();
+    fwsync();
     double xmax = 0.0;
     for (int j = 0; j < m; ++j) xmax = fmax(xmax, sqrt(XX[j]));
     const bool reorth = reo != 0;
     RY[lane] = (in && r <= c) ? D[r] * RT[lane] : 0.0;  // R_Y = D R
-    __syncthreads();
+    fwsync();
     double est = 0.0;
     if (reorth) {
         if (lane < FM) finv_col(RY, Ri, lane, m);  // R_Y^-1 (Inf / NaN at a zero pivot)
-        __syncthreads();
+        fwsync();
         // W = C2 R_Y^-1 (w x m)
         for (int e = lane; e < 9 * FM; e += 64) {
             const int i = e % 9, cc = e / 9;
@@ -389,7 +409,7 @@ __global__ __launch_bounds__(64) void k_fold_coef1(const double* __restrict__ T1
             for (int k = 0; k <= cc; ++k) v = v + C2s[i + k * 9] * Ri[k + cc * FM];
             Ws[i + cc * 9] = v;
         }
-        __syncthreads();
+        fwsync();
         // A = I - W'W (entry per lane); ||W||_F^2, ||R_Y^-1||_F^2
         double a = (r == c && r < m) ? 1.0 : 0.0;
         if (in)
@@ -423,9 +443,9 @@ __global__ __launch_bounds__(64) void k_fold_coef1(const double* __restrict__ T1
         }
         if (!bad) U[lane] = (in && r <= c) ? uv : 0.0;
         if (lane == 0) fail = bad;
-        __syncthreads();
+        fwsync();
         if (!fail && lane < FM) finv_col(U, Ui, lane, m);
-        __syncthreads();
+        fwsync();
     }
     if (lane == 0) {
         out[513] = fail ? 1.0 : 0.0;
@@ -453,18 +473,34 @@ __global__ __launch_bounds__(64) void k_fold_coef1(const double* __restrict__ T1
             out[256 + e] = Cs[i + j * 9] + (reorth ? C2s[i + j * 9] : 0.0);
         }
     }
-    __syncthreads();
-    if (hout) {
-        for (int e = lane; e < m * m; e += 64) hout[e] = out[e];
-        for (int e = lane; e < w * m; e += 64) hout[256 + e] = out[256 + e];
-        if (lane < 4) hout[512 + lane] = out[512 + lane];
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (lane == 0) {
-            __threadfence_system();
-            __hip_atomic_store(hseq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+    if (Sl) Sl[lane] = fail ? 0.0 : D[r] * Ui[lane];
+    fwsync();
+}
+
+// R, RY and the flags (out) to pinned host memory, then the sequence word
+// (system-scope release): the host's wait_published reads them
+__device__ __forceinline__ void fold_publish(const double* out, int w, int m, double* __restrict__ hout,
+                                             unsigned long long* __restrict__ hseq, unsigned long long seq,
+                                             int lane) {
+    for (int e = lane; e < m * m; e += 64) hout[e] = out[e];
+    for (int e = lane; e < w * m; e += 64) hout[256 + e] = out[256 + e];
+    if (lane < 4) hout[512 + lane] = out[512 + lane];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    fwsync();
+    if (lane == 0) {
+        __threadfence_system();
+        __hip_atomic_store(hseq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+__global__ __launch_bounds__(64) void k_fold_coef1(const double* __restrict__ T1, const double* __restrict__ G,
+                                                  const double* __restrict__ Rtop, int ldr, double* __restrict__ out,
+                                                  double* __restrict__ Sbuf, double* __restrict__ Sm,
+                                                  double* __restrict__ Kbuf, int w, int m, int doreorth, double nglob,
+                                                  double* __restrict__ hout,
+                                                  unsigned long long* __restrict__ hseq, unsigned long long seq) {
+    fold_coef1_body(T1, G, Rtop, ldr, out, Sbuf, Sm, Kbuf, w, m, doreorth, nglob, nullptr, threadIdx.x);
+    if (hout) fold_publish(out, w, m, hout, hseq, seq, threadIdx.x);
 }
 
 // Fixed-order reduction of the up launch's Gram partials (entry-major,
@@ -534,6 +570,45 @@ __global__ __launch_bounds__(64 * UW) void k_fold_down_level(FoldArgs a, int L, 
     const int64_t rows = (int64_t)((nb - t * FG) < FG ? (nb - t * FG) : FG) * FM;
     fold_level_down(a.Vu[L - 1] + (int64_t)t * (64 * URPL * UW * FM), a.tbu[L - 1] + (int64_t)t * (2 * FM), Ss, rows,
                     Sb, (int64_t)t * FG, m, lane, wave, xlds);
+}
+
+// One rank: the root level, the s x s algebra and the root's way down in one
+// block (k_fold_tree's root tile, k_fold_coef1 on wave 0, k_fold_down_level's
+// root), the tile's reflectors kept in registers and R / S_top passed through
+// LDS: three latency-bound launches in one.  The publish comes last, off the
+// way to the S blocks of the level below.
+__global__ __launch_bounds__(64 * UW) void k_fold_root(FoldArgs a, const double* __restrict__ T1,
+                                                       const double* __restrict__ G, double* __restrict__ out,
+                                                       double* __restrict__ Sbuf, double* __restrict__ Sm,
+                                                       double* __restrict__ Kbuf, int w, int doreorth, double nglob,
+                                                       double* __restrict__ hout,
+                                                       unsigned long long* __restrict__ hseq, unsigned long long seq) {
+    __shared__ double xlds[2 * UW * 2 * FM];
+    __shared__ double Rl[64], Sl[64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = a.m;
+    const int L = a.nlev;
+    const double* Rin = L == 1 ? a.R0 : a.Ru[L - 2];
+    const int64_t rows = (int64_t)(L == 1 ? a.n0 : a.nu[L - 2]) * FM;  // one tile (<= FG R blocks)
+    double x[URPL][FM], tau[FM], beta[FM];
+    fload_stack<URPL>(Rin, (int64_t)wave * 64 * URPL, rows, lane, x);
+    tile_geqr2_blk<FM, URPL, UW>(x, tau, beta, m, lane, wave, xlds);
+    if (wave == 0) fput_R(Rl, lane, m, x[0]);
+    __syncthreads();
+    if (wave == 0) fold_coef1_body(T1, G, Rl, FM, out, Sbuf, Sm, Kbuf, w, m, doreorth, nglob, Sl, lane);
+    __syncthreads();
+    tile_org2r_blk<FM, URPL, UW>(x, tau, m, lane, wave, xlds);
+    double* Sb = L == 1 ? a.S0 : a.Su[L - 2];
+#pragma unroll
+    for (int i = 0; i < URPL; ++i) {
+        const int64_t r = (int64_t)wave * 64 * URPL + lane + 64 * i;
+        double o[FM];
+        fmul_S(x[i], Sl, m, o);
+        if (r < rows) {
+#pragma unroll
+            for (int cc = 0; cc < FM; ++cc) Sb[(r >> 3) * 64 + (r & 7) + cc * FM] = o[cc];
+        }
+    }
+    if (wave == 0 && hout) fold_publish(out, w, m, hout, hseq, seq, lane);
 }
 
 // Level 0: Q = Q_tile S - Qp K, one store.  Q: output columns (slots >= m
@@ -690,8 +765,8 @@ hipError_t launch_fold_up(const ColList& P, const FoldArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_fold_up, dim3(a.nblk), dim3(256), 0, st, P, a);
     return hipGetLastError();
 }
-hipError_t launch_fold_tree(const FoldArgs& a, hipStream_t st) {
-    for (int L = 1; L <= a.nlev; ++L)
+hipError_t launch_fold_tree(const FoldArgs& a, hipStream_t st, int upto) {
+    for (int L = 1; L <= (upto >= 0 ? upto : a.nlev); ++L)
         hipLaunchKernelGGL(k_fold_tree, dim3(a.nu[L - 1]), dim3(64 * UW), 0, st, a, L);
     return hipGetLastError();
 }
@@ -706,9 +781,16 @@ hipError_t launch_fold_coef1(const double* T1, const double* G, const double* Rt
                        nglob, hout, hseq, seq);
     return hipGetLastError();
 }
-hipError_t launch_fold_down_tree(const FoldArgs& a, const double* Stop, int lds, hipStream_t st) {
-    for (int L = a.nlev; L >= 1; --L)
+hipError_t launch_fold_down_tree(const FoldArgs& a, const double* Stop, int lds, hipStream_t st, int from) {
+    for (int L = from >= 0 ? from : a.nlev; L >= 1; --L)
         hipLaunchKernelGGL(k_fold_down_level, dim3(a.nu[L - 1]), dim3(64 * UW), 0, st, a, L, Stop, lds);
+    return hipGetLastError();
+}
+hipError_t launch_fold_root(const FoldArgs& a, const double* T1, const double* G, double* out, double* Sbuf,
+                            double* Sm, double* Kbuf, int w, int doreorth, double nglob, double* hout,
+                            unsigned long long* hseq, unsigned long long seq, hipStream_t st) {
+    hipLaunchKernelGGL(k_fold_root, dim3(1), dim3(64 * UW), 0, st, a, T1, G, out, Sbuf, Sm, Kbuf, w, doreorth, nglob,
+                       hout, hseq, seq);
     return hipGetLastError();
 }
 hipError_t launch_fold_down(const ColList& P, const OutList& Q, const FoldArgs& a, hipStream_t st) {

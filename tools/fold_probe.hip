@@ -54,6 +54,7 @@ int main(int argc, char** argv) {
         oSu[L] = take((size_t)nu[L] * 64);
     }
     const size_t oRrm = take(64), oK = take(72), oOut = take(520), oPart = take((size_t)272 * nblk);
+    const size_t oT1 = take(272), oG = take(72), oSb = take(64), oSm = take(64), oRt = take(64);
     CK(hipMalloc((void**)&F, off * sizeof(double)));
     hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, P, (int64_t)17 * ld, 1ull, 1.0);
     hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, F, (int64_t)off, 7ull, 0.2);
@@ -116,6 +117,50 @@ int main(int argc, char** argv) {
     if (timeit("tree", 0.0, [&] { return launch_fold_tree(fa, st); })) return 1;
     if (timeit("down_tree", 0.0, [&] { return launch_fold_down_tree(fa, F + oRrm, 8, st); })) return 1;
     if (timeit("down", b_down, [&] { return launch_fold_down(cu, qo, fa, st); })) return 1;
+    // the coefficient step on inputs that take its whole path (second
+    // projection, Cholesky, no decline): X'X = I on the diagonal, C = 0.9,
+    // C2 = 1e-8, root R = 2 I + 0.1 strictly upper
+    {
+        std::vector<double> t1(272, 0.0), g(72, 1e-8), rt(64, 0.0);
+        for (int j = 0; j < 8; ++j) {
+            t1[(8 + j) + (8 + j) * 16] = 1.0;
+            for (int i = 0; i < 8; ++i) t1[i + (8 + j) * 16] = 0.9 / 3.0;
+            t1[256 + 8 + j] = 0.9 / 3.0;
+            for (int i = 0; i <= j; ++i) rt[i + j * 8] = i == j ? 2.0 : 0.1;
+        }
+        CK(hipMemcpy(F + oT1, t1.data(), 272 * 8, hipMemcpyHostToDevice));
+        CK(hipMemcpy(F + oG, g.data(), 72 * 8, hipMemcpyHostToDevice));
+        CK(hipMemcpy(F + oRt, rt.data(), 64 * 8, hipMemcpyHostToDevice));
+    }
+    double* hpin = nullptr;
+    CK(hipHostMalloc((void**)&hpin, 1024 * sizeof(double), hipHostMallocDefault));
+    unsigned long long* hseq = reinterpret_cast<unsigned long long*>(hpin + 516);
+    unsigned long long sq = 0;
+    if (timeit("coef1", 0.0, [&] {
+            return launch_fold_coef1(F + oT1, F + oG, F + oRt, 8, F + oOut, F + oSb, F + oSm, F + oK, w, m, 1,
+                                     (double)n, nullptr, nullptr, 0, st);
+        }))
+        return 1;
+    if (timeit("coef1_pub", 0.0, [&] {
+            return launch_fold_coef1(F + oT1, F + oG, F + oRt, 8, F + oOut, F + oSb, F + oSm, F + oK, w, m, 1,
+                                     (double)n, hpin, hseq, ++sq, st);
+        }))
+        return 1;
+    if (timeit("root_pub", 0.0, [&] {
+            return launch_fold_root(fa, F + oT1, F + oG, F + oOut, F + oSb, F + oSm, F + oK, w, 1, (double)n, hpin,
+                                    hseq, ++sq, st);
+        }))
+        return 1;
+    if (timeit("root", 0.0, [&] {
+            return launch_fold_root(fa, F + oT1, F + oG, F + oOut, F + oSb, F + oSm, F + oK, w, 1, (double)n,
+                                    nullptr, nullptr, 0, st);
+        }))
+        return 1;
+    {
+        std::vector<double> o(520);
+        CK(hipMemcpy(o.data(), F + oOut, 520 * 8, hipMemcpyDeviceToHost));
+        printf("coef flags: reorth %g fail %g est %g\n", o[514], o[513], o[515]);
+    }
     FoldArgs fr = fa;
     fr.V0 = nullptr;  // re-forming down pass, up without the tile store
     if (timeit("up_nost", 17.0 * 8.0 * n, [&] { return launch_fold_up(cu, fr, st); })) return 1;
