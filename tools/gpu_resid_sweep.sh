@@ -5,8 +5,8 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=$GRAFT_REPO_ROOT/gpurun_out/${TAG:-resid_sweep}
 mkdir -p $O
-for v in ${COMBOS:-"4 4" "2 4" "2 8" "1 8" "4 2" "2 2" "4 4"}; do
-  set -- $v
+for v in ${COMBOS:-4x4 2x4 2x8 1x8 4x2 2x2 4x4}; do
+  set -- ${v/x/ }
   CAL_RESID_CPB=$1 CAL_RESID_PPT=$2 DIAG_REPS=2 timeout -k 10 300 python tools/diag_only.py > $O/diag_c$1_p$2.json 2> $O/diag_c$1_p$2.err || exit $?
   echo "cpb=$1 ppt=$2 $(cat $O/diag_c$1_p$2.json)"
 done
