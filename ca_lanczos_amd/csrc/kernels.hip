@@ -1792,9 +1792,8 @@ hipError_t launch_apply(const Panel& P, const double* dM, int wp, int wy, const 
 // starting from 0, as k_apply_rows computes it (the probe compares bitwise).
 // One segment each; Y must not alias P.  Grid: blockIdx.y = 16*NT-column group.
 template <int NT, int WAVES, int KG>
-__global__ __launch_bounds__(64 * WAVES) void k_apply_mt(const double* __restrict__ P, int64_t ldp,
-                                                         const double* __restrict__ M, int wp, int wy,
-                                                         double* __restrict__ Y, int64_t ldy, int64_t n) {
+__device__ __forceinline__ void apply_mt_body(const double* __restrict__ P, int64_t ldp, const double* __restrict__ M,
+                                              int wp, int wy, double* __restrict__ Y, int64_t ldy, int64_t n) {
     extern __shared__ __attribute__((aligned(16))) double Ms[];  // [wpp][16 NT]
     constexpr int ldm = 16 * NT;
     const int wpp = (wp + 3) & ~3;
@@ -1811,58 +1810,48 @@ __global__ __launch_bounds__(64 * WAVES) void k_apply_mt(const double* __restric
     // B operands in groups of KG k-steps, the next group's loads issued before
     // this group's MFMAs (KG per NT from tools/ritz_apply_probe.hip); the last
     // group of a row tile issues the NEXT row tile's first group, so its load
-    // latency hides behind this tile's last MFMAs and stores
-    auto load_group = [&](int64_t rt, int kc0, double (&b)[KG][2]) {
-        const bool fl = rt + 32 <= n;
+    // latency hides behind this tile's last MFMAs and stores.  Full 32-row
+    // tiles load branch-free (a column past wp reads column wp - 1, whose
+    // coefficient rows in Ms are zero): a per-load branch between a 16-B and
+    // a guarded path made the compiler join the two with vmcnt(0) after every
+    // group, i.e. no load was in flight across the MFMAs.  The one partial
+    // tile of the grid runs after the loop with guarded loads.
+    auto load_full = [&](int64_t rt, int kc0, double (&b)[KG][2]) {
         const int64_t rbt = rt + 2 * c16;
 #pragma unroll
         for (int u = 0; u < KG; ++u) {
             const int c = 4 * (kc0 + u) + g;
-            const bool con = c < wp;
-            const double* pc = P + (int64_t)(con ? c : 0) * ldp;
-            double b0, b1;
-            if (fl) {
-                const d2 x = *reinterpret_cast<const d2*>(pc + rbt);
-                b0 = x[0];
-                b1 = x[1];
-            } else {
-                b0 = rbt < n ? pc[rbt] : 0.0;
-                b1 = rbt + 1 < n ? pc[rbt + 1] : 0.0;
-            }
-            b[u][0] = con ? b0 : 0.0;
-            b[u][1] = con ? b1 : 0.0;
+            const d2 x = *reinterpret_cast<const d2*>(P + (int64_t)(c < wp ? c : wp - 1) * ldp + rbt);
+            b[u][0] = x[0];
+            b[u][1] = x[1];
         }
     };
-    double bcur[KG][2], bnxt[KG][2];
-    const int64_t rstart = ((int64_t)blockIdx.x * WAVES + wave) * 32;
-    if (rstart < n) load_group(rstart, 0, bcur);
-    for (int64_t r0 = rstart; r0 < n; r0 += stride) {
-        const bool full = r0 + 32 <= n;
-        const int64_t rb = r0 + 2 * c16;
-        d4 acc[NT][2];
+    auto load_part = [&](int64_t rt, int kc0, double (&b)[KG][2]) {
+        const int64_t rbt = rt + 2 * c16;
 #pragma unroll
-        for (int ty = 0; ty < NT; ++ty) acc[ty][0] = acc[ty][1] = d4{0.0, 0.0, 0.0, 0.0};
-        for (int kc0 = 0; kc0 < nkc; kc0 += KG) {
-            if (kc0 + KG < nkc) load_group(r0, kc0 + KG, bnxt);
-            else if (r0 + stride < n) load_group(r0 + stride, 0, bnxt);
+        for (int u = 0; u < KG; ++u) {
+            const int c = 4 * (kc0 + u) + g;
+            const double* pc = P + (int64_t)(c < wp ? c : wp - 1) * ldp;
+            b[u][0] = rbt < n ? pc[rbt] : 0.0;
+            b[u][1] = rbt + 1 < n ? pc[rbt + 1] : 0.0;
+        }
+    };
+    auto mfma_group = [&](int kc0, const double (&b)[KG][2], d4 (&acc)[NT][2]) {
 #pragma unroll
-            for (int u = 0; u < KG; ++u) {
-                const int c = 4 * (kc0 + u) + g;  // rows of Ms past wpp are never read: kc0 + u < nkc below
-                if (kc0 + u < nkc) {
+        for (int u = 0; u < KG; ++u) {
+            const int c = 4 * (kc0 + u) + g;  // rows of Ms past wpp are never read: kc0 + u < nkc below
+            if (kc0 + u < nkc) {
 #pragma unroll
-                    for (int ty = 0; ty < NT; ++ty) {
-                        const double a = Ms[c * ldm + 16 * ty + c16];
-                        acc[ty][0] = mfma64(a, bcur[u][0], acc[ty][0]);
-                        acc[ty][1] = mfma64(a, bcur[u][1], acc[ty][1]);
-                    }
+                for (int ty = 0; ty < NT; ++ty) {
+                    const double a = Ms[c * ldm + 16 * ty + c16];
+                    acc[ty][0] = mfma64(a, b[u][0], acc[ty][0]);
+                    acc[ty][1] = mfma64(a, b[u][1], acc[ty][1]);
                 }
             }
-#pragma unroll
-            for (int u = 0; u < KG; ++u) {
-                bcur[u][0] = bnxt[u][0];
-                bcur[u][1] = bnxt[u][1];
-            }
         }
+    };
+    auto store_tile = [&](int64_t r0, bool full, const d4 (&acc)[NT][2]) {
+        const int64_t rb = r0 + 2 * c16;
 #pragma unroll
         for (int ty = 0; ty < NT; ++ty)
 #pragma unroll
@@ -1881,7 +1870,43 @@ __global__ __launch_bounds__(64 * WAVES) void k_apply_mt(const double* __restric
                     }
                 }
             }
+    };
+    double bcur[KG][2], bnxt[KG][2];
+    int64_t r0 = ((int64_t)blockIdx.x * WAVES + wave) * 32;
+    if (r0 + 32 <= n) load_full(r0, 0, bcur);
+    for (; r0 + 32 <= n; r0 += stride) {
+        d4 acc[NT][2];
+#pragma unroll
+        for (int ty = 0; ty < NT; ++ty) acc[ty][0] = acc[ty][1] = d4{0.0, 0.0, 0.0, 0.0};
+        for (int kc0 = 0; kc0 < nkc; kc0 += KG) {
+            if (kc0 + KG < nkc) load_full(r0, kc0 + KG, bnxt);
+            else if (r0 + stride + 32 <= n) load_full(r0 + stride, 0, bnxt);
+            mfma_group(kc0, bcur, acc);
+#pragma unroll
+            for (int u = 0; u < KG; ++u) {
+                bcur[u][0] = bnxt[u][0];
+                bcur[u][1] = bnxt[u][1];
+            }
+        }
+        store_tile(r0, true, acc);
     }
+    if (r0 < n) {  // the partial tile
+        d4 acc[NT][2];
+#pragma unroll
+        for (int ty = 0; ty < NT; ++ty) acc[ty][0] = acc[ty][1] = d4{0.0, 0.0, 0.0, 0.0};
+        for (int kc0 = 0; kc0 < nkc; kc0 += KG) {
+            load_part(r0, kc0, bcur);
+            mfma_group(kc0, bcur, acc);
+        }
+        store_tile(r0, false, acc);
+    }
+}
+
+template <int NT, int WAVES, int KG>
+__global__ __launch_bounds__(64 * WAVES) void k_apply_mt(const double* __restrict__ P, int64_t ldp,
+                                                         const double* __restrict__ M, int wp, int wy,
+                                                         double* __restrict__ Y, int64_t ldy, int64_t n) {
+    apply_mt_body<NT, WAVES, KG>(P, ldp, M, wp, wy, Y, ldy, n);
 }
 
 // k-steps per load group of k_apply_mt by tile count
