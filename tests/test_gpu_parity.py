@@ -216,12 +216,15 @@ def test_project_and_normalize_one_block(cal, ref, frac):
 
 
 @pytest.mark.parametrize("n,w,m,frac", [(70001, 9, 8, 0.9), (1200001, 9, 8, 0.9), (1200001, 5, 4, 0.9),
-                                        (300001, 9, 8, 0.1), (1200001, 3, 2, 0.1)])
+                                        (300001, 9, 8, 0.1), (1200001, 3, 2, 0.1), (10001, 9, 8, 0.9),
+                                        (257, 9, 8, 0.9)])
 def test_project_and_normalize_fused_tsqr_tree(cal, ref, n, w, m, frac):
     """The fused TSQR projectAndNormalize (blockorth.cpp pn_tsqr_fold,
     tsqr_fold.hip) with several tiles on every tree level: 70001 rows = 274
     level-0 tiles, 5 level-1 tiles; 1.2 M rows = 4688 / 74 / 2 level tiles
-    under the root; m < 8 pads the stacked R factors.  Against the oracle's
+    under the root; 10001 and 257 rows: 40 and 2 level-0 tiles under a root
+    that stacks level 0 directly (k_fold_root on the first level); m < 8
+    pads the stacked R factors.  Against the oracle's
     projectAndNormalize (explicit Z, Householder QR): RZ to 1e-11 (C) and
     1e-12 ||X|| (R), QZ orthonormal to 1e-13 and to Qp like the oracle's, the
     reorth flag identical; the fold ran and was not declined."""
@@ -315,16 +318,17 @@ def test_ca_lanczos_newton_full(cal, ref):
     assert np.max(out.orth_err) < 1e-12
 
 
-@pytest.mark.parametrize("N,orth", [(24, "local"), (64, "full"), (40, "local")])
+@pytest.mark.parametrize("N,orth", [(24, "local"), (64, "full"), (40, "local"), (25, "local")])
 def test_orth_err_deferred_wide_gram(cal, ref, monkeypatch, N, orth):
     """compute_orth_err (ca_lanczos.m:99-107) of every iteration from one
     block-upper Gram of Q(:,1:sk+1) at the flush (k_gram_wide, lanczos.cpp
     oe_flush; 'local' / 'full' only, Q's columns are final once written)
     against the per-iteration Grams (CAL_OE_DEFER=0) on the same run: the
     same dot products in another summation order.  s = 8, 15 outer
-    iterations (121 columns, the bench's shape), 13.8 k / 262 k / 64 k rows;
-    the 40^3 case is also run with 14 iterations to a flush with fewer
-    columns than the pinned shape."""
+    iterations (121 columns, the bench's shape), 13.8 k / 262 k / 64 k /
+    15.6 k rows (the last not a multiple of the kernel's 32-row steps); the
+    40^3 case is also run with 14 iterations to a flush with fewer columns
+    than the pinned shape."""
     A = cal.matrices.laplacian_3d(N)
     r = ref.matlab_rand(A.shape[0])
     its = [120, 112] if N == 40 else [120]
