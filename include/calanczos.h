@@ -189,7 +189,11 @@ int cal_ca_lanczos(cal_ctx* ctx, const double* r, int s, int iter, const char* b
 /* Step-wise, device-resident form of the same loop (benchmarks, restart
  * drivers).  begin() normalises r and runs the basis set-up (Newton
  * prologue); step() runs one outer iteration (s SpMVs + block orth + T
- * update); get() copies the current T (sk x sk, ldt >= sk) and flags. */
+ * update); get() copies the current T (sk x sk, ldt >= sk) and flags.
+ * With diagnostics the iteration's rn / oe are computed late (rn one
+ * iteration behind; oe of 'local' / 'full' runs of <= 128 columns at the
+ * last step, from one Gram of Q): get() finishes whatever is pending, so
+ * its rn / oe are always complete for the iterations run so far. */
 int cal_lanczos_begin(cal_ctx* ctx, const double* r, int s, int max_outer, const char* basis,
                       const char* orth);
 int cal_lanczos_step(cal_ctx* ctx, int diagnostics);
