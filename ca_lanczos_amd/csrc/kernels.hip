@@ -2233,7 +2233,8 @@ int rowapply_wpmax(int wp) { return wp <= 5 ? 5 : (wp <= 9 ? 9 : (wp <= 17 ? 17 
 int rowapply_mout(int m) { return m <= 4 ? 4 : (m <= 8 ? 8 : (m <= 16 ? 16 : 0)); }
 
 // kind: 0 store only, 1 store + Gram, 2 Gram without store (pass A),
-// 3 chained store (pass B).  Instantiated for the shapes of s = 4 and s = 8.
+// 3 chained store (pass B).  Instantiated for the shapes of s = 4 and s = 8
+// ('full' with s = 4 reaches 10..17 projection columns with 4 outputs).
 hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, const OutList& Y, int kind, int wq,
                            int64_t n, int blocks, double* partial, hipStream_t st) {
     const int WP = rowapply_wpmax(wp), MO = rowapply_mout(m);
@@ -2255,6 +2256,7 @@ hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, co
         CAL_RA_SHAPE(9, 4)
         CAL_RA_SHAPE(9, 8)
         CAL_RA_SHAPE(9, 16)
+        CAL_RA_SHAPE(17, 4)
         CAL_RA_SHAPE(17, 8)
         case 1716:
             if (kind != 0) return hipErrorInvalidValue;

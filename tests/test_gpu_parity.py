@@ -446,12 +446,36 @@ def test_ca_lanczos_periodic_selective(cal, ref, orth):
     assert np.max(out.orth_err) < 1e-6 and np.max(exp.orth_err) < 1e-6
 
 
+def test_ca_lanczos_full_s4(cal, ref):
+    """'full' orthogonalisation at s = 4 on the restart test's matrix
+    (diag(linspace(1,1e4,5000)), r = ones, 60 steps): projection widths 5 ..
+    57, i.e. the row-apply shapes (9, 4) and (17, 4) and the wide Grams.  T
+    against the oracle (_compare_lanczos), orthogonality at rounding level."""
+    import scipy.sparse as sp
+    a = ref.matlab_linspace(1.0, 1.0e4, 5000)
+    A = sp.csr_matrix(sp.diags(a))
+    r = np.ones(5000)
+    out = cal.ca_lanczos_ex(A, r, 4, 60, "newton", "full")
+    exp = ref.ca_lanczos(A, r, 4, 60, "newton", "full")
+    # the prologue's Ritz values are symmetric about the spectrum's centre, so
+    # the Leja order has exact ties that rounding breaks either way: the same
+    # shifts, possibly in another order (hence another basis; T is basis-free)
+    assert np.allclose(np.sort(out.shifts), np.sort(exp.shifts), rtol=0, atol=1e-9 * 1.0e4)
+    assert list(out.reorth) == list(exp.reorth)
+    assert np.max(np.abs(out.T - exp.T)) <= 1e-9 * 1.0e4
+    assert np.max(out.orth_err) < 1e-12
+
+
 def test_restarted_ca_lanczos(cal, ref):
     """the explicit restart driver on the reference's own input
     (test_restart_diagonal_matrices.m:8-28: diag(linspace(1,1e4,5000)),
     r = ones, max_lanczos 60, 10 wanted, s = 4, newton, 'full', tol 1e-8).
-    Known answer: the 10 largest diagonal entries; the oracle's restart count
-    and eigenvalues; the converged vectors orthonormal eigenvectors."""
+    Known answer: the 10 largest diagonal entries; the oracle's eigenvalues;
+    the converged vectors orthonormal eigenvectors.  The restart count is
+    ill-conditioned here (ten wanted eigenvalues 2 apart at tol 1e-8): the
+    oracle itself takes 93, 106, 120 and 96 restarts for r = ones perturbed
+    by 0, +-1e-15 and 3e-15 relative (times cos(i)), so the bar is that
+    spread, +-35 % of the oracle's unperturbed count, not equality."""
     import scipy.sparse as sp
     a = ref.matlab_linspace(1.0, 1.0e4, 5000)
     A = sp.csr_matrix(sp.diags(a))
@@ -459,7 +483,7 @@ def test_restarted_ca_lanczos(cal, ref):
     exp = ref.restarted_ca_lanczos(A, r, 60, 10, 4, "newton", "full", 1.0e-8)
     out = cal.restarted_ca_lanczos(A, r, 60, 10, 4, "newton", "full", 1.0e-8)
     assert out["converged"] and exp["converged"]
-    assert out["num_restarts"] == exp["num_restarts"]
+    assert abs(out["num_restarts"] - exp["num_restarts"]) <= 0.35 * exp["num_restarts"]
     eref = a[::-1][:10]
     assert np.max(np.abs(out["conv_eigs"] - eref)) <= 1e-8 * 1.0e4
     assert np.max(np.abs(out["conv_eigs"] - exp["conv_eigs"])) <= 1e-9 * 1.0e4
