@@ -466,6 +466,22 @@ def test_ca_lanczos_full_s4(cal, ref):
     assert np.max(out.orth_err) < 1e-12
 
 
+@pytest.mark.parametrize("s", [2, 3, 5, 6])
+def test_ca_lanczos_full_block_sizes(cal, ref, s):
+    """'full' orthogonalisation at s = 2, 3, 5, 6 (lap2d 24^2, 8 blocks): every
+    (projection columns, outputs) shape the device block orthogonalisation
+    reaches on the way from 1 to 9 projection columns.  Shifts as a set (Leja
+    ties on the symmetric spectrum), flags, T to 1e-9 ||A||, orthogonality."""
+    A = cal.matrices.laplacian_2d(24)
+    r = ref.matlab_rand(A.shape[0])
+    out = cal.ca_lanczos_ex(A, r, s, 8 * s, "newton", "full")
+    exp = ref.ca_lanczos(A, r, s, 8 * s, "newton", "full")
+    assert np.allclose(np.sort(out.shifts), np.sort(exp.shifts), rtol=0, atol=1e-9 * 8.0)
+    assert list(out.reorth) == list(exp.reorth)
+    assert np.max(np.abs(out.T - exp.T)) <= 1e-9 * 8.0
+    assert np.max(out.orth_err) < 1e-12
+
+
 def test_restarted_ca_lanczos(cal, ref):
     """the explicit restart driver on the reference's own input
     (test_restart_diagonal_matrices.m:8-28: diag(linspace(1,1e4,5000)),
