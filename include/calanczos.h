@@ -59,8 +59,9 @@ int cal_timer_reset(cal_ctx* ctx);
 
 /* ---- the sparse matrix A ------------------------------------------------ */
 /* MATLAB mxArray sparse storage (CSC: jc colptr, ir rowidx, pr values, all
- * mwIndex = int64).  A is symmetric, so CSC(A) == CSR(A) and the arrays are
- * consumed as CSR.  Replaces the `A` argument of SpMV.m:6, ca_lanczos.m:24. */
+ * mwIndex = int64), transposed into CSR on the host, so the device holds A
+ * (not A') for any A; rows keep ascending columns, MATLAB's accumulation
+ * order.  Replaces the `A` argument of SpMV.m:6, ca_lanczos.m:24. */
 int cal_set_matrix_csc(cal_ctx* ctx, int64_t n, const int64_t* jc, const int64_t* ir, const double* pr);
 /* CSR with int64 row pointers and int32 column indices (SciPy layout). */
 int cal_set_matrix_csr(cal_ctx* ctx, int64_t n, const int64_t* rowptr, const int32_t* colind, const double* val);
