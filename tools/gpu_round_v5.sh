@@ -1,0 +1,19 @@
+# Round verification on a rebuilt tree: full GPU suite, smoke, default bench (with CPU baseline),
+# rocprofv3 kernel stats of the headline. Each GPU step time-limited; stops at the first hard failure.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=$GRAFT_REPO_ROOT/gpurun_out/v5
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 600 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -4 $O/pytest.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -2 $O/smoke.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
+rc=$?; echo "bench rc=$rc"; cut -c1-300 $O/bench.json
+[ $rc -eq 0 ] || exit $rc
+cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
+    python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline > $O/prof.log 2>&1
+echo "prof rc=$?"
