@@ -485,6 +485,8 @@ def main():
     host_rt_ms = None
     pat_spmv = None
     csr_leg = None
+    lap2d_leg = None
+    irl_leg = None
     # the same outer iteration with the Householder TSQR normalize (tsqr.m,
     # BASELINE configs 3/4: "TSQR" / "RCCL TSQR tree"), every rank
     tsqr_leg = None
@@ -517,6 +519,18 @@ def main():
             # SURVEY §8d's 619 / 691 outer-it/s bound is for this format
             csr_leg = timed_leg(ctx2, r_full[r0:r1], s, min(K, 10), min(W, 2), args.basis, args.orth, None)
         ctx2.close()
+        if not args.no_legs:
+            # north_star's literal target (a ~10M-row 5-pt Laplacian at s = 8)
+            # and BASELINE config 5's driver on the G3_circuit stand-in
+            if wl.name != "lap2d_3162":
+                try:
+                    lap2d_leg = workload_leg(cal, local, "lap2d_3162", s, min(K, 15), min(W, 2), args.basis)
+                except cal.CalError as e:
+                    lap2d_leg = {"error": str(e)}
+            try:
+                irl_leg = irl_workload_leg(cal, local, "circuit_1259", s, args.basis)
+            except cal.CalError as e:
+                irl_leg = {"error": str(e)}
         # tier-1 host-pointer SpMV (MATLAB-boundary semantics: PCIe in and out)
         v = np.ones(n)
         ctx.spmv(v)
@@ -618,6 +632,10 @@ def main():
         csr_leg["spmv_frac"] = csr_leg["spmv_gbps"] / HBM_PEAK_GBS
         csr_leg["survey_bound_outer_iters_per_s"] = HBM_PEAK_GBS * 1e9 / (b_outer + 8 * n * (2 * s + 1))
         line["csr_step"] = csr_leg
+    if lap2d_leg is not None:
+        line["lap2d_3162_step"] = lap2d_leg
+    if irl_leg is not None:
+        line["irl"] = irl_leg
     if csr_spmv is not None:
         line["spmv_csr_kernel"] = {"avg_us": csr_spmv[0] * 1e3, "min_us": csr_spmv[1] * 1e3,
                                    "gbps": b_csr / (csr_spmv[0] * 1e-3) / 1e9, "bytes_per_launch": b_csr}
@@ -673,6 +691,77 @@ def timed_leg(ctx, r, s, K, W, basis, orth, dist):
             "kernel_launches": {k: v[0] for k, v in tm.items()}}
 
 
+def leg_roofline(leg, fmt, npairpat, n_loc, nnz_loc, s):
+    """SpMV GB/s and the roofline of the leg's dominant kernel class, from its
+    HIP-event per-launch averages (the algorithmic bytes of DESIGN.md §3)."""
+    b_spmv = ((17 if npairpat else 18) * n_loc) if fmt == "pattern" else 12 * nnz_loc + 20 * n_loc + 4
+    bytes_per = {"spmv": b_spmv, "gram": (2 * s + 1) * 8 * n_loc, "apply": (3 * s + 1) * 8 * n_loc}
+    avg = leg["kernel_avg_launch_us"]
+    per = {k: leg["kernel_ms_per_step"][k] for k in bytes_per}
+    dom = max(per, key=per.get)
+    leg["spmv_gbps"] = b_spmv / (avg["spmv"] * 1e-6) / 1e9
+    leg["spmv_frac"] = leg["spmv_gbps"] / HBM_PEAK_GBS
+    ach = bytes_per[dom] / (avg[dom] * 1e-6) / 1e9
+    leg["roofline"] = {"bound": "hbm", "kernel_class": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": ach / HBM_PEAK_GBS, "bytes_per_launch": bytes_per[dom], "avg_launch_us": avg[dom]}
+    return leg
+
+
+def workload_leg(cal, local, name, s, K, W, basis):
+    """The headline's outer iteration (same s, basis, 'local', default
+    normalize) on another resident workload, one GPU: outer-it/s, SpMV GB/s
+    and the dominant kernel class's roofline fraction."""
+    wl2 = Workload(name)
+    c = cal.Context(device=local)
+    try:
+        c.set_matrix(wl2.full())
+        r = np.random.RandomState(5489).random_sample(wl2.n)
+        leg = timed_leg(c, r, s, K, W, basis, "local", None)
+        fmt, npat, nent = c.spmv_format()
+        npairpat, npent, nsplit = c.spmv_pair_info()
+        nnz = c.matrix_info()["nnz_local"]
+        leg["workload"] = wl2.desc % (wl2.n, nnz)
+        leg["spmv_format"] = ("%s (%d pair patterns, %d split pairs)" % (fmt, npairpat, nsplit)
+                              if fmt == "pattern" else fmt)
+        leg_roofline(leg, fmt, npairpat, wl2.n, nnz, s)
+        if fmt == "pattern":
+            b2b = c.bench_spmv(20, 1.0)
+            leg["spmv_kernel_back_to_back"] = {"avg_us": b2b[0] * 1e3,
+                                               "gbps": (17 if npairpat else 18) * wl2.n / (b2b[0] * 1e-3) / 1e9}
+    finally:
+        c.close()
+    return leg
+
+
+def irl_workload_leg(cal, local, name, s, basis, ml=64, nw=8, tol=1.0e-8):
+    """BASELINE config 5's driver as a leg of the default line: whole
+    impl_restarted_ca_lanczos solves on the resident G3_circuit stand-in
+    (CSR SpMV), solves/s and the SpMV's roofline inside the solve."""
+    wl2 = Workload(name)
+    c = cal.Context(device=local)
+    try:
+        c.set_matrix(wl2.full())
+        r = np.random.RandomState(5489).random_sample(wl2.n)
+        M = irl_measure(cal, c, r, ml, nw, s, basis, tol, 3, 1, None)
+        fmt = c.spmv_format()[0]
+        nnz = c.matrix_info()["nnz_local"]
+    finally:
+        c.close()
+    b_spmv = (12 * nnz + 20 * wl2.n + 4) if fmt == "csr" else 18 * wl2.n
+    ach = b_spmv / (M["spmv_avg_ms"] * 1e-3) / 1e9
+    t = M["timers"]
+    return {"solves_per_s": M["K"] / M["elapsed"], "ms_per_solve": 1e3 * M["elapsed"] / M["K"], "solves": M["K"],
+            "workload": wl2.desc % (wl2.n, nnz), "driver": "impl_restarted_ca_lanczos",
+            "max_lanczos": ml, "n_wanted_eigs": nw, "m": M["m"], "s": s, "orth": "full", "tol": tol,
+            "num_restarts": M["out"]["num_restarts"], "converged": M["out"]["converged"],
+            "blocks_per_s": M["blocks"] / M["elapsed"], "spmv_format": fmt,
+            "kernel_ms_per_solve": {"spmv": t[1], "gram": t[3], "apply": t[5]},
+            "kernel_launches_per_solve": {"spmv": t[0], "gram": t[2], "apply": t[4]},
+            "roofline": {"bound": "hbm", "kernel": "SpMV (%s) inside the solve" % fmt, "achieved": ach,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                         "bytes_per_launch": b_spmv, "avg_launch_us": M["spmv_avg_ms"] * 1e3}}
+
+
 def diagnostics_run(ctx, r, s, args, t=15):
     """The reference-faithful cost: ca_lanczos.m computes the
     Ritz residual norms and the orthogonality error at every outer iteration
@@ -692,28 +781,20 @@ def diagnostics_run(ctx, r, s, args, t=15):
                     "the orthogonality error after every outer iteration, as the reference always runs"}
 
 
-def main_irl(args):
-    """BASELINE config 5: whole impl_restarted_ca_lanczos solves (normest,
-    Newton prologue, CA blocks, shifts, compression) on resident A."""
-    E = setup(args)
-    world, rank, wl, cal, dist, ctx = (E[k] for k in ("world", "rank", "wl", "cal", "dist", "ctx"))
-    r0, r1, nnz_local, nnz_total = E["r0"], E["r1"], E["nnz_local"], E["nnz_total"]
-    n = wl.n
-    s = args.s
-    ml, nw = (int(x) for x in args.irl.split(","))
+def irl_measure(cal, ctx, r_loc, ml, nw, s, basis, tol, K, W, dist):
+    """Time K whole impl_restarted_ca_lanczos solves after W warm-up solves
+    (barrier + synchronize on both sides, max over ranks), then one solve
+    with the per-kernel HIP-event timers and one that downloads Q_conv."""
     # k kept, p shifts, m = k + p (impl_restarted_ca_lanczos.m:72-74, k >= s; include/calanczos.h)
     k = max(nw + 4, s)
     p = s * ((ml - k) // s)
     m = k + p
-    r_full = np.random.RandomState(5489).random_sample(n)
-    r_loc = r_full[r0:r1]
-    K, W = max(1, min(args.steps, 5)), max(0, min(args.warmup, 1))
 
     def solve(return_Q=False):
         # timed solves leave the Ritz vectors Q_conv on the device (the bench's
         # inputs and outputs are HBM-resident); one more solve below returns
         # them over PCIe and is reported beside the line
-        return cal.impl_restarted_ca_lanczos(None, r_loc, ml, nw, s, args.basis, "full", args.irl_tol, ctx=ctx,
+        return cal.impl_restarted_ca_lanczos(None, r_loc, ml, nw, s, basis, "full", tol, ctx=ctx,
                                              return_Q=return_Q)
 
     for _ in range(W):
@@ -733,14 +814,34 @@ def main_irl(args):
     ctx.timer_enable(True)
     ctx.timer_reset()
     out = solve()
-    spmv_cnt, spmv_ms = ctx.timer_read("spmv")
-    gram_cnt, gram_ms = ctx.timer_read("gram")
-    apply_cnt, apply_ms = ctx.timer_read("apply")
+    timers = []
+    for kind in ("spmv", "gram", "apply"):
+        timers += list(ctx.timer_read(kind))
     ctx.timer_enable(False)
     t_q = time.perf_counter()
     solve(return_Q=True)
     solve_q_ms = (time.perf_counter() - t_q) * 1e3
-    elapsed, spmv_avg_ms = max_over_ranks(dist, [elapsed, spmv_ms / max(spmv_cnt, 1)])
+    elapsed, spmv_avg_ms = max_over_ranks(dist, [elapsed, timers[1] / max(timers[0], 1)])
+    return {"k": k, "p": p, "m": m, "out": out, "elapsed": elapsed, "spmv_avg_ms": spmv_avg_ms,
+            "timers": timers, "blocks": blocks, "solve_q_ms": solve_q_ms, "K": K}
+
+
+def main_irl(args):
+    """BASELINE config 5: whole impl_restarted_ca_lanczos solves (normest,
+    Newton prologue, CA blocks, shifts, compression) on resident A."""
+    E = setup(args)
+    world, rank, wl, cal, dist, ctx = (E[k] for k in ("world", "rank", "wl", "cal", "dist", "ctx"))
+    r0, r1, nnz_local, nnz_total = E["r0"], E["r1"], E["nnz_local"], E["nnz_total"]
+    n = wl.n
+    s = args.s
+    ml, nw = (int(x) for x in args.irl.split(","))
+    r_full = np.random.RandomState(5489).random_sample(n)
+    K, W = max(1, min(args.steps, 5)), max(0, min(args.warmup, 1))
+    M = irl_measure(cal, ctx, r_full[r0:r1], ml, nw, s, args.basis, args.irl_tol, K, W, dist)
+    k, m, out = M["k"], M["m"], M["out"]
+    elapsed, spmv_avg_ms = M["elapsed"], M["spmv_avg_ms"]
+    spmv_cnt, spmv_ms, gram_cnt, gram_ms, apply_cnt, apply_ms = M["timers"]
+    blocks, solve_q_ms = M["blocks"], M["solve_q_ms"]
     if rank != 0:
         dist.barrier()
         return

@@ -38,6 +38,13 @@ def test_bench_contract_fields():
     assert {"value", "unit", "cores", "kind", "sample"} <= set(cb)
     assert cb["value"] > 0 and cb["unit"] == "outer-iters/s" and cb["kind"] in ("port", "reference")
     assert d["reorth_passes"].endswith("/3")
+    # the legs of the default line: north_star's 5-pt 10M workload and config 5's driver
+    l2 = d["lap2d_3162_step"]
+    assert l2["outer_iters_per_s"] > 0 and l2["workload"].startswith("lap2d_3162")
+    assert 0 < l2["spmv_frac"] < 1.5 and 0 < l2["roofline"]["frac"] < 1.5
+    irl = d["irl"]
+    assert irl["converged"] and irl["solves_per_s"] > 0 and irl["spmv_format"] == "csr"
+    assert 0 < irl["roofline"]["frac"] < 1.5
 
 
 def test_bench_epochs_keep_the_line_valid():

@@ -12,6 +12,10 @@ benchmark sizes, plus size-independent properties where it cannot:
     15-iteration bench run, extreme Ritz values to 1e-10 * ||A||, the top Ritz
     pair's residual norm recomputed on the host from the device's Q, and the
     size-independent properties (spectrum bounds, last Q block orthonormal);
+  * config 3 as named (TSQR normalize): the same 15-iteration comparison
+    with the fused Householder TSQR projectAndNormalize on every block;
+  * north_star's ~10M-row 5-pt Laplacian (lap2d_3162, n = 9,998,244):
+    bit-exact SpMV and the same 15-iteration comparison;
   * config 2 (lap2d_1000, n = 10^6): the whole t = 15 run against the NumPy
     oracle (T to 1e-9 * ||A||, identical flags, extreme Ritz values);
   * config 5 at its full size (the G3_circuit stand-in circuit_1259, n =
@@ -67,36 +71,32 @@ def test_matrix_powers_newton_fullsize_bitexact(cal, ctx3d, lap3d, ref):
     assert np.array_equal(V, Ve)
 
 
-def test_ca_lanczos_fullsize_vs_omp(ctx3d, lap3d, ref):
-    """The whole bench run (t = 15 outer iterations, s = 8, Newton, 'local',
-    same start vector) against the C/OpenMP restatement (ca_lanczos.m:
-    150-245 with Householder tsqr): T to 1e-9 ||A||, identical reorth flags,
-    the extreme Ritz values to 1e-10 ||A||.  Diagnostics on: the last
-    iteration's residual norm of the largest Ritz pair (compute_ritz_rnorm,
-    ca_lanczos.m:88-97) recomputed on the host -- x = Q y from the device's Q
-    (streamed in blocks), ||A x - l x|| / ||l x|| with SciPy's SpMV -- to
-    1e-8 relative.  Plus the size-independent properties: Ritz values inside
-    the analytic spectrum, the last Q block orthonormal to 1e-13."""
+def _run_vs_omp(ctx, A, r, t, nA, lmin, lmax):
+    """t outer iterations of ca_lanczos_basic 'local' (s = 8, Newton, the same
+    start vector) on the device, diagnostics on, against the C/OpenMP
+    restatement (ca_lanczos.m:150-245 with Householder tsqr, tsqr.m:7-12):
+    T to 1e-9 ||A||, identical reorth flags, the extreme Ritz values to
+    1e-10 ||A||.  The last iteration's residual norm of the largest Ritz pair
+    (compute_ritz_rnorm, ca_lanczos.m:88-97) is recomputed on the host --
+    x = Q y from the device's Q (streamed in blocks), ||A x - l x|| / ||l x||
+    with SciPy's SpMV -- to 1e-8 relative.  Size-independent properties: Ritz
+    values inside the analytic spectrum [lmin, lmax], the last Q block
+    orthonormal to 1e-13.  Returns the reorth flags."""
     from oracle import omp
 
-    n = lap3d.shape[0]
-    nA = 12.0
-    r = ref.matlab_rand(n)
-    t = 15
-    ctx3d.lanczos_begin(r, S, t, "newton", "local")
+    n = A.shape[0]
+    ctx.lanczos_begin(r, S, t, "newton", "local")
     for _ in range(t):
-        ctx3d.lanczos_step(True)
-    T, rn, _, flags, _ = ctx3d.lanczos_get()
-    Te, fe = omp.ca_lanczos(lap3d, r, S, S * t, "newton")
+        ctx.lanczos_step(True)
+    T, rn, _, flags, _ = ctx.lanczos_get()
+    Te, fe = omp.ca_lanczos(A, r, S, S * t, "newton")
     assert T.shape == Te.shape == (S * t, S * t)
     assert list(bool(f) for f in flags) == list(fe)
-    assert sum(flags) == t - 1  # every k > 1 takes the second pass on this input
-    assert np.max(np.abs(T - Te)) <= 1e-9 * nA
+    dT = np.max(np.abs(T - Te))
+    assert dT <= 1e-9 * nA, dT
     w = np.sort(np.linalg.eigvals(T).real)
     we = np.sort(np.linalg.eigvals(Te).real)
     assert abs(w[-1] - we[-1]) <= 1e-10 * nA and abs(w[0] - we[0]) <= 1e-10 * nA
-    lmax = _lap_max(3, 215)
-    lmin = 3 * (2.0 - 2.0 * math.cos(math.pi / 216))
     assert w[0] >= lmin * (1 - 1e-9) and w[-1] <= lmax * (1 + 1e-12)
     assert np.max(np.abs(T - T.T)) <= 1e-10 * lmax
     # residual of the largest Ritz pair, recomputed from the device's Q
@@ -105,12 +105,72 @@ def test_ca_lanczos_fullsize_vs_omp(ctx3d, lap3d, ref):
     lam, y = ev[i].real, V[:, i].real
     x = np.zeros(n)
     for c0 in range(0, S * t, S):
-        x += ctx3d.lanczos_get_Q(c0, S) @ y[c0:c0 + S]
-    Qb = ctx3d.lanczos_get_Q(S * (t - 1), S + 1)  # the last block Q(:, s(t-1)+1 : st+1)
-    ctx3d.lanczos_end()
-    rn_host = np.linalg.norm(lap3d @ x - lam * x) / np.linalg.norm(lam * x)
+        x += ctx.lanczos_get_Q(c0, S) @ y[c0:c0 + S]
+    Qb = ctx.lanczos_get_Q(S * (t - 1), S + 1)  # the last block Q(:, s(t-1)+1 : st+1)
+    ctx.lanczos_end()
+    rn_host = np.linalg.norm(A @ x - lam * x) / np.linalg.norm(lam * x)
     assert abs(rn[t - 1, 0] / rn_host - 1.0) <= 1e-8, (rn[t - 1, 0], rn_host)
     assert np.max(np.abs(Qb.T @ Qb - np.eye(S + 1))) < 1e-13
+    print("T max |dT| %.3e (bar %.1e), top Ritz %.15f (omp %.15f), rn %.6e (host %.6e), flags %d/%d"
+          % (dT, 1e-9 * nA, w[-1], we[-1], rn[t - 1, 0], rn_host, sum(flags), t))
+    return flags
+
+
+def _lap3d_bounds():
+    return 3 * (2.0 - 2.0 * math.cos(math.pi / 216)), _lap_max(3, 215)
+
+
+def test_ca_lanczos_fullsize_vs_omp(ctx3d, lap3d, ref):
+    """BASELINE config 3's workload with the loop's default normalize (the
+    fused CholQR2 sweeps): the whole bench run, t = 15, against C/OpenMP."""
+    r = ref.matlab_rand(lap3d.shape[0])
+    flags = _run_vs_omp(ctx3d, lap3d, r, 15, 12.0, *_lap3d_bounds())
+    assert sum(flags) == 15 - 1  # every k > 1 takes the second pass on this input
+
+
+def test_ca_lanczos_config3_tsqr_fullsize_vs_omp(cal, lap3d, ref):
+    """BASELINE config 3 as named: lap3d_215, s = 8 Newton, **TSQR** normalize
+    (tsqr.m:7-12 at ca_lanczos.m:178,187), t = 15, against the C/OpenMP
+    restatement (whose normalize is Householder TSQR too).  Every block k > 1
+    must take the fused TSQR projectAndNormalize (tsqr_fold.hip: 14 runs, 0
+    declined), so the 15-step bench run of tsqr_step is pinned end to end."""
+    ctx = cal.Context(normalize="tsqr").set_matrix(lap3d)
+    try:
+        f0 = ctx.tsqr_fold_stats()
+        r = ref.matlab_rand(lap3d.shape[0])
+        flags = _run_vs_omp(ctx, lap3d, r, 15, 12.0, *_lap3d_bounds())
+        f1 = ctx.tsqr_fold_stats()
+    finally:
+        ctx.close()
+    assert sum(flags) == 15 - 1
+    assert f1["runs"] - f0["runs"] == 14 and f1["declined"] - f0["declined"] == 0, (f0, f1)
+    assert f1["last_est"] < 1e-14
+
+
+@pytest.fixture(scope="module")
+def lap2d_10m(cal):
+    return cal.matrices.laplacian_2d(3162)
+
+
+def test_ca_lanczos_lap2d_3162_vs_omp(cal, lap2d_10m, ref):
+    """north_star's literal target, the ~10M-row 5-pt Laplacian (3162^2 =
+    9,998,244 rows) at s = 8: SpMV bit-exact against the oracle's sequential
+    CSR SpMV (SpMV.m:8), then the whole t = 15 run (default normalize)
+    against the C/OpenMP restatement with the same bars as config 3."""
+    A = lap2d_10m
+    n = A.shape[0]
+    assert n == 9998244
+    ctx = cal.Context().set_matrix(A)
+    try:
+        v = ref.matlab_rand(n, seed=7)
+        assert np.array_equal(ctx.spmv(v), ref.SpMV(A, v))
+        y = ctx.spmv(np.ones(n))  # A * ones: 0 inside, 1 on the edges, 2 at the corners
+        assert y.min() == 0.0 and y.max() == 2.0 and np.all(y == np.round(y))
+        r = ref.matlab_rand(n)
+        lmin = 2 * (2.0 - 2.0 * math.cos(math.pi / 3163))
+        _run_vs_omp(ctx, A, r, 15, 8.0, lmin, _lap_max(2, 3162))
+    finally:
+        ctx.close()
 
 
 def test_ca_lanczos_config2_vs_oracle(cal, ref):
