@@ -14,11 +14,15 @@ from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_void_
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcalanczos.so")
+# CAL_LIBRARY=testhooks loads the test build (libcalanczos_testhooks.so: the
+# same sources with -DCAL_TEST_HOOKS, csrc/Makefile), which alone carries the
+# result-altering test hooks; the production library has none compiled in
+LIB_PATH = os.path.join(_HERE, "libcalanczos_testhooks.so" if os.environ.get("CAL_LIBRARY") == "testhooks"
+                        else "libcalanczos.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
-        "libcalanczos.so not found at %s: build it with `make -C ca_lanczos_amd/csrc` "
+        "%s not found: build it with `make -C ca_lanczos_amd/csrc` "
         "(or __graft_entry__.build()); there is no CPU fallback" % LIB_PATH)
 
 lib = ctypes.CDLL(LIB_PATH)
@@ -80,6 +84,9 @@ SIGNATURES = [
     ("cal_mpk_schedule", c_int, [c_void_p, ip]),
     ("cal_tsqr_fold_stats", c_int, [c_void_p, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong),
                                      ctypes.POINTER(ctypes.c_double)]),
+    ("cal_set_tsqr_fold_tol", c_int, [c_void_p, ctypes.c_double]),
+    ("cal_residency_generation", ctypes.c_longlong, []),
+    ("cal_residency_invalidate", ctypes.c_longlong, []),
     ("cal_set_normalize", c_int, [c_void_p, c_char_p]),
     ("cal_get_normalize", c_int, [c_void_p, ip]),
     ("cal_set_orth_coef", c_int, [c_void_p, c_char_p]),

@@ -87,6 +87,13 @@ class Context:
         check(self.h, lib.cal_tsqr_fold_stats(self.h, ctypes.byref(r), ctypes.byref(d), ctypes.byref(e)))
         return dict(runs=r.value, declined=d.value, last_est=e.value)
 
+    def set_tsqr_fold_tol(self, tol: float):
+        """The fused TSQR's loss-of-orthogonality acceptance threshold
+        (cal_set_tsqr_fold_tol; default 1e-14, 0 declines every block that
+        takes the second projection, a negative value every block)."""
+        check(self.h, lib.cal_set_tsqr_fold_tol(self.h, float(tol)), "tsqr fold tol")
+        return self
+
     def set_orth_coef(self, where: str):
         """Run the block-orthogonalisation s x s algebra on the "device"
         (default) or on the "host" (same bits; for testing)."""

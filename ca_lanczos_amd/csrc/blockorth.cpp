@@ -598,31 +598,41 @@ static int ensure_zbuf(cal_ctx* c, int64_t n, int m, double** p, int64_t* ld) {
 // host waits once, for the published R.  Returns 2 when the shape does not
 // apply, 1 when the fold declined after running (||W|| too large, or a
 // non-finite value): the caller then takes the explicit-Z path.
-static bool fold_enabled() {
-    static const int on = [] {
-        const char* e = std::getenv("CAL_TSQR_FOLD");
-        return e ? std::atoi(e) : 1;
-    }();
-    return on != 0;
-}
-
-// CAL_TSQR_REFORM=1: the down pass re-forms and refactors each level-0 tile
-// instead of reloading the factored tile the up pass stored
-static bool fold_reform() {
-    static const int on = [] {
-        const char* e = std::getenv("CAL_TSQR_REFORM");
-        return e ? std::atoi(e) : 0;
-    }();
-    return on != 0;
+// The fold/no-fold decision must be the same on every rank: the two paths
+// issue different collectives.  The shape conditions that depend on the
+// panel's local rows are checked for every rank's slab (the slab table of
+// the resident matrix), or, for a panel of another height, agreed by one
+// all-reduce of the ranks' votes.
+static int fold_shape_all_ranks(cal_ctx* c, int64_t n, int m, int w, bool* ok) {
+    const int P = c->comm ? c->comm->nranks : 1;
+    *ok = fold_shape_ok(n, m, w);
+    if (P == 1) return 0;
+    const std::vector<int64_t>& st = c->A.slabs;
+    if (c->has_A && (int)st.size() == P + 1 && n == c->A.n_local) {
+        for (int q = 0; q < P; ++q) *ok = *ok && fold_shape_ok(st[q + 1] - st[q], m, w);
+        return 0;
+    }
+    CAL_TRY(ensure_partial(c, 1));
+    const double vote = *ok ? 0.0 : 1.0;
+    double sum = 0.0;
+    CAL_HIP(c, hipMemcpyAsync(c->d_partial, &vote, sizeof(double), hipMemcpyHostToDevice, c->stream));
+    CAL_TRY(allreduce_sum(c, c->d_partial, 1));
+    CAL_HIP(c, hipMemcpyAsync(&sum, c->d_partial, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    CAL_HIP(c, hipStreamSynchronize(c->stream));
+    *ok = sum == 0.0;
+    return 0;
 }
 
 static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, bool doreorth, const PanelOut& Qout,
                         double* Rq, double* R, PNResult* res) {
     const int w = Qp.total, m = X.total, nq = w < 8 ? w : 8;
     const int P = c->comm ? c->comm->nranks : 1;
-    if (!fold_enabled() || !fold_shape_ok(n, m, w) || Qp.nseg + X.nseg > kMaxSeg || Qout.total != m ||
+    if (m < 1 || m > 8 || w < 1 || w > 9 || Qp.nseg + X.nseg > kMaxSeg || Qout.total != m ||
         Qout.nseg > kMaxSeg || (int64_t)P * m > 512)
         return 2;
+    bool shape_ok = false;
+    CAL_TRY(fold_shape_all_ranks(c, n, m, w, &shape_ok));
+    if (!shape_ok) return 2;
     const int me = c->comm ? c->comm->rank : 0;
     const int64_t n0 = fold_tiles(n), nblk = fold_blocks(n);
     const std::vector<int> nu = fold_levels(n);
@@ -665,7 +675,8 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
     fa.C = F + oT1;
     fa.flags = d_out + 512;
     fa.K = F + oK;
-    fa.V0 = fold_reform() ? nullptr : F + oV0;
+    fa.tol = c->fold_tol;
+    fa.V0 = F + oV0;
     fa.tb0 = F + otb0;
     fa.R0 = F + oR0;
     fa.S0 = F + oS0;
@@ -705,12 +716,8 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
         timer_end(c, t);
     }
     // one rank: the root level, the algebra and the root's way down merged
-    // (k_fold_root; CAL_FOLD_ROOT=0: the three launches)
-    static const bool merged_root = [] {
-        const char* e = std::getenv("CAL_FOLD_ROOT");
-        return !e || std::atoi(e) != 0;
-    }();
-    const bool merged = P == 1 && merged_root;
+    // (k_fold_root: three latency-bound launches in one)
+    const bool merged = P == 1;
     // (the C2 reduction on a side stream beside the tree levels, and the
     // publish beside the way down, measured 656-661 -> 626-633 outer-it/s:
     // the cross-stream waits cost more than the two short kernels)
@@ -755,7 +762,7 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
             ldr = m;
         }
         CAL_HIP(c, launch_fold_coef1(F + oT1, F + oT2, Rtop, ldr, d_out, F + oSb, F + oSm, F + oK, w, m,
-                                     doreorth ? 1 : 0, nglob, c->d_pub, d_seq, seq, c->stream));
+                                     doreorth ? 1 : 0, nglob, c->fold_tol, c->d_pub, d_seq, seq, c->stream));
         // down: [the global levels,] the group and block levels, level 0
         const double* Stop = F + oSb;
         int lds = 8;

@@ -325,8 +325,12 @@ hipError_t launch_tsqr(bool down, int src, const TsqrLevelArgs& a, const TsqrCol
 // below: Vu / tbu / Ru / Su; level nlev is the root, one tile; Rroot_m its R
 // with ld m), the P1 tile C, K (9 x 8), the flags (out[512..515]) and the
 // C2 = Qp'Y partials (72 x nblk, entry-major).
+// largest accepted loss-of-orthogonality estimate of the fused TSQR (its
+// default; cal_set_tsqr_fold_tol)
+constexpr double kFoldTol = 1e-14;
 struct FoldArgs {
     int64_t n = 0;
+    double tol = kFoldTol;
     int m = 0, w = 0, nblk = 0, n0 = 0, nlev = 0;
     int nu[3] = {0, 0, 0};
     const double* C = nullptr;  // the reduced P1 tile (272 doubles): C = Qp'X is read from it
@@ -355,7 +359,8 @@ hipError_t launch_fold_reduce(const double* partial, int nparts, double* out, hi
 // and publishes R / RY / flags to hout, then seq to *hseq
 hipError_t launch_fold_coef1(const double* T1, const double* G, const double* Rtop, int ldr, double* out,
                              double* Sbuf, double* Sm, double* Kbuf, int w, int m, int doreorth, double nglob,
-                             double* hout, unsigned long long* hseq, unsigned long long seq, hipStream_t st);
+                             double tol, double* hout, unsigned long long* hseq, unsigned long long seq,
+                             hipStream_t st);
 // one rank: the root level, k_fold_coef1's algebra and the root's way down in
 // one block (the root's R is its own, ld 8); S blocks of level nlev - 1 out
 hipError_t launch_fold_root(const FoldArgs& a, const double* T1, const double* G, double* out, double* Sbuf,
@@ -442,6 +447,7 @@ struct cal_ctx {
     size_t fold_cap = 0;
     long fold_runs = 0, fold_declined = 0;  // fused-TSQR blocks run / declined (explicit-Z path taken)
     double fold_last_est = 0.0;             // the last block's loss-of-orthogonality estimate
+    double fold_tol = cal::kFoldTol;        // its acceptance threshold (cal_set_tsqr_fold_tol)
 };
 
 // ---- helpers shared by the host-side translation units -----------------

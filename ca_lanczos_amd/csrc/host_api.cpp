@@ -5,6 +5,7 @@
 // with g++ -fsanitize=address,undefined into the host checker
 // (csrc/Makefile `host-san`, tests/test_host_sanitized.py), together with
 // dense.cpp, leja.cpp and the TSQR tree plan.
+#include <atomic>
 #include <random>
 
 #include "../../include/calanczos_host.h"
@@ -49,5 +50,11 @@ int cal_matlab_rand(int64_t count, unsigned seed, double* out) {
     dense::matlab_rand(g, count, out);
     return 0;
 }
+
+static std::atomic<long long> g_residency_gen{0};
+
+long long cal_residency_generation(void) { return g_residency_gen.load(std::memory_order_acquire); }
+
+long long cal_residency_invalidate(void) { return g_residency_gen.fetch_add(1, std::memory_order_acq_rel) + 1; }
 
 }  // extern "C"

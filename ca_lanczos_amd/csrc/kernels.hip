@@ -28,6 +28,7 @@
 //   k_dot, k_axpy_sub(_dev), k_div(_sqrt), k_gather, k_spmv_resid,
 //   k_form_projM, k_abs_rowsum: small vector kernels.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 #include <utility>
@@ -159,12 +160,8 @@ static hipError_t launch_spmv_mode(const SpmvArgs& a, int nit, hipStream_t st) {
 
 hipError_t launch_spmv(const SpmvArgs& a0, hipStream_t st) {
     if (a0.nblk <= 0) return hipSuccess;
-    static const int xcd = [] {  // CAL_SPMV_XCD=0: hardware block order (A/B)
-        const char* e = std::getenv("CAL_SPMV_XCD");
-        return e ? std::atoi(e) : 1;
-    }();
     SpmvArgs a = a0;
-    a.xcd = xcd;
+    a.xcd = 1;  // XCD-contiguous row blocks (hardware order measured 1.08x -> 1.35x traffic)
     // a.mode carries the per-matrix iteration count in bits 8..15
     const int nit = (a.mode >> 8) & 0xff;
     switch (a.mode & 0xff) {
@@ -559,268 +556,6 @@ __global__ __launch_bounds__(256) void k_spmv_pair_resid(PatArgs a, const uint16
     }
 }
 
-// k_spmv_pair_resid over many Ritz pairs in one launch: blockIdx.y takes
-// pairs [CPB y, CPB y + CPB) of the list (x = X + col[i] * ldx, l = lam[i]);
-// the pair table is staged once per block.  Each thread takes PPT row pairs
-// of the block's contiguous run (pair b*256*PPT + j*256 + tid), reads each
-// pair's id and table entries once for all CPB Ritz pairs, and keeps its
-// sums per Ritz pair in registers, so the table staging, the wave sums and
-// the partial writes are paid once per 256*PPT row pairs.  Per row the
-// products and their order are k_spmv_pair's MODE 1 (y = A x - l x); the
-// block's two sums of Ritz pair i go to partial[(2 out[i] + e) * pstride + b].
-template <int MAXLEN, int CPB, int PPT>
-__global__ __launch_bounds__(256) void k_spmv_pair_resid_multi(PatArgs a, const uint16_t* __restrict__ ppat,
-                                                              const int* __restrict__ ppoff,
-                                                              const double2* __restrict__ ppval,
-                                                              const double* __restrict__ X, int64_t ldx,
-                                                              const int* __restrict__ col,
-                                                              const double* __restrict__ lam,
-                                                              const int* __restrict__ out, int npairs_ritz,
-                                                              double* __restrict__ partial, int64_t pstride) {
-    extern __shared__ __attribute__((aligned(16))) double lds_pair[];
-    double2* s_pv = reinterpret_cast<double2*>(lds_pair);
-    int* s_poff = reinterpret_cast<int*>(s_pv + a.npent);
-    __shared__ double ws[CPB][2][4];
-    const int tid = threadIdx.x;
-    const int64_t npairs = (a.n + 1) >> 1;
-    const int64_t b0 = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 256 * PPT;
-    for (int i = tid; i < a.npent; i += 256) {
-        s_pv[i] = ppval[i];
-        s_poff[i] = ppoff[i];
-    }
-    __syncthreads();
-    const int i0 = blockIdx.y * CPB;
-    const int nq = npairs_ritz - i0 < CPB ? npairs_ritz - i0 : CPB;  // uniform over the block
-    const int lane = tid & 63, wave = tid >> 6;
-    const double* xq[CPB];
-    double lq[CPB], num[CPB], den[CPB];
-#pragma unroll
-    for (int q = 0; q < CPB; ++q) {
-        const int qq = q < nq ? q : 0;
-        xq[q] = X + (int64_t)col[i0 + qq] * ldx;
-        lq[q] = lam[i0 + qq];
-        num[q] = 0.0;
-        den[q] = 0.0;
-    }
-    for (int j = 0; j < PPT; ++j) {
-        const int64_t t = b0 + (int64_t)j * 256 + tid;
-        if (b0 + (int64_t)j * 256 >= npairs) break;  // uniform over the block
-        const int64_t tcl = t < npairs ? t : npairs - 1;
-        const int id = ppat[tcl];
-        const int64_t r0 = 2 * tcl;
-        const bool two = r0 + 1 < a.n;  // see k_spmv_pair_resid (odd distributed slab)
-        const int base = id != kPairSplit ? id * MAXLEN : 0;
-        int code[MAXLEN];
-        double2 v[MAXLEN];
-#pragma unroll
-        for (int e = 0; e < MAXLEN; ++e) {
-            code[e] = s_poff[base + e];
-            v[e] = s_pv[base + e];
-        }
-        const int64_t rs = r0 < a.xhi - 2 ? r0 : a.xhi - 2;
-        int64_t b0 = 0;
-        const bool run = pair_lane_run<MAXLEN>(a, tcl, b0);
-        const bool mid = MAXLEN >= 3 && (MAXLEN & 1) && a.pmid == MAXLEN / 2;
-#pragma unroll
-        for (int q = 0; q < CPB; ++q) {
-            if (q >= nq) break;
-            const double* x = xq[q];
-            const double l = lq[q];
-            double2 xc[MAXLEN];
-            pair_slot_loads<MAXLEN>(a, x, r0, run, b0, xc);
-            const double2 xs = mid ? xc[MAXLEN / 2] : ld16(x + rs);
-            if (t < npairs) {
-                if (id != kPairSplit) {
-                    double y0 = 0.0, y1 = 0.0;
-#pragma unroll
-                    for (int e = 0; e < MAXLEN; ++e) {
-                        const double t0 = v[e].x * xc[e].x, t1 = v[e].y * xc[e].y;
-                        double a0 = y0 + t0, a1 = y1 + t1;
-                        asm volatile("" : "+v"(a0), "+v"(a1));
-                        y0 = (code[e] & 1) ? a0 : y0;
-                        y1 = (code[e] & 2) ? a1 : y1;
-                    }
-                    const double u0 = l * xs.x, u1 = l * xs.y;
-                    y0 = y0 - u0;
-                    y1 = y1 - u1;
-                    num[q] = num[q] + (y0 * y0 + (two ? y1 * y1 : 0.0));
-                    den[q] = den[q] + (u0 * u0 + (two ? u1 * u1 : 0.0));
-                } else {
-                    double nu = 0.0, de = 0.0;
-                    for (int k = 0; k < 2 && r0 + k < a.n; ++k) {
-                        const int64_t rr = r0 + k;
-                        const int2 pi = a.pinfo[a.pat[rr]];
-                        double sum = 0.0;
-                        for (int e = 0; e < pi.y; ++e) {
-                            const double tv = a.pval[pi.x + e] * x[rr + a.pdelta[pi.x + e]];
-                            sum = sum + tv;
-                        }
-                        const double u = l * x[rr];
-                        const double y = sum - u;
-                        nu = nu + y * y;
-                        de = de + u * u;
-                    }
-                    num[q] = num[q] + nu;
-                    den[q] = den[q] + de;
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < CPB; ++q) {
-        if (q < nq) {
-            const double nu = wave_sum(num[q]), de = wave_sum(den[q]);
-            if (lane == 0) {
-                ws[q][0][wave] = nu;
-                ws[q][1][wave] = de;
-            }
-        }
-    }
-    __syncthreads();
-    if (tid < 2 * CPB) {
-        const int q = tid >> 1, e = tid & 1;
-        if (i0 + q < npairs_ritz)
-            partial[(2 * (int64_t)out[i0 + q] + e) * pstride + blockIdx.x] =
-                ((ws[q][e][0] + ws[q][e][1]) + ws[q][e][2]) + ws[q][e][3];
-    }
-}
-
-// Persistent variant of k_spmv_pair_resid_multi (CAL_RESID_PERS=1; measured
-// slower, off by default: diagnostics-on lap3d_215 117-120 outer-it/s at 1, 2
-// or 4 pairs per pass against 137 for the 2-D grid, profiles/r03/diag/): the
-// kernel is bound by its gather requests, not by the re-read bytes.
-// gridDim.x = 8 nbx blocks; XCD x (blockIdx.x & 7 on a 1-D grid) owns
-// one contiguous range of 256-row-pair chunks and its nbx blocks stride
-// through it, CPB Ritz pairs at a time (pair groups the outer loop).  At any
-// moment an XCD's blocks then work on a window of ~nbx * 512 rows, so a row's
-// +-N^2 (plane) neighbours are read while that XCD's L2 still holds them; the
-// 2-D grid spread each XCD's in-flight rows over ~11 planes times 4 pairs and
-// fetched 2.65x the algorithmic bytes.  The pair table is staged once per
-// block.  Same products and per-row order as the single-pair kernel.
-template <int MAXLEN, int CPB>
-__global__ __launch_bounds__(256) void k_spmv_pair_resid_pers(PatArgs a, const uint16_t* __restrict__ ppat,
-                                                             const int* __restrict__ ppoff,
-                                                             const double2* __restrict__ ppval,
-                                                             const double* __restrict__ X, int64_t ldx,
-                                                             const int* __restrict__ col,
-                                                             const double* __restrict__ lam,
-                                                             const int* __restrict__ out, int npairs_ritz,
-                                                             double* __restrict__ partial, int64_t pstride) {
-    extern __shared__ __attribute__((aligned(16))) double lds_pair[];
-    double2* s_pv = reinterpret_cast<double2*>(lds_pair);
-    int* s_poff = reinterpret_cast<int*>(s_pv + a.npent);
-    __shared__ double ws[CPB][2][4];
-    const int tid = threadIdx.x;
-    const int64_t npairs = (a.n + 1) >> 1;
-    for (int i = tid; i < a.npent; i += 256) {
-        s_pv[i] = ppval[i];
-        s_poff[i] = ppoff[i];
-    }
-    __syncthreads();
-    const int xcd = blockIdx.x & 7, jb = blockIdx.x >> 3, nbx = gridDim.x >> 3;
-    const int64_t nch = (npairs + 255) / 256;
-    const int64_t lo = xcd * nch / 8, hi = (xcd + 1) * nch / 8;
-    const int lane = tid & 63, wave = tid >> 6;
-    for (int i0 = 0; i0 < npairs_ritz; i0 += CPB) {
-        const int nq = npairs_ritz - i0 < CPB ? npairs_ritz - i0 : CPB;  // uniform over the block
-        const double* xq[CPB];
-        double lq[CPB], num[CPB], den[CPB];
-#pragma unroll
-        for (int q = 0; q < CPB; ++q) {
-            const int qq = q < nq ? q : 0;
-            xq[q] = X + (int64_t)col[i0 + qq] * ldx;
-            lq[q] = lam[i0 + qq];
-            num[q] = 0.0;
-            den[q] = 0.0;
-        }
-        for (int64_t ch = lo + jb; ch < hi; ch += nbx) {
-            const int64_t t = ch * 256 + tid;
-            const int64_t tcl = t < npairs ? t : npairs - 1;
-            const int id = ppat[tcl];
-            const int64_t r0 = 2 * tcl;
-            const bool two = r0 + 1 < a.n;  // see k_spmv_pair_resid (odd distributed slab)
-            const int base = id != kPairSplit ? id * MAXLEN : 0;
-            int code[MAXLEN];
-            double2 v[MAXLEN];
-#pragma unroll
-            for (int e = 0; e < MAXLEN; ++e) {
-                code[e] = s_poff[base + e];
-                v[e] = s_pv[base + e];
-            }
-            int64_t ad[MAXLEN];
-#pragma unroll
-            for (int e = 0; e < MAXLEN; ++e) {
-                const int64_t d = r0 + a.pslot[e];
-                ad[e] = d < a.xlo ? a.xlo : (d > a.xhi - 2 ? a.xhi - 2 : d);
-            }
-            const int64_t rs = r0 < a.xhi - 2 ? r0 : a.xhi - 2;
-#pragma unroll
-            for (int q = 0; q < CPB; ++q) {
-                if (q >= nq) break;
-                const double* x = xq[q];
-                const double l = lq[q];
-                double2 xc[MAXLEN];
-#pragma unroll
-                for (int e = 0; e < MAXLEN; ++e) xc[e] = ld16(x + ad[e]);
-                const double2 xs = ld16(x + rs);
-                if (t < npairs) {
-                    if (id != kPairSplit) {
-                        double y0 = 0.0, y1 = 0.0;
-#pragma unroll
-                        for (int e = 0; e < MAXLEN; ++e) {
-                            const double t0 = v[e].x * xc[e].x, t1 = v[e].y * xc[e].y;
-                            double a0 = y0 + t0, a1 = y1 + t1;
-                            asm volatile("" : "+v"(a0), "+v"(a1));
-                            y0 = (code[e] & 1) ? a0 : y0;
-                            y1 = (code[e] & 2) ? a1 : y1;
-                        }
-                        const double u0 = l * xs.x, u1 = l * xs.y;
-                        y0 = y0 - u0;
-                        y1 = y1 - u1;
-                        num[q] = num[q] + (y0 * y0 + (two ? y1 * y1 : 0.0));
-                        den[q] = den[q] + (u0 * u0 + (two ? u1 * u1 : 0.0));
-                    } else {
-                        double nu = 0.0, de = 0.0;
-                        for (int k = 0; k < 2 && r0 + k < a.n; ++k) {
-                            const int64_t rr = r0 + k;
-                            const int2 pi = a.pinfo[a.pat[rr]];
-                            double sum = 0.0;
-                            for (int e = 0; e < pi.y; ++e) {
-                                const double tv = a.pval[pi.x + e] * x[rr + a.pdelta[pi.x + e]];
-                                sum = sum + tv;
-                            }
-                            const double u = l * x[rr];
-                            const double y = sum - u;
-                            nu = nu + y * y;
-                            de = de + u * u;
-                        }
-                        num[q] = num[q] + nu;
-                        den[q] = den[q] + de;
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < CPB; ++q) {
-            if (q < nq) {
-                const double nu = wave_sum(num[q]), de = wave_sum(den[q]);
-                if (lane == 0) {
-                    ws[q][0][wave] = nu;
-                    ws[q][1][wave] = de;
-                }
-            }
-        }
-        __syncthreads();
-        if (tid < 2 * CPB) {
-            const int q = tid >> 1, e = tid & 1;
-            if (q < nq)
-                partial[(2 * (int64_t)out[i0 + q] + e) * pstride + blockIdx.x] =
-                    ((ws[q][e][0] + ws[q][e][1]) + ws[q][e][2]) + ws[q][e][3];
-        }
-        __syncthreads();  // ws is rewritten by the next pair group
-    }
-}
-
 constexpr size_t kPatLdsMax = 64 * 1024;
 
 // the pair kernel needs 16-B aligned columns, rows <= 8 entries and an LDS-sized pair table
@@ -836,29 +571,15 @@ static hipError_t launch_pat_mode(const PatArgs& a, hipStream_t st) {
     const size_t lds2 = (size_t)a.npent * 20 + (size_t)a.nppat * 8 + 16;
     if (spmv_pat_pair_path(a)) {
         const int64_t npairs = (a.n + 1) / 2;
-        // threads per block: 512 (1024 rows; half the table stagings of 256 threads:
-        // lap3d_215 in the loop 45.2 -> 42.7 us per SpMV, 809 -> 825 outer-it/s);
-        // CAL_PAIR_TB = 256 / 1024 for A/B
-        static const int tb = [] {
-            const char* e = std::getenv("CAL_PAIR_TB");
-            const int v = e ? std::atoi(e) : 512;
-            return v == 256 || v == 1024 ? v : 512;
-        }();
+        // 512 threads per block (1024 rows; half the table stagings of 256
+        // threads: lap3d_215 in the loop 45.2 -> 42.7 us per SpMV, 809 -> 825
+        // outer-it/s; 1024 measured no better)
+        constexpr int tb = 512;
         dim3 g((unsigned)((npairs + tb - 1) / tb)), b(tb);
 #define CAL_PR(ML)                                                                                                    \
-    if (tb == 512) {                                                                                                   \
-        if (a.pcanon) hipLaunchKernelGGL((k_spmv_pair<MODE, ML, true, 512>), g, b, lds2, st, a, a.ppat, a.ppinfo,     \
-                                         a.ppoff, a.ppval);                                                            \
-        else hipLaunchKernelGGL((k_spmv_pair<MODE, ML, false, 512>), g, b, lds2, st, a, a.ppat, a.ppinfo, a.ppoff,    \
-                                a.ppval);                                                                              \
-    } else if (tb == 1024) {                                                                                           \
-        if (a.pcanon) hipLaunchKernelGGL((k_spmv_pair<MODE, ML, true, 1024>), g, b, lds2, st, a, a.ppat, a.ppinfo,    \
-                                         a.ppoff, a.ppval);                                                            \
-        else hipLaunchKernelGGL((k_spmv_pair<MODE, ML, false, 1024>), g, b, lds2, st, a, a.ppat, a.ppinfo, a.ppoff,   \
-                                a.ppval);                                                                              \
-    } else if (a.pcanon) hipLaunchKernelGGL((k_spmv_pair<MODE, ML, true>), g, b, lds2, st, a, a.ppat, a.ppinfo,       \
-                                            a.ppoff, a.ppval);                                                        \
-    else hipLaunchKernelGGL((k_spmv_pair<MODE, ML, false>), g, b, lds2, st, a, a.ppat, a.ppinfo, a.ppoff, a.ppval);
+    if (a.pcanon) hipLaunchKernelGGL((k_spmv_pair<MODE, ML, true, tb>), g, b, lds2, st, a, a.ppat, a.ppinfo, a.ppoff, \
+                                     a.ppval);                                                                        \
+    else hipLaunchKernelGGL((k_spmv_pair<MODE, ML, false, tb>), g, b, lds2, st, a, a.ppat, a.ppinfo, a.ppoff, a.ppval);
         switch (a.pmaxlen) {
             case 1: CAL_PR(1); break;
             case 2: CAL_PR(2); break;
@@ -933,112 +654,274 @@ hipError_t launch_spmv_pair_resid(const PatArgs& a, double lr, double* partial, 
     return hipGetLastError();
 }
 
-// row pairs per thread of the batched residual kernel (CAL_RESID_PPT = 1, 2,
-// 4 or 8 for A/B) and its grid
-static int resid_ppt() {
-    static const int ppt = [] {
-        const char* e = std::getenv("CAL_RESID_PPT");
-        const int v = e ? std::atoi(e) : 4;
-        return v == 1 || v == 2 || v == 8 ? v : 4;
-    }();
-    return ppt;
+// Ritz residual partials of many real Ritz pairs in one launch
+// (compute_ritz_rnorm, ca_lanczos.m:88-97): blockIdx.y takes pairs
+// [CPB y, CPB y + CPB) of the list (x = X + col[i] * ldx, l = lam[i]).  Each
+// thread takes PPT row pairs of the block's contiguous run (pair
+// b*256*PPT + j*256 + tid) and, per row pair, serves all CPB Ritz pairs with
+// work done once: the pair id, the slot offsets and the table entries.  The
+// kernel is built to issue few VALU instructions per (row pair, Ritz pair),
+// which is what bounded its predecessor (≈170 per row pair and Ritz pair:
+// 64-bit address clamps and per-entry selects redone for every Ritz pair):
+//   * x is read through one buffer descriptor per Ritz pair (wave-uniform,
+//     SGPRs) with the row pair's 32-bit slot offsets computed once; a slot
+//     outside the column's range returns 0 from the range check instead of
+//     being clamped.  A slot a row uses is always inside (the pair build
+//     checks both halves, runtime.cpp build_pair_patterns);
+//   * the pair table is staged with the entries a row does not use set to
+//     +0.0, so every slot is a plain multiply-add: the running sum of a row
+//     starts at +0.0 and gains ±0 terms only where the reference adds
+//     nothing, which leaves its bits unchanged (a sum that starts at +0.0 is
+//     never -0.0; x + ±0 = x for x != 0).  Each row therefore still adds its
+//     own entries in CSR column order, and y = A x - l x has the bits of
+//     k_spmv_pair's MODE 1 (the Ritz vectors are finite);
+//   * the centre slot (offset 0) doubles as the shift operand when present.
+// Split pairs and a row pair whose second row lies past the local rows (an
+// odd distributed slab's last row pairs with the first ghost row) take the
+// per-row path.  The block's two sums of Ritz pair i go to
+// partial[(2 out[i] + e) * pstride + b], as before.
+template <int MAXLEN, int CPB, int PPT, bool MID, bool LANE>
+__global__ __launch_bounds__(256) void k_resid_pairs(PatArgs a, const uint16_t* __restrict__ ppat,
+                                                    const int* __restrict__ ppoff, const double2* __restrict__ ppval,
+                                                    const double* __restrict__ X, int64_t ldx,
+                                                    const int* __restrict__ col, const double* __restrict__ lam,
+                                                    const int* __restrict__ out, int npairs_ritz,
+                                                    double* __restrict__ partial, int64_t pstride) {
+    extern __shared__ __attribute__((aligned(16))) double lds_pair[];
+    double2* s_pz = reinterpret_cast<double2*>(lds_pair);
+    __shared__ double ws[CPB][2][4];
+    const int tid = threadIdx.x;
+    const int64_t npairs = (a.n + 1) >> 1;
+    const int64_t b0 = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 256 * PPT;
+    for (int i = tid; i < a.npent; i += 256) {
+        const int code = ppoff[i];
+        const double2 v = ppval[i];
+        s_pz[i] = make_double2((code & 1) ? v.x : 0.0, (code & 2) ? v.y : 0.0);
+    }
+    const int i0 = blockIdx.y * CPB;
+    const int nq = npairs_ritz - i0 < CPB ? npairs_ritz - i0 : CPB;  // uniform over the block
+    // one descriptor per Ritz pair over its column's addressable range [xlo, xhi)
+    const uint32_t nbytes = (uint32_t)((a.xhi - a.xlo) * 8);
+    __amdgpu_buffer_rsrc_t rs[CPB];
+    const double* xq[CPB];
+    double lq[CPB], num[CPB], den[CPB];
+#pragma unroll
+    for (int q = 0; q < CPB; ++q) {
+        const int qq = q < nq ? q : 0;
+        const double* xb = X + (int64_t)col[i0 + qq] * ldx;
+        xq[q] = xb;
+        const double* lo = xb + a.xlo;
+        const uint64_t pl = (uint64_t)(uintptr_t)lo;
+        const uint32_t plo = __builtin_amdgcn_readfirstlane((uint32_t)pl);
+        const uint32_t phi = __builtin_amdgcn_readfirstlane((uint32_t)(pl >> 32));
+        rs[q] = __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)phi << 32) | plo), (short)0,
+                                                  (int)__builtin_amdgcn_readfirstlane(nbytes), 0x00020000);
+        lq[q] = lam[i0 + qq];
+        num[q] = 0.0;
+        den[q] = 0.0;
+    }
+    __syncthreads();
+    for (int j = 0; j < PPT; ++j) {
+        const int64_t t = b0 + (int64_t)j * 256 + tid;
+        if (b0 + (int64_t)j * 256 >= npairs) break;  // uniform over the block
+        const int64_t tcl = t < npairs ? t : npairs - 1;
+        const int id = ppat[tcl];
+        const int64_t r0 = 2 * tcl;
+        const bool pairpath = id != kPairSplit && r0 + 1 < a.n;
+        const int base = pairpath ? id * MAXLEN : 0;
+        uint32_t off[MAXLEN];
+#pragma unroll
+        for (int e = 0; e < MAXLEN; ++e) off[e] = (uint32_t)(r0 + a.pslot[e] - a.xlo) * 8u;
+        const uint32_t offc = (uint32_t)(r0 - a.xlo) * 8u;
+        double2 z[MAXLEN];
+#pragma unroll
+        for (int e = 0; e < MAXLEN; ++e) z[e] = s_pz[base + e];
+        // y = A x - l x of both rows from the zeroed table (see above)
+        // run: the wave's 64 lanes hold 64 consecutive row pairs (the fast
+        // path), so with LANE the -1 / +1 slots are the neighbouring lanes'
+        // centre loads moved over by one DPP wave shift, and the wave's two
+        // outer values come from scalar loads (pair_slot_loads' scheme)
+        auto pair_sums = [&](int q, double& nu, double& de, bool run) {
+            typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+            constexpr int Z = MAXLEN / 2;
+            constexpr bool LN = LANE && MID && MAXLEN >= 3;
+            double2 xc[MAXLEN];
+#pragma unroll
+            for (int e = 0; e < MAXLEN; ++e) {
+                if (LN && run && (e == Z - 1 || e == Z + 1)) continue;
+                const u4 w = __builtin_amdgcn_raw_buffer_load_b128(rs[q], (int)off[e], 0, 0);
+                xc[e] = make_double2(__builtin_bit_cast(double, ((uint64_t)w.y << 32) | w.x),
+                                     __builtin_bit_cast(double, ((uint64_t)w.w << 32) | w.z));
+            }
+            if constexpr (LN) {
+                if (run) {
+                    const int64_t tw = (int64_t)__builtin_amdgcn_readfirstlane((unsigned)(t & 0xffffffff)) |
+                                       ((int64_t)__builtin_amdgcn_readfirstlane((unsigned)((uint64_t)t >> 32)) << 32);
+                    int64_t el = 2 * tw - 1, er = 2 * tw + 128;  // x[lane 0's r0 - 1], x[lane 63's r0 + 2]
+                    el = el < a.xlo ? a.xlo : (el > a.xhi - 1 ? a.xhi - 1 : el);
+                    er = er < a.xlo ? a.xlo : (er > a.xhi - 1 ? a.xhi - 1 : er);
+                    const double xl = xq[q][el], xr = xq[q][er];
+                    xc[Z - 1] = make_double2(dpp_wave_shift<kDppWaveShr1>(xc[Z].y, xl), xc[Z].x);
+                    xc[Z + 1] = make_double2(xc[Z].y, dpp_wave_shift<kDppWaveShl1>(xc[Z].x, xr));
+                }
+            }
+            double2 xs;
+            if constexpr (MID) {
+                xs = xc[MAXLEN / 2];
+            } else {
+                const u4 w = __builtin_amdgcn_raw_buffer_load_b128(rs[q], (int)offc, 0, 0);
+                xs = make_double2(__builtin_bit_cast(double, ((uint64_t)w.y << 32) | w.x),
+                                  __builtin_bit_cast(double, ((uint64_t)w.w << 32) | w.z));
+            }
+            double y0 = 0.0, y1 = 0.0;
+#pragma unroll
+            for (int e = 0; e < MAXLEN; ++e) {
+                const double t0 = z[e].x * xc[e].x, t1 = z[e].y * xc[e].y;
+                y0 = y0 + t0;
+                y1 = y1 + t1;
+            }
+            const double u0 = lq[q] * xs.x, u1 = lq[q] * xs.y;
+            y0 = y0 - u0;
+            y1 = y1 - u1;
+            nu = y0 * y0 + y1 * y1;
+            de = u0 * u0 + u1 * u1;
+        };
+        const bool fast = pairpath && t < npairs;
+        if (__builtin_amdgcn_ballot_w64(!fast) == 0) {  // the whole wave on the pair path (wave-uniform)
+#pragma unroll
+            for (int q = 0; q < CPB; ++q) {
+                if (q >= nq) break;
+                double nu, de;
+                pair_sums(q, nu, de, true);
+                num[q] = num[q] + nu;
+                den[q] = den[q] + de;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < CPB; ++q) {
+                if (q >= nq) break;
+                if (t >= npairs) continue;
+                double nu = 0.0, de = 0.0;
+                if (pairpath) {
+                    pair_sums(q, nu, de, false);
+                } else {
+                    const double* x = xq[q];
+                    for (int k = 0; k < 2 && r0 + k < a.n; ++k) {
+                        const int64_t rr = r0 + k;
+                        const int2 pi = a.pinfo[a.pat[rr]];
+                        double sum = 0.0;
+                        for (int e = 0; e < pi.y; ++e) {
+                            const double tv = a.pval[pi.x + e] * x[rr + a.pdelta[pi.x + e]];
+                            sum = sum + tv;
+                        }
+                        const double u = lq[q] * x[rr];
+                        const double y = sum - u;
+                        nu = nu + y * y;
+                        de = de + u * u;
+                    }
+                }
+                num[q] = num[q] + nu;
+                den[q] = den[q] + de;
+            }
+        }
+    }
+    const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int q = 0; q < CPB; ++q) {
+        if (q < nq) {
+            const double nu = wave_sum(num[q]), de = wave_sum(den[q]);
+            if (lane == 0) {
+                ws[q][0][wave] = nu;
+                ws[q][1][wave] = de;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid < 2 * CPB) {
+        const int q = tid >> 1, e = tid & 1;
+        if (i0 + q < npairs_ritz)
+            partial[(2 * (int64_t)out[i0 + q] + e) * pstride + blockIdx.x] =
+                ((ws[q][e][0] + ws[q][e][1]) + ws[q][e][2]) + ws[q][e][3];
+    }
 }
 
-// the persistent residual kernel (CAL_RESID_PERS=1, A/B only; default the
-// 2-D grid) and its pairs per pass (CAL_RESID_PCPB = 1, 2 or 4)
-static int resid_pers() {
-    static const int v = [] {
-        const char* e = std::getenv("CAL_RESID_PERS");
-        return e ? std::atoi(e) : 0;
+// the batched residual kernel's shape: Ritz pairs per block, row pairs per
+// thread (CAL_RESID_SHAPE=<cpb>x<ppt> for A/B while tuning)
+static void resid_shape(int* cpb, int* ppt) {
+    static const int2 v = [] {
+        int c = 4, p = 4;
+        if (const char* e = std::getenv("CAL_RESID_SHAPE")) std::sscanf(e, "%dx%d", &c, &p);
+        if (c != 1 && c != 2 && c != 4 && c != 8) c = 4;
+        if (p != 1 && p != 2 && p != 4 && p != 8) p = 4;
+        return make_int2(c, p);
     }();
-    return v;
-}
-static int resid_pcpb() {
-    static const int v = [] {
-        const char* e = std::getenv("CAL_RESID_PCPB");
-        const int x = e ? std::atoi(e) : 2;
-        return x == 1 || x == 4 ? x : 2;
-    }();
-    return v;
+    *cpb = v.x;
+    *ppt = v.y;
 }
 
 int spmv_pair_resid_multi_blocks(const PatArgs& a) {
     const int nb = spmv_pair_resid_blocks(a);
     if (nb <= 0) return 0;
-    if (resid_pers()) {  // 8 XCDs x up to 256 blocks (8 per CU), a multiple of 8
-        const int per = std::max(1, std::min(256, (nb + 7) / 8));
-        return 8 * per;
-    }
-    return (nb + resid_ppt() - 1) / resid_ppt();
+    int cpb, ppt;
+    resid_shape(&cpb, &ppt);
+    return (nb + ppt - 1) / ppt;
 }
 
 hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64_t ldx, const int* col,
                                         const double* lam, const int* out, int npr, double* partial,
                                         int64_t pstride, hipStream_t st) {
-    // Ritz pairs per block (CAL_RESID_CPB = 2 / 4 / 8 for A/B)
-    static const int cpb = [] {
-        const char* e = std::getenv("CAL_RESID_CPB");
-        const int v = e ? std::atoi(e) : 4;
-        return v == 1 || v == 2 || v == 8 ? v : 4;
-    }();
     const int blocks = spmv_pair_resid_multi_blocks(a);
     if (blocks <= 0 || pstride < blocks) return hipErrorInvalidValue;
     if (npr <= 0) return hipSuccess;
-    if (a.pmaxlen > 8) return hipErrorInvalidValue;
-    const size_t lds = (size_t)a.npent * 20 + 16;
-    if (resid_pers()) {
-        auto gop = [&](auto cpb_c) {
-            constexpr int CPB = decltype(cpb_c)::value;
-#define CAL_PRP(ML)                                                                                           \
-    hipLaunchKernelGGL((k_spmv_pair_resid_pers<ML, CPB>), dim3(blocks), dim3(256), lds, st, a, a.ppat, a.ppoff, \
-                       a.ppval, X, ldx, col, lam, out, npr, partial, pstride)
-            switch (a.pmaxlen) {
-                case 1: CAL_PRP(1); break;
-                case 2: CAL_PRP(2); break;
-                case 3: CAL_PRP(3); break;
-                case 4: CAL_PRP(4); break;
-                case 5: CAL_PRP(5); break;
-                case 6: CAL_PRP(6); break;
-                case 7: CAL_PRP(7); break;
-                default: CAL_PRP(8); break;
-            }
-#undef CAL_PRP
-        };
-        if (resid_pcpb() == 1) gop(std::integral_constant<int, 1>{});
-        else if (resid_pcpb() == 4) gop(std::integral_constant<int, 4>{});
-        else gop(std::integral_constant<int, 2>{});
-        return hipGetLastError();
-    }
-    auto go2 = [&](auto cpb_c, auto ppt_c) {
+    if (a.pmaxlen > 8 || !a.pcanon) return hipErrorInvalidValue;
+    // 32-bit slot offsets: the column's range must fit the descriptor
+    if ((a.xhi - a.xlo) * 8 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+    int cpb, ppt;
+    resid_shape(&cpb, &ppt);
+    const size_t lds = (size_t)a.npent * 16 + 16;
+    const bool mid = (a.pmaxlen & 1) && a.pslot[a.pmaxlen / 2] == 0;
+    // the +-1 slots from the neighbouring lanes (CAL_RESID_LANE=0/1 while tuning)
+    static const bool lane_env = [] {
+        const char* e = std::getenv("CAL_RESID_LANE");
+        return e && std::atoi(e) != 0;
+    }();
+    const bool lane = lane_env && mid && a.pmaxlen >= 3 && a.pslot[a.pmaxlen / 2 - 1] == -1 &&
+                      a.pslot[a.pmaxlen / 2 + 1] == 1;
+    auto go = [&](auto cpb_c, auto ppt_c) {
         constexpr int CPB = decltype(cpb_c)::value, PPT = decltype(ppt_c)::value;
         dim3 g(blocks, (npr + CPB - 1) / CPB), bl(256);
-#define CAL_PRM(ML)                                                                                             \
-    hipLaunchKernelGGL((k_spmv_pair_resid_multi<ML, CPB, PPT>), g, bl, lds, st, a, a.ppat, a.ppoff, a.ppval, X, \
-                       ldx, col, lam, out, npr, partial, pstride)
+#define CAL_PRM(ML, M, LN)                                                                                          \
+    hipLaunchKernelGGL((k_resid_pairs<ML, CPB, PPT, M, LN>), g, bl, lds, st, a, a.ppat, a.ppoff, a.ppval, X, ldx, col, \
+                       lam, out, npr, partial, pstride)
+#define CAL_PRM_ODD(ML)                 \
+    if (lane) CAL_PRM(ML, true, true);  \
+    else if (mid) CAL_PRM(ML, true, false); \
+    else CAL_PRM(ML, false, false)
         switch (a.pmaxlen) {
-            case 1: CAL_PRM(1); break;
-            case 2: CAL_PRM(2); break;
-            case 3: CAL_PRM(3); break;
-            case 4: CAL_PRM(4); break;
-            case 5: CAL_PRM(5); break;
-            case 6: CAL_PRM(6); break;
-            case 7: CAL_PRM(7); break;
-            default: CAL_PRM(8); break;
+            case 1: if (mid) CAL_PRM(1, true, false); else CAL_PRM(1, false, false); break;
+            case 2: CAL_PRM(2, false, false); break;
+            case 3: CAL_PRM_ODD(3); break;
+            case 4: CAL_PRM(4, false, false); break;
+            case 5: CAL_PRM_ODD(5); break;
+            case 6: CAL_PRM(6, false, false); break;
+            case 7: CAL_PRM_ODD(7); break;
+            default: CAL_PRM(8, false, false); break;
         }
+#undef CAL_PRM_ODD
 #undef CAL_PRM
     };
-    auto go = [&](auto cpb_c) {
-        switch (resid_ppt()) {
-            case 1: go2(cpb_c, std::integral_constant<int, 1>{}); break;
-            case 2: go2(cpb_c, std::integral_constant<int, 2>{}); break;
-            case 8: go2(cpb_c, std::integral_constant<int, 8>{}); break;
-            default: go2(cpb_c, std::integral_constant<int, 4>{}); break;
+    auto go1 = [&](auto cpb_c) {
+        switch (ppt) {
+            case 1: go(cpb_c, std::integral_constant<int, 1>{}); break;
+            case 2: go(cpb_c, std::integral_constant<int, 2>{}); break;
+            case 8: go(cpb_c, std::integral_constant<int, 8>{}); break;
+            default: go(cpb_c, std::integral_constant<int, 4>{}); break;
         }
     };
-    if (cpb == 1) go(std::integral_constant<int, 1>{});
-    else if (cpb == 2) go(std::integral_constant<int, 2>{});
-    else if (cpb == 8) go(std::integral_constant<int, 8>{});
-    else go(std::integral_constant<int, 4>{});
+    if (cpb == 1) go1(std::integral_constant<int, 1>{});
+    else if (cpb == 2) go1(std::integral_constant<int, 2>{});
+    else if (cpb == 8) go1(std::integral_constant<int, 8>{});
+    else go1(std::integral_constant<int, 4>{});
     return hipGetLastError();
 }
 
@@ -1441,21 +1324,13 @@ hipError_t launch_gram_wide(const double* Q, int64_t ld, int w, int64_t n, doubl
     return hipGetLastError();
 }
 
-bool gram_lds_on() {  // CAL_GRAM_LDS=0: the direct-load k_gram (A/B; same bits)
-    static const bool on = [] {
-        const char* e = std::getenv("CAL_GRAM_LDS");
-        return !e || std::atoi(e) != 0;
-    }();
-    return on;
-}
-
 hipError_t launch_gram(const Panel& A, const Panel& B, int64_t n, const GramPlan& pl, double* partial,
                        hipStream_t st) {
     dim3 g(pl.blocks), b(256);
     // the staged loads pay from 33 A columns on (tools/gram_probe.hip: +5-15 %
     // at 48-128 columns; RUN = 16 stages 256-row blocks in 70 KB of LDS and
     // loses to the direct loads at <= 32 columns)
-    if (gram_lds_on() && pl.nta >= 3) {
+    if (pl.nta >= 3) {
         switch (pl.nta) {
             case 3: launch_gram_lds<3, 8>(A, B, n, pl.blocks, partial, st); break;
             case 4: launch_gram_lds<4, 8>(A, B, n, pl.blocks, partial, st); break;
@@ -1722,12 +1597,8 @@ __global__ __launch_bounds__(256) void k_apply_rows(Panel P, const double* __res
 // columns, wider output chunks (32, 64) while M fits 64 KB of LDS
 int apply_rows_max_wy(int wp) {
     if (wp < 1 || wp > 256) return 0;
-    static const bool wide = [] {  // CAL_APPLY_ROWS_WIDE=0: <= 16 outputs (A/B)
-        const char* e = std::getenv("CAL_APPLY_ROWS_WIDE");
-        return !e || std::atoi(e) != 0;
-    }();
     int wy = 16;
-    while (wide && wy < 64 && (size_t)wp * (2 * wy) * sizeof(double) <= 65536) wy *= 2;
+    while (wy < 64 && (size_t)wp * (2 * wy) * sizeof(double) <= 65536) wy *= 2;
     return wy;
 }
 bool apply_rows_ok(int wp, int wy) { return wy >= 1 && wy <= apply_rows_max_wy(wp); }

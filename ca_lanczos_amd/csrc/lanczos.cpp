@@ -424,29 +424,15 @@ struct StreamScope {
 
 // The GPU work of one job: the orthogonality-error Grams, the Ritz-vector
 // apply (bound by the f64 matrix cores), the residual sums (bound by the
-// gather), one reduction and copy.  Optionally (A/B switches below) on two
-// streams: the apply on the context stream in column chunks, the Grams and
-// each chunk's residuals on an auxiliary stream behind that chunk's apply.
-// The context stream waits for the job's last event, so what follows it (the
-// next step, a reuse of the work columns) is ordered after it.
+// gather), one reduction and copy, all on the context stream.  (A second
+// stream for the Grams and residuals, and the apply in column chunks so a
+// chunk's residuals overlap the next chunk's apply, measured slower: lap3d_215,
+// 15 iterations, 130.5 outer-it/s on one stream, 125.3 on two, 117-120 with
+// two chunks -- the residual blocks take LDS and CU slots from the apply's.)
 static int diag_launch(cal_ctx* c, LanczosState& L, DiagJob& J) {
     const int s = L.s, sk = s * J.k;
     const int64_t n = c->A.n_local, ld = c->A.ld;
-    // CAL_DIAG_AUX=1 (second stream), CAL_DIAG_CHUNKS=2..4 (apply chunks): the
-    // overlap below, measured slower (lap3d_215, 15 iterations: one stream, one
-    // chunk 130.5 outer-it/s; two streams 125.3; two chunks 117-120: the
-    // residual blocks take LDS and CU slots from the 120-KB-LDS apply blocks),
-    // so both are off by default
-    static const int use_aux = [] {
-        const char* e = std::getenv("CAL_DIAG_AUX");
-        return e ? std::atoi(e) : 0;
-    }();
-    static const int chunks_env = [] {
-        const char* e = std::getenv("CAL_DIAG_CHUNKS");
-        return e ? std::atoi(e) : 1;
-    }();
-    if (use_aux && !c->aux_stream) CAL_HIP(c, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
-    const hipStream_t main = c->stream, aux = use_aux ? c->aux_stream : c->stream;
+    const hipStream_t main = c->stream, aux = c->stream;
     // compute_orth_err(Q(:,1:sk+1), s): Q(:,1:j-s-1)'Q(:,j-s:j) for j > s+1,
     // else Q'Q - I; Grams in chunks of 128 x 16 columns (gram_async)
     const int jq = sk + 1;
@@ -463,10 +449,10 @@ static int diag_launch(cal_ctx* c, LanczosState& L, DiagJob& J) {
             oe_part = std::max(oe_part, (size_t)pl.blocks * pl.entries);
         }
     CAL_TRY(grow_pinned(c, &L.d_dres, &L.h_dres, &L.dres_cap, off));
-    // the Ritz vectors in column chunks (two from 48 columns: the second
-    // chunk's apply overlaps the first chunk's residuals)
+    // the Ritz vectors (one column chunk; the chunked form is kept for the
+    // pair grouping below)
     const bool mt = apply_mt_ok(sk, sk);
-    const int nch = mt && sk >= 48 ? std::max(1, std::min(4, chunks_env)) : 1;
+    const int nch = 1;
     const int cw = nch == 1 ? sk : ((sk + nch * 16 - 1) / (nch * 16)) * 16;
     auto chunk_of = [&](int col) { return std::min(nch - 1, col / cw); };
     // inputs: Vp, then the batched pairs grouped by chunk (Ritz value, column,
@@ -774,6 +760,7 @@ static int extend_T(cal_ctx* c, LanczosState& L, const std::vector<double>& Rkk_
     return 0;
 }
 
+#ifdef CAL_TEST_HOOKS  // the test build only (csrc/Makefile libcalanczos_testhooks.so)
 // TEST HOOK (CAL_TEST_EIG_PAIR set; tests/test_gpu_parity.py): no converged
 // complex Ritz pair arises on the inputs the tests can reach, so the test
 // rewrites every all-real eig(T) the way tests/test_oracle.py's hook rewrites
@@ -831,6 +818,7 @@ static void test_eig_pair(int sk, std::vector<double>& wr, std::vector<double>& 
     wi.swap(wi2);
     V.swap(V2);
 }
+#endif
 
 // selective (ca_lanczos.m:321-340): the Ritz pairs of T(1:sk,1:sk) with
 // b(k)|Vp(sk,i)| < normest(A) sqrt(eps) (unit-norm eigenvectors, as MATLAB's
@@ -846,7 +834,9 @@ static int selective_update(cal_ctx* c, LanczosState& L) {
         for (int i = 0; i < sk; ++i) Tk[i + (size_t)j * sk] = L.T[i + (size_t)j * L.Tld];
     if (cal_eig(sk, Tk.data(), sk, wr.data(), wi.data(), V.data()) != 0)
         return set_error(c, CAL_ERR_NUMERIC, "eig(T) did not converge");
+#ifdef CAL_TEST_HOOKS
     if (std::getenv("CAL_TEST_EIG_PAIR")) test_eig_pair(sk, wr, wi, V);
+#endif
     const double thresh = L.norm_A * std::sqrt(std::numeric_limits<double>::epsilon());
     const double bk = L.b.back();
     std::vector<int> conv;  // columns of V: real pairs, or (Re v, Im v) of a complex pair

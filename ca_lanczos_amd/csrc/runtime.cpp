@@ -1,5 +1,6 @@
 // runtime.cpp -- context lifecycle, device buffers, matrix upload, timers.
 #include <algorithm>
+#include <cmath>
 #include <thread>
 #include <cstdio>
 #include <cstdlib>
@@ -454,13 +455,9 @@ static PatArgs pat_args(const DevMatrix& A, int64_t o, int64_t len, const double
     p.pcanon = A.pcanon ? 1 : 0;
     for (int k = 0; k < 8; ++k) p.pslot[k] = A.pslot[k];
     {
-        // the +-1 slots from the neighbouring lanes (k_spmv_pair*); CAL_LANE_SLOTS=0 loads them
-        static const bool lane_slots = [] {
-            const char* e = std::getenv("CAL_LANE_SLOTS");
-            return !e || std::atoi(e) != 0;
-        }();
+        // the +-1 slots from the neighbouring lanes (k_spmv_pair*)
         const int z = A.pmaxlen / 2;
-        p.pmid = (lane_slots && A.pcanon && (A.pmaxlen & 1) && A.pmaxlen >= 3 && A.pslot[z] == 0 &&
+        p.pmid = (A.pcanon && (A.pmaxlen & 1) && A.pmaxlen >= 3 && A.pslot[z] == 0 &&
                   A.pslot[z - 1] == -1 && A.pslot[z + 1] == 1)
                      ? z
                      : -1;
@@ -926,6 +923,13 @@ int cal_tsqr_fold_stats(cal_ctx* c, long long* runs, long long* declined, double
     if (runs) *runs = c->fold_runs;
     if (declined) *declined = c->fold_declined;
     if (last_est) *last_est = c->fold_last_est;
+    return 0;
+}
+
+int cal_set_tsqr_fold_tol(cal_ctx* c, double tol) {
+    if (!c) return CAL_ERR_ARG;
+    if (std::isnan(tol)) return set_error(c, CAL_ERR_ARG, "cal_set_tsqr_fold_tol: tol is NaN");
+    c->fold_tol = tol;
     return 0;
 }
 

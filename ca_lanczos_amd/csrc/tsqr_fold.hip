@@ -58,7 +58,6 @@ constexpr int kProbe = FOLD_PROBE;  // bit 1: no Gram, 2: no tile QR, 3: no tile
 #ifndef FOLD_UP_WPE
 #define FOLD_UP_WPE 4  // k_fold_up waves per SIMD (VGPR budget 512 / WPE)
 #endif
-constexpr double kFoldTol = 1e-14;  // largest accepted loss-of-orthogonality estimate
 
 __device__ __forceinline__ fd4 fmfma(double a, double b, fd4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -152,8 +151,7 @@ __device__ __forceinline__ void fmul_S(const double (&q)[FM], const double* S, i
 // LDS rows tlw onto the matrix cores: one v_mfma_f64_16x16x4f64 per 4 rows
 // with A = the rows' first 16 columns, B = the 16 columns from column 9 on,
 // so acc(i, j) accumulates C2(i, j) = Qp(:,i)'Y(:,j) for i < 9, j < 8 (the
-// other outputs are unused; tlw has FTLD + 16 spare doubles for B's tail).  k_fold_up and k_fold_down_reform run the same code on the
-// same inputs, so the tile QR that follows gives the same reflectors in both.
+// other outputs are unused; tlw has FTLD + 16 spare doubles for B's tail).
 template <bool GRAM>
 __device__ __forceinline__ void fform(const ColList P, const double* Cs, double* tlw, int64_t base, int64_t n,
                                       int lane, int m, int w, double (&x)[L0RPL][FM], fd4& acc) {
@@ -331,7 +329,7 @@ __device__ __forceinline__ void finv_col(const double* T, double* Ti, int j, int
 __device__ __forceinline__ void fold_coef1_body(const double* T1, const double* G, const double* Rtop, int ldr,
                                                 double* __restrict__ out, double* __restrict__ Sbuf,
                                                 double* __restrict__ Sm, double* __restrict__ Kbuf, int w, int m,
-                                                int doreorth, double nglob, double* Sl, int lane) {
+                                                int doreorth, double nglob, double tol, double* Sl, int lane) {
     __shared__ double Cs[9 * FM], C2s[9 * FM], RT[64], XX[64];
     __shared__ double RY[64], Ri[64], Ws[9 * FM], U[64], Ui[64], D[FM];
     __shared__ int fail, reo;
@@ -424,9 +422,10 @@ __device__ __forceinline__ void fold_coef1_body(const double* T1, const double* 
         // the fold's loss of orthogonality ~ 2 ||W|| ||E||, E = Qp'Q_Y - W
         // (the rounding of C2 and of Y's factorization through R_Y^-1):
         // ||E|| <~ u sqrt(n) max||X_j|| ||R_Y^-1||; decline (explicit Z)
-        // unless that is below kFoldTol and ||W||_F <= 1/2
+        // unless that is below tol (FoldArgs::tol: kFoldTol unless the context sets another)
+        // and ||W||_F <= 1/2
         est = 2.0 * sqrt(nw) * 0x1p-53 * sqrt(nglob) * xmax * sqrt(nri);
-        int bad = !(nw <= 0.25) || !(est <= kFoldTol);  // also NaN / Inf
+        int bad = !(nw <= 0.25) || !(est <= tol);  // also NaN / Inf
         // U = chol(A), upper, in registers: lane (r, c), pivot rows by
         // shuffles (dense::chol_upper's operations and order)
         double uv = 0.0;
@@ -445,6 +444,10 @@ __device__ __forceinline__ void fold_coef1_body(const double* T1, const double* 
         if (lane == 0) fail = bad;
         fwsync();
         if (!fail && lane < FM) finv_col(U, Ui, lane, m);
+        fwsync();
+    }
+    if (!reorth && !(est <= tol)) {  // est = 0 here: only a negative tol (decline every block)
+        if (lane == 0) fail = 1;
         fwsync();
     }
     if (lane == 0) {
@@ -497,9 +500,9 @@ __global__ __launch_bounds__(64) void k_fold_coef1(const double* __restrict__ T1
                                                   const double* __restrict__ Rtop, int ldr, double* __restrict__ out,
                                                   double* __restrict__ Sbuf, double* __restrict__ Sm,
                                                   double* __restrict__ Kbuf, int w, int m, int doreorth, double nglob,
-                                                  double* __restrict__ hout,
+                                                  double tol, double* __restrict__ hout,
                                                   unsigned long long* __restrict__ hseq, unsigned long long seq) {
-    fold_coef1_body(T1, G, Rtop, ldr, out, Sbuf, Sm, Kbuf, w, m, doreorth, nglob, nullptr, threadIdx.x);
+    fold_coef1_body(T1, G, Rtop, ldr, out, Sbuf, Sm, Kbuf, w, m, doreorth, nglob, tol, nullptr, threadIdx.x);
     if (hout) fold_publish(out, w, m, hout, hseq, seq, threadIdx.x);
 }
 
@@ -594,7 +597,7 @@ __global__ __launch_bounds__(64 * UW) void k_fold_root(FoldArgs a, const double*
     tile_geqr2_blk<FM, URPL, UW>(x, tau, beta, m, lane, wave, xlds);
     if (wave == 0) fput_R(Rl, lane, m, x[0]);
     __syncthreads();
-    if (wave == 0) fold_coef1_body(T1, G, Rl, FM, out, Sbuf, Sm, Kbuf, w, m, doreorth, nglob, Sl, lane);
+    if (wave == 0) fold_coef1_body(T1, G, Rl, FM, out, Sbuf, Sm, Kbuf, w, m, doreorth, nglob, a.tol, Sl, lane);
     __syncthreads();
     tile_org2r_blk<FM, URPL, UW>(x, tau, m, lane, wave, xlds);
     double* Sb = L == 1 ? a.S0 : a.Su[L - 2];
@@ -626,8 +629,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         Ks[e] = (k < w && cc < m) ? a.K[e] : 0.0;
     }
     const bool corr = a.flags[2] != 0.0;
+    // a declined fold (flags[1], written by the coefficient step before this
+    // launch) stores nothing: S and K are stale then, and Q may alias X,
+    // which the explicit-Z path that follows reads again
+    const bool declined = a.flags[1] != 0.0;
     __syncthreads();
-    if (tile >= ntiles) return;
+    if (tile >= ntiles || declined) return;
     double x[L0RPL][FM], tau[FM];
     fload_tile<L0RPL>(a.V0 + tile * (64 * L0RPL * FM), lane, x);
     fload_tau(a.tb0 + tile * (2 * FM), tau);
@@ -635,76 +642,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     fwsync();
     tile_org2r<FM, L0RPL>(x, tau, m, lane);
     const int64_t base = tile * FTR0;
-    double q[9];
-    auto loadq = [&](int i) {
-        const int64_t r = base + lane + 64 * i;
-        const int64_t rr = r < n ? r : n - 1;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) q[k] = P.p[k][rr];
-    };
-    if (corr) loadq(0);
-#pragma unroll
-    for (int i = 0; i < L0RPL; ++i) {
-        asm volatile("" ::: "memory");
-        double o[FM];
-        fmul_S(x[i], Ss[wave], m, o);
-        if (corr) {
-            double t[FM];
-#pragma unroll
-            for (int cc = 0; cc < FM; ++cc) t[cc] = 0.0;
-#pragma unroll
-            for (int k = 0; k < 9; ++k) {
-#pragma unroll
-                for (int cc = 0; cc < FM; ++cc) asm volatile("" : "+v"(t[cc]));
-#pragma unroll
-                for (int cc = 0; cc < FM; ++cc) t[cc] = __builtin_fma(q[k], Ks[k + cc * 9], t[cc]);
-            }
-            if (i + 1 < L0RPL) loadq(i + 1);
-#pragma unroll
-            for (int cc = 0; cc < FM; ++cc) o[cc] = o[cc] - t[cc];
-        }
-        const int64_t r = base + lane + 64 * i;
-        if (r < n) {
-#pragma unroll
-            for (int cc = 0; cc < FM; ++cc)
-                if (cc < m) Q.p[cc][r] = o[cc];
-        }
-    }
-}
-
-// Level 0 without stored tiles: re-form Y and refactor it (the up pass's
-// code on the same inputs: the same reflectors), then Q = Q_tile S - Qp K;
-// Qp is read again for the correction (the rows this wave just formed from,
-// mostly served by the caches).  Reads (w + m) 8n, writes m 8n.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FOLD_UP_WPE))) void k_fold_down_reform(
-    ColList P, OutList Q, FoldArgs a) {
-    __shared__ double Cs[9 * FM];
-    __shared__ double Ss[FTPB][64];
-    __shared__ double Ks[9 * FM];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = a.m, w = a.w;
-    const int64_t n = a.n;
-    const int64_t ntiles = (n + FTR0 - 1) / FTR0;
-    const int64_t tile = (int64_t)blockIdx.x * FTPB + wave;
-    {
-        const int nq = w < 8 ? w : 8;
-        for (int e = tid; e < 9 * FM; e += 256) {
-            const int k = e / FM, cc = e % FM;
-            Cs[e] = (k < w && cc < m) ? (k < 8 ? a.C[k + (nq + cc) * 16] : a.C[256 + nq + cc]) : 0.0;
-            const int k2 = e % 9, c2 = e / 9;
-            Ks[e] = (k2 < w && c2 < m) ? a.K[e] : 0.0;
-        }
-    }
-    const bool corr = a.flags[2] != 0.0;
-    __syncthreads();
-    if (tile >= ntiles) return;
-    Ss[wave][lane] = a.S0[tile * 64 + lane];
-    const int64_t base = tile * FTR0;
-    double x[L0RPL][FM], tau[FM], beta[FM];
-    fd4 d0 = fd4{0.0, 0.0, 0.0, 0.0};
-    fform<false>(P, Cs, nullptr, base, n, lane, m, w, x, d0);
-    tile_geqr2<FM, L0RPL>(x, tau, beta, m, lane);
-    tile_org2r<FM, L0RPL>(x, tau, m, lane);
-    fwsync();
     double q[9];
     auto loadq = [&](int i) {
         const int64_t r = base + lane + 64 * i;
@@ -776,9 +713,10 @@ hipError_t launch_fold_reduce(const double* partial, int nparts, double* outv, h
 }
 hipError_t launch_fold_coef1(const double* T1, const double* G, const double* Rtop, int ldr, double* out,
                              double* Sbuf, double* Sm, double* Kbuf, int w, int m, int doreorth, double nglob,
-                             double* hout, unsigned long long* hseq, unsigned long long seq, hipStream_t st) {
+                             double tol, double* hout, unsigned long long* hseq, unsigned long long seq,
+                             hipStream_t st) {
     hipLaunchKernelGGL(k_fold_coef1, dim3(1), dim3(64), 0, st, T1, G, Rtop, ldr, out, Sbuf, Sm, Kbuf, w, m, doreorth,
-                       nglob, hout, hseq, seq);
+                       nglob, tol, hout, hseq, seq);
     return hipGetLastError();
 }
 hipError_t launch_fold_down_tree(const FoldArgs& a, const double* Stop, int lds, hipStream_t st, int from) {
@@ -794,8 +732,7 @@ hipError_t launch_fold_root(const FoldArgs& a, const double* T1, const double* G
     return hipGetLastError();
 }
 hipError_t launch_fold_down(const ColList& P, const OutList& Q, const FoldArgs& a, hipStream_t st) {
-    if (a.V0) hipLaunchKernelGGL(k_fold_down, dim3(a.nblk), dim3(256), 0, st, P, Q, a);
-    else hipLaunchKernelGGL(k_fold_down_reform, dim3(a.nblk), dim3(256), 0, st, P, Q, a);
+    hipLaunchKernelGGL(k_fold_down, dim3(a.nblk), dim3(256), 0, st, P, Q, a);
     return hipGetLastError();
 }
 

@@ -45,6 +45,16 @@ int cal_tridiag_eigvals(int n, const double* alpha, const double* beta, double* 
  * column signs).  H (ldh >= m) and W (ldw >= m) column-major, in place. */
 int cal_qrstep(int m, double* H, int ldh, double* W, int ldw, double mu);
 
+/* Residency generation of the MEX shims' device copies of A (mex/
+ * cal_mex_common.h).  Every shim keeps A resident across calls and re-uploads
+ * it when the pointers, nnz, a sampled digest of jc/ir/pr or this
+ * process-wide generation change.  An in-place edit of A's values that the
+ * sampled digest does not cover needs the explicit invalidation, which bumps
+ * the generation for every shim of the process (MATLAB:
+ * calanczos_invalidate(), or `clear mex`).  Thread-safe. */
+long long cal_residency_generation(void);
+long long cal_residency_invalidate(void); /* returns the new generation */
+
 #ifdef __cplusplus
 }
 #endif

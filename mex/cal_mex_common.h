@@ -1,16 +1,25 @@
 /* cal_mex_common.h -- shared by every MEX shim in mex/ (a MEX file
  * of the same name shadows the reference's .m file).
  *
- * One cal_ctx per MATLAB session keeps A (and the CA-Lanczos state) resident
- * in HBM across calls; it is re-uploaded only when a different sparse matrix
- * arrives and destroyed at mexAtExit (`clear mex` forces a fresh upload).
- * "Different" compares the jc / ir / pr pointers, nnz AND a 64-bit digest of
- * the ir and pr contents: an in-place edit A(i,j)=v of an existing nonzero, or
- * a new matrix MATLAB allocates at freed addresses with the same nnz, keeps
- * all four equal, and must not run on the stale device copy.  The digest reads
- * 16 bytes per nonzero on the host (~0.1 s at nnz = 7e7, against ~1 s for the
- * upload and format analysis it saves).  MATLAB calls mexFunction on one thread, which matches the
- * ABI's one-thread-per-context rule. */
+ * One cal_ctx per shim keeps A (and the CA-Lanczos state) resident in HBM
+ * across calls; it is destroyed at mexAtExit (`clear mex` forces a fresh
+ * upload).  The residency decision must cost far less than the call it
+ * serves (SpMV.mexa64 is called s times per outer iteration from the
+ * unchanged matrix_powers_newton.m:32, against ~1 ms of device work), so it
+ * reads a bounded number of entries, independent of nnz:
+ *   - the jc / ir / pr pointers, n and nnz;
+ *   - a digest of a fixed sample of the arrays: the first and last 32
+ *     entries of each and up to kCalMexSamples evenly spaced entries of jc,
+ *     ir and pr (≈1 ms at nnz = 7e7, tests/test_mex_shims.py);
+ *   - the library's process-wide residency generation
+ *     (cal_residency_generation, calanczos_host.h).
+ * A different matrix that MATLAB allocates at freed addresses with the same
+ * nnz, or an edit of a sampled entry, re-uploads.  An in-place edit
+ * A(i,j) = v of an existing nonzero that the sample misses is not seen: after
+ * such an edit call calanczos_invalidate() (mex/calanczos_invalidate_mex.c,
+ * which bumps the generation for every shim of the process) or `clear mex`.
+ * MATLAB calls mexFunction on one thread, which matches the ABI's
+ * one-thread-per-context rule. */
 #ifndef CAL_MEX_COMMON_H
 #define CAL_MEX_COMMON_H
 #include <stdint.h>
@@ -18,30 +27,60 @@
 
 #include "mex.h"
 #include "calanczos.h"
+#include "calanczos_host.h"
+
+#define kCalMexSamples 16384
 
 static cal_ctx* g_ctx = NULL;
 static const void* g_jc = NULL;
 static const void* g_ir = NULL;
 static const void* g_pr = NULL;
+static mwSize g_n = 0;
 static mwSize g_nnz = 0;
 static uint64_t g_digest = 0;
+static long long g_gen = -1;
 
-/* order-sensitive 64-bit digest of a byte range (multiply-xorshift per word) */
-static uint64_t cal_mex_digest(uint64_t h, const void* p, size_t bytes) {
+/* order-sensitive 64-bit mix of one word */
+static uint64_t cal_mex_mix(uint64_t h, uint64_t w) {
+    h ^= w + 0x9e3779b97f4a7c15ULL + (h << 6) + (h >> 2);
+    h *= 0xff51afd7ed558ccdULL;
+    h ^= h >> 33;
+    return h;
+}
+
+/* digest of a bounded sample of an array of `count` 8-byte words: the first
+ * and last 32 and up to kCalMexSamples evenly spaced ones */
+static uint64_t cal_mex_sample(uint64_t h, const void* p, size_t count) {
     const unsigned char* b = (const unsigned char*)p;
-    size_t i = 0;
-    for (; i + 8 <= bytes; i += 8) {
-        uint64_t w;
-        memcpy(&w, b + i, 8);
-        h ^= w + 0x9e3779b97f4a7c15ULL + (h << 6) + (h >> 2);
-        h *= 0xff51afd7ed558ccdULL;
-        h ^= h >> 33;
+    uint64_t w;
+    size_t i, edge = count < 64 ? count : 32;
+    for (i = 0; i < edge; ++i) {
+        memcpy(&w, b + 8 * i, 8);
+        h = cal_mex_mix(h, w);
     }
-    for (; i < bytes; ++i) {
-        h ^= b[i];
-        h *= 0x100000001b3ULL;
+    for (i = count > edge ? count - edge : edge; i < count; ++i) {
+        memcpy(&w, b + 8 * i, 8);
+        h = cal_mex_mix(h, w);
+    }
+    if (count > 64) {
+        const size_t step = count / kCalMexSamples > 1 ? count / kCalMexSamples : 1;
+        for (i = 0; i < count; i += step) {
+            memcpy(&w, b + 8 * i, 8);
+            h = cal_mex_mix(h, w);
+        }
     }
     return h;
+}
+
+/* the residency decision: 1 when the device copy must be (re)uploaded */
+static int cal_mex_stale(const mwIndex* jc, const mwIndex* ir, const double* pr, mwSize n, long long gen,
+                         uint64_t* digest) {
+    const mwSize nnz = jc[n];
+    uint64_t d = cal_mex_sample(0xcbf29ce484222325ULL ^ (uint64_t)n, jc, n + 1);
+    d = cal_mex_sample(d, ir, nnz);
+    d = cal_mex_sample(d, pr, nnz);
+    *digest = d;
+    return jc != g_jc || ir != g_ir || pr != g_pr || n != g_n || nnz != g_nnz || gen != g_gen || d != g_digest;
 }
 
 static void cal_mex_exit(void) {
@@ -71,18 +110,19 @@ static cal_ctx* cal_mex_ctx(const mxArray* A) {
         mexErrMsgIdAndTxt("calanczos:arg", "A must be a real square sparse matrix");
     cal_ctx* c = cal_mex_plain_ctx();
     const mwIndex* jc = mxGetJc(A);
-    const mwSize n = mxGetN(A), nnz = jc[n];
-    uint64_t d = cal_mex_digest(0xcbf29ce484222325ULL, jc, (n + 1) * sizeof(mwIndex));
-    d = cal_mex_digest(d, mxGetIr(A), nnz * sizeof(mwIndex));
-    d = cal_mex_digest(d, mxGetPr(A), nnz * sizeof(double));
-    if (jc != g_jc || mxGetIr(A) != g_ir || mxGetPr(A) != g_pr || nnz != g_nnz || d != g_digest) {
+    const mwSize n = mxGetN(A);
+    const long long gen = cal_residency_generation();
+    uint64_t d = 0;
+    if (cal_mex_stale(jc, mxGetIr(A), mxGetPr(A), n, gen, &d)) {
         cal_mex_check(cal_set_matrix_csc(c, (int64_t)n, (const int64_t*)jc, (const int64_t*)mxGetIr(A),
                                          mxGetPr(A)));
         g_jc = jc;
         g_ir = mxGetIr(A);
         g_pr = mxGetPr(A);
-        g_nnz = nnz;
+        g_n = n;
+        g_nnz = jc[n];
         g_digest = d;
+        g_gen = gen;
     }
     return c;
 }

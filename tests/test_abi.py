@@ -132,3 +132,13 @@ def test_matlab_rand_matches_mt19937(cal, ref):
     for seed in (5489, 7):
         assert np.array_equal(cal.matlab_rand(1000, seed), ref.matlab_rand(1000, seed=seed))
 
+
+
+def test_residency_generation_is_process_wide(cal):
+    """cal_residency_invalidate (calanczos_host.h; the MEX tier's explicit
+    invalidation after an in-place edit of A, mex/calanczos_invalidate_mex.c)
+    bumps the one process-wide generation every shim compares.  Host only."""
+    from ca_lanczos_amd._lib import lib
+    g0 = lib.cal_residency_generation()
+    assert lib.cal_residency_invalidate() == g0 + 1
+    assert lib.cal_residency_generation() == g0 + 1

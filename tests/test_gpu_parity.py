@@ -9,6 +9,8 @@ Bars:
     1e-9 * ||A||, converged Ritz values within 1e-10 * ||A||, residual norms
     above 1e-10 within a factor 2 of the oracle's.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -491,7 +493,8 @@ def test_restarted_ca_lanczos(cal, ref):
     ill-conditioned here (ten wanted eigenvalues 2 apart at tol 1e-8): the
     oracle itself takes 93, 106, 120 and 96 restarts for r = ones perturbed
     by 0, +-1e-15 and 3e-15 relative (times cos(i)), so the bar is that
-    spread, +-35 % of the oracle's unperturbed count, not equality."""
+    measured spread, [93, 120], not equality; the oracle's own unperturbed
+    count is pinned at 93."""
     import scipy.sparse as sp
     a = ref.matlab_linspace(1.0, 1.0e4, 5000)
     A = sp.csr_matrix(sp.diags(a))
@@ -499,7 +502,10 @@ def test_restarted_ca_lanczos(cal, ref):
     exp = ref.restarted_ca_lanczos(A, r, 60, 10, 4, "newton", "full", 1.0e-8)
     out = cal.restarted_ca_lanczos(A, r, 60, 10, 4, "newton", "full", 1.0e-8)
     assert out["converged"] and exp["converged"]
-    assert abs(out["num_restarts"] - exp["num_restarts"]) <= 0.35 * exp["num_restarts"]
+    print("restarts: device %d, oracle %d (oracle spread under 1e-15 perturbations of r: 93..120)"
+          % (out["num_restarts"], exp["num_restarts"]))
+    assert exp["num_restarts"] == 93
+    assert 93 <= out["num_restarts"] <= 120
     eref = a[::-1][:10]
     assert np.max(np.abs(out["conv_eigs"] - eref)) <= 1e-8 * 1.0e4
     assert np.max(np.abs(out["conv_eigs"] - exp["conv_eigs"])) <= 1e-9 * 1.0e4
@@ -988,12 +994,55 @@ def test_ca_lanczos_selective_complex_pair(cal, ref, monkeypatch):
     monkeypatch.setattr(ref, "matlab_eig", paired)
     monkeypatch.setattr(ref, "newton_change_of_basis", ncb)
     exp = ref.ca_lanczos(A, r, 8, 160, "newton", "selective", diagnostics=False)
-    monkeypatch.setenv("CAL_TEST_EIG_PAIR", "1")
-    out = cal.ca_lanczos_ex(A, r, 8, 160, "newton", "selective", diagnostics=False)
+    # the device side in a child process on the test build of the library
+    # (libcalanczos_testhooks.so, CAL_TEST_HOOKS): the production library
+    # carries no result-altering hook
+    import json
+    import subprocess
+    import sys
+    import tempfile
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, json, numpy as np, scipy.sparse as sp; sys.path.insert(0, %r)\n"
+            "import ca_lanczos_amd as cal\n"
+            "from oracle import ca_lanczos_ref as ref\n"
+            "A = sp.csr_matrix(sp.diags(ref.matlab_linspace(1.0, 100.0, 500)))\n"
+            "out = cal.ca_lanczos_ex(A, np.ones(500), 8, 160, 'newton', 'selective', diagnostics=False)\n"
+            "np.save(sys.argv[1], out.T)\n"
+            "print(json.dumps({'info': {k: int(out.info[k]) for k in ('n_ritz_complex', 'n_orth_breaks', "
+            "'n_ritz_locked')}, 'reorth': [bool(f) for f in out.reorth]}))\n" % root)
+    with tempfile.TemporaryDirectory() as td:
+        tpath = os.path.join(td, "T.npy")
+        env = dict(os.environ, CAL_LIBRARY="testhooks", CAL_TEST_EIG_PAIR="1")
+        p = subprocess.run([sys.executable, "-c", code, tpath], env=env, capture_output=True, text=True,
+                           timeout=240)
+        assert p.returncode == 0, p.stderr[-2000:]
+        res = json.loads(p.stdout.strip().splitlines()[-1])
+        T = np.load(tpath)
     last = max(i for i, b in enumerate(exp.breaks) if b)
     assert exp.ncomplex[last] == 2
-    assert out.info["n_ritz_complex"] == 2
-    assert out.info["n_orth_breaks"] == sum(exp.breaks)
-    assert out.info["n_ritz_locked"] == exp.nritz[-1]
-    assert list(out.reorth) == list(exp.reorth)
-    assert np.max(np.abs(out.T - exp.T)) <= 1e-8 * 100.0
+    assert res["info"]["n_ritz_complex"] == 2
+    assert res["info"]["n_orth_breaks"] == sum(exp.breaks)
+    assert res["info"]["n_ritz_locked"] == exp.nritz[-1]
+    assert res["reorth"] == list(exp.reorth)
+    assert np.max(np.abs(T - exp.T)) <= 1e-8 * 100.0
+
+
+def test_production_library_has_no_test_hooks(cal, ref):
+    """The same 'selective' run on the production library with
+    CAL_TEST_EIG_PAIR set in its environment: the hook is not compiled in,
+    so eig(T) is left alone and no complex Ritz pair appears."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, numpy as np, scipy.sparse as sp; sys.path.insert(0, %r)\n"
+            "import ca_lanczos_amd as cal\n"
+            "from oracle import ca_lanczos_ref as ref\n"
+            "assert cal._lib.LIB_PATH.endswith('/libcalanczos.so')\n"
+            "A = sp.csr_matrix(sp.diags(ref.matlab_linspace(1.0, 100.0, 500)))\n"
+            "out = cal.ca_lanczos_ex(A, np.ones(500), 8, 160, 'newton', 'selective', diagnostics=False)\n"
+            "print(int(out.info['n_ritz_complex']))\n" % root)
+    env = dict(os.environ, CAL_TEST_EIG_PAIR="1")
+    env.pop("CAL_LIBRARY", None)
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert p.stdout.strip().splitlines()[-1] == "0"

@@ -98,3 +98,37 @@ def test_ca_lanczos_normalize_backends(cal, ref, backend):
     we = np.sort(np.linalg.eigvals(exp.T).real)
     assert abs(w[-1] - we[-1]) <= 1e-10 * nA and abs(w[0] - we[0]) <= 1e-10 * nA
     ctx.close()
+
+
+@pytest.mark.parametrize("orth,tol", [("local", 0.0), ("full", -1.0)])
+def test_tsqr_fold_declined_fallback(cal, ref, orth, tol):
+    """The fused TSQR projectAndNormalize's fallback (blockorth.cpp pn_tsqr:
+    a declined fold redoes the block on the explicit-Z path, i.e.
+    projectAndNormalize.m:25-26,63-64 literally), forced through
+    cal_set_tsqr_fold_tol: 0 declines every block that takes the second
+    projection, a negative value every block.  'full' includes the in-place
+    re-projection against all of Q (ca_lanczos.m:197, whose output aliases
+    its input X) at k = 2, where the fold applies: the declined fold must not
+    have stored its stale Q over X before the fallback reads X.  Same bars as
+    the backend test, plus 'full''s orthogonality."""
+    A = cal.matrices.laplacian_2d(32)
+    r = ref.matlab_rand(A.shape[0])
+    ctx = cal.Context(normalize="tsqr").set_matrix(A).set_tsqr_fold_tol(tol)
+    f0 = ctx.tsqr_fold_stats()
+    out = cal.ca_lanczos_ex(A, r, 8, 80, "newton", orth, diagnostics=True, ctx=ctx)
+    f1 = ctx.tsqr_fold_stats()
+    ctx.close()
+    exp = ref.ca_lanczos(A, r, 8, 80, "newton", orth, diagnostics=True)
+    runs, declined = f1["runs"] - f0["runs"], f1["declined"] - f0["declined"]
+    if orth == "local":
+        assert runs == 9 and declined == sum(out.reorth) > 0
+    else:
+        assert runs > 0 and declined == runs
+    nA = 8.0
+    assert list(out.reorth) == list(exp.reorth)
+    assert np.max(np.abs(out.T - exp.T)) <= 1e-9 * nA
+    w = np.sort(np.linalg.eigvals(out.T).real)
+    we = np.sort(np.linalg.eigvals(exp.T).real)
+    assert abs(w[-1] - we[-1]) <= 1e-10 * nA and abs(w[0] - we[0]) <= 1e-10 * nA
+    if orth == "full":
+        assert np.max(out.orth_err) < 1e-12
