@@ -114,6 +114,22 @@ struct PatArgs {
     int pslot[8];          // canonical slot offsets (the matrix's distinct col - row, ascending)
     int pmid = -1;         // pmaxlen / 2 when slots pmid - 1, pmid, pmid + 1 are the offsets -1, 0, +1
     int64_t xlo, xhi;      // addressable range of a vector column around its origin
+    // plane march (k_resid_planes): the canonical slots' values per row
+    // pattern with +0.0 where the row has no entry (npat x pmaxlen), the
+    // plane stride P = pslot[pmaxlen-1] = -pslot[0] and the in-plane reach H
+    // (the other slots' largest |offset|, rounded up to even); plane_P = 0:
+    // the matrix has no plane structure for it
+    const double* rzval = nullptr;
+    const uint8_t* rzmask = nullptr;  // bit e: the row pattern has an entry at slot e
+    // uniform slot values (every row with an entry at slot e has the value
+    // cval[e], as in the Laplacians): the plane march keys each row by its
+    // slot mask byte (rowmask, one per row) instead of its pattern id
+    const uint8_t* rowmask = nullptr;
+    int cuniform = 0;
+    double cval[8] = {};
+    int64_t plane_P = 0;
+    int plane_H = 0;
+    int64_t ld = 0;  // the vector columns' leading dimension (the descriptor's range)
     // two-range launch (pair kernel): compact pair index t >= gap_at maps to
     // stored pair t + gap, i.e. rows [0, 2 gap_at) and [2 (gap_at + gap),
     // 2 gap + n) relative to the origin; n counts the rows of both ranges
@@ -162,6 +178,14 @@ struct DevMatrix {
     int64_t npsplit = 0;
     bool pcanon = false;
     int pslot[8] = {};
+    // plane-march residual table (PatArgs::rzval; single rank, no halos)
+    double* rzval = nullptr;
+    uint8_t* rzmask = nullptr;
+    uint8_t* rowmask = nullptr;
+    bool cuniform = false;
+    double cval[8] = {};
+    int64_t plane_P = 0;
+    int plane_H = 0;
     // halo plan (distributed); ghost entries grouped by owning peer
     std::vector<int> peers;              // neighbour ranks
     std::vector<int64_t> recv_off;       // ghost destination per peer, relative to the local origin

@@ -42,6 +42,10 @@ typedef double d2 __attribute__((ext_vector_type(2)));
 
 constexpr int kSpmvThreads = 256;
 constexpr int kSpmvNnz = 2048;  // LDS-staged nonzeros per row block (16 KiB)
+// the plane march (k_spmv_planes, k_resid_planes): planes per block of the
+// residual kernel, rows of a plane per block
+constexpr int kResidPlanes = 32;
+constexpr int kResidPlaneRows = 512;
 
 // Column c of a panel.  The segment table is taken by value and read with
 // static indices only: binding a reference to a by-value kernel argument
@@ -90,7 +94,18 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
-template <int MODE, int NIT>
+// NT: col / val stream once per SpMV, so they are loaded non-temporally and
+// leave the caches to x, whose lines the neighbouring rows gather again.
+// V = 2: each thread loads two consecutive nonzeros (one 8-B col pair, one
+// 16-B val pair), half the load instructions of V = 1.  Same products, same
+// per-row order.
+template <bool NT, typename T>
+__device__ __forceinline__ T ldnt(const T* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+template <int MODE, int NIT, bool NT, int V>
 __global__ __launch_bounds__(kSpmvThreads) void k_spmv(SpmvArgs a) {
     __shared__ double prod[kSpmvNnz];
     const int b = a.xcd ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
@@ -103,21 +118,29 @@ __global__ __launch_bounds__(kSpmvThreads) void k_spmv(SpmvArgs a) {
             // all loads first (clamped, never branched around: one vmcnt wait
             // per phase), then the dependent x gathers, then LDS products.
             const int pl = p1 - 1;
-            int ci[NIT];
-            double v[NIT], xv[NIT];
+            constexpr int NI = (NIT + V - 1) / V;
+            int ci[NI][V];
+            double v[NI][V], xv[NI][V];
 #pragma unroll
-            for (int it = 0; it < NIT; ++it) {
-                int p = min(p0 + it * kSpmvThreads + tid, pl);
-                ci[it] = a.col[p];
-                v[it] = a.val[p];
+            for (int it = 0; it < NI; ++it) {
+#pragma unroll
+                for (int u = 0; u < V; ++u) {
+                    const int p = min(p0 + (it * kSpmvThreads + tid) * V + u, pl);
+                    ci[it][u] = ldnt<NT>(a.col + p);
+                    v[it][u] = ldnt<NT>(a.val + p);
+                }
             }
 #pragma unroll
-            for (int it = 0; it < NIT; ++it) xv[it] = a.x[ci[it]];
+            for (int it = 0; it < NI; ++it)
 #pragma unroll
-            for (int it = 0; it < NIT; ++it) {
-                int q = it * kSpmvThreads + tid;
-                if (q < cnt) prod[q] = v[it] * xv[it];
-            }
+                for (int u = 0; u < V; ++u) xv[it][u] = a.x[ci[it][u]];
+#pragma unroll
+            for (int it = 0; it < NI; ++it)
+#pragma unroll
+                for (int u = 0; u < V; ++u) {
+                    const int q = (it * kSpmvThreads + tid) * V + u;
+                    if (q < cnt) prod[q] = v[it][u] * xv[it][u];
+                }
         }
         __syncthreads();
         const int r = r0 + tid;
@@ -142,20 +165,40 @@ __global__ __launch_bounds__(kSpmvThreads) void k_spmv(SpmvArgs a) {
     }
 }
 
-template <int MODE>
-static hipError_t launch_spmv_mode(const SpmvArgs& a, int nit, hipStream_t st) {
+// CAL_SPMV_CSR = <nt><v> while tuning: "00" plain, "10" non-temporal, "02"
+// two nonzeros per thread, "12" both
+static int spmv_csr_variant() {
+    static const int v = [] {
+        const char* e = std::getenv("CAL_SPMV_CSR");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+
+template <int MODE, bool NT, int V>
+static hipError_t launch_spmv_mode2(const SpmvArgs& a, int nit, hipStream_t st) {
     dim3 g(a.nblk), b(kSpmvThreads);
     switch (nit) {
-        case 1: hipLaunchKernelGGL((k_spmv<MODE, 1>), g, b, 0, st, a); break;
-        case 2: hipLaunchKernelGGL((k_spmv<MODE, 2>), g, b, 0, st, a); break;
-        case 3: hipLaunchKernelGGL((k_spmv<MODE, 3>), g, b, 0, st, a); break;
-        case 4: hipLaunchKernelGGL((k_spmv<MODE, 4>), g, b, 0, st, a); break;
-        case 5: hipLaunchKernelGGL((k_spmv<MODE, 5>), g, b, 0, st, a); break;
-        case 6: hipLaunchKernelGGL((k_spmv<MODE, 6>), g, b, 0, st, a); break;
-        case 7: hipLaunchKernelGGL((k_spmv<MODE, 7>), g, b, 0, st, a); break;
-        default: hipLaunchKernelGGL((k_spmv<MODE, 8>), g, b, 0, st, a); break;
+        case 1: hipLaunchKernelGGL((k_spmv<MODE, 1, NT, V>), g, b, 0, st, a); break;
+        case 2: hipLaunchKernelGGL((k_spmv<MODE, 2, NT, V>), g, b, 0, st, a); break;
+        case 3: hipLaunchKernelGGL((k_spmv<MODE, 3, NT, V>), g, b, 0, st, a); break;
+        case 4: hipLaunchKernelGGL((k_spmv<MODE, 4, NT, V>), g, b, 0, st, a); break;
+        case 5: hipLaunchKernelGGL((k_spmv<MODE, 5, NT, V>), g, b, 0, st, a); break;
+        case 6: hipLaunchKernelGGL((k_spmv<MODE, 6, NT, V>), g, b, 0, st, a); break;
+        case 7: hipLaunchKernelGGL((k_spmv<MODE, 7, NT, V>), g, b, 0, st, a); break;
+        default: hipLaunchKernelGGL((k_spmv<MODE, 8, NT, V>), g, b, 0, st, a); break;
     }
     return hipGetLastError();
+}
+
+template <int MODE>
+static hipError_t launch_spmv_mode(const SpmvArgs& a, int nit, hipStream_t st) {
+    switch (spmv_csr_variant()) {
+        case 10: return launch_spmv_mode2<MODE, true, 1>(a, nit, st);
+        case 2: return launch_spmv_mode2<MODE, false, 2>(a, nit, st);
+        case 12: return launch_spmv_mode2<MODE, true, 2>(a, nit, st);
+        default: return launch_spmv_mode2<MODE, false, 1>(a, nit, st);
+    }
 }
 
 hipError_t launch_spmv(const SpmvArgs& a0, hipStream_t st) {
@@ -565,8 +608,278 @@ bool spmv_pat_pair_path(const PatArgs& a) {
     return a.ppat && al16 && a.maxlen <= 8 && lds2 <= kPatLdsMax;
 }
 
+// ---- the plane march -------------------------------------------------------
+// For matrices in canonical slots -P < ... < +P (pslot[0] = -P, pslot[L-1] =
+// +P, P >= 256) whose inner slots reach H <= 512 rows -- the 7-point (P =
+// N^2) and 5-point (P = N) Laplacians -- on a single slab.  A block owns the
+// rows xy0 .. xy0 + 511 of every plane (r = xy + z P) for Z planes.  Per plane
+// it stages into LDS, two planes ahead of their use (three buffers):
+//   * the window x[zP + xy0 - H, zP + xy0 + 512 + H) by contiguous 16-B
+//     buffer loads (reads outside the column return 0 from the range check);
+//   * the rows' keys by aligned dword loads: with uniform slot values (cval)
+//     the row's slot mask (PatArgs::rowmask, 1 B), else its pattern id (2 B)
+//     with the value / mask tables staged in LDS once.
+// Each lane then takes its row pair (xy0 + lr, + 1): the inner slots from the
+// window, the -P / +P slots the same lane's centre pair of the previous /
+// next plane (register, next buffer).  Each x value leaves HBM about once
+// ((Z + 2) / Z: a block also stages its neighbours' first / last plane), the
+// in-plane gathers are LDS reads, and every load instruction is issued two
+// planes before its data is needed (tools/resid_probe.hip: 15 us per Ritz
+// pair at n = 215^3 against 25 us for the row-pair gather, 12 us for a bare
+// read of x).  When P is odd the plane's last pair straddles into the next
+// plane: only its first row belongs to the block.
+template <int MAXLEN, bool CU>
+struct PlaneMarch {
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+    static constexpr int KB = CU ? 1 : 2;             // key bytes per row
+    static constexpr int KD = (512 * KB + 6) / 4 + 1;  // key dwords per plane (with the alignment slack)
+    static constexpr int LPT = (kResidPlaneRows + 2 * 512) / 2 / 256;  // window pairs per thread (H <= 512)
+    // plain scalars and pointers only: a reference to the by-value kernel
+    // argument would make every thread copy it to scratch
+    int H, WR, WP, tid, lr, wi, zend;
+    int64_t P, n, ld, xy0, z0;
+    bool in0, in1;
+    double* win;      // [3][WR]
+    uint32_t* keys;   // [3][KD]
+    double* s_rz;     // !CU: npat x MAXLEN values (0 where the row has no entry)
+    uint8_t* s_rm;    // !CU: npat slot masks
+    __amdgpu_buffer_rsrc_t rx, rk;
+    int ps[MAXLEN];   // slot offsets (compile-time indices only)
+    double cv[MAXLEN];
+    double2 st[LPT];
+    uint32_t kst[2];
+
+    __device__ static __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
+        const uint64_t pl = (uint64_t)(uintptr_t)p;
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pl);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(pl >> 32));
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0,
+                                                 (int)__builtin_amdgcn_readfirstlane((uint32_t)bytes), 0x00020000);
+    }
+    __host__ __device__ static size_t lds_bytes(const PatArgs& a) {
+        return (size_t)3 * (kResidPlaneRows + 2 * a.plane_H) * 8 + (size_t)3 * KD * 4 +
+               (CU ? 0 : (size_t)a.npat * MAXLEN * 8 + (size_t)a.npat) + 16;
+    }
+    // the fields are passed one by one from the kernel's by-value PatArgs
+    __device__ PlaneMarch(int64_t P_, int H_, int64_t n_, int64_t ld_, const double* x, const uint8_t* rowmask,
+                          const uint16_t* pat, const double* rzval, const uint8_t* rzmask, int npat, double* lds,
+                          int bi, int Z) {
+        H = H_;
+        WR = kResidPlaneRows + 2 * H;
+        WP = WR / 2;
+        tid = threadIdx.x;
+        P = P_;
+        n = n_;
+        ld = ld_;
+        const int64_t nxy = (P + kResidPlaneRows - 1) / kResidPlaneRows;
+        const int64_t nz = (n + P - 1) / P;
+        xy0 = (bi % nxy) * kResidPlaneRows;
+        z0 = (bi / nxy) * Z;
+        zend = (int)(nz - z0 < Z ? nz - z0 : Z);
+        lr = 2 * tid;
+        wi = lr + H;
+        in0 = xy0 + lr < P;
+        in1 = xy0 + lr + 1 < P;
+        win = lds;
+        keys = reinterpret_cast<uint32_t*>(win + 3 * WR);
+        s_rz = reinterpret_cast<double*>(keys + 3 * KD);
+        s_rm = reinterpret_cast<uint8_t*>(s_rz + (CU ? 0 : npat * MAXLEN));
+        if (!CU) {
+            for (int i = tid; i < npat * MAXLEN; i += 256) s_rz[i] = rzval[i];
+            for (int i = tid; i < npat; i += 256) s_rm[i] = rzmask[i];
+        }
+        rx = rsrc(x, ld * 8);
+        // the key arrays carry >= 4 zero bytes past the rows (upload_matrix), so
+        // every aligned dword load that reaches a real row lies inside
+        rk = CU ? rsrc(rowmask, (n + 7) & ~(int64_t)3) : rsrc(pat, (2 * n + 7) & ~(int64_t)3);
+    }
+    // x[row .. row + 1]; rows outside the column read 0.  A load that
+    // straddles the descriptor's end returns 0 as a whole (measured), so the
+    // column's last row is loaded on its own.
+    __device__ double2 ld2(int64_t row) const {
+        if (row == ld - 1) {
+            const u2 w = __builtin_amdgcn_raw_buffer_load_b64(rx, (int)(row * 8), 0, 0);
+            return make_double2(__builtin_bit_cast(double, ((uint64_t)w.y << 32) | w.x), 0.0);
+        }
+        const uint32_t off = row >= 0 && row < ld ? (uint32_t)(row * 8) : 0xFFFFFFF0u;
+        const u4 w = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)off, 0, 0);
+        return make_double2(__builtin_bit_cast(double, ((uint64_t)w.y << 32) | w.x),
+                            __builtin_bit_cast(double, ((uint64_t)w.w << 32) | w.z));
+    }
+    // issue plane z's loads (window + keys) into registers
+    __device__ void load(int64_t z) {
+        const int64_t g = z * P + xy0 - H;
+#pragma unroll
+        for (int k = 0; k < LPT; ++k) {
+            const int pi = tid + 256 * k;
+            if (pi < WP) st[k] = ld2(g + 2 * pi);
+        }
+        const int64_t al = ((z * P + xy0) * KB) & ~(int64_t)3;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int d = tid + 256 * k;
+            kst[k] = d < KD ? __builtin_amdgcn_raw_buffer_load_b32(rk, (int)(al + 4 * (int64_t)d), 0, 0) : 0u;
+        }
+    }
+    __device__ void store(int b) {
+#pragma unroll
+        for (int k = 0; k < LPT; ++k) {
+            const int pi = tid + 256 * k;
+            if (pi < WP) {
+                win[b * WR + 2 * pi] = st[k].x;
+                win[b * WR + 2 * pi + 1] = st[k].y;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int d = tid + 256 * k;
+            if (d < KD) keys[b * KD + d] = kst[k];
+        }
+    }
+    // the lane's two row keys of plane z (buffer b)
+    __device__ void row_keys(int b, int64_t z, unsigned& k0, unsigned& k1) const {
+        const int kofs = (int)(((z * P + xy0) * KB) & 3);
+        const uint8_t* kp = reinterpret_cast<const uint8_t*>(keys + b * KD) + kofs + lr * KB;
+        if (CU) {
+            k0 = kp[0];
+            k1 = kp[1];
+        } else {
+            k0 = *reinterpret_cast<const uint16_t*>(kp);
+            k1 = *reinterpret_cast<const uint16_t*>(kp + 2);
+        }
+    }
+    __device__ double2 slot(int b, int bn, int e, const double2& xp) const {
+        if (e == 0) return xp;
+        if (e == MAXLEN - 1) return make_double2(win[bn * WR + wi], win[bn * WR + wi + 1]);
+        const int i = b * WR + wi + ps[e];
+        return make_double2(win[i], win[i + 1]);
+    }
+    __device__ double coef(unsigned key, int e) const {  // the row's value at slot e, 0 where it has none
+        if (CU) return ((key >> e) & 1u) ? cv[e] : 0.0;
+        return s_rz[key * MAXLEN + e];
+    }
+    __device__ unsigned mask(unsigned key) const { return CU ? key : s_rm[key]; }
+};
+
+#define CAL_PLANE_MARCH(PM, XPTR, Zv)                                                                          \
+    PlaneMarch<MAXLEN, CU> PM(a.plane_P, a.plane_H, a.n, a.ld, XPTR, a.rowmask, a.pat, a.rzval, a.rzmask, a.npat, \
+                              lds_plane, xcd_remap(blockIdx.x, gridDim.x), Zv);                               \
+    _Pragma("unroll") for (int e_ = 0; e_ < MAXLEN; ++e_) {                                                   \
+        PM.ps[e_] = a.pslot[e_];                                                                              \
+        PM.cv[e_] = a.cval[e_];                                                                               \
+    }
+
+// SpMV (with the Newton shift) on the plane march: each row adds its own
+// entries in canonical (= column) order, selected by its slot mask (an entry
+// the row does not have is skipped, not multiplied by zero, so non-finite x
+// values outside a row cannot leak into it): bit-identical to k_spmv /
+// k_spmv_pair.  One 16-B store per row pair (8-B aligned on the odd planes
+// of an odd P).
+__device__ __forceinline__ void st16(double* p, double2 v) { __builtin_memcpy(p, &v, 16); }
+
+template <int MODE, int MAXLEN, int Z, bool CU>
+__global__ __launch_bounds__(256) void k_spmv_planes(PatArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double lds_plane[];
+    CAL_PLANE_MARCH(pm, a.x, Z)
+    double2 xp = pm.ld2((pm.z0 - 1) * pm.P + pm.xy0 + pm.lr);
+    pm.load(pm.z0);
+    pm.store(0);
+    pm.load(pm.z0 + 1);
+    pm.store(1);
+    __syncthreads();
+    for (int z = 0; z < pm.zend; ++z) {
+        const int bc = z % 3, bn = (z + 1) % 3, bs = (z + 2) % 3;
+        if (z + 2 <= pm.zend) pm.load(pm.z0 + z + 2);
+        const int64_t r = (pm.z0 + z) * pm.P + pm.xy0 + pm.lr;
+        const bool v0 = pm.in0 && r < pm.n, v1 = pm.in1 && r + 1 < pm.n;
+        unsigned k0, k1;
+        pm.row_keys(bc, pm.z0 + z, k0, k1);
+        const unsigned m0 = pm.mask(k0), m1 = pm.mask(k1);
+        const double2 xc = make_double2(pm.win[bc * pm.WR + pm.wi], pm.win[bc * pm.WR + pm.wi + 1]);
+        double y0 = 0.0, y1 = 0.0;
+#pragma unroll
+        for (int e = 0; e < MAXLEN; ++e) {
+            const double2 v = pm.slot(bc, bn, e, xp);
+            const double t0 = pm.coef(k0, e) * v.x, t1 = pm.coef(k1, e) * v.y;
+            double s0 = y0 + t0, s1 = y1 + t1;
+            asm volatile("" : "+v"(s0), "+v"(s1));
+            y0 = ((m0 >> e) & 1u) ? s0 : y0;
+            y1 = ((m1 >> e) & 1u) ? s1 : y1;
+        }
+        if (MODE != 0) {
+            const double u0 = a.shift * xc.x, u1 = a.shift * xc.y;
+            y0 = y0 - u0;
+            y1 = y1 - u1;
+            if (MODE == 2) {
+                const double q0 = a.xprev[v0 ? r : 0], q1 = a.xprev[v1 ? r + 1 : 0];
+                const double w0 = a.im2 * q0, w1 = a.im2 * q1;
+                y0 = y0 + w0;
+                y1 = y1 + w1;
+            }
+        }
+        if (v0 && v1) st16(a.y + r, make_double2(y0, y1));
+        else if (v0) a.y[r] = y0;
+        xp = xc;
+        if (z + 2 <= pm.zend) pm.store(bs);
+        __syncthreads();
+    }
+}
+
+// the plane march applies to a whole single slab (pat_args sets the tables)
+static bool planes_ok(const PatArgs& a) {
+    return a.rzval && a.rzmask && a.plane_P >= 256 && a.plane_H <= 512 && a.pmaxlen >= 2 && a.pmaxlen <= 8 &&
+           a.pcanon && a.gap == 0 && a.xlo == 0 && a.ld * 8 < ((int64_t)1 << 31) && a.n * 2 < ((int64_t)1 << 31) &&
+           (!a.cuniform || a.rowmask);
+}
+static int planes_blocks(const PatArgs& a, int Z) {
+    const int64_t nxy = (a.plane_P + kResidPlaneRows - 1) / kResidPlaneRows;
+    const int64_t nz = (a.n + a.plane_P - 1) / a.plane_P;
+    return (int)(nxy * ((nz + Z - 1) / Z));
+}
+
+// CAL_SPMV_PLANES = 0 (off) / 8 / 16 / 32 planes per block while tuning
+static int spmv_planes_z() {
+    static const int z = [] {
+        const char* e = std::getenv("CAL_SPMV_PLANES");
+        const int v = e ? std::atoi(e) : 16;
+        return v == 0 || v == 8 || v == 32 ? v : 16;
+    }();
+    return z;
+}
+
+template <int MODE>
+static hipError_t launch_spmv_planes(const PatArgs& a, hipStream_t st) {
+    const int Zc = spmv_planes_z();
+    auto go = [&](auto zc, auto cu) {
+        constexpr int Z = decltype(zc)::value;
+        constexpr bool CU = decltype(cu)::value;
+        dim3 g((unsigned)planes_blocks(a, Z)), b(256);
+#define CAL_SPL(ML) \
+    hipLaunchKernelGGL((k_spmv_planes<MODE, ML, Z, CU>), g, b, (PlaneMarch<ML, CU>::lds_bytes(a)), st, a)
+        switch (a.pmaxlen) {
+            case 2: CAL_SPL(2); break;
+            case 3: CAL_SPL(3); break;
+            case 4: CAL_SPL(4); break;
+            case 5: CAL_SPL(5); break;
+            case 6: CAL_SPL(6); break;
+            case 7: CAL_SPL(7); break;
+            default: CAL_SPL(8); break;
+        }
+#undef CAL_SPL
+    };
+    auto gz = [&](auto zc) {
+        if (a.cuniform) go(zc, std::true_type{});
+        else go(zc, std::false_type{});
+    };
+    if (Zc == 8) gz(std::integral_constant<int, 8>{});
+    else if (Zc == 32) gz(std::integral_constant<int, 32>{});
+    else gz(std::integral_constant<int, 16>{});
+    return hipGetLastError();
+}
 template <int MODE>
 static hipError_t launch_pat_mode(const PatArgs& a, hipStream_t st) {
+    if (spmv_planes_z() != 0 && planes_ok(a)) return launch_spmv_planes<MODE>(a, st);
     const size_t lds = (size_t)a.npat * 8 + (size_t)a.nent * 12 + 16;
     const size_t lds2 = (size_t)a.npent * 20 + (size_t)a.nppat * 8 + 16;
     if (spmv_pat_pair_path(a)) {
@@ -845,6 +1158,66 @@ __global__ __launch_bounds__(256) void k_resid_pairs(PatArgs a, const uint16_t* 
     }
 }
 
+// Ritz residual partials on the plane march (the geometry above): one Ritz
+// pair per block row (blockIdx.y), kResidPlanes planes per block.  The slot
+// values come zeroed where a row has no entry, so every slot is a plain
+// multiply-add: a row's sum gains +-0 terms only where the reference adds
+// nothing, which leaves its bits unchanged (x finite, as k_resid_pairs).
+template <int MAXLEN, bool CU>
+__global__ __launch_bounds__(256) void k_resid_planes(PatArgs a, const double* __restrict__ X, int64_t ldx,
+                                                     const int* __restrict__ col, const double* __restrict__ lam,
+                                                     const int* __restrict__ out, double* __restrict__ partial,
+                                                     int64_t pstride) {
+    extern __shared__ __attribute__((aligned(16))) double lds_plane[];
+    __shared__ double ws[2][4];
+    const int i = blockIdx.y;
+    CAL_PLANE_MARCH(pm, X + (int64_t)col[i] * ldx, kResidPlanes)
+    const double l = lam[i];
+    double2 xp = pm.ld2((pm.z0 - 1) * pm.P + pm.xy0 + pm.lr);
+    pm.load(pm.z0);
+    pm.store(0);
+    pm.load(pm.z0 + 1);
+    pm.store(1);
+    __syncthreads();
+    double num = 0.0, den = 0.0;
+    for (int z = 0; z < pm.zend; ++z) {
+        const int bc = z % 3, bn = (z + 1) % 3, bs = (z + 2) % 3;
+        if (z + 2 <= pm.zend) pm.load(pm.z0 + z + 2);
+        const int64_t r = (pm.z0 + z) * pm.P + pm.xy0 + pm.lr;
+        const bool v0 = pm.in0 && r < pm.n, v1 = pm.in1 && r + 1 < pm.n;
+        unsigned k0, k1;
+        pm.row_keys(bc, pm.z0 + z, k0, k1);
+        const double2 xc = make_double2(pm.win[bc * pm.WR + pm.wi], pm.win[bc * pm.WR + pm.wi + 1]);
+        double y0 = 0.0, y1 = 0.0;
+#pragma unroll
+        for (int e = 0; e < MAXLEN; ++e) {
+            const double2 v = pm.slot(bc, bn, e, xp);
+            const double t0 = pm.coef(k0, e) * v.x, t1 = pm.coef(k1, e) * v.y;
+            y0 = y0 + t0;
+            y1 = y1 + t1;
+        }
+        const double u0 = l * xc.x, u1 = l * xc.y;
+        y0 = y0 - u0;
+        y1 = y1 - u1;
+        num = num + ((v0 ? y0 * y0 : 0.0) + (v1 ? y1 * y1 : 0.0));
+        den = den + ((v0 ? u0 * u0 : 0.0) + (v1 ? u1 * u1 : 0.0));
+        xp = xc;
+        if (z + 2 <= pm.zend) pm.store(bs);
+        __syncthreads();
+    }
+    num = wave_sum(num);
+    den = wave_sum(den);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+        ws[0][wave] = num;
+        ws[1][wave] = den;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2)
+        partial[(2 * (int64_t)out[i] + threadIdx.x) * pstride + blockIdx.x] =
+            ((ws[threadIdx.x][0] + ws[threadIdx.x][1]) + ws[threadIdx.x][2]) + ws[threadIdx.x][3];
+}
+
 // the batched residual kernel's shape: Ritz pairs per block, row pairs per
 // thread (CAL_RESID_SHAPE=<cpb>x<ppt> for A/B while tuning)
 static void resid_shape(int* cpb, int* ppt) {
@@ -862,6 +1235,7 @@ static void resid_shape(int* cpb, int* ppt) {
 int spmv_pair_resid_multi_blocks(const PatArgs& a) {
     const int nb = spmv_pair_resid_blocks(a);
     if (nb <= 0) return 0;
+    if (planes_ok(a)) return planes_blocks(a, kResidPlanes);
     int cpb, ppt;
     resid_shape(&cpb, &ppt);
     return (nb + ppt - 1) / ppt;
@@ -876,6 +1250,28 @@ hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64
     if (a.pmaxlen > 8 || !a.pcanon) return hipErrorInvalidValue;
     // 32-bit slot offsets: the column's range must fit the descriptor
     if ((a.xhi - a.xlo) * 8 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+    if (planes_ok(a)) {
+        auto go = [&](auto cu) {
+            constexpr bool CU = decltype(cu)::value;
+            dim3 g(blocks, npr), bl(256);
+#define CAL_RPL(ML)                                                                                         \
+    hipLaunchKernelGGL((k_resid_planes<ML, CU>), g, bl, (PlaneMarch<ML, CU>::lds_bytes(a)), st, a, X, ldx, col, \
+                       lam, out, partial, pstride)
+            switch (a.pmaxlen) {
+                case 2: CAL_RPL(2); break;
+                case 3: CAL_RPL(3); break;
+                case 4: CAL_RPL(4); break;
+                case 5: CAL_RPL(5); break;
+                case 6: CAL_RPL(6); break;
+                case 7: CAL_RPL(7); break;
+                default: CAL_RPL(8); break;
+            }
+#undef CAL_RPL
+        };
+        if (a.cuniform) go(std::true_type{});
+        else go(std::false_type{});
+        return hipGetLastError();
+    }
     int cpb, ppt;
     resid_shape(&cpb, &ppt);
     const size_t lds = (size_t)a.npent * 16 + 16;

@@ -17,8 +17,15 @@ namespace cal {
 constexpr int kRowBlockRows = 256;   // rows per CSR-stream block (= threads)
 constexpr int kRowBlockNnz = 2048;   // nonzeros staged in LDS per block
 
+// A library-owned worker thread (the host-staged overlap schedule's comm
+// thread) points this at its own string, so it never writes the context's
+// error state concurrently with the caller's thread; the caller moves the
+// message into the context after the join.
+static thread_local std::string* tl_err_sink = nullptr;
+
 int set_error(cal_ctx* c, int code, const std::string& msg) {
-    if (c) c->err = msg;
+    if (tl_err_sink) *tl_err_sink = msg;
+    else if (c) c->err = msg;
     return code;
 }
 
@@ -163,6 +170,9 @@ static void free_matrix(cal_ctx* c) {
     if (A.ppinfo) hipFree(A.ppinfo);
     if (A.ppoff) hipFree(A.ppoff);
     if (A.ppval) hipFree(A.ppval);
+    if (A.rzval) hipFree(A.rzval);
+    if (A.rzmask) hipFree(A.rzmask);
+    if (A.rowmask) hipFree(A.rowmask);
     A = DevMatrix();
     if (c->d_work) hipFree(c->d_work);
     c->d_work = nullptr;
@@ -365,7 +375,9 @@ int upload_matrix(cal_ctx* c, int64_t n_rows, int64_t ext_off, int64_t n_local, 
             A.npat = (int)pinfo.size();
             A.nent = (int)pdelta.size();
             A.maxlen = mx <= 8 ? std::max(mx, 1) : (mx <= 16 ? 16 : 32);
-            CAL_HIP(c, hipMalloc((void**)&A.pat, n_rows * sizeof(uint16_t)));
+            // 8 zero bytes past the ids: the plane march's aligned dword key loads
+            CAL_HIP(c, hipMalloc((void**)&A.pat, n_rows * sizeof(uint16_t) + 8));
+            CAL_HIP(c, hipMemset(A.pat, 0, n_rows * sizeof(uint16_t) + 8));
             CAL_HIP(c, hipMalloc((void**)&A.pinfo, pinfo.size() * sizeof(int2)));
             CAL_HIP(c, hipMalloc((void**)&A.pdelta, pdelta.size() * sizeof(int)));
             CAL_HIP(c, hipMalloc((void**)&A.pval, pval.size() * sizeof(double)));
@@ -395,6 +407,56 @@ int upload_matrix(cal_ctx* c, int64_t n_rows, int64_t ext_off, int64_t n_local, 
                 CAL_HIP(c, hipMemcpy(A.ppinfo, ppinfo.data(), ppinfo.size() * sizeof(int2), hipMemcpyHostToDevice));
                 CAL_HIP(c, hipMemcpy(A.ppoff, ppoff.data(), ppoff.size() * sizeof(int), hipMemcpyHostToDevice));
                 CAL_HIP(c, hipMemcpy(A.ppval, ppval.data(), ppval.size() * sizeof(double), hipMemcpyHostToDevice));
+                // the plane march (k_resid_planes): a single slab without halos whose
+                // canonical slots include -P and +P (the largest offset) and whose
+                // other slots reach H <= 512 rows: lap3d (P = N^2, H = N + 1) and
+                // lap2d (P = N, H = 2) qualify
+                const int L = A.pmaxlen;
+                if (A.pcanon && L >= 2 && ext_off == 0 && n_rows == n_local && A.lpad == 0 &&
+                    A.pslot[L - 1] >= 256 && A.pslot[0] == -A.pslot[L - 1] && (size_t)A.npat * L <= 2048) {
+                    int H = 0;
+                    for (int e = 1; e < L - 1; ++e) H = std::max(H, std::abs(A.pslot[e]));
+                    H = (H + 1) & ~1;
+                    if (H <= 512) {
+                        std::vector<double> rz((size_t)A.npat * L, 0.0);
+                        std::vector<uint8_t> rm((size_t)A.npat, 0);
+                        for (int q = 0; q < A.npat; ++q)
+                            for (int e = 0; e < pinfo[q].y; ++e) {
+                                const int o = pdelta[pinfo[q].x + e];
+                                for (int k = 0; k < L; ++k)
+                                    if (A.pslot[k] == o) {
+                                        rz[(size_t)q * L + k] = pval[pinfo[q].x + e];
+                                        rm[q] |= (uint8_t)(1u << k);
+                                    }
+                            }
+                        CAL_HIP(c, hipMalloc((void**)&A.rzval, rz.size() * sizeof(double)));
+                        CAL_HIP(c, hipMemcpy(A.rzval, rz.data(), rz.size() * sizeof(double), hipMemcpyHostToDevice));
+                        CAL_HIP(c, hipMalloc((void**)&A.rzmask, rm.size()));
+                        CAL_HIP(c, hipMemcpy(A.rzmask, rm.data(), rm.size(), hipMemcpyHostToDevice));
+                        // uniform slot values: one value per slot over every pattern that has it
+                        bool uni = true;
+                        for (int k = 0; k < L && uni; ++k) {
+                            bool seen = false;
+                            for (int q = 0; q < A.npat && uni; ++q)
+                                if (rm[q] >> k & 1u) {
+                                    const double v = rz[(size_t)q * L + k];
+                                    if (!seen) A.cval[k] = v;
+                                    else uni = std::memcmp(&v, &A.cval[k], 8) == 0;
+                                    seen = true;
+                                }
+                        }
+                        if (uni) {
+                            std::vector<uint8_t> rowm((size_t)n_rows);
+                            for (int64_t r = 0; r < n_rows; ++r) rowm[(size_t)r] = rm[pat[(size_t)r]];
+                            rowm.resize((size_t)n_rows + 8, 0);  // zero bytes past the rows (dword key loads)
+                            CAL_HIP(c, hipMalloc((void**)&A.rowmask, rowm.size()));
+                            CAL_HIP(c, hipMemcpy(A.rowmask, rowm.data(), rowm.size(), hipMemcpyHostToDevice));
+                            A.cuniform = true;
+                        }
+                        A.plane_P = A.pslot[L - 1];
+                        A.plane_H = H;
+                    }
+                }
             }
         } else if (c->spmv_format == 2) {
             return set_error(c, CAL_ERR_UNSUPPORTED, "row-pattern format requested but the matrix has too many "
@@ -464,6 +526,16 @@ static PatArgs pat_args(const DevMatrix& A, int64_t o, int64_t len, const double
     }
     p.xlo = -(A.lpad + d);
     p.xhi = A.ld - (A.lpad + d);
+    p.ld = A.ld;
+    if (A.rzval && o == A.ext_off && len == A.n_local) {
+        p.rzval = A.rzval;
+        p.rzmask = A.rzmask;
+        p.rowmask = A.rowmask;
+        p.cuniform = A.cuniform ? 1 : 0;
+        for (int k = 0; k < 8; ++k) p.cval[k] = A.cval[k];
+        p.plane_P = A.plane_P;
+        p.plane_H = A.plane_H;
+    }
     return p;
 }
 
@@ -649,6 +721,7 @@ int powers_dev(cal_ctx* c, int s, const double* q, double* const* Y, const doubl
     // recorded before a stream can wait for it).
     std::thread comm_thread;
     int comm_status = 0;
+    std::string comm_err;
     if (comm_stream) {
         CAL_HIP(c, hipEventRecord(m->ev_q, c->stream));
         CAL_HIP(c, hipStreamWaitEvent(m->stream, m->ev_q, 0));
@@ -656,11 +729,13 @@ int powers_dev(cal_ctx* c, int s, const double* q, double* const* Y, const doubl
             CAL_TRY(halo_exchange_deep(c, const_cast<double*>(q), s, m->stream));
             CAL_HIP(c, hipEventRecord(m->ev_halo, m->stream));
         } else {
-            comm_thread = std::thread([c, m, q, s, &comm_status]() {
+            comm_thread = std::thread([c, m, q, s, &comm_status, &comm_err]() {
+                tl_err_sink = &comm_err;
                 hipSetDevice(c->device);
                 comm_status = halo_exchange_deep(c, const_cast<double*>(q), s, m->stream);
                 if (comm_status == 0 && hipEventRecord(m->ev_halo, m->stream) != hipSuccess)
                     comm_status = set_error(c, CAL_ERR_HIP, "halo event record");
+                tl_err_sink = nullptr;
             });
         }
     } else if (mpk) {
@@ -671,7 +746,7 @@ int powers_dev(cal_ctx* c, int s, const double* q, double* const* Y, const doubl
         interior_status = launch(j, stored_range(A, ilo(j), ihi(j)), PowRange{0, 0});
     if (comm_thread.joinable()) comm_thread.join();
     CAL_TRY(interior_status);
-    CAL_TRY(comm_status);
+    if (comm_status != 0) return set_error(c, comm_status, comm_err);
     if (comm_stream) CAL_HIP(c, hipStreamWaitEvent(c->stream, m->ev_halo, 0));
     for (int j = 1; j <= s; ++j) {
         const PowRange lo = dep_lo ? stored_range(A, glo(j), ilo(j)) : PowRange{0, 0};

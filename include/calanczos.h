@@ -255,7 +255,13 @@ int cal_impl_restarted_ca_lanczos(cal_ctx* ctx, const double* r, int max_lanczos
 int cal_comm_unique_id(void* id128);
 int cal_comm_init_rccl(cal_ctx* ctx, int nranks, int rank, const void* id128);
 /* Host-staged communicator (tests, CPU rendezvous): device buffers are
- * staged through pinned host memory and handed to these callbacks. */
+ * staged through pinned host memory and handed to these callbacks.  The
+ * callbacks run on the caller's thread, except with the opt-in overlapped
+ * matrix-powers schedule (environment CAL_MPK_OVERLAP=1, a rehearsal of the
+ * RCCL schedule): there the exchange callback runs on a library-owned thread
+ * while the caller's thread enqueues the interior powers, so the transport
+ * must allow calls from another thread (MPI_THREAD_MULTIPLE or
+ * MPI_THREAD_SERIALIZED with no concurrent use by the caller). */
 typedef int (*cal_allreduce_fn)(void* user, double* buf, int64_t count);
 typedef int (*cal_exchange_fn)(void* user, int peer, const double* send, int64_t nsend, double* recv,
                                int64_t nrecv);
