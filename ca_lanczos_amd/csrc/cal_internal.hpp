@@ -121,9 +121,11 @@ struct PatArgs {
     // the matrix has no plane structure for it
     const double* rzval = nullptr;
     const uint8_t* rzmask = nullptr;  // bit e: the row pattern has an entry at slot e
+    // the row pattern ids as bytes (npat <= 256; the plane march's keys)
+    const uint8_t* rowkey8 = nullptr;
     // uniform slot values (every row with an entry at slot e has the value
     // cval[e], as in the Laplacians): the plane march keys each row by its
-    // slot mask byte (rowmask, one per row) instead of its pattern id
+    // slot mask byte (rowmask) and takes the values from cval
     const uint8_t* rowmask = nullptr;
     int cuniform = 0;
     double cval[8] = {};
@@ -181,6 +183,7 @@ struct DevMatrix {
     // plane-march residual table (PatArgs::rzval; single rank, no halos)
     double* rzval = nullptr;
     uint8_t* rzmask = nullptr;
+    uint8_t* rowkey8 = nullptr;
     uint8_t* rowmask = nullptr;
     bool cuniform = false;
     double cval[8] = {};

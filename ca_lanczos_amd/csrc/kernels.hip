@@ -165,16 +165,6 @@ __global__ __launch_bounds__(kSpmvThreads) void k_spmv(SpmvArgs a) {
     }
 }
 
-// CAL_SPMV_CSR = <nt><v> while tuning: "00" plain, "10" non-temporal, "02"
-// two nonzeros per thread, "12" both
-static int spmv_csr_variant() {
-    static const int v = [] {
-        const char* e = std::getenv("CAL_SPMV_CSR");
-        return e ? std::atoi(e) : 0;
-    }();
-    return v;
-}
-
 template <int MODE, bool NT, int V>
 static hipError_t launch_spmv_mode2(const SpmvArgs& a, int nit, hipStream_t st) {
     dim3 g(a.nblk), b(kSpmvThreads);
@@ -191,14 +181,12 @@ static hipError_t launch_spmv_mode2(const SpmvArgs& a, int nit, hipStream_t st) 
     return hipGetLastError();
 }
 
+// plain loads, one nonzero per thread and iteration: non-temporal col / val
+// loads measured 200 vs 208 us on lap3d_215 in CSR but 31.5 vs 23.0 us on
+// circuit_1259, two nonzeros per thread slower on both (profiles/r04/csr_variants)
 template <int MODE>
 static hipError_t launch_spmv_mode(const SpmvArgs& a, int nit, hipStream_t st) {
-    switch (spmv_csr_variant()) {
-        case 10: return launch_spmv_mode2<MODE, true, 1>(a, nit, st);
-        case 2: return launch_spmv_mode2<MODE, false, 2>(a, nit, st);
-        case 12: return launch_spmv_mode2<MODE, true, 2>(a, nit, st);
-        default: return launch_spmv_mode2<MODE, false, 1>(a, nit, st);
-    }
+    return launch_spmv_mode2<MODE, false, 1>(a, nit, st);
 }
 
 hipError_t launch_spmv(const SpmvArgs& a0, hipStream_t st) {
@@ -613,41 +601,56 @@ bool spmv_pat_pair_path(const PatArgs& a) {
 // +P, P >= 256) whose inner slots reach H <= 512 rows -- the 7-point (P =
 // N^2) and 5-point (P = N) Laplacians -- on a single slab.  A block owns the
 // rows xy0 .. xy0 + 511 of every plane (r = xy + z P) for Z planes.  Per plane
-// it stages into LDS, two planes ahead of their use (three buffers):
+// it stages into LDS:
 //   * the window x[zP + xy0 - H, zP + xy0 + 512 + H) by contiguous 16-B
 //     buffer loads (reads outside the column return 0 from the range check);
-//   * the rows' keys by aligned dword loads: with uniform slot values (cval)
-//     the row's slot mask (PatArgs::rowmask, 1 B), else its pattern id (2 B)
-//     with the value / mask tables staged in LDS once.
-// Each lane then takes its row pair (xy0 + lr, + 1): the inner slots from the
-// window, the -P / +P slots the same lane's centre pair of the previous /
-// next plane (register, next buffer).  Each x value leaves HBM about once
-// ((Z + 2) / Z: a block also stages its neighbours' first / last plane), the
-// in-plane gathers are LDS reads, and every load instruction is issued two
-// planes before its data is needed (tools/resid_probe.hip: 15 us per Ritz
-// pair at n = 215^3 against 25 us for the row-pair gather, 12 us for a bare
-// read of x).  When P is odd the plane's last pair straddles into the next
-// plane: only its first row belongs to the block.
-template <int MAXLEN, bool CU>
+//   * the rows' keys (their pattern ids, 1 B when npat <= 256, else 2 B) by
+//     aligned dword loads;
+// and once per block the pattern table: per pattern its slot values with 0.0
+// where the row has no entry (stride L2 = L rounded up to even), and slot
+// masks.  Each lane takes its row pair (xy0 + lr, + 1): the inner slots from
+// the window, the -P / +P slots the same lane's centre pair of the previous /
+// next plane (register, next buffer), the coefficients by broadcast-friendly
+// 16-B LDS reads of its rows' table rows.  Plane z0 + j is loaded three
+// planes ahead into register set j & 1 and stored to LDS two planes ahead,
+// so every load has a whole plane's work to land.  Each x value leaves HBM
+// about once ((Z + 2) / Z: a block also stages its neighbours' first and
+// last plane) and the in-plane gathers are LDS reads (tools/resid_probe.hip:
+// 15 us per vector at n = 215^3 against 25 us for the row-pair gather and
+// 12 us for a bare read of x).  When P is odd the plane's last pair straddles
+// into the next plane: only its first row belongs to the block.
+//
+// A slot a row has no entry at contributes 0.0 * x: for finite x the running
+// sum (which starts at +0.0 and so is never -0.0) is unchanged, so the sums
+// have the reference's bits.  Each lane also flags non-finite x values it
+// stages; a plane whose window holds one is recomputed with the entries
+// selected by the slot masks, so a non-finite x outside a row never leaks into
+// it (the SpMV's contract, k_spmv_pair).
+// KM = 0: uniform slot values (cval; every row with an entry at slot e has
+// the value cval[e], as in the Laplacians): the keys are the rows' slot mask
+// bytes.  KM = 1 / 2: the keys are the rows' pattern ids (1 / 2 B) into the
+// LDS value / mask tables.
+template <int MAXLEN, int KM>
 struct PlaneMarch {
+    static constexpr int KB = KM == 2 ? 2 : 1;             // key bytes per row
     typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
-    static constexpr int KB = CU ? 1 : 2;             // key bytes per row
-    static constexpr int KD = (512 * KB + 6) / 4 + 1;  // key dwords per plane (with the alignment slack)
+    static constexpr int L2 = (MAXLEN + 1) & ~1;          // table row stride (16-B reads)
+    static constexpr int KD = (512 * KB + 6) / 4 + 1;      // key dwords per plane (with the alignment slack)
     static constexpr int LPT = (kResidPlaneRows + 2 * 512) / 2 / 256;  // window pairs per thread (H <= 512)
     // plain scalars and pointers only: a reference to the by-value kernel
-    // argument would make every thread copy it to scratch
-    int H, WR, WP, tid, lr, wi, zend;
-    int64_t P, n, ld, xy0, z0;
+    // argument would make every thread copy it to scratch; row indices are
+    // 32-bit (planes_ok: ld < 2^28)
+    int H, WR, WP, tid, lr, wi, zend, P, n, ld, xy0, z0, nk;
     bool in0, in1;
     double* win;      // [3][WR]
     uint32_t* keys;   // [3][KD]
-    double* s_rz;     // !CU: npat x MAXLEN values (0 where the row has no entry)
-    uint8_t* s_rm;    // !CU: npat slot masks
+    double* s_rz;     // npat x L2 slot values (0 where the row has no entry)
+    uint8_t* s_rm;    // npat slot masks
     __amdgpu_buffer_rsrc_t rx, rk;
     int ps[MAXLEN];   // slot offsets (compile-time indices only)
-    double cv[MAXLEN];
-    double2 st[LPT];
+    double cv[MAXLEN];  // KM = 0: the slot values
+    unsigned fullm;     // the interior rows' mask (every slot)
+    double2 st[LPT];     // the prefetched plane (registers)
     uint32_t kst[2];
 
     __device__ static __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
@@ -657,91 +660,111 @@ struct PlaneMarch {
         return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0,
                                                  (int)__builtin_amdgcn_readfirstlane((uint32_t)bytes), 0x00020000);
     }
-    __host__ __device__ static size_t lds_bytes(const PatArgs& a) {
-        return (size_t)3 * (kResidPlaneRows + 2 * a.plane_H) * 8 + (size_t)3 * KD * 4 +
-               (CU ? 0 : (size_t)a.npat * MAXLEN * 8 + (size_t)a.npat) + 16;
+    __host__ __device__ static size_t lds_bytes(int H, int npat) {
+        return (size_t)3 * (kResidPlaneRows + 2 * H) * 8 + (size_t)3 * KD * 4 + 16 + (size_t)npat * L2 * 8 +
+               (size_t)npat + 16;
     }
     // the fields are passed one by one from the kernel's by-value PatArgs
-    __device__ PlaneMarch(int64_t P_, int H_, int64_t n_, int64_t ld_, const double* x, const uint8_t* rowmask,
-                          const uint16_t* pat, const double* rzval, const uint8_t* rzmask, int npat, double* lds,
-                          int bi, int Z) {
+    __device__ PlaneMarch(int64_t P_, int H_, int64_t n_, int64_t ld_, const double* x, const void* key,
+                          const double* rzval, const uint8_t* rzmask, int npat, double* lds, int bi, int Z) {
         H = H_;
         WR = kResidPlaneRows + 2 * H;
         WP = WR / 2;
+        nk = (WP + 255) / 256;
         tid = threadIdx.x;
-        P = P_;
-        n = n_;
-        ld = ld_;
-        const int64_t nxy = (P + kResidPlaneRows - 1) / kResidPlaneRows;
-        const int64_t nz = (n + P - 1) / P;
+        P = (int)P_;
+        n = (int)n_;
+        ld = (int)ld_;
+        const int nxy = (P + kResidPlaneRows - 1) / kResidPlaneRows;
+        const int nz = (n + P - 1) / P;
         xy0 = (bi % nxy) * kResidPlaneRows;
         z0 = (bi / nxy) * Z;
-        zend = (int)(nz - z0 < Z ? nz - z0 : Z);
+        zend = nz - z0 < Z ? nz - z0 : Z;
         lr = 2 * tid;
         wi = lr + H;
         in0 = xy0 + lr < P;
         in1 = xy0 + lr + 1 < P;
         win = lds;
         keys = reinterpret_cast<uint32_t*>(win + 3 * WR);
-        s_rz = reinterpret_cast<double*>(keys + 3 * KD);
-        s_rm = reinterpret_cast<uint8_t*>(s_rz + (CU ? 0 : npat * MAXLEN));
-        if (!CU) {
-            for (int i = tid; i < npat * MAXLEN; i += 256) s_rz[i] = rzval[i];
+        s_rz = reinterpret_cast<double*>(keys + 3 * KD + (3 * KD & 1));
+        s_rm = reinterpret_cast<uint8_t*>(s_rz + npat * L2);
+        if (KM != 0) {
+            for (int i = tid; i < npat * L2; i += 256) {
+                const int q = i / L2, e = i % L2;
+                s_rz[i] = e < MAXLEN ? rzval[q * MAXLEN + e] : 0.0;
+            }
             for (int i = tid; i < npat; i += 256) s_rm[i] = rzmask[i];
         }
-        rx = rsrc(x, ld * 8);
+        fullm = (1u << MAXLEN) - 1u;
+        rx = rsrc(x, ld_ * 8);
         // the key arrays carry >= 4 zero bytes past the rows (upload_matrix), so
         // every aligned dword load that reaches a real row lies inside
-        rk = CU ? rsrc(rowmask, (n + 7) & ~(int64_t)3) : rsrc(pat, (2 * n + 7) & ~(int64_t)3);
+        rk = rsrc(key, (KB * n_ + 7) & ~(int64_t)3);
     }
-    // x[row .. row + 1]; rows outside the column read 0.  A load that
-    // straddles the descriptor's end returns 0 as a whole (measured), so the
-    // column's last row is loaded on its own.
-    __device__ double2 ld2(int64_t row) const {
-        if (row == ld - 1) {
-            const u2 w = __builtin_amdgcn_raw_buffer_load_b64(rx, (int)(row * 8), 0, 0);
-            return make_double2(__builtin_bit_cast(double, ((uint64_t)w.y << 32) | w.x), 0.0);
-        }
-        const uint32_t off = row >= 0 && row < ld ? (uint32_t)(row * 8) : 0xFFFFFFF0u;
+    // x[row .. row + 1]; rows outside the column read 0 (the range check).  A
+    // load that straddles the descriptor's end returns 0 as a whole
+    // (measured), so planes_ok requires ld >= n + 2: only padding rows can
+    // straddle.  No branches: a branch around a load makes the compiler wait
+    // for every outstanding load at the join.
+    __device__ double2 ld2(int row) const {
+        const uint32_t off = row >= 0 && row < ld ? (uint32_t)row * 8u : 0xFFFFFFF0u;
         const u4 w = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)off, 0, 0);
         return make_double2(__builtin_bit_cast(double, ((uint64_t)w.y << 32) | w.x),
                             __builtin_bit_cast(double, ((uint64_t)w.w << 32) | w.z));
     }
-    // issue plane z's loads (window + keys) into registers
-    __device__ void load(int64_t z) {
-        const int64_t g = z * P + xy0 - H;
+    // issue plane z's loads (window + keys) into registers: nk uniform rounds
+    // of 256 window pairs, one or two key dwords.  Lanes past the end load
+    // (and later store) the last pair / dword again: the same data to the
+    // same place, and no divergent branch.
+    __device__ void load(int z) {
+        const int g = z * P + xy0 - H;
 #pragma unroll
-        for (int k = 0; k < LPT; ++k) {
-            const int pi = tid + 256 * k;
-            if (pi < WP) st[k] = ld2(g + 2 * pi);
-        }
-        const int64_t al = ((z * P + xy0) * KB) & ~(int64_t)3;
+        for (int k = 0; k < LPT; ++k)
+            if (k < nk) st[k] = ld2(g + 2 * min(tid + 256 * k, WP - 1));
+        const int al = ((z * P + xy0) * KB) & ~3;
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int d = tid + 256 * k;
-            kst[k] = d < KD ? __builtin_amdgcn_raw_buffer_load_b32(rk, (int)(al + 4 * (int64_t)d), 0, 0) : 0u;
-        }
+        for (int k = 0; k < 2; ++k)
+            if (256 * k < KD)
+                kst[k] = __builtin_amdgcn_raw_buffer_load_b32(rk, al + 4 * min(tid + 256 * k, KD - 1), 0, 0);
     }
+    // the prefetched plane into LDS buffer b
     __device__ void store(int b) {
 #pragma unroll
         for (int k = 0; k < LPT; ++k) {
-            const int pi = tid + 256 * k;
-            if (pi < WP) {
-                win[b * WR + 2 * pi] = st[k].x;
-                win[b * WR + 2 * pi + 1] = st[k].y;
+            if (k < nk) {
+                const int pi = min(tid + 256 * k, WP - 1);
+                *reinterpret_cast<double2*>(win + b * WR + 2 * pi) = st[k];
             }
         }
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int d = tid + 256 * k;
-            if (d < KD) keys[b * KD + d] = kst[k];
+        for (int k = 0; k < 2; ++k)
+            if (256 * k < KD) keys[b * KD + min(tid + 256 * k, KD - 1)] = kst[k];
+    }
+    // The march (tools/resid_probe.hip's schedule): plane z0 + j + 2 is loaded
+    // into registers at the top of step j, the step computes plane z0 + j
+    // from LDS, then stores the prefetched plane into buffer (j + 2) % 3 and
+    // synchronizes.  Latency is hidden by occupancy (the kernels stay within
+    // 64 VGPRs: 8 waves per SIMD).  f(j, bc, bn) computes plane z0 + j from
+    // buffers bc (current) and bn (next).
+    template <typename F>
+    __device__ void march(F&& f) {
+        load(z0);
+        store(0);
+        load(z0 + 1);
+        store(1);
+        __syncthreads();
+        for (int j = 0; j < zend; ++j) {
+            if (j + 2 <= zend) load(z0 + j + 2);
+            f(j, j % 3, (j + 1) % 3);
+            if (j + 2 <= zend) store((j + 2) % 3);
+            __syncthreads();
         }
     }
     // the lane's two row keys of plane z (buffer b)
-    __device__ void row_keys(int b, int64_t z, unsigned& k0, unsigned& k1) const {
-        const int kofs = (int)(((z * P + xy0) * KB) & 3);
+    __device__ void row_keys(int b, int z, unsigned& k0, unsigned& k1) const {
+        const int kofs = ((z * P + xy0) * KB) & 3;
         const uint8_t* kp = reinterpret_cast<const uint8_t*>(keys + b * KD) + kofs + lr * KB;
-        if (CU) {
+        if (KB == 1) {
             k0 = kp[0];
             k1 = kp[1];
         } else {
@@ -749,64 +772,74 @@ struct PlaneMarch {
             k1 = *reinterpret_cast<const uint16_t*>(kp + 2);
         }
     }
+    // y0 / y1: the slot sums of the lane's two rows (A x of plane b; xp the
+    // previous plane's centre pair), each row's own entries in slot (=
+    // column) order.  A wave whose rows all have every slot (the interior,
+    // wave-uniform test) adds every product; otherwise each entry is selected
+    // by the row's mask -- skipped, not multiplied by zero, so a non-finite x
+    // outside a row never leaks into it.  Bit-identical to k_spmv_pair.
+    __device__ void sums(int b, int bn, const double2& xp, unsigned k0, unsigned k1, double& y0, double& y1) const {
+        const unsigned m0 = KM == 0 ? k0 : s_rm[k0], m1 = KM == 0 ? k1 : s_rm[k1];
+        const double* c0 = s_rz + (KM == 0 ? 0 : k0 * L2);
+        const double* c1 = s_rz + (KM == 0 ? 0 : k1 * L2);
+        const bool interior = __builtin_amdgcn_ballot_w64((m0 & m1) != fullm) == 0;
+        y0 = 0.0;
+        y1 = 0.0;
+        if (interior) {
+#pragma unroll
+            for (int e = 0; e < MAXLEN; ++e) {
+                const double2 v = slot(b, bn, e, xp);
+                const double t0 = (KM == 0 ? cv[e] : c0[e]) * v.x, t1 = (KM == 0 ? cv[e] : c1[e]) * v.y;
+                y0 = y0 + t0;
+                y1 = y1 + t1;
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < MAXLEN; ++e) {
+                const double2 v = slot(b, bn, e, xp);
+                const double t0 = (KM == 0 ? cv[e] : c0[e]) * v.x, t1 = (KM == 0 ? cv[e] : c1[e]) * v.y;
+                double s0 = y0 + t0, s1 = y1 + t1;
+                asm volatile("" : "+v"(s0), "+v"(s1));
+                y0 = ((m0 >> e) & 1u) ? s0 : y0;
+                y1 = ((m1 >> e) & 1u) ? s1 : y1;
+            }
+        }
+    }
     __device__ double2 slot(int b, int bn, int e, const double2& xp) const {
         if (e == 0) return xp;
         if (e == MAXLEN - 1) return make_double2(win[bn * WR + wi], win[bn * WR + wi + 1]);
-        const int i = b * WR + wi + ps[e];
-        return make_double2(win[i], win[i + 1]);
+        return make_double2(win[b * WR + wi + ps[e]], win[b * WR + wi + ps[e] + 1]);
     }
-    __device__ double coef(unsigned key, int e) const {  // the row's value at slot e, 0 where it has none
-        if (CU) return ((key >> e) & 1u) ? cv[e] : 0.0;
-        return s_rz[key * MAXLEN + e];
-    }
-    __device__ unsigned mask(unsigned key) const { return CU ? key : s_rm[key]; }
 };
 
 #define CAL_PLANE_MARCH(PM, XPTR, Zv)                                                                          \
-    PlaneMarch<MAXLEN, CU> PM(a.plane_P, a.plane_H, a.n, a.ld, XPTR, a.rowmask, a.pat, a.rzval, a.rzmask, a.npat, \
-                              lds_plane, xcd_remap(blockIdx.x, gridDim.x), Zv);                               \
+    PlaneMarch<MAXLEN, KM> PM(a.plane_P, a.plane_H, a.n, a.ld, XPTR,                                           \
+                              KM == 0 ? (const void*)a.rowmask                                                \
+                                      : (KM == 1 ? (const void*)a.rowkey8 : (const void*)a.pat),              \
+                              a.rzval, a.rzmask, a.npat, lds_plane, xcd_remap(blockIdx.x, gridDim.x), Zv);    \
     _Pragma("unroll") for (int e_ = 0; e_ < MAXLEN; ++e_) {                                                   \
         PM.ps[e_] = a.pslot[e_];                                                                              \
         PM.cv[e_] = a.cval[e_];                                                                               \
     }
 
-// SpMV (with the Newton shift) on the plane march: each row adds its own
-// entries in canonical (= column) order, selected by its slot mask (an entry
-// the row does not have is skipped, not multiplied by zero, so non-finite x
-// values outside a row cannot leak into it): bit-identical to k_spmv /
+// SpMV (with the Newton shift) on the plane march, bit-identical to k_spmv /
 // k_spmv_pair.  One 16-B store per row pair (8-B aligned on the odd planes
 // of an odd P).
 __device__ __forceinline__ void st16(double* p, double2 v) { __builtin_memcpy(p, &v, 16); }
 
-template <int MODE, int MAXLEN, int Z, bool CU>
-__global__ __launch_bounds__(256) void k_spmv_planes(PatArgs a) {
+template <int MODE, int MAXLEN, int Z, int KM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_spmv_planes(PatArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds_plane[];
     CAL_PLANE_MARCH(pm, a.x, Z)
     double2 xp = pm.ld2((pm.z0 - 1) * pm.P + pm.xy0 + pm.lr);
-    pm.load(pm.z0);
-    pm.store(0);
-    pm.load(pm.z0 + 1);
-    pm.store(1);
-    __syncthreads();
-    for (int z = 0; z < pm.zend; ++z) {
-        const int bc = z % 3, bn = (z + 1) % 3, bs = (z + 2) % 3;
-        if (z + 2 <= pm.zend) pm.load(pm.z0 + z + 2);
-        const int64_t r = (pm.z0 + z) * pm.P + pm.xy0 + pm.lr;
+    pm.march([&](int j, int bc, int bn) {
+        const int r = (pm.z0 + j) * pm.P + pm.xy0 + pm.lr;
         const bool v0 = pm.in0 && r < pm.n, v1 = pm.in1 && r + 1 < pm.n;
         unsigned k0, k1;
-        pm.row_keys(bc, pm.z0 + z, k0, k1);
-        const unsigned m0 = pm.mask(k0), m1 = pm.mask(k1);
+        pm.row_keys(bc, pm.z0 + j, k0, k1);
         const double2 xc = make_double2(pm.win[bc * pm.WR + pm.wi], pm.win[bc * pm.WR + pm.wi + 1]);
-        double y0 = 0.0, y1 = 0.0;
-#pragma unroll
-        for (int e = 0; e < MAXLEN; ++e) {
-            const double2 v = pm.slot(bc, bn, e, xp);
-            const double t0 = pm.coef(k0, e) * v.x, t1 = pm.coef(k1, e) * v.y;
-            double s0 = y0 + t0, s1 = y1 + t1;
-            asm volatile("" : "+v"(s0), "+v"(s1));
-            y0 = ((m0 >> e) & 1u) ? s0 : y0;
-            y1 = ((m1 >> e) & 1u) ? s1 : y1;
-        }
+        double y0, y1;
+        pm.sums(bc, bn, xp, k0, k1, y0, y1);
         if (MODE != 0) {
             const double u0 = a.shift * xc.x, u1 = a.shift * xc.y;
             y0 = y0 - u0;
@@ -821,42 +854,36 @@ __global__ __launch_bounds__(256) void k_spmv_planes(PatArgs a) {
         if (v0 && v1) st16(a.y + r, make_double2(y0, y1));
         else if (v0) a.y[r] = y0;
         xp = xc;
-        if (z + 2 <= pm.zend) pm.store(bs);
-        __syncthreads();
-    }
+    });
 }
 
 // the plane march applies to a whole single slab (pat_args sets the tables)
 static bool planes_ok(const PatArgs& a) {
     return a.rzval && a.rzmask && a.plane_P >= 256 && a.plane_H <= 512 && a.pmaxlen >= 2 && a.pmaxlen <= 8 &&
-           a.pcanon && a.gap == 0 && a.xlo == 0 && a.ld * 8 < ((int64_t)1 << 31) && a.n * 2 < ((int64_t)1 << 31) &&
-           (!a.cuniform || a.rowmask);
+           a.pcanon && a.gap == 0 && a.xlo == 0 && a.ld >= a.n + 2 && a.ld < ((int64_t)1 << 28) &&
+           (a.cuniform ? a.rowmask != nullptr : (a.npat > 256 || a.rowkey8));
 }
 static int planes_blocks(const PatArgs& a, int Z) {
     const int64_t nxy = (a.plane_P + kResidPlaneRows - 1) / kResidPlaneRows;
     const int64_t nz = (a.n + a.plane_P - 1) / a.plane_P;
     return (int)(nxy * ((nz + Z - 1) / Z));
 }
-
-// CAL_SPMV_PLANES = 0 (off) / 8 / 16 / 32 planes per block while tuning
-static int spmv_planes_z() {
-    static const int z = [] {
-        const char* e = std::getenv("CAL_SPMV_PLANES");
-        const int v = e ? std::atoi(e) : 16;
-        return v == 0 || v == 8 || v == 32 ? v : 16;
-    }();
-    return z;
+static size_t planes_lds(const PatArgs& a) {  // (the KB = 2 layout bounds both)
+    return PlaneMarch<8, 2>::lds_bytes(a.plane_H, a.npat);
 }
+
+// planes per block of the plane-march SpMV (round 4, lap3d_215 in the loop:
+// 16 -> 40.5 us per SpMV, 32.8 back to back; 8 -> 40.3 / 34.3; 32 -> 47.7 /
+// 42.1; the row-pair kernel 41.4 / 34.5)
+constexpr int kSpmvPlanes = 16;
 
 template <int MODE>
 static hipError_t launch_spmv_planes(const PatArgs& a, hipStream_t st) {
-    const int Zc = spmv_planes_z();
-    auto go = [&](auto zc, auto cu) {
-        constexpr int Z = decltype(zc)::value;
-        constexpr bool CU = decltype(cu)::value;
+    const size_t lds = planes_lds(a);
+    auto go = [&](auto zc, auto km) {
+        constexpr int Z = decltype(zc)::value, KM = decltype(km)::value;
         dim3 g((unsigned)planes_blocks(a, Z)), b(256);
-#define CAL_SPL(ML) \
-    hipLaunchKernelGGL((k_spmv_planes<MODE, ML, Z, CU>), g, b, (PlaneMarch<ML, CU>::lds_bytes(a)), st, a)
+#define CAL_SPL(ML) hipLaunchKernelGGL((k_spmv_planes<MODE, ML, Z, KM>), g, b, lds, st, a)
         switch (a.pmaxlen) {
             case 2: CAL_SPL(2); break;
             case 3: CAL_SPL(3); break;
@@ -869,17 +896,17 @@ static hipError_t launch_spmv_planes(const PatArgs& a, hipStream_t st) {
 #undef CAL_SPL
     };
     auto gz = [&](auto zc) {
-        if (a.cuniform) go(zc, std::true_type{});
-        else go(zc, std::false_type{});
+        if (a.cuniform) go(zc, std::integral_constant<int, 0>{});
+        else if (a.npat <= 256) go(zc, std::integral_constant<int, 1>{});
+        else go(zc, std::integral_constant<int, 2>{});
     };
-    if (Zc == 8) gz(std::integral_constant<int, 8>{});
-    else if (Zc == 32) gz(std::integral_constant<int, 32>{});
-    else gz(std::integral_constant<int, 16>{});
+    gz(std::integral_constant<int, kSpmvPlanes>{});
     return hipGetLastError();
 }
+
 template <int MODE>
 static hipError_t launch_pat_mode(const PatArgs& a, hipStream_t st) {
-    if (spmv_planes_z() != 0 && planes_ok(a)) return launch_spmv_planes<MODE>(a, st);
+    if (planes_ok(a)) return launch_spmv_planes<MODE>(a, st);
     const size_t lds = (size_t)a.npat * 8 + (size_t)a.nent * 12 + 16;
     const size_t lds2 = (size_t)a.npent * 20 + (size_t)a.nppat * 8 + 16;
     if (spmv_pat_pair_path(a)) {
@@ -1159,12 +1186,12 @@ __global__ __launch_bounds__(256) void k_resid_pairs(PatArgs a, const uint16_t* 
 }
 
 // Ritz residual partials on the plane march (the geometry above): one Ritz
-// pair per block row (blockIdx.y), kResidPlanes planes per block.  The slot
-// values come zeroed where a row has no entry, so every slot is a plain
-// multiply-add: a row's sum gains +-0 terms only where the reference adds
-// nothing, which leaves its bits unchanged (x finite, as k_resid_pairs).
-template <int MAXLEN, bool CU>
-__global__ __launch_bounds__(256) void k_resid_planes(PatArgs a, const double* __restrict__ X, int64_t ldx,
+// pair per block row (blockIdx.y), kResidPlanes planes per block; y = A x -
+// l x of each row with the SpMV's bits, then the block's sums of y^2 and
+// (l x)^2.
+template <int MAXLEN, int KM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_resid_planes(
+    PatArgs a, const double* __restrict__ X, int64_t ldx,
                                                      const int* __restrict__ col, const double* __restrict__ lam,
                                                      const int* __restrict__ out, double* __restrict__ partial,
                                                      int64_t pstride) {
@@ -1174,37 +1201,22 @@ __global__ __launch_bounds__(256) void k_resid_planes(PatArgs a, const double* _
     CAL_PLANE_MARCH(pm, X + (int64_t)col[i] * ldx, kResidPlanes)
     const double l = lam[i];
     double2 xp = pm.ld2((pm.z0 - 1) * pm.P + pm.xy0 + pm.lr);
-    pm.load(pm.z0);
-    pm.store(0);
-    pm.load(pm.z0 + 1);
-    pm.store(1);
-    __syncthreads();
     double num = 0.0, den = 0.0;
-    for (int z = 0; z < pm.zend; ++z) {
-        const int bc = z % 3, bn = (z + 1) % 3, bs = (z + 2) % 3;
-        if (z + 2 <= pm.zend) pm.load(pm.z0 + z + 2);
-        const int64_t r = (pm.z0 + z) * pm.P + pm.xy0 + pm.lr;
+    pm.march([&](int j, int bc, int bn) {
+        const int r = (pm.z0 + j) * pm.P + pm.xy0 + pm.lr;
         const bool v0 = pm.in0 && r < pm.n, v1 = pm.in1 && r + 1 < pm.n;
         unsigned k0, k1;
-        pm.row_keys(bc, pm.z0 + z, k0, k1);
+        pm.row_keys(bc, pm.z0 + j, k0, k1);
         const double2 xc = make_double2(pm.win[bc * pm.WR + pm.wi], pm.win[bc * pm.WR + pm.wi + 1]);
-        double y0 = 0.0, y1 = 0.0;
-#pragma unroll
-        for (int e = 0; e < MAXLEN; ++e) {
-            const double2 v = pm.slot(bc, bn, e, xp);
-            const double t0 = pm.coef(k0, e) * v.x, t1 = pm.coef(k1, e) * v.y;
-            y0 = y0 + t0;
-            y1 = y1 + t1;
-        }
+        double y0, y1;
+        pm.sums(bc, bn, xp, k0, k1, y0, y1);
         const double u0 = l * xc.x, u1 = l * xc.y;
         y0 = y0 - u0;
         y1 = y1 - u1;
         num = num + ((v0 ? y0 * y0 : 0.0) + (v1 ? y1 * y1 : 0.0));
         den = den + ((v0 ? u0 * u0 : 0.0) + (v1 ? u1 * u1 : 0.0));
         xp = xc;
-        if (z + 2 <= pm.zend) pm.store(bs);
-        __syncthreads();
-    }
+    });
     num = wave_sum(num);
     den = wave_sum(den);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1218,27 +1230,17 @@ __global__ __launch_bounds__(256) void k_resid_planes(PatArgs a, const double* _
             ((ws[threadIdx.x][0] + ws[threadIdx.x][1]) + ws[threadIdx.x][2]) + ws[threadIdx.x][3];
 }
 
-// the batched residual kernel's shape: Ritz pairs per block, row pairs per
-// thread (CAL_RESID_SHAPE=<cpb>x<ppt> for A/B while tuning)
-static void resid_shape(int* cpb, int* ppt) {
-    static const int2 v = [] {
-        int c = 4, p = 4;
-        if (const char* e = std::getenv("CAL_RESID_SHAPE")) std::sscanf(e, "%dx%d", &c, &p);
-        if (c != 1 && c != 2 && c != 4 && c != 8) c = 4;
-        if (p != 1 && p != 2 && p != 4 && p != 8) p = 4;
-        return make_int2(c, p);
-    }();
-    *cpb = v.x;
-    *ppt = v.y;
-}
+// the batched residual kernel's shape: one Ritz pair per block, 8 row pairs
+// per thread, the +-1 slots from the neighbouring lanes (the same-box sweep
+// of round 4, diagnostics-only lap3d_215: 1x8 with lane slots 43.2 ms per
+// 15 iterations against 44.3-51.4 ms for 1x2 .. 8x2 and 4x4 with or without)
+constexpr int kResidCpb = 1, kResidPpt = 8;
 
 int spmv_pair_resid_multi_blocks(const PatArgs& a) {
     const int nb = spmv_pair_resid_blocks(a);
     if (nb <= 0) return 0;
     if (planes_ok(a)) return planes_blocks(a, kResidPlanes);
-    int cpb, ppt;
-    resid_shape(&cpb, &ppt);
-    return (nb + ppt - 1) / ppt;
+    return (nb + kResidPpt - 1) / kResidPpt;
 }
 
 hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64_t ldx, const int* col,
@@ -1251,12 +1253,12 @@ hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64
     // 32-bit slot offsets: the column's range must fit the descriptor
     if ((a.xhi - a.xlo) * 8 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
     if (planes_ok(a)) {
-        auto go = [&](auto cu) {
-            constexpr bool CU = decltype(cu)::value;
+        const size_t lds = planes_lds(a);
+        auto go = [&](auto km) {
+            constexpr int KM = decltype(km)::value;
             dim3 g(blocks, npr), bl(256);
-#define CAL_RPL(ML)                                                                                         \
-    hipLaunchKernelGGL((k_resid_planes<ML, CU>), g, bl, (PlaneMarch<ML, CU>::lds_bytes(a)), st, a, X, ldx, col, \
-                       lam, out, partial, pstride)
+#define CAL_RPL(ML) \
+    hipLaunchKernelGGL((k_resid_planes<ML, KM>), g, bl, lds, st, a, X, ldx, col, lam, out, partial, pstride)
             switch (a.pmaxlen) {
                 case 2: CAL_RPL(2); break;
                 case 3: CAL_RPL(3); break;
@@ -1268,20 +1270,14 @@ hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64
             }
 #undef CAL_RPL
         };
-        if (a.cuniform) go(std::true_type{});
-        else go(std::false_type{});
+        if (a.cuniform) go(std::integral_constant<int, 0>{});
+        else if (a.npat <= 256) go(std::integral_constant<int, 1>{});
+        else go(std::integral_constant<int, 2>{});
         return hipGetLastError();
     }
-    int cpb, ppt;
-    resid_shape(&cpb, &ppt);
     const size_t lds = (size_t)a.npent * 16 + 16;
     const bool mid = (a.pmaxlen & 1) && a.pslot[a.pmaxlen / 2] == 0;
-    // the +-1 slots from the neighbouring lanes (CAL_RESID_LANE=0/1 while tuning)
-    static const bool lane_env = [] {
-        const char* e = std::getenv("CAL_RESID_LANE");
-        return e && std::atoi(e) != 0;
-    }();
-    const bool lane = lane_env && mid && a.pmaxlen >= 3 && a.pslot[a.pmaxlen / 2 - 1] == -1 &&
+    const bool lane = mid && a.pmaxlen >= 3 && a.pslot[a.pmaxlen / 2 - 1] == -1 &&
                       a.pslot[a.pmaxlen / 2 + 1] == 1;
     auto go = [&](auto cpb_c, auto ppt_c) {
         constexpr int CPB = decltype(cpb_c)::value, PPT = decltype(ppt_c)::value;
@@ -1306,18 +1302,7 @@ hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64
 #undef CAL_PRM_ODD
 #undef CAL_PRM
     };
-    auto go1 = [&](auto cpb_c) {
-        switch (ppt) {
-            case 1: go(cpb_c, std::integral_constant<int, 1>{}); break;
-            case 2: go(cpb_c, std::integral_constant<int, 2>{}); break;
-            case 8: go(cpb_c, std::integral_constant<int, 8>{}); break;
-            default: go(cpb_c, std::integral_constant<int, 4>{}); break;
-        }
-    };
-    if (cpb == 1) go1(std::integral_constant<int, 1>{});
-    else if (cpb == 2) go1(std::integral_constant<int, 2>{});
-    else if (cpb == 8) go1(std::integral_constant<int, 8>{});
-    else go1(std::integral_constant<int, 4>{});
+    go(std::integral_constant<int, kResidCpb>{}, std::integral_constant<int, kResidPpt>{});
     return hipGetLastError();
 }
 

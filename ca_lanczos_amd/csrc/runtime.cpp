@@ -172,6 +172,7 @@ static void free_matrix(cal_ctx* c) {
     if (A.ppval) hipFree(A.ppval);
     if (A.rzval) hipFree(A.rzval);
     if (A.rzmask) hipFree(A.rzmask);
+    if (A.rowkey8) hipFree(A.rowkey8);
     if (A.rowmask) hipFree(A.rowmask);
     A = DevMatrix();
     if (c->d_work) hipFree(c->d_work);
@@ -445,13 +446,17 @@ int upload_matrix(cal_ctx* c, int64_t n_rows, int64_t ext_off, int64_t n_local, 
                                     seen = true;
                                 }
                         }
-                        if (uni) {
-                            std::vector<uint8_t> rowm((size_t)n_rows);
-                            for (int64_t r = 0; r < n_rows; ++r) rowm[(size_t)r] = rm[pat[(size_t)r]];
-                            rowm.resize((size_t)n_rows + 8, 0);  // zero bytes past the rows (dword key loads)
-                            CAL_HIP(c, hipMalloc((void**)&A.rowmask, rowm.size()));
-                            CAL_HIP(c, hipMemcpy(A.rowmask, rowm.data(), rowm.size(), hipMemcpyHostToDevice));
+                        if (uni) {  // 1-B mask keys (8 zero bytes past the rows: dword key loads)
+                            std::vector<uint8_t> km((size_t)n_rows + 8, 0);
+                            for (int64_t r = 0; r < n_rows; ++r) km[(size_t)r] = rm[pat[(size_t)r]];
+                            CAL_HIP(c, hipMalloc((void**)&A.rowmask, km.size()));
+                            CAL_HIP(c, hipMemcpy(A.rowmask, km.data(), km.size(), hipMemcpyHostToDevice));
                             A.cuniform = true;
+                        } else if (A.npat <= 256) {  // 1-B keys (8 zero bytes past the rows: dword key loads)
+                            std::vector<uint8_t> k8((size_t)n_rows + 8, 0);
+                            for (int64_t r = 0; r < n_rows; ++r) k8[(size_t)r] = (uint8_t)pat[(size_t)r];
+                            CAL_HIP(c, hipMalloc((void**)&A.rowkey8, k8.size()));
+                            CAL_HIP(c, hipMemcpy(A.rowkey8, k8.data(), k8.size(), hipMemcpyHostToDevice));
                         }
                         A.plane_P = A.pslot[L - 1];
                         A.plane_H = H;
@@ -530,6 +535,7 @@ static PatArgs pat_args(const DevMatrix& A, int64_t o, int64_t len, const double
     if (A.rzval && o == A.ext_off && len == A.n_local) {
         p.rzval = A.rzval;
         p.rzmask = A.rzmask;
+        p.rowkey8 = A.rowkey8;
         p.rowmask = A.rowmask;
         p.cuniform = A.cuniform ? 1 : 0;
         for (int k = 0; k < 8; ++k) p.cval[k] = A.cval[k];
