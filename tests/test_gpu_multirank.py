@@ -193,7 +193,7 @@ def test_config4_lap3d_215_wide(cal, ref, config4_single, world):
 
 
 # ------------------------------------------------- config 5's topology (CSR)
-def _config5_worker(rank, world, port, out_q):
+def _config5_worker(rank, world, port, nc, out_q):
     import sys
     sys.path.insert(0, ROOT)
     dist, allreduce, exchange = _gloo_callbacks(rank, world, port)
@@ -201,7 +201,7 @@ def _config5_worker(rank, world, port, out_q):
     from oracle import ca_lanczos_ref as ref
     from ca_lanczos_amd._lib import check, lib, ptr
 
-    A = cal.matrices.circuit_like(NC)
+    A = cal.matrices.circuit_like(nc)
     n = A.shape[0]
     b = cal.matrices.slab_bounds(n, world, 1)
     r0, r1 = b[rank], b[rank + 1]
@@ -227,12 +227,15 @@ def _config5_worker(rank, world, port, out_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.timeout(600)
-@pytest.mark.parametrize("world", [2, 3])
-def test_config5_irregular_compact_halo(cal, ref, world):
-    A = cal.matrices.circuit_like(NC)
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("nc,world", [(NC, 2), (NC, 3), (1259, 8)])
+def test_config5_irregular_compact_halo(cal, ref, nc, world):
+    """(1259, 8) is config 5's own decomposition at full size (VERDICT r03
+    "next" #6): the G3_circuit stand-in, n = 1,585,081, in 8 row slabs of
+    198,135 rows, all eight ranks on the one GPU."""
+    A = cal.matrices.circuit_like(nc)
     n = A.shape[0]
-    res = _run_ranks(_config5_worker, world, (), timeout=500)
+    res = _run_ranks(_config5_worker, world, (nc,), timeout=800)
     c1 = cal.Context(0).set_matrix(A)
     single = cal.ca_lanczos_ex(A, ref.matlab_rand(n), S, IT5, "newton", "local", diagnostics=True,
                                return_Q=False, ctx=c1)
@@ -241,9 +244,13 @@ def test_config5_irregular_compact_halo(cal, ref, world):
     c1.close()
     nA = float(abs(A).sum(axis=1).max())
     assert irl1["converged"]
+    print("circuit_%d x%d: single-GPU IRL %d restarts" % (nc, world, irl1["num_restarts"]))
     for rank, rr in res:
+        print("  rank %d rows %s nghost %d restarts %d" % (rank, rr["rows"], rr["info"]["nghost"],
+                                                        rr["irl"]["num_restarts"]))
         assert rr["spmv"], rank                                  # bit-identical SpMV
         assert rr["fmt"] == "csr" and rr["info"]["nghost"] > 0
+        print("    mpk %s sched %d" % (rr["mpk"], rr["sched"]))
         assert rr["mpk"]["depth"] == 1 and rr["sched"] == 0      # compact ghosts: one exchange per SpMV
         T, rn, flags = rr["local"]
         assert flags == list(single.reorth)
