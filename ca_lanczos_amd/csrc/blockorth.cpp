@@ -594,7 +594,7 @@ static int ensure_zbuf(cal_ctx* c, int64_t n, int m, double** p, int64_t* ld) {
 // P1 Gram (C = Qp'X) -> k_fold_up (Y formed, tile QR, Qp'Y on the matrix
 // cores) -> the tree up -> the Gram reduced -> [several ranks: root
 // all-gather + the global levels] -> k_fold_coef1 (reorth flag, R, RY, S, K;
-// published) -> the tree walked down -> k_fold_down (Q = Q_Y S - Qp K).  The
+// published) -> k_fold_down (each tile's S from the root's, Q = Q_Y S - Qp K).  The
 // host waits once, for the published R.  Returns 2 when the shape does not
 // apply, 1 when the fold declined after running (||W|| too large, or a
 // non-finite value): the caller then takes the explicit-Z path.
@@ -646,13 +646,12 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
         off += (cnt + 7) & ~size_t(7);
         return o;
     };
-    const size_t oV0 = take(n0 * t0), otb0 = take(n0 * 16), oR0 = take(n0 * 64), oS0 = take(n0 * 64);
-    size_t oVu[3], otbu[3], oRu[3], oSu[3];
+    const size_t oV0 = take(n0 * t0), otb0 = take(n0 * 16), oR0 = take(n0 * 64);
+    size_t oVu[3], oRu[3], oMu[3];
     for (int L = 0; L < nlev; ++L) {
         oVu[L] = take((size_t)nu[L] * tu);
-        otbu[L] = take((size_t)nu[L] * 16);
         oRu[L] = take((size_t)nu[L] * 64);
-        oSu[L] = take((size_t)nu[L] * 64);
+        oMu[L] = take((size_t)nu[L] * 64);
     }
     const size_t oRrm = take(64), oSb = take(64), oSm = take(64), oK = take(72);
     const size_t oOut = take(520), oT1 = take(272), oT2 = take(272);
@@ -679,13 +678,11 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
     fa.V0 = F + oV0;
     fa.tb0 = F + otb0;
     fa.R0 = F + oR0;
-    fa.S0 = F + oS0;
     for (int L = 0; L < nlev; ++L) {
         fa.nu[L] = nu[L];
         fa.Vu[L] = F + oVu[L];
-        fa.tbu[L] = F + otbu[L];
         fa.Ru[L] = F + oRu[L];
-        fa.Su[L] = F + oSu[L];
+        fa.Mu[L] = F + oMu[L];
     }
     fa.Rroot_m = F + oRrm;
     const Panel W = panel_concat(Qp, X);
@@ -715,18 +712,20 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
         CAL_HIP(c, launch_fold_up(cu, fa, c->stream));
         timer_end(c, t);
     }
-    // one rank: the root level, the algebra and the root's way down merged
-    // (k_fold_root: three latency-bound launches in one)
+    // one rank: the root level and the algebra merged (k_fold_root)
     const bool merged = P == 1;
     // (the C2 reduction on a side stream beside the tree levels, and the
     // publish beside the way down, measured 656-661 -> 626-633 outer-it/s:
-    // the cross-stream waits cost more than the two short kernels)
+    // the cross-stream waits cost more than the two short kernels.)  The
+    // reduction rides on 72 extra blocks of the level-1 launch.
+    const int tree_top = merged ? nlev - 1 : nlev;
+    if (tree_top >= 1) fa.red_out = F + oT2;
     {
         const int t = timer_begin(c, 3);
-        CAL_HIP(c, launch_fold_tree(fa, c->stream, merged ? nlev - 1 : nlev));
+        CAL_HIP(c, launch_fold_tree(fa, c->stream, tree_top));
         timer_end(c, t);
     }
-    CAL_HIP(c, launch_fold_reduce(c->d_partial, (int)nblk, F + oT2, c->stream));
+    if (!fa.red_out) CAL_HIP(c, launch_fold_reduce(c->d_partial, (int)nblk, F + oT2, c->stream));
     CAL_TRY(allreduce_sum(c, F + oT2, 72));
     CAL_TRY(ensure_pub(c));
     const unsigned long long seq = ++c->pub_seq;
@@ -738,8 +737,9 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
         const int t = timer_begin(c, 3);
         CAL_HIP(c, launch_fold_root(fa, F + oT1, F + oT2, d_out, F + oSb, F + oSm, F + oK, w, doreorth ? 1 : 0,
                                     nglob, c->d_pub, d_seq, seq, c->stream));
-        CAL_HIP(c, launch_fold_down_tree(fa, nullptr, 8, c->stream, nlev - 1));
         timer_end(c, t);
+        fa.Stop = F + oSb;
+        fa.lds = 8;
     } else {
         // the root over the ranks: all-gather the local roots, factor the stack
         // (the tree kernel's stack level, redundantly on every rank)
@@ -763,21 +763,18 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
         }
         CAL_HIP(c, launch_fold_coef1(F + oT1, F + oT2, Rtop, ldr, d_out, F + oSb, F + oSm, F + oK, w, m,
                                      doreorth ? 1 : 0, nglob, c->fold_tol, c->d_pub, d_seq, seq, c->stream));
-        // down: [the global levels,] the group and block levels, level 0
-        const double* Stop = F + oSb;
-        int lds = 8;
+        // down: [the global levels to this rank's root S,] then k_fold_down
+        fa.Stop = F + oSb;
+        fa.lds = 8;
         if (P > 1) {
             ga.S = F + oSm;
             ga.out = F + oGdn;
             const int t = timer_begin(c, 3);
             CAL_HIP(c, launch_tsqr(true, 0, ga, gcols, gq, c->stream));
             timer_end(c, t);
-            Stop = F + oGdn + (size_t)me * mm;
-            lds = m;
+            fa.Stop = F + oGdn + (size_t)me * mm;
+            fa.lds = m;
         }
-        const int t = timer_begin(c, 3);
-        CAL_HIP(c, launch_fold_down_tree(fa, Stop, lds, c->stream));
-        timer_end(c, t);
     }
     OutList qo{};
     for (int j = 0; j < 16; ++j) qo.p[j] = panel_out_slice(Qout, j < m ? j : 0, 1).ptr[0];

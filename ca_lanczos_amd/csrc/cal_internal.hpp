@@ -347,11 +347,12 @@ hipError_t launch_tsqr(bool down, int src, const TsqrLevelArgs& a, const TsqrCol
 
 // ---- projectAndNormalize with the fused TSQR (tsqr_fold.hip) ----------------
 // Workspace of one fused block (8-wide register tiles): level 0 (n0 tiles of
-// 256 rows: factored tiles V0 / tau-beta tb0, R factors R0, S blocks S0), the
-// upper levels L = 1 .. nlev (nu[L-1] tiles of 64 R factors of the level
-// below: Vu / tbu / Ru / Su; level nlev is the root, one tile; Rroot_m its R
-// with ld m), the P1 tile C, K (9 x 8), the flags (out[512..515]) and the
-// C2 = Qp'Y partials (72 x nblk, entry-major).
+// 256 rows: factored tiles V0 / tau-beta tb0, R factors R0), the upper
+// levels L = 1 .. nlev (nu[L-1] tiles of 64 R factors of the level below:
+// reflectors Vu, R factors Ru, WY matrices Mu; level nlev is the root, one
+// tile; Rroot_m its R with ld m), the P1 tile C, K (9 x 8), the flags
+// (out[512..515]), the C2 = Qp'Y partials (72 x nblk, entry-major; red_out:
+// where level 1 reduces them, or null) and the root's S (Stop, ld lds).
 // largest accepted loss-of-orthogonality estimate of the fused TSQR (its
 // default; cal_set_tsqr_fold_tol)
 constexpr double kFoldTol = 1e-14;
@@ -363,13 +364,15 @@ struct FoldArgs {
     const double* C = nullptr;  // the reduced P1 tile (272 doubles): C = Qp'X is read from it
     const double* flags = nullptr;
     const double* K = nullptr;
-    double *V0 = nullptr, *tb0 = nullptr, *R0 = nullptr, *S0 = nullptr;
+    double *V0 = nullptr, *tb0 = nullptr, *R0 = nullptr;
     double* Vu[3] = {nullptr, nullptr, nullptr};
-    double* tbu[3] = {nullptr, nullptr, nullptr};
     double* Ru[3] = {nullptr, nullptr, nullptr};
-    double* Su[3] = {nullptr, nullptr, nullptr};
+    double* Mu[3] = {nullptr, nullptr, nullptr};
     double* Rroot_m = nullptr;
     double* partial = nullptr;
+    double* red_out = nullptr;
+    const double* Stop = nullptr;
+    int lds = 8;
 };
 int fold_tiles(int64_t n);                 // level-0 tiles
 int fold_blocks(int64_t n);                // k_fold_up / k_fold_down blocks
@@ -388,13 +391,11 @@ hipError_t launch_fold_coef1(const double* T1, const double* G, const double* Rt
                              double* Sbuf, double* Sm, double* Kbuf, int w, int m, int doreorth, double nglob,
                              double tol, double* hout, unsigned long long* hseq, unsigned long long seq,
                              hipStream_t st);
-// one rank: the root level, k_fold_coef1's algebra and the root's way down in
-// one block (the root's R is its own, ld 8); S blocks of level nlev - 1 out
+// one rank: the root level and k_fold_coef1's algebra in one block (the
+// root's R is its own, ld 8)
 hipError_t launch_fold_root(const FoldArgs& a, const double* T1, const double* G, double* out, double* Sbuf,
                             double* Sm, double* Kbuf, int w, int doreorth, double nglob, double* hout,
                             unsigned long long* hseq, unsigned long long seq, hipStream_t st);
-// levels from .. 1 (-1: from the root, whose S is Stop, ld lds)
-hipError_t launch_fold_down_tree(const FoldArgs& a, const double* Stop, int lds, hipStream_t st, int from = -1);
 hipError_t launch_fold_down(const ColList& P, const OutList& Q, const FoldArgs& a, hipStream_t st);
 
 

@@ -21,9 +21,13 @@
 //           its job (||W|| << 1): the explicit-Z path (blockorth.cpp pn_tsqr)
 //           is taken instead when ||W||_F > 1/2.  R = R_Z, RY = C + C2
 //           (:71-73), the flag, published to pinned host memory.
-//   down    k_fold_down_level: the tree walked down (explicit Q factors of
-//           the stored tiles times the parent's S); k_fold_down: level 0,
-//           Q = Q_tile S - Qp K, one store.
+//   down    k_fold_down: level 0, Q = Q_tile S - Qp K, one store.  Every
+//           tile's Q factor is used in its compact-WY form Q = E - V M,
+//           M = T V_top' (dlarft's T from V'V and tau): the up pass stores M
+//           per upper tile, so a level-0 wave forms its own S block by walking
+//           the tree down from the root's S through 8 x 8 products (no
+//           launch per level), and its 256 rows as E S - V (M S) (no
+//           reflector-by-reflector sweep).
 //
 // HBM traffic per block (n rows): P1 (w+m)·8n, up (w+m)·8n + m·8n (the
 // factored tiles), down m·8n (tiles) + w·8n (Qp, only when the second
@@ -57,6 +61,9 @@ constexpr int FTLD = 17;        // padded LDS row of the Gram transpose
 constexpr int kProbe = FOLD_PROBE;  // bit 1: no Gram, 2: no tile QR, 3: no tile store, 4: tree level 1 only
 #ifndef FOLD_UP_WPE
 #define FOLD_UP_WPE 4  // k_fold_up waves per SIMD (VGPR budget 512 / WPE)
+#endif
+#ifndef FOLD_DOWN_WPE
+#define FOLD_DOWN_WPE 3  // k_fold_down waves per SIMD (150 VGPRs)
 #endif
 
 __device__ __forceinline__ fd4 fmfma(double a, double b, fd4 c) {
@@ -139,6 +146,142 @@ __device__ __forceinline__ void fmul_S(const double (&q)[FM], const double* S, i
                 const double u = q[k] * S[k + c * FM];
                 o[c] = o[c] + u;
             }
+        }
+    }
+}
+
+// ---- compact WY (dlarft, forward, columnwise) ------------------------------
+// V, the reflector matrix of a factored tile: unit diagonal, zero above it,
+// the stored reflector entries below (columns >= m zero).  Q = H_0 ... H_{m-1}
+// [I; 0] = E - V M with M = T V_top' (m x m), T the upper triangular factor
+// of H_0 ... H_{m-1} = I - V T V'.
+__device__ __forceinline__ double fv(double x, int64_t row, int c, int m) {
+    return c < m ? (row > c ? x : (row == c ? 1.0 : 0.0)) : 0.0;
+}
+// a factored register tile (rows row0 + 64 i) turned into V in place
+template <int RPL>
+__device__ __forceinline__ void fv_tile(double (&x)[RPL][FM], int64_t row0, int m) {
+#pragma unroll
+    for (int i = 0; i < RPL; ++i)
+#pragma unroll
+        for (int c = 0; c < FM; ++c) x[i][c] = fv(x[i][c], row0 + 64 * i, c, m);
+}
+// this lane's rows' part of V'V (x holds V, see fv_tile), strictly upper
+// entries G(a, b), a < b, numbered e = b (b - 1) / 2 + a; entries E0 .. E0 +
+// NE - 1 into g
+constexpr int NG = FM * (FM - 1) / 2;
+__device__ __forceinline__ constexpr int gram_b(int e) {
+    int b = 1;
+    for (int q = 2; q < FM; ++q) b = e >= q * (q - 1) / 2 ? q : b;
+    return b;
+}
+template <int RPL, int E0, int NE>
+__device__ __forceinline__ void fgram_v(const double (&x)[RPL][FM], double (&g)[NE]) {
+#pragma unroll
+    for (int e = 0; e < NE; ++e) g[e] = 0.0;
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const int b = gram_b(E0 + e), a = E0 + e - b * (b - 1) / 2;
+            g[e] = __builtin_fma(x[i][a], x[i][b], g[e]);
+        }
+    }
+}
+// The NE wave sums of g (fixed order) into out[a + 8 b] (LDS).  One DPP step
+// folds lane pairs; the even lanes' pair sums go through the wave's LDS
+// scratch (32 x NE doubles), where lanes 2e and 2e + 1 each add one half of
+// value e's 32 rows and a second DPP step joins the halves: ~150
+// instructions for the 28 sums instead of ~560 for 28 butterflies.
+template <int E0, int NE>
+__device__ __forceinline__ void wave_gram_sums(double (&g)[NE], double* scratch, double* out, int lane) {
+#pragma unroll
+    for (int e = 0; e < NE; ++e) g[e] = g[e] + dpp_f64<0xB1, 0xF>(g[e]);  // quad_perm [1,0,3,2]
+    if ((lane & 1) == 0) {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) scratch[(lane >> 1) * NE + e] = g[e];
+    }
+    fwsync();
+    const int e = lane >> 1, h = lane & 1;
+    double s = 0.0;
+    if (e < NE) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s = s + scratch[(16 * h + r) * NE + e];
+    }
+    const double sw = dpp_f64<0xB1, 0xF>(s);  // the partner lane's half (all lanes active)
+    const double lo = h ? sw : s, hi = h ? s : sw;
+    if (e < NE && h == 0) {
+        const int b = gram_b(E0 + e), a = E0 + e - b * (b - 1) / 2;
+        out[a + FM * b] = lo + hi;
+    }
+    fwsync();
+}
+// all NG sums in two halves (half the partial registers live at a time)
+template <int RPL>
+__device__ __forceinline__ void wave_gram(const double (&x)[RPL][FM], double* scratch, double* out, int lane) {
+    // (scheduling barriers: the halves' partial products must not overlap)
+    __builtin_amdgcn_sched_barrier(0);
+    {
+        double g[NG / 2];
+        fgram_v<RPL, 0, NG / 2>(x, g);
+        wave_gram_sums<0, NG / 2>(g, scratch, out, lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {
+        double g[NG - NG / 2];
+        fgram_v<RPL, NG / 2, NG - NG / 2>(x, g);
+        wave_gram_sums<NG / 2, NG - NG / 2>(g, scratch, out, lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+// Row r of T, then row r of M = T V_top' (r < m; zero otherwise).  G: V'V
+// (entry a + 8 b, a < b), Vt: V's top 8 rows (entry r + 8 c), both in LDS.
+// T(r, r) = tau_r, T(r, i) = -tau_i sum_{r <= k < i} T(r, k) G(k, i): a row of
+// T depends only on its own earlier entries.
+__device__ __forceinline__ void fwy_row(const double* G, const double* Vt, const double (&tau)[FM], int m, int r,
+                                        double (&mrow)[FM]) {
+    double t[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < i; ++k) s = k >= r ? __builtin_fma(t[k], G[k + FM * i], s) : s;
+        t[i] = i < m ? (i == r ? tau[i] : (i > r ? -tau[i] * s : 0.0)) : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k <= j; ++k) s = k >= r ? __builtin_fma(t[k], Vt[j + FM * k], s) : s;
+        mrow[j] = (j < m && r < m) ? s : 0.0;
+    }
+}
+// M of an upper-level tile spread over the NW waves of a block (rows wave *
+// 64 RPLW + lane + 64 i) into Mout (entry r + 8 c); x is turned into V.
+// All waves call it.
+template <int RPLW, int NW>
+__device__ __forceinline__ void fold_wy_blk(double (&x)[RPLW][FM], const double (&tau)[FM], int m, int lane,
+                                            int wave, double (*gw)[64], double (*scr)[32 * (NG - NG / 2)], double* Vt,
+                                            double* __restrict__ Mout) {
+    fv_tile<RPLW>(x, (int64_t)wave * 64 * RPLW + lane, m);
+    wave_gram<RPLW>(x, scr[wave], gw[wave], lane);
+    if (wave == 0 && lane < FM) {
+#pragma unroll
+        for (int c = 0; c < FM; ++c) Vt[lane + FM * c] = x[0][c];
+    }
+    __syncthreads();
+    if (wave == 0) {
+        double sum = gw[0][lane];
+#pragma unroll
+        for (int v = 1; v < NW; ++v) sum = sum + gw[v][lane];
+        fwsync();
+        gw[0][lane] = sum;
+        fwsync();
+        if (lane < FM) {
+            double mrow[FM];
+            fwy_row(gw[0], Vt, tau, m, lane, mrow);
+#pragma unroll
+            for (int j = 0; j < FM; ++j) Mout[lane + FM * j] = mrow[j];
         }
     }
 }
@@ -279,13 +422,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FOLD_UP_WPE
 // QR deep: ~18 us for one wave alone, ~8 us over 4 waves (2048-row tiles over
 // 8 or 16 waves, one level fewer, measured 2x and 9x slower per level: the
 // per-reflector LDS exchange grows with the waves).  Level L = 1 .. nlev, the
-// last one the root (one tile): three levels up to 67 M rows.
+// last one the root (one tile): three levels up to 67 M rows.  Each tile
+// stores its reflectors and its WY matrix M (the down pass's input).
 // Kernel boundaries order the levels (a device-scope release in every block
 // of a launch writes each XCD's L2 back: 2.8 ms measured when k_fold_up did).
+// With red_out set, level 1 has 72 extra blocks that reduce the up launch's
+// C2 partials, one entry each (k_fold_reduce's job, without its launch).
 __global__ __launch_bounds__(64 * UW) void k_fold_tree(FoldArgs a, int L) {
     __shared__ double xlds[2 * UW * 2 * FM];
+    __shared__ double gw[UW][64], Vt[64];
+    __shared__ double scr[UW][32 * (NG - NG / 2)];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = a.m;
     const int t = blockIdx.x;
+    if (L == 1 && a.red_out && t >= a.nu[0]) {  // the 72 extra blocks: one C2 entry each
+        const int e = t - a.nu[0];
+        const double* p = a.partial + (int64_t)e * a.nblk;
+        double s = 0.0;
+        for (int i = tid; i < a.nblk; i += 64 * UW) s = s + p[i];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s = s + __shfl_xor(s, o, 64);
+        if (lane == 0) xlds[wave] = s;
+        __syncthreads();
+        if (tid == 0) {
+            double v = 0.0;
+            for (int k = 0; k < UW; ++k) v = v + xlds[k];
+            a.red_out[e] = v;
+        }
+        return;
+    }
     const double* Rin = L == 1 ? a.R0 : a.Ru[L - 2];
     const int nin = L == 1 ? a.n0 : a.nu[L - 2];
     const int64_t rows = (int64_t)((nin - t * FG) < FG ? (nin - t * FG) : FG) * FM;
@@ -294,13 +458,13 @@ __global__ __launch_bounds__(64 * UW) void k_fold_tree(FoldArgs a, int L) {
     tile_geqr2_blk<FM, URPL, UW>(x, tau, beta, m, lane, wave, xlds);
     fstore_tile<URPL>(a.Vu[L - 1] + (int64_t)t * (64 * URPL * UW * FM) + (int64_t)wave * URPL * FM * 64, lane, x);
     if (wave == 0) {
-        fstore_tb(a.tbu[L - 1] + (int64_t)t * (2 * FM), lane, tau, beta);
         fput_R(a.Ru[L - 1] + (int64_t)t * 64, lane, m, x[0]);
         // the root's R with leading dimension m as well (the stack layout of
         // tsqr.hip, for the all-gather of the local roots over several ranks)
         if (L == a.nlev && lane < m)
             for (int cc = 0; cc < m; ++cc) a.Rroot_m[lane + cc * m] = cc >= lane ? x[0][cc] : 0.0;
     }
+    fold_wy_blk<URPL, UW>(x, tau, m, lane, wave, gw, scr, Vt, a.Mu[L - 1] + (int64_t)t * 64);
 }
 
 // ---- the s x s algebra --------------------------------------------------
@@ -527,59 +691,10 @@ __global__ __launch_bounds__(1024) void k_fold_reduce(const double* __restrict__
     }
 }
 
-// ---- down the tree ---------------------------------------------------------
-// Stack row r of a level's input is row r & 7 of R block r >> 3 (rows >= m
-// are zero rows: their Q rows are zero, so the S rows written there are zero).
-// One upper-level tile down, one block: its Q factor (from the stored
-// reflectors) times its S block (Ss, LDS) -> the S blocks of the level below
-// (rows r < rows of the tile: block blk0 + (r >> 3) of Sb, row r & 7).
-__device__ __forceinline__ void fold_level_down(const double* V, const double* tb, const double* Ss, int64_t rows,
-                                                double* Sb, int64_t blk0, int m, int lane, int wave, double* xlds) {
-    double x[URPL][FM], tau[FM];
-    fload_tile<URPL>(V + (int64_t)wave * URPL * FM * 64, lane, x);
-    fload_tau(tb, tau);
-    tile_org2r_blk<FM, URPL, UW>(x, tau, m, lane, wave, xlds);
-#pragma unroll
-    for (int i = 0; i < URPL; ++i) {
-        const int64_t r = (int64_t)wave * 64 * URPL + lane + 64 * i;
-        double o[FM];
-        fmul_S(x[i], Ss, m, o);
-        if (r < rows) {
-#pragma unroll
-            for (int cc = 0; cc < FM; ++cc) Sb[(blk0 + (r >> 3)) * 64 + (r & 7) + cc * FM] = o[cc];
-        }
-    }
-}
-
-// Level L down (L = nlev: the root, whose S is S_top, ld lds; below it the
-// level's own S blocks), one block per tile -> the S blocks of level L - 1.
-__global__ __launch_bounds__(64 * UW) void k_fold_down_level(FoldArgs a, int L, const double* __restrict__ Stop,
-                                                             int lds) {
-    __shared__ double Ss[64];
-    __shared__ double xlds[2 * UW * 2 * FM];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = a.m;
-    const int t = blockIdx.x;
-    if (tid < 64) {
-        if (L == a.nlev) {
-            const int k = tid & 7, cc = tid >> 3;
-            Ss[tid] = (k < m && cc < m) ? Stop[k + cc * lds] : 0.0;
-        } else {
-            Ss[tid] = a.Su[L - 1][(int64_t)t * 64 + tid];
-        }
-    }
-    __syncthreads();
-    const int nb = L == 1 ? a.n0 : a.nu[L - 2];
-    double* Sb = L == 1 ? a.S0 : a.Su[L - 2];
-    const int64_t rows = (int64_t)((nb - t * FG) < FG ? (nb - t * FG) : FG) * FM;
-    fold_level_down(a.Vu[L - 1] + (int64_t)t * (64 * URPL * UW * FM), a.tbu[L - 1] + (int64_t)t * (2 * FM), Ss, rows,
-                    Sb, (int64_t)t * FG, m, lane, wave, xlds);
-}
-
-// One rank: the root level, the s x s algebra and the root's way down in one
-// block (k_fold_tree's root tile, k_fold_coef1 on wave 0, k_fold_down_level's
-// root), the tile's reflectors kept in registers and R / S_top passed through
-// LDS: three latency-bound launches in one.  The publish comes last, off the
-// way to the S blocks of the level below.
+// One rank: the root level and the s x s algebra in one block (k_fold_tree's
+// root tile, then k_fold_coef1 on wave 0): two latency-bound launches in one.
+// The root's reflectors and WY matrix are stored like any tile's; the
+// publish comes last.
 __global__ __launch_bounds__(64 * UW) void k_fold_root(FoldArgs a, const double* __restrict__ T1,
                                                        const double* __restrict__ G, double* __restrict__ out,
                                                        double* __restrict__ Sbuf, double* __restrict__ Sm,
@@ -587,7 +702,9 @@ __global__ __launch_bounds__(64 * UW) void k_fold_root(FoldArgs a, const double*
                                                        double* __restrict__ hout,
                                                        unsigned long long* __restrict__ hseq, unsigned long long seq) {
     __shared__ double xlds[2 * UW * 2 * FM];
-    __shared__ double Rl[64], Sl[64];
+    __shared__ double Rl[64];
+    __shared__ double gw[UW][64], Vt[64];
+    __shared__ double scr[UW][32 * (NG - NG / 2)];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = a.m;
     const int L = a.nlev;
     const double* Rin = L == 1 ? a.R0 : a.Ru[L - 2];
@@ -596,31 +713,26 @@ __global__ __launch_bounds__(64 * UW) void k_fold_root(FoldArgs a, const double*
     fload_stack<URPL>(Rin, (int64_t)wave * 64 * URPL, rows, lane, x);
     tile_geqr2_blk<FM, URPL, UW>(x, tau, beta, m, lane, wave, xlds);
     if (wave == 0) fput_R(Rl, lane, m, x[0]);
+    fstore_tile<URPL>(a.Vu[L - 1] + (int64_t)wave * URPL * FM * 64, lane, x);
     __syncthreads();
-    if (wave == 0) fold_coef1_body(T1, G, Rl, FM, out, Sbuf, Sm, Kbuf, w, m, doreorth, nglob, a.tol, Sl, lane);
-    __syncthreads();
-    tile_org2r_blk<FM, URPL, UW>(x, tau, m, lane, wave, xlds);
-    double* Sb = L == 1 ? a.S0 : a.Su[L - 2];
-#pragma unroll
-    for (int i = 0; i < URPL; ++i) {
-        const int64_t r = (int64_t)wave * 64 * URPL + lane + 64 * i;
-        double o[FM];
-        fmul_S(x[i], Sl, m, o);
-        if (r < rows) {
-#pragma unroll
-            for (int cc = 0; cc < FM; ++cc) Sb[(r >> 3) * 64 + (r & 7) + cc * FM] = o[cc];
-        }
-    }
+    if (wave == 0) fold_coef1_body(T1, G, Rl, FM, out, Sbuf, Sm, Kbuf, w, m, doreorth, nglob, a.tol, nullptr, lane);
+    fold_wy_blk<URPL, UW>(x, tau, m, lane, wave, gw, scr, Vt, a.Mu[L - 1]);
     if (wave == 0 && hout) fold_publish(out, w, m, hout, hseq, seq, lane);
 }
 
 // Level 0: Q = Q_tile S - Qp K, one store.  Q: output columns (slots >= m
-// unused); P as in k_fold_up (Qp in slots 0..8).  Independent waves.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_fold_down(ColList P, OutList Q,
+// unused); P as in k_fold_up (Qp in slots 0..8).  Independent waves.  Each
+// wave first forms its tile's S block: from the root's S (Stop, ld lds) down
+// the levels, S_child = E S - V(rows) (M S) on the 8 stack rows of its
+// ancestor at each level (lane r + 8 c holds entry (r, c); 8 x 8 products by
+// shuffles), then its own tile's M from V'V, and the rows as
+// E S - V (M S) - Qp K.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FOLD_DOWN_WPE))) void k_fold_down(ColList P, OutList Q,
                                                                                            FoldArgs a) {
-    __shared__ double Ss[FTPB][64];
     __shared__ double Ks[9 * FM];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = a.m, w = a.w;
+    __shared__ double Vts[FTPB][64], Ms[FTPB][64], Ss[FTPB][64], Ns[FTPB][64];
+    const int tid = threadIdx.x, lane = tid & 63, m = a.m, w = a.w;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: the tile's scalars by scalar loads
     const int64_t n = a.n;
     const int64_t ntiles = (n + FTR0 - 1) / FTR0;
     const int64_t tile = (int64_t)blockIdx.x * FTPB + wave;
@@ -635,26 +747,79 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     const bool declined = a.flags[1] != 0.0;
     __syncthreads();
     if (tile >= ntiles || declined) return;
+    const int r8 = lane & 7, c8 = lane >> 3;
+    const int nlev = a.nlev;
+    // the ancestors' V rows and M (loads first: they do not depend on S)
+    double vv[3], mv[3];
+#pragma unroll
+    for (int l = 0; l < 3; ++l) {
+        vv[l] = 0.0;
+        mv[l] = 0.0;
+        if (l < nlev) {
+            const int64_t tl = tile >> (6 * (l + 1));
+            const int row = 8 * (int)((tile >> (6 * l)) & 63) + r8;
+            const double* V = a.Vu[l] + tl * (64 * URPL * UW * FM) + (row >> 7) * (URPL * FM * 64) +
+                              (((row >> 6) & 1) * FM + c8) * 64 + (row & 63);
+            vv[l] = fv(*V, row, c8, m);
+            mv[l] = a.Mu[l][tl * 64 + lane];
+        }
+    }
+    double S = (r8 < m && c8 < m) ? a.Stop[r8 + c8 * a.lds] : 0.0;
     double x[L0RPL][FM], tau[FM];
     fload_tile<L0RPL>(a.V0 + tile * (64 * L0RPL * FM), lane, x);
     fload_tau(a.tb0 + tile * (2 * FM), tau);
-    Ss[wave][lane] = a.S0[tile * 64 + lane];
-    fwsync();
-    tile_org2r<FM, L0RPL>(x, tau, m, lane);
+    // the wave's loads issued before its s x s work: the first two row
+    // chunks of Qp for the correction too (in flight during the chain and
+    // the Gram)
     const int64_t base = tile * FTR0;
-    double q[9];
-    auto loadq = [&](int i) {
-        const int64_t r = base + lane + 64 * i;
-        const int64_t rr = r < n ? r : n - 1;
+    constexpr int CH = 2;  // row chunks per pass of the row phase
+    double q[CH][9];
+    auto loadq = [&](int i0) {
 #pragma unroll
-        for (int k = 0; k < 9; ++k) q[k] = P.p[k][rr];
+        for (int ii = 0; ii < CH; ++ii) {
+            const int64_t r = base + lane + 64 * (i0 + ii);
+            const int64_t rr = r < n ? r : n - 1;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) q[ii][k] = P.p[k][rr];
+        }
     };
     if (corr) loadq(0);
+    // the chain through LDS (wave-private arrays, free until the tile's own M)
+    double* const Sw = Ss[wave];
+    double* const Mw = Ms[wave];
+    double* const Vw = Vts[wave];
+    double* const Nw0 = Ns[wave];
+#pragma unroll
+    for (int l = 2; l >= 0; --l) {
+        if (l < nlev) {
+            Sw[lane] = S;
+            Mw[lane] = mv[l];
+            Vw[lane] = vv[l];
+            fwsync();
+            double nv = 0.0;
+#pragma unroll
+            for (int j = 0; j < FM; ++j) nv = __builtin_fma(Mw[r8 + FM * j], Sw[j + FM * c8], nv);
+            Nw0[lane] = nv;
+            fwsync();
+            double sn = ((tile >> (6 * l)) & 63) == 0 ? S : 0.0;
+#pragma unroll
+            for (int k = 0; k < FM; ++k) sn = sn - Vw[r8 + FM * k] * Nw0[k + FM * c8];
+            fwsync();
+            S = sn;
+        }
+    }
+    // level 0: the tile's explicit Q factor (dorg2r in registers; measured
+    // 384 us a launch against 422 for E S - V (M S) with M from V'V here:
+    // the Gram's reductions cost more than the reflector sweep)
+    Ss[wave][lane] = S;
+    fwsync();
+    tile_org2r<FM, L0RPL>(x, tau, m, lane);
 #pragma unroll
     for (int i = 0; i < L0RPL; ++i) {
         asm volatile("" ::: "memory");
         double o[FM];
         fmul_S(x[i], Ss[wave], m, o);
+        const int ii = i % CH;
         if (corr) {
             double t[FM];
 #pragma unroll
@@ -664,11 +829,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 #pragma unroll
                 for (int cc = 0; cc < FM; ++cc) asm volatile("" : "+v"(t[cc]));
 #pragma unroll
-                for (int cc = 0; cc < FM; ++cc) t[cc] = __builtin_fma(q[k], Ks[k + cc * 9], t[cc]);
+                for (int cc = 0; cc < FM; ++cc) t[cc] = __builtin_fma(q[ii][k], Ks[k + cc * 9], t[cc]);
             }
-            if (i + 1 < L0RPL) loadq(i + 1);
 #pragma unroll
             for (int cc = 0; cc < FM; ++cc) o[cc] = o[cc] - t[cc];
+            if (ii == CH - 1 && i + 1 < L0RPL) loadq(i + 1);
         }
         const int64_t r = base + lane + 64 * i;
         if (r < n) {
@@ -704,7 +869,8 @@ hipError_t launch_fold_up(const ColList& P, const FoldArgs& a, hipStream_t st) {
 }
 hipError_t launch_fold_tree(const FoldArgs& a, hipStream_t st, int upto) {
     for (int L = 1; L <= (upto >= 0 ? upto : a.nlev); ++L)
-        hipLaunchKernelGGL(k_fold_tree, dim3(a.nu[L - 1]), dim3(64 * UW), 0, st, a, L);
+        hipLaunchKernelGGL(k_fold_tree, dim3(a.nu[L - 1] + (L == 1 && a.red_out ? 72 : 0)), dim3(64 * UW), 0, st, a,
+                           L);
     return hipGetLastError();
 }
 hipError_t launch_fold_reduce(const double* partial, int nparts, double* outv, hipStream_t st) {
@@ -717,11 +883,6 @@ hipError_t launch_fold_coef1(const double* T1, const double* G, const double* Rt
                              hipStream_t st) {
     hipLaunchKernelGGL(k_fold_coef1, dim3(1), dim3(64), 0, st, T1, G, Rtop, ldr, out, Sbuf, Sm, Kbuf, w, m, doreorth,
                        nglob, tol, hout, hseq, seq);
-    return hipGetLastError();
-}
-hipError_t launch_fold_down_tree(const FoldArgs& a, const double* Stop, int lds, hipStream_t st, int from) {
-    for (int L = from >= 0 ? from : a.nlev; L >= 1; --L)
-        hipLaunchKernelGGL(k_fold_down_level, dim3(a.nu[L - 1]), dim3(64 * UW), 0, st, a, L, Stop, lds);
     return hipGetLastError();
 }
 hipError_t launch_fold_root(const FoldArgs& a, const double* T1, const double* G, double* out, double* Sbuf,

@@ -31,7 +31,7 @@ __global__ void k_fill(double* p, int64_t cnt, unsigned long long seed, double s
 int main(int argc, char** argv) {
     using namespace cal;
     const int64_t n = 9938375;
-    const int m = 8, w = 9, reps = 10;
+    const int m = 8, w = 9, reps = 30;
     const int64_t ld = (n + 63) / 64 * 64;
     double *P, *Q, *F;
     CK(hipMalloc((void**)&P, (size_t)17 * ld * sizeof(double)));
@@ -45,13 +45,12 @@ int main(int argc, char** argv) {
         return o;
     };
     const size_t t0 = fold_l0_tile_doubles(), tu = fold_tile_doubles();
-    const size_t oV0 = take(n0 * t0), otb0 = take(n0 * 16), oR0 = take(n0 * 64), oS0 = take(n0 * 64);
-    size_t oVu[3], otbu[3], oRu[3], oSu[3];
+    const size_t oV0 = take(n0 * t0), otb0 = take(n0 * 16), oR0 = take(n0 * 64);
+    size_t oVu[3], oRu[3], oMu[3];
     for (size_t L = 0; L < nu.size(); ++L) {
         oVu[L] = take((size_t)nu[L] * tu);
-        otbu[L] = take((size_t)nu[L] * 16);
         oRu[L] = take((size_t)nu[L] * 64);
-        oSu[L] = take((size_t)nu[L] * 64);
+        oMu[L] = take((size_t)nu[L] * 64);
     }
     const size_t oRrm = take(64), oK = take(72), oOut = take(520), oPart = take((size_t)272 * nblk);
     const size_t oT1 = take(272), oG = take(72), oSb = take(64), oSm = take(64), oRt = take(64);
@@ -75,14 +74,14 @@ int main(int argc, char** argv) {
     fa.V0 = F + oV0;
     fa.tb0 = F + otb0;
     fa.R0 = F + oR0;
-    fa.S0 = F + oS0;
     for (size_t L = 0; L < nu.size(); ++L) {
         fa.nu[L] = nu[L];
         fa.Vu[L] = F + oVu[L];
-        fa.tbu[L] = F + otbu[L];
         fa.Ru[L] = F + oRu[L];
-        fa.Su[L] = F + oSu[L];
+        fa.Mu[L] = F + oMu[L];
     }
+    fa.Stop = F + oRrm;
+    fa.lds = 8;
     fa.Rroot_m = F + oRrm;
     fa.partial = F + oPart;
     ColList cu{};
@@ -95,7 +94,7 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     auto timeit = [&](const char* name, double bytes, auto&& launch) -> int {
-        for (int i = 0; i < 2; ++i) CK(launch());
+        for (int i = 0; i < 5; ++i) CK(launch());
         float tot = 0.0f, mn = 1e30f;
         for (int i = 0; i < reps; ++i) {
             CK(hipEventRecord(a, st));
@@ -108,14 +107,18 @@ int main(int argc, char** argv) {
             mn = ms < mn ? ms : mn;
         }
         const double avg = tot / reps;
-        printf("probe=%d wpe=%d %-10s avg %8.1f us  min %8.1f us  %6.2f TB/s (algorithmic %.3f GB)\n", FOLD_PROBE, FOLD_UP_WPE, name,
+        printf("probe=%d wpe=%d/%d %-10s avg %8.1f us  min %8.1f us  %6.2f TB/s (algorithmic %.3f GB)\n", FOLD_PROBE, FOLD_UP_WPE, FOLD_DOWN_WPE, name,
                avg * 1e3, mn * 1e3, bytes / (avg * 1e-3) / 1e12, bytes / 1e9);
         return 0;
     };
     const double b_up = 25.0 * 8.0 * n, b_down = 25.0 * 8.0 * n;
     if (timeit("up", b_up, [&] { return launch_fold_up(cu, fa, st); })) return 1;
     if (timeit("tree", 0.0, [&] { return launch_fold_tree(fa, st); })) return 1;
-    if (timeit("down_tree", 0.0, [&] { return launch_fold_down_tree(fa, F + oRrm, 8, st); })) return 1;
+    {
+        FoldArgs fred = fa;  // level 1 also reducing the C2 partials
+        fred.red_out = F + oG;
+        if (timeit("tree_red", 0.0, [&] { return launch_fold_tree(fred, st); })) return 1;
+    }
     if (timeit("down", b_down, [&] { return launch_fold_down(cu, qo, fa, st); })) return 1;
     // the coefficient step on inputs that take its whole path (second
     // projection, Cholesky, no decline): X'X = I on the diagonal, C = 0.9,
@@ -138,12 +141,12 @@ int main(int argc, char** argv) {
     unsigned long long sq = 0;
     if (timeit("coef1", 0.0, [&] {
             return launch_fold_coef1(F + oT1, F + oG, F + oRt, 8, F + oOut, F + oSb, F + oSm, F + oK, w, m, 1,
-                                     (double)n, nullptr, nullptr, 0, st);
+                                     (double)n, kFoldTol, nullptr, nullptr, 0, st);
         }))
         return 1;
     if (timeit("coef1_pub", 0.0, [&] {
             return launch_fold_coef1(F + oT1, F + oG, F + oRt, 8, F + oOut, F + oSb, F + oSm, F + oK, w, m, 1,
-                                     (double)n, hpin, hseq, ++sq, st);
+                                     (double)n, kFoldTol, hpin, hseq, ++sq, st);
         }))
         return 1;
     if (timeit("root_pub", 0.0, [&] {
@@ -162,9 +165,8 @@ int main(int argc, char** argv) {
         printf("coef flags: reorth %g fail %g est %g\n", o[514], o[513], o[515]);
     }
     FoldArgs fr = fa;
-    fr.V0 = nullptr;  // re-forming down pass, up without the tile store
+    fr.V0 = nullptr;  // up without the tile store
     if (timeit("up_nost", 17.0 * 8.0 * n, [&] { return launch_fold_up(cu, fr, st); })) return 1;
-    if (timeit("down_ref", b_down, [&] { return launch_fold_down(cu, qo, fr, st); })) return 1;
     CK(hipDeviceSynchronize());
     return 0;
 }
