@@ -550,15 +550,22 @@ def main():
     #   Gram sweeps (P1 and pass A): (w + m) * 8 read per row
     b_csr = 12 * nnz_local + 20 * n_loc + 4
     #   pair patterns: 1 B of id per row (one 2-B id per row pair)
-    b_spmv_launch = (17 if npairpat else 18) * n_loc if fmt == "pattern" else b_csr
+    b_spmv1 = (17 if npairpat else 18) * n_loc if fmt == "pattern" else b_csr
+    #   fused powers (k_powers_planes, schedule 5): F powers per launch read x
+    #   and the row keys once and store F columns: (8 + 1 + 8 F) B per row
+    lpp = max(1, int(round(spmv_cnt / KT)))  # SpMV-class launches per outer iteration
+    b_spmv_launch = spmv_launch_bytes(fmt, npairpat, n_loc, s, lpp, b_csr)
     b_apply = (2 * s + 1 + s) * 8 * n_loc
     b_gram = (2 * s + 1) * 8 * n_loc
     spmv_gbps = b_spmv_launch / (spmv_avg_ms * 1e-3) / 1e9
     # (the first timed step's powers were prefetched untimed: SpMV = avg launch x s)
-    per_step = {"spmv": spmv_avg_ms * s, "gram": gram_ms / KT, "apply": apply_ms / KT}
+    per_step = {"spmv": spmv_avg_ms * lpp, "gram": gram_ms / KT, "apply": apply_ms / KT}
     dominant = max(per_step, key=per_step.get)
-    dom = {"spmv": (b_spmv_launch, spmv_avg_ms, ("k_spmv_pair (row-pattern SpMV, two rows per lane, + Newton shift)"
-                                                 if npairpat else "k_spmv_pat_lds (row-pattern SpMV + Newton shift)")
+    fused = sched == 5
+    dom = {"spmv": (b_spmv_launch, spmv_avg_ms,
+                    ("k_powers_planes (%d Newton powers per launch on the plane march)" % (s // lpp)) if fused else
+                    ("k_spmv_planes / k_spmv_pair (row-pattern SpMV + Newton shift)"
+                     if npairpat else "k_spmv_pat_lds (row-pattern SpMV + Newton shift)")
                     if fmt == "pattern" else "k_spmv (CSR-stream SpMV + Newton shift)"),
            "gram": (b_gram, gram_avg_ms, "k_rowapply Gram sweeps ([Qp|X]'X and pass A, MFMA tile Gram, no store)"),
            "apply": (b_apply, apply_avg_ms, "k_rowapply<17,8,chained> (block orthogonalisation pass B)")}[dominant]
@@ -567,7 +574,7 @@ def main():
     n_reorth = int(np.sum(flags[W:W + K]))
     # whole-step algorithmic HBM bytes of this implementation:
     # s SpMVs + P1 + pass A (Gram sweeps) + pass B (chained apply), per rank
-    b_step = s * b_spmv_launch + 2 * b_gram + b_apply
+    b_step = lpp * b_spmv_launch + 2 * b_gram + b_apply
     b_outer = s * (12 * nnz_total + 20 * n + 4) + 8 * n * (5 * s + 2)
     line = {
         "metric": "CA-Lanczos outer-iters/sec (n~10M, s=8)",
@@ -596,6 +603,8 @@ def main():
                         % (fmt, npat, nent, npairpat, npent, nsplit)) if fmt == "pattern" else fmt,
         "spmv_gbps": spmv_gbps,
         "spmv_avg_us": spmv_avg_ms * 1e3,
+        "spmv_launches_per_step": lpp,
+        "spmv_bytes_per_launch": b_spmv_launch,
         "reorth_passes": "%d/%d" % (n_reorth, K),
         "csr_outer_algorithmic_GB": b_outer / 1e9,
         "kernel_ms_per_step": per_step,
@@ -615,8 +624,8 @@ def main():
     }
     if pat_spmv is not None:
         line["spmv_kernel_back_to_back"] = {"avg_us": pat_spmv[0] * 1e3, "min_us": pat_spmv[1] * 1e3,
-                                            "gbps": b_spmv_launch / (pat_spmv[0] * 1e-3) / 1e9,
-                                            "bytes_per_launch": b_spmv_launch}
+                                            "gbps": b_spmv1 / (pat_spmv[0] * 1e-3) / 1e9,
+                                            "bytes_per_launch": b_spmv1}
     if tsqr_leg is not None and "error" not in tsqr_leg:
         # per step: P1 Gram + pass-A projection Gram + TSQR up (leaf sweep
         # "gram") + TSQR down (leaf sweep "apply") + tree levels ("other")
@@ -683,7 +692,8 @@ def timed_leg(ctx, r, s, K, W, basis, orth, dist):
     # the first timed step's matrix powers were prefetched by the untimed step
     # before it: SpMV per step = average launch x s
     per = {k: v[1] / KT for k, v in tm.items()}
-    per["spmv"] = tm["spmv"][1] / max(tm["spmv"][0], 1) * s
+    lpp = max(1, int(round(tm["spmv"][0] / KT)))
+    per["spmv"] = tm["spmv"][1] / max(tm["spmv"][0], 1) * lpp
     return {"outer_iters_per_s": K / elapsed, "ms_per_step": 1e3 * elapsed / K, "steps": K,
             "reorth_passes": "%d/%d" % (int(np.sum(flags[W:W + K])), K),
             "kernel_ms_per_step": per,
@@ -691,10 +701,24 @@ def timed_leg(ctx, r, s, K, W, basis, orth, dist):
             "kernel_launches": {k: v[0] for k, v in tm.items()}}
 
 
+def spmv_launch_bytes(fmt, npairpat, n_loc, s, lpp, b_csr):
+    """Algorithmic HBM bytes per SpMV-class launch when an outer iteration's
+    s powers take lpp launches: a row-pattern SpMV reads x and the row's key
+    (1 B per row with pair patterns / plane-march mask keys, 2 B otherwise) and
+    stores y; the fused plane-march powers (k_powers_planes) read x and the
+    keys once per launch for its s / lpp stored powers."""
+    if fmt != "pattern":
+        return b_csr
+    kb = 1 if npairpat else 2
+    return ((8 + kb) * lpp + 8 * s) * n_loc / lpp
+
+
 def leg_roofline(leg, fmt, npairpat, n_loc, nnz_loc, s):
     """SpMV GB/s and the roofline of the leg's dominant kernel class, from its
     HIP-event per-launch averages (the algorithmic bytes of DESIGN.md §3)."""
-    b_spmv = ((17 if npairpat else 18) * n_loc) if fmt == "pattern" else 12 * nnz_loc + 20 * n_loc + 4
+    lpp = max(1, int(round(leg["kernel_launches"]["spmv"] / 3)))
+    b_spmv = spmv_launch_bytes(fmt, npairpat, n_loc, s, lpp, 12 * nnz_loc + 20 * n_loc + 4)
+    leg["spmv_launches_per_step"] = lpp
     bytes_per = {"spmv": b_spmv, "gram": (2 * s + 1) * 8 * n_loc, "apply": (3 * s + 1) * 8 * n_loc}
     avg = leg["kernel_avg_launch_us"]
     per = {k: leg["kernel_ms_per_step"][k] for k in bytes_per}
