@@ -551,9 +551,7 @@ def main():
     b_csr = 12 * nnz_local + 20 * n_loc + 4
     #   pair patterns: 1 B of id per row (one 2-B id per row pair)
     b_spmv1 = (17 if npairpat else 18) * n_loc if fmt == "pattern" else b_csr
-    #   fused powers (k_powers_planes, schedule 5): F powers per launch read x
-    #   and the row keys once and store F columns: (8 + 1 + 8 F) B per row
-    lpp = max(1, int(round(spmv_cnt / KT)))  # SpMV-class launches per outer iteration
+    lpp = max(1, ctx.powers_launches())  # SpMV-class launches per outer iteration
     b_spmv_launch = spmv_launch_bytes(fmt, npairpat, n_loc, s, lpp, b_csr)
     b_apply = (2 * s + 1 + s) * 8 * n_loc
     b_gram = (2 * s + 1) * 8 * n_loc
@@ -561,9 +559,7 @@ def main():
     # (the first timed step's powers were prefetched untimed: SpMV = avg launch x s)
     per_step = {"spmv": spmv_avg_ms * lpp, "gram": gram_ms / KT, "apply": apply_ms / KT}
     dominant = max(per_step, key=per_step.get)
-    fused = sched == 5
     dom = {"spmv": (b_spmv_launch, spmv_avg_ms,
-                    ("k_powers_planes (%d Newton powers per launch on the plane march)" % (s // lpp)) if fused else
                     ("k_spmv_planes / k_spmv_pair (row-pattern SpMV + Newton shift)"
                      if npairpat else "k_spmv_pat_lds (row-pattern SpMV + Newton shift)")
                     if fmt == "pattern" else "k_spmv (CSR-stream SpMV + Newton shift)"),
@@ -692,21 +688,22 @@ def timed_leg(ctx, r, s, K, W, basis, orth, dist):
     # the first timed step's matrix powers were prefetched by the untimed step
     # before it: SpMV per step = average launch x s
     per = {k: v[1] / KT for k, v in tm.items()}
-    lpp = max(1, int(round(tm["spmv"][0] / KT)))
+    lpp = max(1, ctx.powers_launches())
     per["spmv"] = tm["spmv"][1] / max(tm["spmv"][0], 1) * lpp
     return {"outer_iters_per_s": K / elapsed, "ms_per_step": 1e3 * elapsed / K, "steps": K,
             "reorth_passes": "%d/%d" % (int(np.sum(flags[W:W + K])), K),
             "kernel_ms_per_step": per,
             "kernel_avg_launch_us": {k: 1e3 * v[1] / max(v[0], 1) for k, v in tm.items()},
-            "kernel_launches": {k: v[0] for k, v in tm.items()}}
+            "kernel_launches": {k: v[0] for k, v in tm.items()},
+            "spmv_launches_per_step": lpp}
 
 
 def spmv_launch_bytes(fmt, npairpat, n_loc, s, lpp, b_csr):
     """Algorithmic HBM bytes per SpMV-class launch when an outer iteration's
     s powers take lpp launches: a row-pattern SpMV reads x and the row's key
     (1 B per row with pair patterns / plane-march mask keys, 2 B otherwise) and
-    stores y; the fused plane-march powers (k_powers_planes) read x and the
-    keys once per launch for its s / lpp stored powers."""
+    stores y (a launch that computed several powers would read x and the keys
+    once for its s / lpp stored powers)."""
     if fmt != "pattern":
         return b_csr
     kb = 1 if npairpat else 2
@@ -716,9 +713,8 @@ def spmv_launch_bytes(fmt, npairpat, n_loc, s, lpp, b_csr):
 def leg_roofline(leg, fmt, npairpat, n_loc, nnz_loc, s):
     """SpMV GB/s and the roofline of the leg's dominant kernel class, from its
     HIP-event per-launch averages (the algorithmic bytes of DESIGN.md §3)."""
-    lpp = max(1, int(round(leg["kernel_launches"]["spmv"] / 3)))
+    lpp = leg["spmv_launches_per_step"]
     b_spmv = spmv_launch_bytes(fmt, npairpat, n_loc, s, lpp, 12 * nnz_loc + 20 * n_loc + 4)
-    leg["spmv_launches_per_step"] = lpp
     bytes_per = {"spmv": b_spmv, "gram": (2 * s + 1) * 8 * n_loc, "apply": (3 * s + 1) * 8 * n_loc}
     avg = leg["kernel_avg_launch_us"]
     per = {k: leg["kernel_ms_per_step"][k] for k in bytes_per}

@@ -82,6 +82,7 @@ SIGNATURES = [
     ("cal_set_mpk_depth", c_int, [c_void_p, c_int]),
     ("cal_mpk_info", c_int, [c_void_p, ip, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64)]),
     ("cal_mpk_schedule", c_int, [c_void_p, ip]),
+    ("cal_powers_launches", c_int, [c_void_p, ip]),
     ("cal_tsqr_fold_stats", c_int, [c_void_p, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong),
                                      ctypes.POINTER(ctypes.c_double)]),
     ("cal_set_tsqr_fold_tol", c_int, [c_void_p, ctypes.c_double]),

@@ -72,13 +72,18 @@ class Context:
     MPK_SCHEDULES = {-1: "none", 0: "one exchange per SpMV", 1: "one deep exchange",
                      2: "one deep exchange overlapped with the interior powers",
                      3: "split schedule, no exchange (single-rank stand-in band)",
-                     4: "one deep exchange on the host-staged comm thread overlapped with the interior powers",
-                     5: "one slab, up to 4 powers per launch on the fused plane march"}
+                     4: "one deep exchange on the host-staged comm thread overlapped with the interior powers"}
 
     def mpk_schedule(self):
         """Schedule the last matrix-powers call took (cal_mpk_schedule)."""
         v = ctypes.c_int()
         check(self.h, lib.cal_mpk_schedule(self.h, ctypes.byref(v)))
+        return v.value
+
+    def powers_launches(self):
+        """SpMV-class launches of the last matrix-powers call (cal_powers_launches)."""
+        v = ctypes.c_int()
+        check(self.h, lib.cal_powers_launches(self.h, ctypes.byref(v)))
         return v.value
 
     def tsqr_fold_stats(self):

@@ -206,12 +206,6 @@ struct LanczosState;  // lanczos.cpp
 // Launchers (kernels.hip).  All enqueue on `st` and return hipError_t.
 hipError_t launch_spmv(const SpmvArgs& a, hipStream_t st);
 hipError_t launch_spmv_pat(const PatArgs& a, hipStream_t st);
-// fused matrix powers on the plane march (k_powers_planes): the most powers
-// one launch takes for this matrix (0: not eligible), and the launch of F
-// consecutive powers (power k -> y[k-1], shift / im2 / mode per power)
-int powers_planes_fmax(const PatArgs& a);
-hipError_t launch_powers_planes(const PatArgs& a, int F, double* const* y, const double* shift, const double* im2,
-                                const int* mode, hipStream_t st);
 // C (wa x wb, column-major ldc = 16*ceil(wa/16)) partials; see kernels.hip.
 struct GramPlan {
     int nta;    // A tiles of 16 columns
@@ -451,8 +445,8 @@ struct cal_ctx {
     // schedule of the last powers_dev call (cal_mpk_schedule): 0 one halo
     // exchange per SpMV, 1 one deep exchange, 2 deep exchange on the RCCL
     // stream overlapped with the interior powers, 3 split schedule with a
-    // synchronous exchange, 4 the host-staged twin of 2, 5 fused powers on
-    // the plane march (one slab); -1 none yet
+    // synchronous exchange, 4 the host-staged twin of 2; -1 none yet
+    int powers_launches = 0;   // SpMV-class launches of the last powers_dev call
     int powers_schedule = -1;  // ghost depth of the distributed matrix-powers kernel (next set_matrix; 1 = off)
     bool orth_coef_device = true;  // block-orth s x s algebra on the device (blockorth.cpp)
     // set by lanczos_step: work to enqueue after a block orthogonalisation is

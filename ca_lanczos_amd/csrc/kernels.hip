@@ -112,10 +112,6 @@ __global__ __launch_bounds__(kSpmvThreads) void k_spmv(SpmvArgs a) {
     const int tid = threadIdx.x;
     const int r0 = a.blk[b], r1 = a.blk[b + 1];
     const int p0 = a.rowptr[r0], p1 = a.rowptr[r1];
-    // the lane's own row bounds, loaded next to the block's (not after the
-    // barrier: one dependent round trip less per row block)
-    const int r = r0 + tid;
-    const int rq0 = a.rowptr[min(r, r1)], rq1 = a.rowptr[min(r + 1, r1)];
     const int cnt = p1 - p0;
     if (cnt <= kSpmvNnz) {
         if (cnt > 0) {
@@ -147,8 +143,9 @@ __global__ __launch_bounds__(kSpmvThreads) void k_spmv(SpmvArgs a) {
                 }
         }
         __syncthreads();
+        const int r = r0 + tid;
         if (r < r1) {
-            const int q0 = rq0 - p0, q1 = rq1 - p0;
+            const int q0 = a.rowptr[r] - p0, q1 = a.rowptr[r + 1] - p0;
             double sum = 0.0;
             for (int j = q0; j < q1; ++j) sum = sum + prod[j];
             a.y[r] = spmv_epilogue<MODE>(sum, a, r);
@@ -1306,338 +1303,6 @@ hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64
 #undef CAL_PRM
     };
     go(std::integral_constant<int, kResidCpb>{}, std::integral_constant<int, kResidPpt>{});
-    return hipGetLastError();
-}
-
-// --------------------------------------------------------------------------
-// Fused matrix powers on the plane march: F consecutive powers of the Newton
-// (or monomial) basis in one launch (matrix_powers_newton.m:31-47,
-// matrix_powers_monomial.m:6-12), each bit-identical to a k_spmv_planes /
-// k_spmv_pair launch.  Power k (1..F) is kept in LDS only as long as power
-// k+1 needs it, so per row HBM sees one read of x, F stores and the row keys
-// instead of F reads, F stores and F key reads.
-//
-// Geometry: a block owns the rows xy0 .. xy0 + R - 1 of the
-// planes z0 .. z1 - 1.  Power F is computed on exactly those rows; power k on
-// a window widened by (F - k) H rows on either side of the strip (the rows
-// power k + 1 reads in-plane), power 0 (x) is staged on R + 2 F H rows.  The
-// block walks t upwards; at step t it stages x's plane t + 1 and computes
-// power k on plane t - k + 1 (k = 1 .. F), from power k - 1's planes
-// t - k .. t - k + 2, which stay in a 3-plane LDS ring per power.  Power k
-// also runs on F - k planes before z0 and after z1 (the planes power k + 1
-// reads across the block's z ends).  Window positions map linearly to rows
-// (row = z P + xy0 - (F - k) H + i), so a window that runs past the plane's
-// end holds the next plane's rows, with their own keys and neighbours: the
-// values of every row power F depends on are exact, whatever slots the rows
-// have.  Rows outside [0, n) have key 0 (mask 0 / a pattern whose entries
-// are selected by the mask) and are never a present slot of a row inside.
-// x is staged from the even row at or below the window start (16-B pair
-// loads never straddle row 0), so ring-0 plane z is offset by del(z) =
-// (window start) & 1.  Keys are staged for power 1's window (F + 2 planes in
-// flight: plane z's keys serve power 1 at step z up to power F at step
-// z + F - 1).
-// --------------------------------------------------------------------------
-constexpr int kPowMaxF = 4;
-
-struct PowersArgs {
-    PatArgs a;                    // tables; a.x = power 0, a.xprev = power -1 (MODE 2 at k = 1)
-    double* y[kPowMaxF];          // power k -> y[k - 1]
-    double shift[kPowMaxF], im2[kPowMaxF];
-    int mode[kPowMaxF];
-    int R, Z;                     // rows of a plane per block strip (even), planes per block
-};
-
-__host__ __device__ inline int pow_w0s(int R, int H, int F) { return R + 2 * F * H + 2; }
-__host__ __device__ inline int pow_kdw(int R, int H, int F, int KB) { return (((R + 2 * (F - 1) * H) * KB + 6) >> 2) + 1; }
-
-static size_t powers_lds_bytes(int R, int H, int F, int KB, int npat, int L2) {
-    size_t d = 3 * (size_t)pow_w0s(R, H, F);
-    for (int k = 1; k < F; ++k) d += 3 * (size_t)(R + 2 * (F - k) * H);
-    size_t kd = (size_t)(F + 2) * pow_kdw(R, H, F, KB);
-    kd += kd & 1;
-    return d * 8 + kd * 4 + (size_t)npat * L2 * 8 + (size_t)npat + 16;
-}
-
-template <int MAXLEN, int F, int KM>
-__global__ __launch_bounds__(256) void k_powers_planes(PowersArgs pa) {
-    extern __shared__ __attribute__((aligned(16))) double lds_pw[];
-    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-    constexpr int KB = KM == 2 ? 2 : 1;
-    constexpr int L2 = (MAXLEN + 1) & ~1;
-    constexpr int KR = F + 2;
-    const int tid = threadIdx.x;
-    const int P = (int)pa.a.plane_P, H = pa.a.plane_H, n = (int)pa.a.n, ld = (int)pa.a.ld, R = pa.R;
-    const int nxy = (P + R - 1) / R, nz = (n + P - 1) / P;
-    const int bi = xcd_remap(blockIdx.x, gridDim.x);
-    const int xy0 = (bi % nxy) * R, z0 = (bi / nxy) * pa.Z;
-    const int z1 = min(z0 + pa.Z, nz);
-    const int xyend = min(xy0 + R, P);  // owned rows of a plane: [xy0, xyend)
-    // LDS: ring 0 (3 x W0s), rings 1 .. F-1 (3 x W[k]), keys (KR x KDW dwords), tables
-    const int W0s = pow_w0s(R, H, F), WP0 = W0s / 2, nk0 = (WP0 + 255) / 256;
-    const int KDW = pow_kdw(R, H, F, KB);
-    int W[F], base[F], rings_end = 3 * W0s;
-    base[0] = 0;
-    W[0] = W0s;
-#pragma unroll
-    for (int k = 1; k < F; ++k) {
-        W[k] = R + 2 * (F - k) * H;
-        base[k] = rings_end;
-        rings_end += 3 * W[k];
-    }
-    uint32_t* keys = reinterpret_cast<uint32_t*>(lds_pw + rings_end);
-    const int kdtot = KR * KDW + ((KR * KDW) & 1);
-    double* s_rz = reinterpret_cast<double*>(keys + kdtot);
-    uint8_t* s_rm = reinterpret_cast<uint8_t*>(s_rz + pa.a.npat * L2);
-    if (KM != 0) {
-        for (int i = tid; i < pa.a.npat * L2; i += 256) {
-            const int q = i / L2, e = i % L2;
-            s_rz[i] = e < MAXLEN ? pa.a.rzval[q * MAXLEN + e] : 0.0;
-        }
-        for (int i = tid; i < pa.a.npat; i += 256) s_rm[i] = pa.a.rzmask[i];
-    }
-    int ps[MAXLEN];
-    double cv[MAXLEN];
-#pragma unroll
-    for (int e = 0; e < MAXLEN; ++e) {
-        ps[e] = pa.a.pslot[e];
-        cv[e] = pa.a.cval[e];
-    }
-    const unsigned fullm = (1u << MAXLEN) - 1u;
-    const __amdgpu_buffer_rsrc_t rx = PlaneMarch<MAXLEN, KM>::rsrc(pa.a.x, (int64_t)ld * 8);
-    const void* keyp = KM == 0 ? (const void*)pa.a.rowmask : (KM == 1 ? (const void*)pa.a.rowkey8 : (const void*)pa.a.pat);
-    const __amdgpu_buffer_rsrc_t rk = PlaneMarch<MAXLEN, KM>::rsrc(keyp, (KB * (int64_t)n + 7) & ~(int64_t)3);
-
-    auto slot3 = [](int z) { return (z + 3 * 64) % 3; };
-    auto slotk = [](int z) { return (z + KR * 64) % KR; };
-    // window start rows: x (power 0) and the keys (power 1's window)
-    auto xstart = [&](int z) { return z * P + xy0 - F * H; };
-    auto kstart = [&](int z) { return (z * P + xy0 - (F - 1) * H) * KB; };
-
-    double2 st[3];
-    uint32_t kst[2];
-    auto load = [&](int z) {
-        const int g = xstart(z) & ~1;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            if (k < nk0) {
-                const int row = g + 2 * min(tid + 256 * k, WP0 - 1);
-                const uint32_t off = row >= 0 && row < ld ? (uint32_t)row * 8u : 0xFFFFFFF0u;
-                const u4 w = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)off, 0, 0);
-                st[k] = make_double2(__builtin_bit_cast(double, ((uint64_t)w.y << 32) | w.x),
-                                     __builtin_bit_cast(double, ((uint64_t)w.w << 32) | w.z));
-            }
-        }
-        const int al = kstart(z) & ~3;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            if (256 * k < KDW) {
-                const int dw = al + 4 * min(tid + 256 * k, KDW - 1);
-                kst[k] = __builtin_amdgcn_raw_buffer_load_b32(rk, dw >= 0 ? dw : (int)0xFFFFFFF0u, 0, 0);
-            }
-        }
-    };
-    auto store = [&](int z) {
-        double* w = lds_pw + slot3(z) * W0s;
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-            if (k < nk0) *reinterpret_cast<double2*>(w + 2 * min(tid + 256 * k, WP0 - 1)) = st[k];
-        uint32_t* kk = keys + slotk(z) * KDW;
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-            if (256 * k < KDW) kk[min(tid + 256 * k, KDW - 1)] = kst[k];
-    };
-    // power kk's plane z, window position i (power kk - 1 is read at i + H)
-    auto level = [&](auto kc, int z) {
-        constexpr int kk = decltype(kc)::value;
-        const int Wk = R + 2 * (F - kk) * H;
-        const int dc = kk == 1 ? (xstart(z) & 1) : 0, dp = kk == 1 ? (xstart(z - 1) & 1) : 0,
-                  dn = kk == 1 ? (xstart(z + 1) & 1) : 0;
-        const double* src = lds_pw + base[kk - 1];
-        const int sw = W[kk - 1];
-        const double* sc = src + slot3(z) * sw + dc + H;
-        const double* sp = src + slot3(z - 1) * sw + dp + H;
-        const double* sn = src + slot3(z + 1) * sw + dn + H;
-        const uint8_t* kp = reinterpret_cast<const uint8_t*>(keys + slotk(z) * KDW) + (kstart(z) & 3) + (kk - 1) * H * KB;
-        const double* xq = nullptr;  // power kk - 2 (MODE 2), kk >= 2
-        if (kk >= 2) xq = lds_pw + base[kk >= 2 ? kk - 2 : 0] + slot3(z) * W[kk >= 2 ? kk - 2 : 0] +
-                          (kk == 2 ? (xstart(z) & 1) : 0) + 2 * H;
-        const int md = pa.mode[kk - 1];
-        const double sh = pa.shift[kk - 1], im = pa.im2[kk - 1];
-        double* yo = pa.y[kk - 1];
-        const bool own_z = z >= z0 && z < z1;
-        double* dst = kk < F ? lds_pw + base[kk < F ? kk : 0] + slot3(z) * W[kk < F ? kk : 0] : nullptr;
-        const int row0 = z * P + xy0 - (F - kk) * H;
-        for (int pp = tid; pp < Wk / 2; pp += 256) {
-            const int i = 2 * pp;
-            unsigned k0, k1;
-            if (KB == 1) {
-                k0 = kp[i];
-                k1 = kp[i + 1];
-            } else {
-                k0 = *reinterpret_cast<const uint16_t*>(kp + 2 * i);
-                k1 = *reinterpret_cast<const uint16_t*>(kp + 2 * i + 2);
-            }
-            const unsigned m0 = KM == 0 ? k0 : s_rm[k0], m1 = KM == 0 ? k1 : s_rm[k1];
-            const double* c0 = s_rz + (KM == 0 ? 0 : k0 * L2);
-            const double* c1 = s_rz + (KM == 0 ? 0 : k1 * L2);
-            auto slotv = [&](int e) {
-                if (e == 0) return make_double2(sp[i], sp[i + 1]);
-                if (e == MAXLEN - 1) return make_double2(sn[i], sn[i + 1]);
-                return make_double2(sc[i + ps[e]], sc[i + ps[e] + 1]);
-            };
-            const bool interior = __builtin_amdgcn_ballot_w64((m0 & m1) != fullm) == 0;
-            double y0 = 0.0, y1 = 0.0;
-            if (interior) {
-#pragma unroll
-                for (int e = 0; e < MAXLEN; ++e) {
-                    const double2 v = slotv(e);
-                    const double t0 = (KM == 0 ? cv[e] : c0[e]) * v.x, t1 = (KM == 0 ? cv[e] : c1[e]) * v.y;
-                    y0 = y0 + t0;
-                    y1 = y1 + t1;
-                }
-            } else {
-#pragma unroll
-                for (int e = 0; e < MAXLEN; ++e) {
-                    const double2 v = slotv(e);
-                    const double t0 = (KM == 0 ? cv[e] : c0[e]) * v.x, t1 = (KM == 0 ? cv[e] : c1[e]) * v.y;
-                    double s0 = y0 + t0, s1 = y1 + t1;
-                    asm volatile("" : "+v"(s0), "+v"(s1));
-                    y0 = ((m0 >> e) & 1u) ? s0 : y0;
-                    y1 = ((m1 >> e) & 1u) ? s1 : y1;
-                }
-            }
-            const int r = row0 + i;
-            if (md != 0) {
-                const double u0 = sh * sc[i], u1 = sh * sc[i + 1];
-                y0 = y0 - u0;
-                y1 = y1 - u1;
-                if (md == 2) {
-                    double q0, q1;
-                    if (kk == 1) {
-                        q0 = r >= 0 && r < n ? pa.a.xprev[r] : 0.0;
-                        q1 = r + 1 >= 0 && r + 1 < n ? pa.a.xprev[r + 1] : 0.0;
-                    } else {
-                        q0 = xq[i];
-                        q1 = xq[i + 1];
-                    }
-                    const double w0 = im * q0, w1 = im * q1;
-                    y0 = y0 + w0;
-                    y1 = y1 + w1;
-                }
-            }
-            if (kk < F) *reinterpret_cast<double2*>(dst + i) = make_double2(y0, y1);
-            if (own_z) {
-                const int xy = xy0 - (F - kk) * H + i;
-                const bool o0 = xy >= xy0 && xy < xyend && r < n, o1 = xy + 1 >= xy0 && xy + 1 < xyend && r + 1 < n;
-                if (o0 && o1) st16(yo + r, make_double2(y0, y1));
-                else if (o0) yo[r] = y0;
-                else if (o1) yo[r + 1] = y1;
-            }
-        }
-    };
-
-    const int tA = z0 - F + 1, tB = z1 + F - 2;
-    load(tA - 1);
-    store(tA - 1);
-    load(tA);
-    store(tA);
-    load(tA + 1);
-    for (int t = tA; t <= tB; ++t) {
-        store(t + 1);
-        if (t + 2 <= tB + 1) load(t + 2);
-        __syncthreads();
-        level(std::integral_constant<int, 1>{}, t);
-        if constexpr (F >= 2) {
-            __syncthreads();
-            if (t - 1 >= z0 - (F - 2)) level(std::integral_constant<int, 2>{}, t - 1);
-        }
-        if constexpr (F >= 3) {
-            __syncthreads();
-            if (t - 2 >= z0 - (F - 3)) level(std::integral_constant<int, (F >= 3 ? 3 : 1)>{}, t - 2);
-        }
-        if constexpr (F >= 4) {
-            __syncthreads();
-            if (t - 3 >= z0 - (F - 4)) level(std::integral_constant<int, (F >= 4 ? 4 : 1)>{}, t - 3);
-        }
-        // power 2 in MODE 2 reads x's plane t - 1, whose ring-0 slot the next
-        // step's store overwrites; with F > 2 a barrier follows it anyway
-        if (F == 2 && pa.mode[1] == 2) __syncthreads();
-    }
-}
-
-// Powers per launch of the fused march for this matrix (0: not eligible):
-// the plane-march tables, the strip geometry and LDS within the budget.
-static int powers_geometry(const PatArgs& a, int F, int& R, int& Z, size_t& lds) {
-    const int64_t P = a.plane_P, H = a.plane_H;
-    const int nstrip = (int)((P + kResidPlaneRows - 1) / kResidPlaneRows);
-    R = (int)((P + nstrip - 1) / nstrip);
-    R += R & 1;
-    const int KB = a.cuniform ? 1 : (a.npat <= 256 ? 1 : 2);
-    if ((int64_t)F * H > 512 || pow_kdw(R, (int)H, F, KB) > 512) return 0;
-    lds = powers_lds_bytes(R, (int)H, F, KB, a.cuniform ? 0 : a.npat, 8);
-    if (lds > 64 * 1024) return 0;
-    // planes per block: about three resident rounds of blocks
-    const int64_t nz = (a.n + P - 1) / P;
-    const char* e = std::getenv("CAL_POW_Z");
-    Z = e ? std::atoi(e) : (F >= 4 ? 32 : 16);
-    if (Z < 1) Z = 1;
-    if (Z > nz) Z = (int)nz;
-    return F;
-}
-
-int powers_planes_fmax(const PatArgs& a) {
-    if (!planes_ok(a)) return 0;
-    const char* e = std::getenv("CAL_POW_FMAX");
-    const int cap = e ? std::atoi(e) : kPowMaxF;
-    for (int F = std::min(cap, kPowMaxF); F >= 2; --F) {
-        int R, Z;
-        size_t lds;
-        if (powers_geometry(a, F, R, Z, lds)) return F;
-    }
-    return 0;
-}
-
-hipError_t launch_powers_planes(const PatArgs& a, int F, double* const* y, const double* shift, const double* im2,
-                                const int* mode, hipStream_t st) {
-    PowersArgs pa;
-    pa.a = a;
-    int R = 0, Z = 0;
-    size_t lds = 0;
-    if (F < 2 || F > kPowMaxF || !planes_ok(a) || !powers_geometry(a, F, R, Z, lds)) return hipErrorInvalidValue;
-    for (int k = 0; k < kPowMaxF; ++k) {
-        pa.y[k] = k < F ? y[k] : nullptr;
-        pa.shift[k] = k < F ? shift[k] : 0.0;
-        pa.im2[k] = k < F ? im2[k] : 0.0;
-        pa.mode[k] = k < F ? mode[k] : 0;
-    }
-    pa.R = R;
-    pa.Z = Z;
-    const int64_t nxy = (a.plane_P + R - 1) / R, nz = (a.n + a.plane_P - 1) / a.plane_P;
-    dim3 g((unsigned)(nxy * ((nz + Z - 1) / Z))), b(256);
-    auto go = [&](auto fc, auto km) {
-        constexpr int FF = decltype(fc)::value, KM = decltype(km)::value;
-#define CAL_PWL(ML) hipLaunchKernelGGL((k_powers_planes<ML, FF, KM>), g, b, lds, st, pa)
-        switch (a.pmaxlen) {
-            case 2: CAL_PWL(2); break;
-            case 3: CAL_PWL(3); break;
-            case 4: CAL_PWL(4); break;
-            case 5: CAL_PWL(5); break;
-            case 6: CAL_PWL(6); break;
-            case 7: CAL_PWL(7); break;
-            default: CAL_PWL(8); break;
-        }
-#undef CAL_PWL
-    };
-    auto gk = [&](auto fc) {
-        if (a.cuniform) go(fc, std::integral_constant<int, 0>{});
-        else if (a.npat <= 256) go(fc, std::integral_constant<int, 1>{});
-        else go(fc, std::integral_constant<int, 2>{});
-    };
-    switch (F) {
-        case 2: gk(std::integral_constant<int, 2>{}); break;
-        case 3: gk(std::integral_constant<int, 3>{}); break;
-        default: gk(std::integral_constant<int, 4>{}); break;
-    }
     return hipGetLastError();
 }
 

@@ -682,6 +682,7 @@ static int64_t mpk_fake_band() {
 int powers_dev(cal_ctx* c, int s, const double* q, double* const* Y, const double* shift, const double* im2,
                const double* const* xprev) {
     const DevMatrix& A = c->A;
+    c->powers_launches = s;  // one SpMV-class launch per power
     auto mode_of = [&](int j) { return shift ? ((im2 && im2[j] != 0.0) ? 2 : 1) : 0; };
     auto launch = [&](int j, const PowRange& r1, const PowRange& r2) {  // power j (1-based)
         return spmv_range2(c, r1.o, r1.len, r2.o, r2.len, j == 1 ? q : Y[j - 2], Y[j - 1], mode_of(j - 1),
@@ -692,45 +693,6 @@ int powers_dev(cal_ctx* c, int s, const double* q, double* const* Y, const doubl
     const int64_t fake = (!mpk && !A.mpk && A.use_pat && s > 1 && A.nghost == 0) ? mpk_fake_band() : 0;
     if (!mpk && fake <= 0) {
         c->powers_schedule = 0;
-        if (A.use_pat && s >= 2 && (!c->comm || c->comm->nranks <= 1)) {
-            // F powers per launch on the plane march (k_powers_planes); power
-            // j's MODE-2 predecessor must be the power two before it inside a
-            // launch (as matrix_powers_newton.m:40-41 has it)
-            const PatArgs p0 = pat_args(A, A.ext_off, A.n_local, q, nullptr, 0, 0.0, 0.0, nullptr);
-            const int fmax = powers_planes_fmax(p0);
-            if (fmax >= 2) {
-                c->powers_schedule = 5;
-                int j = 0;
-                while (j < s) {
-                    int f = std::min(fmax, s - j);
-                    for (int k = 1; k < f; ++k)
-                        if (mode_of(j + k) == 2 && (!xprev || xprev[j + k] != (j + k == 1 ? q : Y[j + k - 2]))) {
-                            f = k;
-                            break;
-                        }
-                    if (f == 1) {
-                        CAL_TRY(spmv_dev(c, j == 0 ? q : Y[j - 1], Y[j], mode_of(j), shift ? shift[j] : 0.0,
-                                         im2 ? im2[j] : 0.0, xprev ? xprev[j] : nullptr));
-                        ++j;
-                        continue;
-                    }
-                    PatArgs p = pat_args(A, A.ext_off, A.n_local, j == 0 ? q : Y[j - 1], nullptr, 0, 0.0, 0.0,
-                                         xprev ? xprev[j] : nullptr);
-                    double sh[4], i2[4];
-                    int md[4];
-                    for (int k = 0; k < f; ++k) {
-                        sh[k] = shift ? shift[j + k] : 0.0;
-                        i2[k] = im2 ? im2[j + k] : 0.0;
-                        md[k] = mode_of(j + k);
-                    }
-                    const int t = timer_begin(c, 0);
-                    CAL_HIP(c, launch_powers_planes(p, f, Y + j, sh, i2, md, c->stream));
-                    timer_end(c, t);
-                    j += f;
-                }
-                return 0;
-            }
-        }
         for (int j = 0; j < s; ++j)
             CAL_TRY(spmv_dev(c, j == 0 ? q : Y[j - 1], Y[j], mode_of(j), shift ? shift[j] : 0.0,
                              im2 ? im2[j] : 0.0, xprev ? xprev[j] : nullptr));
@@ -1056,6 +1018,12 @@ int cal_set_tsqr_fold_tol(cal_ctx* c, double tol) {
 int cal_mpk_schedule(cal_ctx* c, int* schedule) {
     if (!c || !schedule) return CAL_ERR_ARG;
     *schedule = c->powers_schedule;
+    return 0;
+}
+
+int cal_powers_launches(cal_ctx* c, int* launches) {
+    if (!c || !launches) return CAL_ERR_ARG;
+    *launches = c->powers_launches;
     return 0;
 }
 

@@ -86,9 +86,12 @@ int cal_mpk_info(cal_ctx* ctx, int* depth, int64_t* band_l, int64_t* band_r, int
  * with the interior powers, 3 the split schedule without an exchange (one
  * rank, CAL_MPK_FAKE_BAND), 4 the host-staged twin of 2 (the exchange's
  * copies on the communicator's stream, its callbacks on a comm thread, the
- * same ev_q / ev_halo event graph), 5 one slab, up to 4 powers per launch
- * on the fused plane march (k_powers_planes); -1 before the first call. */
+ * same ev_q / ev_halo event graph); -1 before the first call. */
 int cal_mpk_schedule(cal_ctx* ctx, int* schedule);
+/* SpMV-class kernel launches the last matrix-powers call made on this rank
+ * (one per power: split schedules count their powers, not their two-range
+ * pieces); 0 before the first call. */
+int cal_powers_launches(cal_ctx* ctx, int* launches);
 /* Device storage of A, chosen at the next cal_set_matrix_*: "auto" (default:
  * row patterns when A has <= 65535 distinct rows of <= 32 entries, else
  * CSR), "csr", or "pattern".  Both are lossless and give bit-identical SpMV

@@ -1046,63 +1046,3 @@ def test_production_library_has_no_test_hooks(cal, ref):
     p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-2000:]
     assert p.stdout.strip().splitlines()[-1] == "0"
-
-
-# ---------------------------------------------------------------- a2/a3 fused powers
-def _alt_diag_2d(cal, N):
-    """5-point Laplacian plus 0.5 on every other diagonal entry: slot values
-    that are not uniform per slot (the fused march's pattern-id keys)."""
-    A = cal.matrices.laplacian_2d(N).tolil()
-    d = np.zeros(N * N)
-    d[::2] = 0.5
-    A.setdiag(A.diagonal() + d)
-    return A.tocsr()
-
-
-@pytest.mark.parametrize("name,s,lam,modifiedp", [
-    ("lap3d_25", 8, None, 0),                                   # F = 4, odd plane stride
-    ("lap3d_25", 7, "real", 0),                                 # 4 + 3
-    ("lap3d_25", 8, "complex", 1),                              # MODE 2 on powers 2 and 4 of a launch
-    ("lap3d_25", 8, "complex1", 1),                             # MODE 2 on a launch's first power
-    ("lap3d_151", 8, "real", 0),                                # F = 2 (in-plane reach 152)
-    ("lap3d_151", 6, "complex", 1),                             # MODE 2 on F = 2's second power
-    ("lap3d_151", 7, "complex1", 1),
-    ("lap2d_301", 8, "real", 0),                                # F = 4, reach 2
-    ("lap2d_301", 5, "complex", 1),                             # 4 + 1
-    ("lap2d_256", 8, None, 0),
-    ("alt2d_300", 8, "real", 0),                                # pattern-id keys
-])
-def test_matrix_powers_fused_planes_bitexact(cal, ref, name, s, lam, modifiedp):
-    """The fused plane-march matrix powers (k_powers_planes, schedule 5)
-    against the oracle's sequential SpMV recurrences, bit for bit
-    (matrix_powers_monomial.m:6-12, matrix_powers_newton.m:15-54)."""
-    kind, N = name.split("_")
-    N = int(N)
-    A = {"lap3d": cal.matrices.laplacian_3d, "lap2d": cal.matrices.laplacian_2d,
-         "alt2d": lambda m: _alt_diag_2d(cal, m)}[kind](N)
-    n = A.shape[0]
-    ctx = cal.Context().set_matrix(A)
-    v = ref.matlab_rand(n, seed=11)
-    if lam is None:
-        q = v / np.linalg.norm(v)
-        got = cal.matrix_powers_monomial(A, q, s, ctx=ctx)
-        exp = ref.matrix_powers_monomial(A, q, s)
-    else:
-        hi = 12.0 if kind == "lap3d" else 8.0
-        if lam == "real":
-            shifts = np.linspace(0.1, hi, s)[np.random.RandomState(s).permutation(s)]
-        else:
-            shifts = [hi * 0.9] if lam == "complex1" else []
-            while len(shifts) < s:
-                if len(shifts) + 2 <= s:
-                    c = hi * (0.2 + 0.1 * len(shifts)) + 0.3j * (1 + len(shifts))
-                    shifts += [c, np.conj(c)]
-                else:
-                    shifts.append(hi * 0.05)
-            shifts = np.array(shifts)
-        got = cal.matrix_powers_newton(A, v, s, shifts, modifiedp, ctx=ctx)
-        exp = ref.matrix_powers_newton(A, v, s, shifts, modifiedp)
-    assert ctx.mpk_schedule() == 5, "the fused plane march did not run"
-    ctx.close()
-    bad = [j for j in range(got.shape[1]) if not np.array_equal(got[:, j], exp[:, j])]
-    assert not bad, "columns %s differ (max %.3e)" % (bad, np.max(np.abs(got - exp)))
