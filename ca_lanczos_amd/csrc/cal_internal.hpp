@@ -85,6 +85,7 @@ struct SpmvArgs {
     double im2;           //     + im2 * xprev
     int mode;             // 0: y = A x, 1: shifted, 2: shifted + im2 term
     int xcd;              // XCD-contiguous block order (set by launch_spmv)
+    int nt = 0;           // col / val loaded non-temporally (matrix larger than the Infinity Cache)
 };
 
 // Row-pattern storage ("PSR"): row r is pattern pat[r], a sequence of

@@ -181,12 +181,16 @@ static hipError_t launch_spmv_mode2(const SpmvArgs& a, int nit, hipStream_t st) 
     return hipGetLastError();
 }
 
-// plain loads, one nonzero per thread and iteration: non-temporal col / val
-// loads measured 200 vs 208 us on lap3d_215 in CSR but 31.5 vs 23.0 us on
-// circuit_1259, two nonzeros per thread slower on both (profiles/r04/csr_variants)
+// one nonzero per thread and iteration (two: slower on both matrices below).
+// col / val stream once per SpMV: when the matrix is larger than the
+// Infinity Cache (a.nt, set by spmv_dev) they are loaded non-temporally, so
+// the cache keeps x's lines for the neighbouring rows' gathers -- 200 vs
+// 208 us on lap3d_215 in CSR (1.03 GB); a matrix that fits (circuit_1259,
+// 123 MB) is still there at the next SpMV and keeps plain loads (23.0 us,
+// 31.5 non-temporal; profiles/r04/csr_variants)
 template <int MODE>
 static hipError_t launch_spmv_mode(const SpmvArgs& a, int nit, hipStream_t st) {
-    return launch_spmv_mode2<MODE, false, 1>(a, nit, st);
+    return a.nt ? launch_spmv_mode2<MODE, true, 1>(a, nit, st) : launch_spmv_mode2<MODE, false, 1>(a, nit, st);
 }
 
 hipError_t launch_spmv(const SpmvArgs& a0, hipStream_t st) {

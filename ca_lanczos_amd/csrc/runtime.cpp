@@ -629,6 +629,8 @@ int spmv_dev(cal_ctx* c, const double* x, double* y, int mode, double shift, dou
     a.shift = shift;
     a.im2 = im2;
     a.mode = mode | (c->A.nit << 8);
+    // col + val of the stored rows against the 256 MB Infinity Cache
+    a.nt = (int64_t)12 * c->A.nnz > ((int64_t)256 << 20) ? 1 : 0;
     const int t = timer_begin(c, 0);
     CAL_HIP(c, launch_spmv(a, c->stream));
     timer_end(c, t);
