@@ -2326,7 +2326,7 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int WPMAX, int MOUT, bool GRAM, bool APPLY = true, bool STORE = true, bool CHAIN = false>
+template <int WPMAX, int MOUT, bool GRAM, bool APPLY = true, bool STORE = true, bool CHAIN = false, bool NTS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_rowapply(ColList P, const double* __restrict__ M, int wp, int m,
                                                   OutList Y, int wq, int64_t n, double* __restrict__ partial) {
     constexpr int TLD = 17;  // padded LDS row (doubles)
@@ -2426,8 +2426,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         }
         if (APPLY && STORE && in) {
 #pragma unroll
-            for (int j = 0; j < MOUT; ++j)
-                if (j < m) yc[j][r] = y[j];
+            for (int j = 0; j < MOUT; ++j) {
+                if (j < m) {
+                    if constexpr (NTS) __builtin_nontemporal_store(y[j], &yc[j][r]);
+                    else yc[j][r] = y[j];
+                }
+            }
         }
         if (GRAM) {
             double* trow = tile + tid * TLD;
@@ -2495,15 +2499,26 @@ hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, co
                            int64_t n, int blocks, double* partial, hipStream_t st) {
     const int WP = rowapply_wpmax(wp), MO = rowapply_mout(m);
     dim3 g(blocks), b(256);
+    // pass B's block Q is read again only after the next step's matrix powers
+    // have streamed through the Infinity Cache (256 MB): when the sweep's
+    // columns do not fit it, Q is stored non-temporally, so its lines are not
+    // written back out of the cache during the powers (lap3d_215: 817/818 ->
+    // 828/829 outer-it/s, profiles/r04/passb_nt/)
+    const bool nts = (int64_t)n * 8 * (wp + m) > ((int64_t)256 << 20);
 #define CAL_RA(W, MM, G, S, C) \
     hipLaunchKernelGGL((k_rowapply<W, MM, G, true, S, C>), g, b, 0, st, P, dM, wp, m, Y, wq, n, partial)
+#define CAL_RA_NT(W, MM) \
+    hipLaunchKernelGGL((k_rowapply<W, MM, false, true, true, true, true>), g, b, 0, st, P, dM, wp, m, Y, wq, n, partial)
 #define CAL_RA_SHAPE(W, MM)                                  \
     case W * 100 + MM:                                       \
         switch (kind) {                                      \
             case 0: CAL_RA(W, MM, false, true, false); break; \
             case 1: CAL_RA(W, MM, true, true, false); break;  \
             case 2: CAL_RA(W, MM, true, false, false); break; \
-            default: CAL_RA(W, MM, false, true, true); break; \
+            default:                                         \
+                if (nts) CAL_RA_NT(W, MM);                   \
+                else CAL_RA(W, MM, false, true, true);       \
+                break;                                       \
         }                                                    \
         break;
     switch (WP * 100 + MO) {
@@ -2521,6 +2536,7 @@ hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, co
         default: return hipErrorInvalidValue;
     }
 #undef CAL_RA_SHAPE
+#undef CAL_RA_NT
 #undef CAL_RA
     return hipGetLastError();
 }

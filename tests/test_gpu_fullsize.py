@@ -61,6 +61,23 @@ def test_spmv_fullsize_bitexact(ctx3d, lap3d, ref):
     assert y.min() == 0.0 and y.max() == 3.0 and np.all(y == np.round(y))
 
 
+def test_spmv_fullsize_csr_nontemporal_bitexact(cal, lap3d, ref):
+    """lap3d_215 in plain CSR (1.03 GB of col / val, larger than the Infinity
+    Cache: the kernel's non-temporal loads) and a shifted SpMV, both bit-exact
+    against the sequential CSR SpMV (SpMV.m:8, matrix_powers_newton.m:32)."""
+    n = lap3d.shape[0]
+    ctx = cal.Context(spmv_format="csr").set_matrix(lap3d)
+    try:
+        assert ctx.spmv_format()[0] == "csr"
+        v = ref.matlab_rand(n, seed=9)
+        assert np.array_equal(ctx.spmv(v), ref.SpMV(lap3d, v))
+        lam = np.array([3.25, 7.5])
+        V = cal.matrix_powers_newton(lap3d, v, 2, lam, 0, ctx=ctx)
+        assert np.array_equal(V, ref.matrix_powers_newton(lap3d, v, 2, lam, 0))
+    finally:
+        ctx.close()
+
+
 def test_matrix_powers_newton_fullsize_bitexact(cal, ctx3d, lap3d, ref):
     n = lap3d.shape[0]
     v = ref.matlab_rand(n, seed=11)
