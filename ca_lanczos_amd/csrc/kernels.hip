@@ -2502,8 +2502,9 @@ hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, co
     // pass B's block Q is read again only after the next step's matrix powers
     // have streamed through the Infinity Cache (256 MB): when the sweep's
     // columns do not fit it, Q is stored non-temporally, so its lines are not
-    // written back out of the cache during the powers (lap3d_215: 817/818 ->
-    // 828/829 outer-it/s, profiles/r04/passb_nt/)
+    // written back out of the cache during the powers (lap3d_215, same-box
+    // A/Bs: 817/818 -> 828/829 and 847/847/846 -> 855/854/855 outer-it/s,
+    // profiles/r04/passb_nt/)
     const bool nts = (int64_t)n * 8 * (wp + m) > ((int64_t)256 << 20);
 #define CAL_RA(W, MM, G, S, C) \
     hipLaunchKernelGGL((k_rowapply<W, MM, G, true, S, C>), g, b, 0, st, P, dM, wp, m, Y, wq, n, partial)

@@ -734,7 +734,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FOLD_DOWN_W
     const int tid = threadIdx.x, lane = tid & 63, m = a.m, w = a.w;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: the tile's scalars by scalar loads
     const int64_t n = a.n;
-    const bool nts = n * 8 * (w + 2 * m) > ((int64_t)256 << 20);  // the sweep vs the Infinity Cache
     const int64_t ntiles = (n + FTR0 - 1) / FTR0;
     const int64_t tile = (int64_t)blockIdx.x * FTPB + wave;
     for (int e = tid; e < 9 * FM; e += 256) {
@@ -838,16 +837,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FOLD_DOWN_W
         }
         const int64_t r = base + lane + 64 * i;
         if (r < n) {
-            // Q is read again after the next step's matrix powers: stored
-            // non-temporally when the sweep does not fit the Infinity Cache
-            // (as k_rowapply's pass B)
+            // (plain stores: non-temporal ones, as pass B's, measured 704/707/703
+            // against 705/703/704 outer-it/s on the TSQR leg, profiles/r04/passb_nt/)
 #pragma unroll
-            for (int cc = 0; cc < FM; ++cc) {
-                if (cc < m) {
-                    if (nts) __builtin_nontemporal_store(o[cc], &Q.p[cc][r]);
-                    else Q.p[cc][r] = o[cc];
-                }
-            }
+            for (int cc = 0; cc < FM; ++cc)
+                if (cc < m) Q.p[cc][r] = o[cc];
         }
     }
 }
