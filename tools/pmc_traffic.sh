@@ -28,6 +28,6 @@ for grp in fetch write hit; do
     if [ -z "$BENCH_ONLY" ]; then
         run spmv $grp "${C[@]}" -- python3 $GRAFT_REPO_ROOT/tools/spmv_sweep.py --reps 10 || exit $?
     fi
-    run bench $grp "${C[@]}" -- python3 $GRAFT_REPO_ROOT/bench.py --steps $STEPS --warmup 1 --no-cpu-baseline || exit $?
+    run bench $grp "${C[@]}" -- python3 $GRAFT_REPO_ROOT/bench.py --steps $STEPS --warmup 1 --no-cpu-baseline $BENCH_ARGS || exit $?
 done
 cd $GRAFT_REPO_ROOT && python3 tools/traffic_json.py gpurun_out/pmc --out gpurun_out/pmc/spmv_traffic.json > /dev/null

@@ -16,6 +16,7 @@ import os
 
 CLASSES = {  # kernel-name prefix -> kernel
     "void cal::k_spmv_pair<1": "spmv",
+    "void cal::k_spmv_planes<1": "spmv",
     "void cal::k_spmv_pat_lds<1": "spmv",
     "void cal::k_spmv<1": "spmv_csr",
     "void cal::k_rowapply<17, 4, true, false": "gram_p1",
