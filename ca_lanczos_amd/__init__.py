@@ -14,6 +14,7 @@ from .api import (  # noqa: F401
     ca_lanczos,
     ca_lanczos_ex,
     cholqr,
+    compute_ritz_rnorm,
     context_for,
     default_context,
     eig,

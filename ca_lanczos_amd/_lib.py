@@ -92,6 +92,7 @@ SIGNATURES = [
     ("cal_get_normalize", c_int, [c_void_p, ip]),
     ("cal_set_orth_coef", c_int, [c_void_p, c_char_p]),
     ("cal_spmv_pair_info", c_int, [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_int64)]),
+    ("cal_spmv_plane_info", c_int, [c_void_p, POINTER(c_int64), POINTER(c_int), POINTER(c_int)]),
     ("cal_spmv_format", c_int, [c_void_p, ip, ip, ip]),
     ("cal_bench_spmv", c_int, [c_void_p, c_int, c_double, dp, dp]),
     ("cal_spmv", c_int, [c_void_p, dp, dp]),
@@ -106,6 +107,7 @@ SIGNATURES = [
      [c_void_p, c_int64, c_int, POINTER(dp), ip, c_int, dp, c_int, dp, POINTER(dp), ip, ip]),
     ("cal_ca_lanczos", c_int,
      [c_void_p, dp, c_int, c_int, c_char_p, c_char_p, c_int, dp, dp, dp, dp, ip, POINTER(LanczosInfo)]),
+    ("cal_compute_ritz_rnorm", c_int, [c_void_p, dp, c_int, dp, dp, dp]),
     ("cal_lanczos_begin", c_int, [c_void_p, dp, c_int, c_int, c_char_p, c_char_p]),
     ("cal_lanczos_step", c_int, [c_void_p, c_int]),
     ("cal_lanczos_state", c_int, [c_void_p, ip, ip, ip]),

@@ -131,6 +131,13 @@ class Context:
         check(self.h, lib.cal_spmv_pair_info(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
         return a.value, b.value, c.value
 
+    def spmv_plane_info(self):
+        """(plane stride P, in-plane reach H, key mode) of the plane-march
+        kernels; (0, 0, -1) when the matrix does not take them."""
+        a, b, c = ctypes.c_int64(), ctypes.c_int(), ctypes.c_int()
+        check(self.h, lib.cal_spmv_plane_info(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, c.value
+
     def close(self):
         if self.h:
             lib.cal_destroy(self.h)
@@ -365,13 +372,13 @@ def _blocks(Q):
     return blocks, widths, arr
 
 
-def project(Q, X, doreorth=False):
+def project(Q, X, doreorth=False, ctx=None):
     """``[X,R] = project(Q,X,doreorth)`` -- project.m:7-58."""
     if isinstance(X, (list, tuple)):
         raise TypeError("Input X (arg 2) project() must be a column matrix.")
     if len(Q) == 0:
         return np.array(X, dtype=np.float64), []
-    ctx = default_context()
+    ctx = ctx or default_context()
     X = f64(X)
     n, m = X.shape
     blocks, widths, arr = _blocks(Q)
@@ -383,11 +390,11 @@ def project(Q, X, doreorth=False):
     return Xout, R
 
 
-def normalize(X, opt="None", tol=1.0e-8):
+def normalize(X, opt="None", tol=1.0e-8, ctx=None):
     """``[Q,R,rank] = normalize(X,opt,tol)`` -- normalize.m:3-36; opt
     'randomizeNullSpace' runs normalize.m:28-31,38-51 (the null-space
     columns drawn from a fresh MATLAB rand stream, seed 5489)."""
-    ctx = default_context()
+    ctx = ctx or default_context()
     X = f64(X)
     n, m = X.shape
     Q = np.zeros((n, m), order="F")
@@ -405,9 +412,10 @@ def matlab_rand(count, seed=5489):
     return out
 
 
-def projectAndNormalize_ex(Q, X, doreorth=True):
-    """projectAndNormalize.m:3-90, also returning (reorth flag, rank)."""
-    ctx = default_context()
+def projectAndNormalize_ex(Q, X, doreorth=True, ctx=None):
+    """projectAndNormalize.m:3-90, also returning (reorth flag, rank).  With
+    a distributed context, Q / X are this rank's local rows."""
+    ctx = ctx or default_context()
     X = f64(X)
     n, m = X.shape
     blocks, widths, arr = _blocks(Q)
@@ -485,6 +493,23 @@ def eig(T):
 # ---------------------------------------------------------------------------
 # a14: the driver
 # ---------------------------------------------------------------------------
+def compute_ritz_rnorm(A, Q, Vp, Dp, ctx=None):
+    """``ritz_rnorm = compute_ritz_rnorm(A,Q,Vp,Dp)`` -- ca_lanczos.m:88-97 (real
+    Dp: a vector of eigenvalues or the diagonal matrix).  The Ritz vectors
+    x = Q*Vp(:,i) are formed on the device; the values are sorted descending
+    as the reference does."""
+    ctx = ctx or context_for(A)
+    Q = np.asfortranarray(f64(Q))
+    Vp = np.asfortranarray(f64(Vp))
+    d = f64(np.diag(Dp) if np.ndim(Dp) == 2 else Dp).ravel().copy()
+    k = Vp.shape[1]
+    if Q.shape[1] != k or Vp.shape[0] != k or d.size != k:
+        raise ValueError("compute_ritz_rnorm: Q is n x k, Vp k x k, Dp k values")
+    rn = np.zeros(k)
+    check(ctx.h, lib.cal_compute_ritz_rnorm(ctx.h, ptr(Q), k, ptr(Vp), ptr(d), ptr(rn)), "compute_ritz_rnorm")
+    return rn
+
+
 @dataclass
 class CALanczosOutput:
     T: np.ndarray

@@ -599,16 +599,21 @@ static int ensure_zbuf(cal_ctx* c, int64_t n, int m, double** p, int64_t* ld) {
 // apply, 1 when the fold declined after running (||W|| too large, or a
 // non-finite value): the caller then takes the explicit-Z path.
 // The fold/no-fold decision must be the same on every rank: the two paths
-// issue different collectives.  The shape conditions that depend on the
-// panel's local rows are checked for every rank's slab (the slab table of
-// the resident matrix), or, for a panel of another height, agreed by one
-// all-reduce of the ranks' votes.
+// issue different collectives.  So is the way it is reached: the branch is
+// chosen by rank-uniform facts only (every rank is in the same entry point,
+// so c->tier1 agrees, and every rank holds the same slab table).  Inside the
+// device-resident loop (not tier 1) a panel is always the resident slab's
+// local rows: the shape is checked for every rank's slab from the table, with
+// no collective.  A tier-1 panel can have any local height: the ranks' votes
+// are agreed by one all-reduce, which every rank issues.
 static int fold_shape_all_ranks(cal_ctx* c, int64_t n, int m, int w, bool* ok) {
     const int P = c->comm ? c->comm->nranks : 1;
     *ok = fold_shape_ok(n, m, w);
     if (P == 1) return 0;
     const std::vector<int64_t>& st = c->A.slabs;
-    if (c->has_A && (int)st.size() == P + 1 && n == c->A.n_local) {
+    if (!c->tier1 && c->has_A && (int)st.size() == P + 1) {
+        // by construction n == n_local here on every rank (a loop panel)
+        if (n != c->A.n_local) return set_error(c, CAL_ERR_ARG, "fold: a loop panel that is not the resident slab");
         for (int q = 0; q < P; ++q) *ok = *ok && fold_shape_ok(st[q + 1] - st[q], m, w);
         return 0;
     }

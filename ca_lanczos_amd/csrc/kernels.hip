@@ -602,60 +602,69 @@ bool spmv_pat_pair_path(const PatArgs& a) {
 
 // ---- the plane march -------------------------------------------------------
 // For matrices in canonical slots -P < ... < +P (pslot[0] = -P, pslot[L-1] =
-// +P, P >= 256) whose inner slots reach H <= 512 rows -- the 7-point (P =
-// N^2) and 5-point (P = N) Laplacians -- on a single slab.  A block owns the
-// rows xy0 .. xy0 + 511 of every plane (r = xy + z P) for Z planes.  Per plane
-// it stages into LDS:
+// +P, P >= 256) whose inner slots reach H <= 256 rows -- the 7-point (P =
+// N^2, N < 256) and 5-point (P = N) Laplacians -- on a single slab.  A block
+// owns the rows xy0 .. xy0 + 511 of every plane (r = xy + z P) for Z planes.
+// Per plane it stages into LDS:
 //   * the window x[zP + xy0 - H, zP + xy0 + 512 + H) by contiguous 16-B
-//     buffer loads (reads outside the column return 0 from the range check);
-//   * the rows' keys (their pattern ids, 1 B when npat <= 256, else 2 B) by
-//     aligned dword loads;
-// and once per block the pattern table: per pattern its slot values with 0.0
-// where the row has no entry (stride L2 = L rounded up to even), and slot
-// masks.  Each lane takes its row pair (xy0 + lr, + 1): the inner slots from
-// the window, the -P / +P slots the same lane's centre pair of the previous /
-// next plane (register, next buffer), the coefficients by broadcast-friendly
-// 16-B LDS reads of its rows' table rows.  Plane z0 + j is loaded three
-// planes ahead into register set j & 1 and stored to LDS two planes ahead,
-// so every load has a whole plane's work to land.  Each x value leaves HBM
-// about once ((Z + 2) / Z: a block also stages its neighbours' first and
-// last plane) and the in-plane gathers are LDS reads (tools/resid_probe.hip:
-// 15 us per vector at n = 215^3 against 25 us for the row-pair gather and
-// 12 us for a bare read of x).  When P is odd the plane's last pair straddles
-// into the next plane: only its first row belongs to the block.
+//     buffer loads (rows outside the column read 0: a negative row's 32-bit
+//     byte offset is >= 2^31, past the descriptor's range, and so is a row at
+//     or past ld; ld < 2^28);
+//   * the rows' keys (slot mask bytes, or pattern ids of 1 / 2 B) by aligned
+//     dword loads;
+// and once per block the pattern table (KM != 0): per pattern its slot values
+// with 0.0 where the row has no entry (stride L2 = L rounded up to even), and
+// slot masks.  Each lane takes its row pair (xy0 + lr, + 1): the inner slots
+// from the window, the -P / +P slots the same lane's centre pair of the
+// previous / next plane (register, next buffer).  With LN (slots -1, 0, +1
+// around the middle) the +-1 pairs are the centre pair plus one value on each
+// side: one two-value LDS read instead of two pairs.  Plane z0 + j + 2 is
+// loaded into registers at the top of step j and stored to LDS at its end, so
+// every load has a plane's work to land.  Each x value leaves HBM about once
+// ((Z + 2) / Z: a block also stages its neighbours' first and last plane) and
+// the in-plane gathers are LDS reads.  When P is odd the plane's last pair
+// straddles into the next plane: only its first row belongs to the block.
 //
-// A slot a row has no entry at contributes 0.0 * x: for finite x the running
-// sum (which starts at +0.0 and so is never -0.0) is unchanged, so the sums
-// have the reference's bits.  Each lane also flags non-finite x values it
-// stages; a plane whose window holds one is recomputed with the entries
-// selected by the slot masks, so a non-finite x outside a row never leaks into
-// it (the SpMV's contract, k_spmv_pair).
+// Every row adds its own entries in slot (= column) order.  Where some row of
+// a wave has no entry at slot e (wave-uniform test: the OR of the rows'
+// missing-slot masks), slot e's x values enter each row ANDed with the row's
+// mask bit, i.e. as +0.0 where the row has no entry: 0 * (+0.0) adds a zero,
+// which leaves a running sum that is never -0.0 unchanged, and a non-finite x
+// outside a row never leaks into it (the SpMV's contract, k_spmv_pair).  A
+// slot every row of the wave has is added unmasked.  So the sums are the bits
+// of k_spmv / k_spmv_pair; the per-row selects of round 4 cost 12 VALU
+// instructions per slot and were taken by nearly every wave of lap3d (each
+// 128-row wave meets an x = 0 / N - 1 row).
 // KM = 0: uniform slot values (cval; every row with an entry at slot e has
 // the value cval[e], as in the Laplacians): the keys are the rows' slot mask
 // bytes.  KM = 1 / 2: the keys are the rows' pattern ids (1 / 2 B) into the
 // LDS value / mask tables.
-template <int MAXLEN, int KM>
+template <int MAXLEN, int KM, bool LN>
 struct PlaneMarch {
-    static constexpr int KB = KM == 2 ? 2 : 1;             // key bytes per row
+    static constexpr int KB = KM == 2 ? 2 : 1;                  // key bytes per row
     typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-    static constexpr int L2 = (MAXLEN + 1) & ~1;          // table row stride (16-B reads)
-    static constexpr int KD = (512 * KB + 6) / 4 + 1;      // key dwords per plane (with the alignment slack)
-    static constexpr int LPT = (kResidPlaneRows + 2 * 512) / 2 / 256;  // window pairs per thread (H <= 512)
+    static constexpr int L2 = (MAXLEN + 1) & ~1;                // table row stride (16-B reads)
+    static constexpr int KD = (kResidPlaneRows * KB + 6) / 4 + 1;  // key dwords per plane (with the alignment slack)
+    static constexpr int KR = (KD + 255) / 256;                 // key dword rounds per thread
+    static constexpr int NK = 2;                                // window pair rounds: WP = 256 + H <= 512
+    static constexpr int MID = MAXLEN / 2;                      // LN: slots MID - 1, MID, MID + 1 = -1, 0, +1
     // plain scalars and pointers only: a reference to the by-value kernel
     // argument would make every thread copy it to scratch; row indices are
     // 32-bit (planes_ok: ld < 2^28)
-    int H, WR, WP, tid, lr, wi, zend, P, n, ld, xy0, z0, nk;
-    bool in0, in1;
+    int H, WR, tid, lr, wi, zend, P, n, xy0, z0;
+    bool in0, in1, full;
     double* win;      // [3][WR]
     uint32_t* keys;   // [3][KD]
     double* s_rz;     // npat x L2 slot values (0 where the row has no entry)
     uint8_t* s_rm;    // npat slot masks
     __amdgpu_buffer_rsrc_t rx, rk;
-    int ps[MAXLEN];   // slot offsets (compile-time indices only)
+    int ps[MAXLEN];     // slot offsets (compile-time indices only)
     double cv[MAXLEN];  // KM = 0: the slot values
-    unsigned fullm;     // the interior rows' mask (every slot)
-    double2 st[LPT];     // the prefetched plane (registers)
-    uint32_t kst[2];
+    unsigned fullm;     // every slot
+    int pi16[NK];       // the lane's window pairs (clamped), byte offsets
+    int k4[KR];         // the lane's key dwords (clamped), byte offsets
+    double2 st[NK];     // the prefetched plane (registers)
+    uint32_t kst[KR];
 
     __device__ static __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
         const uint64_t pl = (uint64_t)(uintptr_t)p;
@@ -665,20 +674,18 @@ struct PlaneMarch {
                                                  (int)__builtin_amdgcn_readfirstlane((uint32_t)bytes), 0x00020000);
     }
     __host__ __device__ static size_t lds_bytes(int H, int npat) {
-        return (size_t)3 * (kResidPlaneRows + 2 * H) * 8 + (size_t)3 * KD * 4 + 16 + (size_t)npat * L2 * 8 +
-               (size_t)npat + 16;
+        return (size_t)3 * (kResidPlaneRows + 2 * H) * 8 + (((size_t)3 * KD * 4 + 15) & ~(size_t)15) +
+               (KM == 0 ? 0 : (size_t)npat * L2 * 8 + (size_t)npat) + 16;
     }
     // the fields are passed one by one from the kernel's by-value PatArgs
     __device__ PlaneMarch(int64_t P_, int H_, int64_t n_, int64_t ld_, const double* x, const void* key,
                           const double* rzval, const uint8_t* rzmask, int npat, double* lds, int bi, int Z) {
         H = H_;
         WR = kResidPlaneRows + 2 * H;
-        WP = WR / 2;
-        nk = (WP + 255) / 256;
+        const int WP = WR / 2;
         tid = threadIdx.x;
         P = (int)P_;
         n = (int)n_;
-        ld = (int)ld_;
         const int nxy = (P + kResidPlaneRows - 1) / kResidPlaneRows;
         const int nz = (n + P - 1) / P;
         xy0 = (bi % nxy) * kResidPlaneRows;
@@ -688,9 +695,10 @@ struct PlaneMarch {
         wi = lr + H;
         in0 = xy0 + lr < P;
         in1 = xy0 + lr + 1 < P;
+        full = xy0 + kResidPlaneRows <= P && (int64_t)(z0 + zend) * P <= n_;
         win = lds;
         keys = reinterpret_cast<uint32_t*>(win + 3 * WR);
-        s_rz = reinterpret_cast<double*>(keys + 3 * KD + (3 * KD & 1));
+        s_rz = reinterpret_cast<double*>(keys + ((3 * KD + 3) & ~3));
         s_rm = reinterpret_cast<uint8_t*>(s_rz + npat * L2);
         if (KM != 0) {
             for (int i = tid; i < npat * L2; i += 256) {
@@ -700,70 +708,78 @@ struct PlaneMarch {
             for (int i = tid; i < npat; i += 256) s_rm[i] = rzmask[i];
         }
         fullm = (1u << MAXLEN) - 1u;
+#pragma unroll
+        for (int k = 0; k < NK; ++k) pi16[k] = 16 * min(tid + 256 * k, WP - 1);
+#pragma unroll
+        for (int k = 0; k < KR; ++k) k4[k] = 4 * min(tid + 256 * k, KD - 1);
         rx = rsrc(x, ld_ * 8);
         // the key arrays carry >= 4 zero bytes past the rows (upload_matrix), so
         // every aligned dword load that reaches a real row lies inside
         rk = rsrc(key, (KB * n_ + 7) & ~(int64_t)3);
     }
-    // x[row .. row + 1]; rows outside the column read 0 (the range check).  A
-    // load that straddles the descriptor's end returns 0 as a whole
-    // (measured), so planes_ok requires ld >= n + 2: only padding rows can
-    // straddle.  No branches: a branch around a load makes the compiler wait
-    // for every outstanding load at the join.
-    __device__ double2 ld2(int row) const {
-        const uint32_t off = row >= 0 && row < ld ? (uint32_t)row * 8u : 0xFFFFFFF0u;
-        const u4 w = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)off, 0, 0);
+    // 16 B at byte offset off of the column: off < 0 (as 32 bits >= 2^31) or
+    // past ld * 8 reads 0.  A load that straddles the descriptor's end returns
+    // 0 as a whole (measured), so planes_ok requires ld >= n + 2: only padding
+    // rows can straddle.  No range branches: a branch around a load makes the
+    // compiler wait for every outstanding load at the join.
+    __device__ double2 ld16(int off) const {
+        const u4 w = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
         return make_double2(__builtin_bit_cast(double, ((uint64_t)w.y << 32) | w.x),
                             __builtin_bit_cast(double, ((uint64_t)w.w << 32) | w.z));
     }
-    // issue plane z's loads (window + keys) into registers: nk uniform rounds
-    // of 256 window pairs, one or two key dwords.  Lanes past the end load
-    // (and later store) the last pair / dword again: the same data to the
-    // same place, and no divergent branch.
+    __device__ double2 ld2(int row) const { return ld16(row * 8); }
+    // issue plane z's loads (window + keys) into registers.  Lanes past the
+    // end load (and later store) the last pair / dword again: the same data
+    // to the same place, and no divergent branch.
     __device__ void load(int z) {
-        const int g = z * P + xy0 - H;
+        const int g8 = (z * P + xy0 - H) * 8;
 #pragma unroll
-        for (int k = 0; k < LPT; ++k)
-            if (k < nk) st[k] = ld2(g + 2 * min(tid + 256 * k, WP - 1));
+        for (int k = 0; k < NK; ++k) st[k] = ld16(g8 + pi16[k]);
         const int al = ((z * P + xy0) * KB) & ~3;
 #pragma unroll
-        for (int k = 0; k < 2; ++k)
-            if (256 * k < KD)
-                kst[k] = __builtin_amdgcn_raw_buffer_load_b32(rk, al + 4 * min(tid + 256 * k, KD - 1), 0, 0);
+        for (int k = 0; k < KR; ++k) kst[k] = __builtin_amdgcn_raw_buffer_load_b32(rk, al + k4[k], 0, 0);
     }
     // the prefetched plane into LDS buffer b
     __device__ void store(int b) {
+        char* wb = reinterpret_cast<char*>(win + b * WR);
 #pragma unroll
-        for (int k = 0; k < LPT; ++k) {
-            if (k < nk) {
-                const int pi = min(tid + 256 * k, WP - 1);
-                *reinterpret_cast<double2*>(win + b * WR + 2 * pi) = st[k];
-            }
-        }
+        for (int k = 0; k < NK; ++k) *reinterpret_cast<double2*>(wb + pi16[k]) = st[k];
+        char* kb = reinterpret_cast<char*>(keys + b * KD);
 #pragma unroll
-        for (int k = 0; k < 2; ++k)
-            if (256 * k < KD) keys[b * KD + min(tid + 256 * k, KD - 1)] = kst[k];
+        for (int k = 0; k < KR; ++k) *reinterpret_cast<uint32_t*>(kb + k4[k]) = kst[k];
     }
-    // The march (tools/resid_probe.hip's schedule): plane z0 + j + 2 is loaded
-    // into registers at the top of step j, the step computes plane z0 + j
-    // from LDS, then stores the prefetched plane into buffer (j + 2) % 3 and
-    // synchronizes.  Latency is hidden by occupancy (the kernels stay within
-    // 64 VGPRs: 8 waves per SIMD).  f(j, bc, bn) computes plane z0 + j from
-    // buffers bc (current) and bn (next).
+    // The march: plane z0 + j + 2 is loaded into registers at the top of step
+    // j, the step computes plane z0 + j from LDS, then stores the prefetched
+    // plane into buffer (j + 2) % 3 and synchronizes.  f(j, bc, bn) computes
+    // plane z0 + j from buffers bc (current) and bn (next).
+    // xp: the lane's -P pair of the first plane, loaded before the march; it
+    // is pinned once the prologue's stores have waited for the loads (loads
+    // return in order), so the loop's first use does not wait for the
+    // prefetch issued at the top of the step (the compiler otherwise places
+    // a vmcnt(0) there for the value carried in from the preheader).
     template <typename F>
-    __device__ void march(F&& f) {
+    __device__ void march(double2& xp, F&& f) {
         load(z0);
         store(0);
         load(z0 + 1);
         store(1);
+        asm volatile("" : "+v"(xp.x), "+v"(xp.y));
         __syncthreads();
         for (int j = 0; j < zend; ++j) {
             if (j + 2 <= zend) load(z0 + j + 2);
             f(j, j % 3, (j + 1) % 3);
-            if (j + 2 <= zend) store((j + 2) % 3);
+            // the plane's arithmetic stays ahead of the stores, which wait for
+            // the prefetch (the compiler otherwise sinks it below them).  The
+            // store is unconditional to keep both in one block: in the last
+            // step it writes the registers again into the buffer of plane
+            // zend - 2, which no step reads any more.
+            __builtin_amdgcn_sched_barrier(0);
+            store((j + 2) % 3);
             __syncthreads();
         }
     }
+    // the lane's centre pair of plane buffer b
+    __device__ double2 centre(int b) const { return *reinterpret_cast<const double2*>(win + b * WR + wi); }
     // the lane's two row keys of plane z (buffer b)
     __device__ void row_keys(int b, int z, unsigned& k0, unsigned& k1) const {
         const int kofs = ((z * P + xy0) * KB) & 3;
@@ -776,51 +792,76 @@ struct PlaneMarch {
             k1 = *reinterpret_cast<const uint16_t*>(kp + 2);
         }
     }
-    // y0 / y1: the slot sums of the lane's two rows (A x of plane b; xp the
-    // previous plane's centre pair), each row's own entries in slot (=
-    // column) order.  A wave whose rows all have every slot (the interior,
-    // wave-uniform test) adds every product; otherwise each entry is selected
-    // by the row's mask -- skipped, not multiplied by zero, so a non-finite x
-    // outside a row never leaks into it.  Bit-identical to k_spmv_pair.
-    __device__ void sums(int b, int bn, const double2& xp, unsigned k0, unsigned k1, double& y0, double& y1) const {
+    // the OR of the wave's lanes (DPP row shifts, then the row broadcasts)
+    __device__ static unsigned wave_or(unsigned v) {
+        v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+        v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+        v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+        v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+        v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+        v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+        return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+    }
+    // x with the row's slot-e bit: x, or +0.0 where the row has no entry
+    __device__ static double keep(double x, unsigned m, int e) {
+        const unsigned k = 0u - ((m >> e) & 1u);
+        uint2 w = __builtin_bit_cast(uint2, x);
+        w.x &= k;
+        w.y &= k;
+        return __builtin_bit_cast(double, w);
+    }
+    // y0 / y1: the slot sums of the lane's two rows of plane z (buffer b; bn
+    // the next plane, xp / xc the previous / current plane's centre pair),
+    // each row's own entries in slot (= column) order.  Z0: the sums start
+    // from +0.0 (the stored SpMV: a zero sum is +0.0, as in k_spmv); the
+    // residual squares its sums and starts from the first product.
+    template <bool Z0>
+    __device__ void sums(int b, int bn, int z, const double2& xp, const double2& xc, double& y0, double& y1) const {
+        unsigned k0, k1;
+        row_keys(b, z, k0, k1);
         const unsigned m0 = KM == 0 ? k0 : s_rm[k0], m1 = KM == 0 ? k1 : s_rm[k1];
-        const double* c0 = s_rz + (KM == 0 ? 0 : k0 * L2);
-        const double* c1 = s_rz + (KM == 0 ? 0 : k1 * L2);
-        const bool interior = __builtin_amdgcn_ballot_w64((m0 & m1) != fullm) == 0;
-        y0 = 0.0;
-        y1 = 0.0;
-        if (interior) {
+        const unsigned wm = wave_or(fullm & ~(m0 & m1));
+        const double* w = win + b * WR + wi;
+        double lo = 0.0, hi = 0.0;
+        if (LN) {
+            lo = w[-1];
+            hi = w[2];
+        }
 #pragma unroll
-            for (int e = 0; e < MAXLEN; ++e) {
-                const double2 v = slot(b, bn, e, xp);
-                const double t0 = (KM == 0 ? cv[e] : c0[e]) * v.x, t1 = (KM == 0 ? cv[e] : c1[e]) * v.y;
+        for (int e = 0; e < MAXLEN; ++e) {
+            double2 v;
+            if (e == 0) v = xp;
+            else if (e == MAXLEN - 1) v = *reinterpret_cast<const double2*>(win + bn * WR + wi);
+            else if (LN && e == MID - 1) v = make_double2(lo, xc.x);
+            else if (LN && e == MID) v = xc;
+            else if (LN && e == MID + 1) v = make_double2(xc.y, hi);
+            else v = make_double2(w[ps[e]], w[ps[e] + 1]);
+            if (wm >> e & 1u) {
+                v.x = keep(v.x, m0, e);
+                v.y = keep(v.y, m1, e);
+            }
+            const double c0 = KM == 0 ? cv[e] : s_rz[k0 * L2 + e];
+            const double c1 = KM == 0 ? cv[e] : s_rz[k1 * L2 + e];
+            const double t0 = c0 * v.x, t1 = c1 * v.y;
+            if (e == 0 && !Z0) {
+                y0 = t0;
+                y1 = t1;
+            } else if (e == 0) {
+                y0 = 0.0 + t0;
+                y1 = 0.0 + t1;
+            } else {
                 y0 = y0 + t0;
                 y1 = y1 + t1;
             }
-        } else {
-#pragma unroll
-            for (int e = 0; e < MAXLEN; ++e) {
-                const double2 v = slot(b, bn, e, xp);
-                const double t0 = (KM == 0 ? cv[e] : c0[e]) * v.x, t1 = (KM == 0 ? cv[e] : c1[e]) * v.y;
-                double s0 = y0 + t0, s1 = y1 + t1;
-                asm volatile("" : "+v"(s0), "+v"(s1));
-                y0 = ((m0 >> e) & 1u) ? s0 : y0;
-                y1 = ((m1 >> e) & 1u) ? s1 : y1;
-            }
         }
-    }
-    __device__ double2 slot(int b, int bn, int e, const double2& xp) const {
-        if (e == 0) return xp;
-        if (e == MAXLEN - 1) return make_double2(win[bn * WR + wi], win[bn * WR + wi + 1]);
-        return make_double2(win[b * WR + wi + ps[e]], win[b * WR + wi + ps[e] + 1]);
     }
 };
 
 #define CAL_PLANE_MARCH(PM, XPTR, Zv)                                                                          \
-    PlaneMarch<MAXLEN, KM> PM(a.plane_P, a.plane_H, a.n, a.ld, XPTR,                                           \
-                              KM == 0 ? (const void*)a.rowmask                                                \
-                                      : (KM == 1 ? (const void*)a.rowkey8 : (const void*)a.pat),              \
-                              a.rzval, a.rzmask, a.npat, lds_plane, xcd_remap(blockIdx.x, gridDim.x), Zv);    \
+    PlaneMarch<MAXLEN, KM, LN> PM(a.plane_P, a.plane_H, a.n, a.ld, XPTR,                                       \
+                                  KM == 0 ? (const void*)a.rowmask                                            \
+                                          : (KM == 1 ? (const void*)a.rowkey8 : (const void*)a.pat),          \
+                                  a.rzval, a.rzmask, a.npat, lds_plane, xcd_remap(blockIdx.x, gridDim.x), Zv); \
     _Pragma("unroll") for (int e_ = 0; e_ < MAXLEN; ++e_) {                                                   \
         PM.ps[e_] = a.pslot[e_];                                                                              \
         PM.cv[e_] = a.cval[e_];                                                                               \
@@ -830,40 +871,50 @@ struct PlaneMarch {
 // k_spmv_pair.  One 16-B store per row pair (8-B aligned on the odd planes
 // of an odd P).
 __device__ __forceinline__ void st16(double* p, double2 v) { __builtin_memcpy(p, &v, 16); }
+__device__ __forceinline__ double2 ld16g(const double* p) {
+    double2 v;
+    __builtin_memcpy(&v, p, 16);
+    return v;
+}
 
-template <int MODE, int MAXLEN, int Z, int KM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_spmv_planes(PatArgs a) {
+template <int MODE, int MAXLEN, int Z, int KM, bool LN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_spmv_planes(PatArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds_plane[];
     CAL_PLANE_MARCH(pm, a.x, Z)
     double2 xp = pm.ld2((pm.z0 - 1) * pm.P + pm.xy0 + pm.lr);
-    pm.march([&](int j, int bc, int bn) {
-        const int r = (pm.z0 + j) * pm.P + pm.xy0 + pm.lr;
-        const bool v0 = pm.in0 && r < pm.n, v1 = pm.in1 && r + 1 < pm.n;
-        unsigned k0, k1;
-        pm.row_keys(bc, pm.z0 + j, k0, k1);
-        const double2 xc = make_double2(pm.win[bc * pm.WR + pm.wi], pm.win[bc * pm.WR + pm.wi + 1]);
-        double y0, y1;
-        pm.sums(bc, bn, xp, k0, k1, y0, y1);
-        if (MODE != 0) {
-            const double u0 = a.shift * xc.x, u1 = a.shift * xc.y;
-            y0 = y0 - u0;
-            y1 = y1 - u1;
-            if (MODE == 2) {
-                const double q0 = a.xprev[v0 ? r : 0], q1 = a.xprev[v1 ? r + 1 : 0];
-                const double w0 = a.im2 * q0, w1 = a.im2 * q1;
-                y0 = y0 + w0;
-                y1 = y1 + w1;
+    auto run = [&](auto fullc) {
+        constexpr bool FULL = decltype(fullc)::value;
+        pm.march(xp, [&](int j, int bc, int bn) {
+            const int r = (pm.z0 + j) * pm.P + pm.xy0 + pm.lr;
+            const bool v0 = FULL || (pm.in0 && r < pm.n), v1 = FULL || (pm.in1 && r + 1 < pm.n);
+            const double2 xc = pm.centre(bc);
+            double y0, y1;
+            pm.template sums<true>(bc, bn, pm.z0 + j, xp, xc, y0, y1);
+            if (MODE != 0) {
+                const double u0 = a.shift * xc.x, u1 = a.shift * xc.y;
+                y0 = y0 - u0;
+                y1 = y1 - u1;
+                if (MODE == 2) {
+                    double2 q;
+                    if (FULL) q = ld16g(a.xprev + r);
+                    else q = make_double2(a.xprev[v0 ? r : 0], a.xprev[v1 ? r + 1 : 0]);
+                    const double w0 = a.im2 * q.x, w1 = a.im2 * q.y;
+                    y0 = y0 + w0;
+                    y1 = y1 + w1;
+                }
             }
-        }
-        if (v0 && v1) st16(a.y + r, make_double2(y0, y1));
-        else if (v0) a.y[r] = y0;
-        xp = xc;
-    });
+            if (v0 && v1) st16(a.y + r, make_double2(y0, y1));
+            else if (v0) a.y[r] = y0;
+            xp = xc;
+        });
+    };
+    if (pm.full) run(std::true_type{});
+    else run(std::false_type{});
 }
 
 // the plane march applies to a whole single slab (pat_args sets the tables)
 static bool planes_ok(const PatArgs& a) {
-    return a.rzval && a.rzmask && a.plane_P >= 256 && a.plane_H <= 512 && a.pmaxlen >= 2 && a.pmaxlen <= 8 &&
+    return a.rzval && a.rzmask && a.plane_P >= 256 && a.plane_H <= 256 && a.pmaxlen >= 2 && a.pmaxlen <= 8 &&
            a.pcanon && a.gap == 0 && a.xlo == 0 && a.ld >= a.n + 2 && a.ld < ((int64_t)1 << 28) &&
            (a.cuniform ? a.rowmask != nullptr : (a.npat > 256 || a.rowkey8));
 }
@@ -872,8 +923,42 @@ static int planes_blocks(const PatArgs& a, int Z) {
     const int64_t nz = (a.n + a.plane_P - 1) / a.plane_P;
     return (int)(nxy * ((nz + Z - 1) / Z));
 }
-static size_t planes_lds(const PatArgs& a) {  // (the KB = 2 layout bounds both)
-    return PlaneMarch<8, 2>::lds_bytes(a.plane_H, a.npat);
+// the key mode of the plane march: 0 mask bytes, 1 / 2 pattern ids of 1 / 2 B
+static int planes_km(const PatArgs& a) { return a.cuniform ? 0 : (a.npat <= 256 ? 1 : 2); }
+static size_t planes_lds(const PatArgs& a) {
+    switch (planes_km(a)) {
+        case 0: return PlaneMarch<8, 0, false>::lds_bytes(a.plane_H, a.npat);
+        case 1: return PlaneMarch<8, 1, false>::lds_bytes(a.plane_H, a.npat);
+        default: return PlaneMarch<8, 2, false>::lds_bytes(a.plane_H, a.npat);
+    }
+}
+// slots MID - 1, MID, MID + 1 (MID = L / 2, L odd) are the offsets -1, 0, +1
+static bool planes_ln(const PatArgs& a) {
+    const int L = a.pmaxlen, m = L / 2;
+    return (L & 1) && L >= 5 && a.pslot[m - 1] == -1 && a.pslot[m] == 0 && a.pslot[m + 1] == 1;
+}
+// dispatch f(MAXLEN, KM, LN) over the plane march's instantiations
+template <typename F>
+static void planes_dispatch(const PatArgs& a, F&& f) {
+    auto km = [&](auto ml, auto ln) {
+        switch (planes_km(a)) {
+            case 0: f(ml, std::integral_constant<int, 0>{}, ln); break;
+            case 1: f(ml, std::integral_constant<int, 1>{}, ln); break;
+            default: f(ml, std::integral_constant<int, 2>{}, ln); break;
+        }
+    };
+    const bool ln = planes_ln(a);
+    using T = std::true_type;
+    using N = std::false_type;
+    switch (a.pmaxlen) {
+        case 2: km(std::integral_constant<int, 2>{}, N{}); break;
+        case 3: km(std::integral_constant<int, 3>{}, N{}); break;
+        case 4: km(std::integral_constant<int, 4>{}, N{}); break;
+        case 5: if (ln) km(std::integral_constant<int, 5>{}, T{}); else km(std::integral_constant<int, 5>{}, N{}); break;
+        case 6: km(std::integral_constant<int, 6>{}, N{}); break;
+        case 7: if (ln) km(std::integral_constant<int, 7>{}, T{}); else km(std::integral_constant<int, 7>{}, N{}); break;
+        default: km(std::integral_constant<int, 8>{}, N{}); break;
+    }
 }
 
 // planes per block of the plane-march SpMV (round 4, lap3d_215 in the loop:
@@ -884,27 +969,12 @@ constexpr int kSpmvPlanes = 16;
 template <int MODE>
 static hipError_t launch_spmv_planes(const PatArgs& a, hipStream_t st) {
     const size_t lds = planes_lds(a);
-    auto go = [&](auto zc, auto km) {
-        constexpr int Z = decltype(zc)::value, KM = decltype(km)::value;
-        dim3 g((unsigned)planes_blocks(a, Z)), b(256);
-#define CAL_SPL(ML) hipLaunchKernelGGL((k_spmv_planes<MODE, ML, Z, KM>), g, b, lds, st, a)
-        switch (a.pmaxlen) {
-            case 2: CAL_SPL(2); break;
-            case 3: CAL_SPL(3); break;
-            case 4: CAL_SPL(4); break;
-            case 5: CAL_SPL(5); break;
-            case 6: CAL_SPL(6); break;
-            case 7: CAL_SPL(7); break;
-            default: CAL_SPL(8); break;
-        }
-#undef CAL_SPL
-    };
-    auto gz = [&](auto zc) {
-        if (a.cuniform) go(zc, std::integral_constant<int, 0>{});
-        else if (a.npat <= 256) go(zc, std::integral_constant<int, 1>{});
-        else go(zc, std::integral_constant<int, 2>{});
-    };
-    gz(std::integral_constant<int, kSpmvPlanes>{});
+    dim3 g((unsigned)planes_blocks(a, kSpmvPlanes)), b(256);
+    planes_dispatch(a, [&](auto ml, auto km, auto ln) {
+        constexpr int ML = decltype(ml)::value, KM = decltype(km)::value;
+        constexpr bool LN = decltype(ln)::value;
+        hipLaunchKernelGGL((k_spmv_planes<MODE, ML, kSpmvPlanes, KM, LN>), g, b, lds, st, a);
+    });
     return hipGetLastError();
 }
 
@@ -1191,14 +1261,13 @@ __global__ __launch_bounds__(256) void k_resid_pairs(PatArgs a, const uint16_t* 
 
 // Ritz residual partials on the plane march (the geometry above): one Ritz
 // pair per block row (blockIdx.y), kResidPlanes planes per block; y = A x -
-// l x of each row with the SpMV's bits, then the block's sums of y^2 and
-// (l x)^2.
-template <int MAXLEN, int KM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_resid_planes(
-    PatArgs a, const double* __restrict__ X, int64_t ldx,
-                                                     const int* __restrict__ col, const double* __restrict__ lam,
-                                                     const int* __restrict__ out, double* __restrict__ partial,
-                                                     int64_t pstride) {
+// l x of each row with the SpMV's bits, then the block's sums of y^2 and,
+// times l^2, of x^2 (||l x||^2 = l^2 ||x||^2: one accumulator less than
+// summing (l x)^2, the same value to rounding).
+template <int MAXLEN, int KM, bool LN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_resid_planes(
+    PatArgs a, const double* __restrict__ X, int64_t ldx, const int* __restrict__ col, const double* __restrict__ lam,
+    const int* __restrict__ out, double* __restrict__ partial, int64_t pstride) {
     extern __shared__ __attribute__((aligned(16))) double lds_plane[];
     __shared__ double ws[2][4];
     const int i = blockIdx.y;
@@ -1206,21 +1275,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     const double l = lam[i];
     double2 xp = pm.ld2((pm.z0 - 1) * pm.P + pm.xy0 + pm.lr);
     double num = 0.0, den = 0.0;
-    pm.march([&](int j, int bc, int bn) {
-        const int r = (pm.z0 + j) * pm.P + pm.xy0 + pm.lr;
-        const bool v0 = pm.in0 && r < pm.n, v1 = pm.in1 && r + 1 < pm.n;
-        unsigned k0, k1;
-        pm.row_keys(bc, pm.z0 + j, k0, k1);
-        const double2 xc = make_double2(pm.win[bc * pm.WR + pm.wi], pm.win[bc * pm.WR + pm.wi + 1]);
-        double y0, y1;
-        pm.sums(bc, bn, xp, k0, k1, y0, y1);
-        const double u0 = l * xc.x, u1 = l * xc.y;
-        y0 = y0 - u0;
-        y1 = y1 - u1;
-        num = num + ((v0 ? y0 * y0 : 0.0) + (v1 ? y1 * y1 : 0.0));
-        den = den + ((v0 ? u0 * u0 : 0.0) + (v1 ? u1 * u1 : 0.0));
-        xp = xc;
-    });
+    auto run = [&](auto fullc) {
+        constexpr bool FULL = decltype(fullc)::value;
+        pm.march(xp, [&](int j, int bc, int bn) {
+            const double2 xc = pm.centre(bc);
+            double y0, y1;
+            pm.template sums<false>(bc, bn, pm.z0 + j, xp, xc, y0, y1);
+            const double u0 = l * xc.x, u1 = l * xc.y;
+            y0 = y0 - u0;
+            y1 = y1 - u1;
+            if (FULL) {
+                num = __builtin_fma(y0, y0, num);
+                num = __builtin_fma(y1, y1, num);
+                den = __builtin_fma(xc.x, xc.x, den);
+                den = __builtin_fma(xc.y, xc.y, den);
+            } else {
+                const int r = (pm.z0 + j) * pm.P + pm.xy0 + pm.lr;
+                const bool v0 = pm.in0 && r < pm.n, v1 = pm.in1 && r + 1 < pm.n;
+                const double a0 = v0 ? y0 : 0.0, a1 = v1 ? y1 : 0.0;
+                const double b0 = v0 ? xc.x : 0.0, b1 = v1 ? xc.y : 0.0;
+                num = __builtin_fma(a0, a0, num);
+                num = __builtin_fma(a1, a1, num);
+                den = __builtin_fma(b0, b0, den);
+                den = __builtin_fma(b1, b1, den);
+            }
+            xp = xc;
+        });
+    };
+    if (pm.full) run(std::true_type{});
+    else run(std::false_type{});
     num = wave_sum(num);
     den = wave_sum(den);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1229,9 +1312,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
         ws[1][wave] = den;
     }
     __syncthreads();
-    if (threadIdx.x < 2)
-        partial[(2 * (int64_t)out[i] + threadIdx.x) * pstride + blockIdx.x] =
-            ((ws[threadIdx.x][0] + ws[threadIdx.x][1]) + ws[threadIdx.x][2]) + ws[threadIdx.x][3];
+    if (threadIdx.x < 2) {
+        const double v = ((ws[threadIdx.x][0] + ws[threadIdx.x][1]) + ws[threadIdx.x][2]) + ws[threadIdx.x][3];
+        partial[(2 * (int64_t)out[i] + threadIdx.x) * pstride + blockIdx.x] = threadIdx.x == 0 ? v : (l * l) * v;
+    }
 }
 
 // the batched residual kernel's shape: one Ritz pair per block, 8 row pairs
@@ -1258,25 +1342,13 @@ hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64
     if ((a.xhi - a.xlo) * 8 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
     if (planes_ok(a)) {
         const size_t lds = planes_lds(a);
-        auto go = [&](auto km) {
-            constexpr int KM = decltype(km)::value;
-            dim3 g(blocks, npr), bl(256);
-#define CAL_RPL(ML) \
-    hipLaunchKernelGGL((k_resid_planes<ML, KM>), g, bl, lds, st, a, X, ldx, col, lam, out, partial, pstride)
-            switch (a.pmaxlen) {
-                case 2: CAL_RPL(2); break;
-                case 3: CAL_RPL(3); break;
-                case 4: CAL_RPL(4); break;
-                case 5: CAL_RPL(5); break;
-                case 6: CAL_RPL(6); break;
-                case 7: CAL_RPL(7); break;
-                default: CAL_RPL(8); break;
-            }
-#undef CAL_RPL
-        };
-        if (a.cuniform) go(std::integral_constant<int, 0>{});
-        else if (a.npat <= 256) go(std::integral_constant<int, 1>{});
-        else go(std::integral_constant<int, 2>{});
+        dim3 g(blocks, npr), bl(256);
+        planes_dispatch(a, [&](auto ml, auto km, auto ln) {
+            constexpr int ML = decltype(ml)::value, KM = decltype(km)::value;
+            constexpr bool LN = decltype(ln)::value;
+            hipLaunchKernelGGL((k_resid_planes<ML, KM, LN>), g, bl, lds, st, a, X, ldx, col, lam, out, partial,
+                               pstride);
+        });
         return hipGetLastError();
     }
     const size_t lds = (size_t)a.npent * 16 + 16;

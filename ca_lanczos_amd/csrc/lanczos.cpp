@@ -1198,6 +1198,86 @@ int cal_lanczos_end(cal_ctx* c) {
     return 0;
 }
 
+// compute_ritz_rnorm (ca_lanczos.m:88-97) for host Q (n_local x k) and a
+// real eigen-decomposition (Vp k x k, d): [d, ix] = sort(d, 'descend'),
+// rn(i) = ||A x - l x|| / ||l x|| with x = Q Vp(:, ix(i)), l = d(ix(i)).  The
+// device path of the diagnostics: X = Q Vp on the matrix cores, the batched
+// residual kernel (the plane march where the matrix takes it), one reduction.
+int cal_compute_ritz_rnorm(cal_ctx* c, const double* Q, int k, const double* Vp, const double* d, double* rn) {
+    if (!c || !Q || !Vp || !d || !rn || k < 1) return CAL_ERR_ARG;
+    if (!c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
+    for (int i = 0; i < k; ++i)
+        if (!std::isfinite(d[i])) return set_error(c, CAL_ERR_ARG, "compute_ritz_rnorm: non-finite eigenvalue");
+    const int64_t n = c->A.n_local, ld = c->A.ld;
+    std::vector<RitzPair> pairs;
+    for (int j = 0; j < k; ++j) pairs.push_back({d[j], 0.0, j, -1});
+    matlab_sort_desc(pairs, false);
+    CAL_TRY(ensure_work(c, 2 * k, ld));
+    double* Qd = work_col(c, 0) + c->A.lpad;
+    double* X = work_col(c, k) + c->A.lpad;
+    CAL_HIP(c, hipMemcpy2DAsync(Qd, ld * sizeof(double), Q, n * sizeof(double), n * sizeof(double), k,
+                                hipMemcpyHostToDevice, c->stream));
+    const int nbp = spmv_resid_pair_multi_blocks(c);
+    const int nbr = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (n + 255) / 256));
+    const size_t npart = (size_t)2 * k * std::max(nbp, nbr);
+    // inputs: Vp, then per pair (Ritz value, column, output slot)
+    const size_t o_lam = (size_t)k * k, o_col = o_lam + k, o_out = o_col + (k + 1) / 2, nin = o_out + (k + 1) / 2;
+    std::vector<double> hin(nin, 0.0);
+    std::copy(Vp, Vp + (size_t)k * k, hin.begin());
+    int* h_col = reinterpret_cast<int*>(hin.data() + o_col);
+    int* h_out = reinterpret_cast<int*>(hin.data() + o_out);
+    for (int i = 0; i < k; ++i) {
+        hin[o_lam + i] = pairs[i].lr;
+        h_col[i] = pairs[i].cr;
+        h_out[i] = i;
+    }
+    double *din = nullptr, *dpart = nullptr, *dres = nullptr;
+    auto fin = [&](int st) {
+        hipFree(din);
+        hipFree(dpart);
+        hipFree(dres);
+        return st;
+    };
+    if (hipMalloc((void**)&din, nin * sizeof(double)) != hipSuccess ||
+        hipMalloc((void**)&dpart, npart * sizeof(double)) != hipSuccess ||
+        hipMalloc((void**)&dres, (size_t)2 * k * sizeof(double)) != hipSuccess)
+        return fin(set_error(c, CAL_ERR_HIP, "compute_ritz_rnorm: device allocation failed"));
+    auto go = [&]() -> int {
+        CAL_HIP(c, hipMemcpyAsync(din, hin.data(), nin * sizeof(double), hipMemcpyHostToDevice, c->stream));
+        if (apply_mt_ok(k, k)) {
+            CAL_HIP(c, launch_apply_mt(Qd, ld, din, k, k, X, ld, n, c->stream));
+        } else {
+            Panel Qp = panel();
+            panel_add(Qp, Qd, ld, k);
+            CAL_TRY(apply_dev(c, n, Qp, din, k, panel_out(X, ld, k)));
+        }
+        for (int i = 0; i < k; ++i) CAL_TRY(halo_exchange(c, X + (int64_t)i * ld));
+        if (nbp > 0) {
+            CAL_TRY(spmv_resid_pair_multi_dev(c, X, ld, reinterpret_cast<const int*>(din + o_col), din + o_lam,
+                                              reinterpret_cast<const int*>(din + o_out), k, dpart, nbp));
+            CAL_HIP(c, launch_reduce(dpart, nbp, 2 * k, dres, c->stream));
+        } else {
+            for (int i = 0; i < k; ++i) {
+                SpmvArgs a{};
+                a.rowptr = c->A.rowptr + c->A.ext_off;
+                a.col = c->A.col;
+                a.val = c->A.val;
+                a.x = X + (int64_t)pairs[i].cr * ld;
+                CAL_HIP(c, launch_spmv_resid(a, nullptr, pairs[i].lr, 0.0, n, dpart + (size_t)2 * i * nbr, nbr,
+                                             c->stream));
+                CAL_HIP(c, launch_reduce(dpart + (size_t)2 * i * nbr, nbr, 2, dres + 2 * i, c->stream));
+            }
+        }
+        CAL_TRY(allreduce_sum(c, dres, 2 * k));
+        std::vector<double> h(2 * k);
+        CAL_HIP(c, hipMemcpyAsync(h.data(), dres, 2 * k * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        CAL_HIP(c, hipStreamSynchronize(c->stream));
+        for (int i = 0; i < k; ++i) rn[i] = std::sqrt(h[2 * i]) / std::sqrt(h[2 * i + 1]);
+        return 0;
+    };
+    return fin(go());
+}
+
 int cal_ca_lanczos(cal_ctx* c, const double* r, int s, int iter, const char* basis, const char* orth,
                    int diagnostics, double* T, double* Q, double* rn, double* oe, int* reorth_flags,
                    cal_lanczos_info* info) {

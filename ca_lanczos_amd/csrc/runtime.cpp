@@ -410,7 +410,7 @@ int upload_matrix(cal_ctx* c, int64_t n_rows, int64_t ext_off, int64_t n_local, 
                 CAL_HIP(c, hipMemcpy(A.ppval, ppval.data(), ppval.size() * sizeof(double), hipMemcpyHostToDevice));
                 // the plane march (k_resid_planes): a single slab without halos whose
                 // canonical slots include -P and +P (the largest offset) and whose
-                // other slots reach H <= 512 rows: lap3d (P = N^2, H = N + 1) and
+                // other slots reach H <= 256 rows: lap3d (P = N^2, H = N + 1) and
                 // lap2d (P = N, H = 2) qualify
                 const int L = A.pmaxlen;
                 if (A.pcanon && L >= 2 && ext_off == 0 && n_rows == n_local && A.lpad == 0 &&
@@ -418,7 +418,7 @@ int upload_matrix(cal_ctx* c, int64_t n_rows, int64_t ext_off, int64_t n_local, 
                     int H = 0;
                     for (int e = 1; e < L - 1; ++e) H = std::max(H, std::abs(A.pslot[e]));
                     H = (H + 1) & ~1;
-                    if (H <= 512) {
+                    if (H <= 256) {
                         std::vector<double> rz((size_t)A.npat * L, 0.0);
                         std::vector<uint8_t> rm((size_t)A.npat, 0);
                         for (int q = 0; q < A.npat; ++q)
@@ -957,6 +957,16 @@ int cal_spmv_pair_info(cal_ctx* c, int* npairpatterns, int* nentries, int64_t* n
     if (npairpatterns) *npairpatterns = c->A.use_pair ? c->A.nppat : 0;
     if (nentries) *nentries = c->A.use_pair ? c->A.npent : 0;
     if (nsplit) *nsplit = c->A.use_pair ? c->A.npsplit : 0;
+    return 0;
+}
+
+int cal_spmv_plane_info(cal_ctx* c, int64_t* plane_P, int* plane_H, int* key_mode) {
+    if (!c) return CAL_ERR_ARG;
+    if (!c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
+    const bool on = c->A.use_pair && c->A.plane_P > 0;
+    if (plane_P) *plane_P = on ? c->A.plane_P : 0;
+    if (plane_H) *plane_H = on ? c->A.plane_H : 0;
+    if (key_mode) *key_mode = !on ? -1 : (c->A.cuniform ? 0 : (c->A.npat <= 256 ? 1 : 2));
     return 0;
 }
 

@@ -101,6 +101,12 @@ int cal_spmv_format(cal_ctx* ctx, int* is_pattern, int* npatterns, int* nentries
 /* Pair patterns of the row-pattern format (two rows per lane): number of
  * merged pair patterns, their table entries, and pairs on the per-row path. */
 int cal_spmv_pair_info(cal_ctx* ctx, int* npairpatterns, int* nentries, int64_t* nsplit);
+/* The plane march of the row-pattern format (k_spmv_planes, k_resid_planes:
+ * a single slab whose canonical slots are -P .. +P with P >= 256 and the
+ * other slots within 256 rows): the plane stride P, the in-plane reach H and
+ * the key mode (0: uniform slot values keyed by slot-mask bytes, 1 / 2: 1-
+ * or 2-byte pattern ids); P = 0, key_mode = -1 when it is not in use. */
+int cal_spmv_plane_info(cal_ctx* ctx, int64_t* plane_P, int* plane_H, int* key_mode);
 /* Where the s x s algebra between the block-orthogonalisation sweeps runs:
  * "device" (default: one kernel, no host round trip inside a block) or
  * "host".  Both give bit-identical results; "host" exists for testing. */
@@ -197,6 +203,13 @@ typedef struct cal_lanczos_info {
 int cal_ca_lanczos(cal_ctx* ctx, const double* r, int s, int iter, const char* basis, const char* orth,
                    int diagnostics, double* T, double* Q, double* rn, double* oe, int* reorth_flags,
                    cal_lanczos_info* info);
+
+/* rn = compute_ritz_rnorm(A,Q,Vp,Dp) for a real eigen-decomposition.  ca_lanczos.m:88-97
+ * Q: n_local x k (host, column-major), Vp: k x k, d: the k eigenvalues
+ * diag(Dp).  [d,ix] = sort(d,'descend') (stable); rn(i) = ||A x - l x|| /
+ * ||l x|| with x = Q*Vp(:,ix(i)), l = d(ix(i)).  The diagnostics' device
+ * path: X = Q*Vp on the matrix cores, then the batched residual kernel. */
+int cal_compute_ritz_rnorm(cal_ctx* ctx, const double* Q, int k, const double* Vp, const double* d, double* rn);
 
 /* Step-wise, device-resident form of the same loop (benchmarks, restart
  * drivers).  begin() normalises r and runs the basis set-up (Newton

@@ -6,7 +6,7 @@
 
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     if (nrhs < 5) mexErrMsgIdAndTxt("calanczos:arg", "[T,Q,rn,oe] = ca_lanczos(A,r,s,iter,basis[,orth])");
-    cal_ctx* c = cal_mex_ctx(prhs[0]);
+    cal_ctx* c = cal_mex_ctx_full(prhs[0]);
     const mwSize n = mxGetN(prhs[0]);
     const int s = (int)mxGetScalar(prhs[2]), iter = (int)mxGetScalar(prhs[3]);
     if (s < 1 || iter < 1) mexErrMsgIdAndTxt("calanczos:arg", "s and iter must be positive");

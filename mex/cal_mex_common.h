@@ -14,10 +14,15 @@
  *   - the library's process-wide residency generation
  *     (cal_residency_generation, calanczos_host.h).
  * A different matrix that MATLAB allocates at freed addresses with the same
- * nnz, or an edit of a sampled entry, re-uploads.  An in-place edit
- * A(i,j) = v of an existing nonzero that the sample misses is not seen: after
- * such an edit call calanczos_invalidate() (mex/calanczos_invalidate_mex.c,
- * which bumps the generation for every shim of the process) or `clear mex`.
+ * nnz, or an edit of a sampled entry, re-uploads.  In the per-power shims
+ * (SpMV, matrix_powers_*), an in-place edit A(i,j) = v of an existing nonzero
+ * that the sample misses is not seen: after such an edit call
+ * calanczos_invalidate() (mex/calanczos_invalidate_mex.c, which bumps the
+ * generation for every shim of the process) or `clear mex`.  The solver shims
+ * (ca_lanczos, restarted_ca_lanczos, impl_restarted_ca_lanczos) run once per
+ * solve, so they digest every entry of jc / ir / pr (cal_mex_ctx_full: about
+ * 0.1 s at nnz = 7e7, next to a solve of seconds) and see every edit, as the
+ * reference's SpMV.m:8 reads the current A.
  * MATLAB calls mexFunction on one thread, which matches the ABI's
  * one-thread-per-context rule. */
 #ifndef CAL_MEX_COMMON_H
@@ -48,12 +53,20 @@ static uint64_t cal_mex_mix(uint64_t h, uint64_t w) {
     return h;
 }
 
-/* digest of a bounded sample of an array of `count` 8-byte words: the first
- * and last 32 and up to kCalMexSamples evenly spaced ones */
-static uint64_t cal_mex_sample(uint64_t h, const void* p, size_t count) {
+/* digest of an array of `count` 8-byte words: every word (full), or a
+ * bounded sample: the first and last 32 and up to kCalMexSamples evenly
+ * spaced ones */
+static uint64_t cal_mex_sample(uint64_t h, const void* p, size_t count, int full) {
     const unsigned char* b = (const unsigned char*)p;
     uint64_t w;
     size_t i, edge = count < 64 ? count : 32;
+    if (full) {
+        for (i = 0; i < count; ++i) {
+            memcpy(&w, b + 8 * i, 8);
+            h = cal_mex_mix(h, w);
+        }
+        return h;
+    }
     for (i = 0; i < edge; ++i) {
         memcpy(&w, b + 8 * i, 8);
         h = cal_mex_mix(h, w);
@@ -74,11 +87,11 @@ static uint64_t cal_mex_sample(uint64_t h, const void* p, size_t count) {
 
 /* the residency decision: 1 when the device copy must be (re)uploaded */
 static int cal_mex_stale(const mwIndex* jc, const mwIndex* ir, const double* pr, mwSize n, long long gen,
-                         uint64_t* digest) {
+                         int full, uint64_t* digest) {
     const mwSize nnz = jc[n];
-    uint64_t d = cal_mex_sample(0xcbf29ce484222325ULL ^ (uint64_t)n, jc, n + 1);
-    d = cal_mex_sample(d, ir, nnz);
-    d = cal_mex_sample(d, pr, nnz);
+    uint64_t d = cal_mex_sample(0xcbf29ce484222325ULL ^ (uint64_t)n, jc, n + 1, full);
+    d = cal_mex_sample(d, ir, nnz, full);
+    d = cal_mex_sample(d, pr, nnz, full);
     *digest = d;
     return jc != g_jc || ir != g_ir || pr != g_pr || n != g_n || nnz != g_nnz || gen != g_gen || d != g_digest;
 }
@@ -105,7 +118,7 @@ static cal_ctx* cal_mex_plain_ctx(void) {
 /* Make A resident (the `A` of SpMV.m:6 / ca_lanczos.m:24).  MATLAB sparse is
  * CSC with mwIndex (int64) jc / ir; cal_set_matrix_csc transposes it into CSR,
  * so the device holds A itself (SpMV.m:8 is a general A*v). */
-static cal_ctx* cal_mex_ctx(const mxArray* A) {
+static cal_ctx* cal_mex_ctx_mode(const mxArray* A, int full) {
     if (!mxIsSparse(A) || mxIsComplex(A) || mxGetM(A) != mxGetN(A))
         mexErrMsgIdAndTxt("calanczos:arg", "A must be a real square sparse matrix");
     cal_ctx* c = cal_mex_plain_ctx();
@@ -113,7 +126,7 @@ static cal_ctx* cal_mex_ctx(const mxArray* A) {
     const mwSize n = mxGetN(A);
     const long long gen = cal_residency_generation();
     uint64_t d = 0;
-    if (cal_mex_stale(jc, mxGetIr(A), mxGetPr(A), n, gen, &d)) {
+    if (cal_mex_stale(jc, mxGetIr(A), mxGetPr(A), n, gen, full, &d)) {
         cal_mex_check(cal_set_matrix_csc(c, (int64_t)n, (const int64_t*)jc, (const int64_t*)mxGetIr(A),
                                          mxGetPr(A)));
         g_jc = jc;
@@ -126,6 +139,11 @@ static cal_ctx* cal_mex_ctx(const mxArray* A) {
     }
     return c;
 }
+
+/* the per-power shims: sampled digest + generation */
+static cal_ctx* cal_mex_ctx(const mxArray* A) { return cal_mex_ctx_mode(A, 0); }
+/* the solver shims: every entry digested */
+static cal_ctx* cal_mex_ctx_full(const mxArray* A) { return cal_mex_ctx_mode(A, 1); }
 
 /* a cell array {Q1, Q2, ...} -> (nblocks, blocks, widths); [] has width 0 */
 static int cal_mex_cell(const mxArray* cell, const double*** Q, int** w) {

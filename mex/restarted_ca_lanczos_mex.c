@@ -5,7 +5,7 @@
 
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     if (nrhs < 3) mexErrMsgIdAndTxt("calanczos:arg", "[E,V,nres,rn,oe] = restarted_ca_lanczos(A,r,max_lanczos,...)");
-    cal_ctx* c = cal_mex_ctx(prhs[0]);
+    cal_ctx* c = cal_mex_ctx_full(prhs[0]);
     const mwSize n = mxGetN(prhs[0]);
     const int ml = (int)mxGetScalar(prhs[2]);
     const int nw = nrhs > 3 ? (int)mxGetScalar(prhs[3]) : 10;          /* :17-33 defaults */

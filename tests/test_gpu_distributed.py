@@ -305,3 +305,75 @@ def test_restart_drivers_two_ranks(cal, ref):
         assert np.max(np.abs(V.T @ V - np.eye(nw))) < 1e-9
         res_n = np.linalg.norm(A @ V - V * outs[0]["conv_eigs"], axis=0)
         assert np.max(res_n) < 1e-6
+
+
+def _pn_worker(rank, world, port, heights, out_q):
+    """Tier-1 projectAndNormalize (TSQR normalize, the fused fold when its
+    shape applies) on row panels whose local heights match the resident
+    slab on one rank and not on the other."""
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import ca_lanczos_amd as cal
+
+    def allreduce(a):
+        t = torch.from_numpy(a)
+        dist.all_reduce(t)
+
+    def exchange(peer, send, recv):  # no halo exchange in this test
+        raise RuntimeError("unexpected exchange")
+
+    A = cal.matrices.laplacian_2d(200)
+    n = A.shape[0]
+    b = cal.matrices.slab_bounds(n, world, 200)
+    r0, r1 = b[rank], b[rank + 1]
+    ctx = cal.Context(0)
+    ctx.comm_init_host(world, rank, allreduce, exchange)
+    ctx.set_matrix_slab(n, r0, A[r0:r1])
+    assert heights[0] == r1 - r0 or rank != 0
+    rng = np.random.RandomState(7)
+    N = sum(heights)
+    Qp = np.linalg.qr(rng.randn(N, 9))[0]
+    X = rng.randn(N, 8)
+    lo = sum(heights[:rank])
+    QZ, RZ, re, rk = cal.projectAndNormalize_ex([Qp[lo:lo + heights[rank]]], X[lo:lo + heights[rank]], True,
+                                                ctx=ctx)
+    out_q.put((rank, QZ, RZ, re, rk))
+    ctx.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_tier1_project_and_normalize_mismatched_heights(cal, ref):
+    """the fold's shape vote must be reached by the same branch on
+    every rank.  Rank 0's panel has its slab's height (20000 rows), rank 1's
+    does not (20037): both ranks vote by one all-reduce (the run used to hang
+    when rank 0 took the slab table and rank 1 the vote).  The result equals
+    the one-rank call on the stacked panel to 1e-12."""
+    world = 2
+    heights = (20000, 20037)
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    procs = [mpc.Process(target=_pn_worker, args=(r, world, port, heights, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rng = np.random.RandomState(7)
+    N = sum(heights)
+    Qp = np.linalg.qr(rng.randn(N, 9))[0]
+    X = rng.randn(N, 8)
+    QZ1, RZ1, re1, rk1 = cal.projectAndNormalize_ex([Qp], X, True)
+    QZ = np.vstack([r[1] for r in res])
+    assert res[0][3] == res[1][3] == re1 and res[0][4] == res[1][4] == rk1
+    for r in res:
+        for a, b in zip(r[2], RZ1):
+            assert np.max(np.abs(a - b)) <= 1e-12 * max(1.0, np.max(np.abs(b)))
+    assert np.max(np.abs(QZ - QZ1)) <= 1e-12
+    assert np.max(np.abs(QZ.T @ QZ - np.eye(8))) < 1e-13

@@ -111,6 +111,17 @@ int main(void) {
         cal_mex_ctx(&B);
         const int inval = uploads - u0;        /* 3 */
         printf("%d %d %d %d %.3f\n", cached, sampled, missed, inval, best);
+        /* the solver shims' full digest: the entry the sample misses is seen */
+        g_jc = NULL;
+        int f0 = uploads;
+        cal_mex_ctx_full(&B);                  /* upload (other mode's digest) */
+        cal_mex_ctx_full(&B);                  /* cached */
+        bpr[12345679] = -11.0;                 /* an entry the sample misses */
+        cal_mex_ctx_full(&B);                  /* re-upload */
+        bir[NNZ - 40] = (bir[NNZ - 40] + 1) % N;  /* a pattern edit outside the sample */
+        cal_mex_ctx_full(&B);                  /* re-upload */
+        cal_mex_ctx_full(&B);                  /* cached */
+        printf("%d\n", uploads - f0);        /* 3 */
     }
 #endif
     return 0;
@@ -141,7 +152,8 @@ def test_mex_residency_decision_is_cheap_at_config3_size(tmp_path):
     ~0.1 s, on every SpMV.mexa64 call).  It still re-uploads after an edit of
     a sampled entry; an edit the sample misses is not seen until the
     documented calanczos_invalidate() (cal_residency_invalidate), after which
-    every shim re-uploads once.  CPU only (≈1.2 GB of host arrays)."""
+    every shim re-uploads once.  The solver shims' full digest sees it.  CPU
+    only (≈1.2 GB of host arrays)."""
     src = tmp_path / "cache.c"
     src.write_text(_CACHE_HARNESS)
     exe = tmp_path / "cache_big"
@@ -154,3 +166,6 @@ def test_mex_residency_decision_is_cheap_at_config3_size(tmp_path):
     cached, sampled, missed, inval, ms = out[1].split()
     assert (int(cached), int(sampled), int(missed), int(inval)) == (1, 2, 2, 3)
     assert float(ms) <= 5.0, ms
+    # the solver shims (ca_lanczos, restarted_*, impl_restarted_*)
+    # digest every entry and re-upload after the edit the sample misses
+    assert int(out[2]) == 3
