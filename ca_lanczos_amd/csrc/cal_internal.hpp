@@ -128,6 +128,7 @@ struct PatArgs {
     // cval[e], as in the Laplacians): the plane march keys each row by its
     // slot mask byte (rowmask) and takes the values from cval
     const uint8_t* rowmask = nullptr;
+    const uint32_t* wavemask = nullptr;  // DevMatrix::wavemask
     int cuniform = 0;
     double cval[8] = {};
     int64_t plane_P = 0;
@@ -139,6 +140,8 @@ struct PatArgs {
     int64_t gap_at = 0, gap = 0;
 };
 constexpr int kPairSplit = 0xFFFF;
+// the plane march: rows of a plane per block (4 waves x 64 lanes x 2 rows)
+constexpr int kPlaneBlockRows = 512;
 
 struct DevMatrix {
     int64_t n_local = 0, n_global = 0, row0 = 0, nnz = 0, nghost = 0;
@@ -186,6 +189,11 @@ struct DevMatrix {
     uint8_t* rzmask = nullptr;
     uint8_t* rowkey8 = nullptr;
     uint8_t* rowmask = nullptr;
+    // per plane z (0 .. nz, the last one zero) and 512-row block xy of the
+    // plane march: byte w = OR over the 128 rows of wave w of the slots those
+    // rows lack (rows past n lack every slot); the march masks only those
+    // slots (kernels.hip, PlaneMarch)
+    uint32_t* wavemask = nullptr;
     bool cuniform = false;
     double cval[8] = {};
     int64_t plane_P = 0;

@@ -43,9 +43,8 @@ typedef double d2 __attribute__((ext_vector_type(2)));
 constexpr int kSpmvThreads = 256;
 constexpr int kSpmvNnz = 2048;  // LDS-staged nonzeros per row block (16 KiB)
 // the plane march (k_spmv_planes, k_resid_planes): planes per block of the
-// residual kernel, rows of a plane per block
+// residual kernel (rows of a plane per block: kPlaneBlockRows)
 constexpr int kResidPlanes = 32;
-constexpr int kResidPlaneRows = 512;
 
 // Column c of a panel.  The segment table is taken by value and read with
 // static indices only: binding a reference to a by-value kernel argument
@@ -604,67 +603,71 @@ bool spmv_pat_pair_path(const PatArgs& a) {
 // For matrices in canonical slots -P < ... < +P (pslot[0] = -P, pslot[L-1] =
 // +P, P >= 256) whose inner slots reach H <= 256 rows -- the 7-point (P =
 // N^2, N < 256) and 5-point (P = N) Laplacians -- on a single slab.  A block
-// owns the rows xy0 .. xy0 + 511 of every plane (r = xy + z P) for Z planes.
-// Per plane it stages into LDS:
-//   * the window x[zP + xy0 - H, zP + xy0 + 512 + H) by contiguous 16-B
-//     buffer loads (rows outside the column read 0: a negative row's 32-bit
-//     byte offset is >= 2^31, past the descriptor's range, and so is a row at
-//     or past ld; ld < 2^28);
-//   * the rows' keys (slot mask bytes, or pattern ids of 1 / 2 B) by aligned
-//     dword loads;
-// and once per block the pattern table (KM != 0): per pattern its slot values
-// with 0.0 where the row has no entry (stride L2 = L rounded up to even), and
-// slot masks.  Each lane takes its row pair (xy0 + lr, + 1): the inner slots
-// from the window, the -P / +P slots the same lane's centre pair of the
-// previous / next plane (register, next buffer).  With LN (slots -1, 0, +1
-// around the middle) the +-1 pairs are the centre pair plus one value on each
-// side: one two-value LDS read instead of two pairs.  Plane z0 + j + 2 is
-// loaded into registers at the top of step j and stored to LDS at its end, so
-// every load has a plane's work to land.  Each x value leaves HBM about once
-// ((Z + 2) / Z: a block also stages its neighbours' first and last plane) and
-// the in-plane gathers are LDS reads.  When P is odd the plane's last pair
-// straddles into the next plane: only its first row belongs to the block.
+// owns the rows xy0 .. xy0 + 511 of every plane (r = xy + z P) for Z planes;
+// lane t owns the row pair xy0 + 2t, + 1.  Per plane the block stages the
+// window x[zP + xy0 - H, zP + xy0 + 512 + H) in LDS, split by row parity:
+// E[p] = x(g + 2p), O[p] = x(g + 2p + 1) with g = zP + xy0 - H, so that
+// every slot of a row pair is read as 8-B values at consecutive addresses
+// across the lanes (ds_read_b64, conflict-free; the pair layout's 16-B lane
+// stride made every 8-B read 2-way and ds_read2_b64 runs at half rate).
+// Each lane loads its own row pair (pair t + H/2 of the window) with one
+// 16-B buffer load and keeps it in registers for three planes: as the +P
+// slot of plane z - 1, the centre of plane z, the -P slot of plane z + 1;
+// lanes t < H also load one halo pair.  Plane z0 + j + 2 is loaded at the
+// top of step j and stored at its end, so the loads have a plane's work to
+// land.  Rows outside the column read 0 (a negative row's 32-bit byte offset
+// is >= 2^31, past the descriptor's range, as is a row at or past ld; ld <
+// 2^28).  Each x value leaves HBM about once ((Z + 2) / Z: a block also
+// stages its neighbours' first and last plane); the in-plane gathers are LDS
+// reads.  When P is odd the plane's last pair straddles into the next plane:
+// only its first row belongs to the block.
 //
 // Every row adds its own entries in slot (= column) order.  Where some row of
-// a wave has no entry at slot e (wave-uniform test: the OR of the rows'
-// missing-slot masks), slot e's x values enter each row ANDed with the row's
-// mask bit, i.e. as +0.0 where the row has no entry: 0 * (+0.0) adds a zero,
-// which leaves a running sum that is never -0.0 unchanged, and a non-finite x
-// outside a row never leaks into it (the SpMV's contract, k_spmv_pair).  A
-// slot every row of the wave has is added unmasked.  So the sums are the bits
-// of k_spmv / k_spmv_pair; the per-row selects of round 4 cost 12 VALU
-// instructions per slot and were taken by nearly every wave of lap3d (each
-// 128-row wave meets an x = 0 / N - 1 row).
+// a wave lacks slot e (the host's per-wave OR of the rows' missing slots,
+// DevMatrix::wavemask, one uniform dword per plane and block), slot e's x
+// values enter each row ANDed with the row's mask bit, i.e. as +0.0 where the
+// row has no entry: 0 * (+0.0) adds a zero, which leaves a running sum that
+// is never -0.0 unchanged, and a non-finite x outside a row never leaks into
+// it (the SpMV's contract, k_spmv_pair).  A slot every row of the wave has is
+// added unmasked.  NEG1 (uniform values, -1 at every slot but the middle: the
+// Laplacians) adds y - x for those slots: (-1) * x is exact, so y + (-1) * x
+// and y - x are the same bits.  So the sums are the bits of k_spmv /
+// k_spmv_pair.
 // KM = 0: uniform slot values (cval; every row with an entry at slot e has
 // the value cval[e], as in the Laplacians): the keys are the rows' slot mask
 // bytes.  KM = 1 / 2: the keys are the rows' pattern ids (1 / 2 B) into the
 // LDS value / mask tables.
-template <int MAXLEN, int KM, bool LN>
+template <int MAXLEN, int KM, bool LN, bool NEG1>
 struct PlaneMarch {
     static constexpr int KB = KM == 2 ? 2 : 1;                  // key bytes per row
     typedef unsigned int u4 __attribute__((ext_vector_type(4)));
     static constexpr int L2 = (MAXLEN + 1) & ~1;                // table row stride (16-B reads)
-    static constexpr int KD = (kResidPlaneRows * KB + 6) / 4 + 1;  // key dwords per plane (with the alignment slack)
+    static constexpr int KD = (kPlaneBlockRows * KB + 6) / 4 + 1;  // key dwords per plane (with the alignment slack)
     static constexpr int KR = (KD + 255) / 256;                 // key dword rounds per thread
-    static constexpr int NK = 2;                                // window pair rounds: WP = 256 + H <= 512
     static constexpr int MID = MAXLEN / 2;                      // LN: slots MID - 1, MID, MID + 1 = -1, 0, +1
+    // one plane buffer: E (window pairs' even rows) then O (odd rows), each
+    // for up to 512 pairs (H <= 256): compile-time strides, so every LDS
+    // access is a per-lane address set up once plus an immediate offset
+    static constexpr int EO = 512, BUF = 2 * EO;
     // plain scalars and pointers only: a reference to the by-value kernel
     // argument would make every thread copy it to scratch; row indices are
     // 32-bit (planes_ok: ld < 2^28)
-    int H, WR, tid, lr, wi, zend, P, n, xy0, z0;
-    bool in0, in1, full;
-    double* win;      // [3][WR]
+    int H, tid, pc, zend, P, n, xy0, z0, nxy, xyb, wsh;
+    bool in0, in1, full, halo;
+    double* win;      // [3][BUF]
     uint32_t* keys;   // [3][KD]
     double* s_rz;     // npat x L2 slot values (0 where the row has no entry)
     uint8_t* s_rm;    // npat slot masks
-    __amdgpu_buffer_rsrc_t rx, rk;
+    __amdgpu_buffer_rsrc_t rx, rk, rw;
     int ps[MAXLEN];     // slot offsets (compile-time indices only)
     double cv[MAXLEN];  // KM = 0: the slot values
-    unsigned fullm;     // every slot
-    int pi16[NK];       // the lane's window pairs (clamped), byte offsets
+    int ia[MAXLEN], ib[MAXLEN];  // in-plane slots: the lane's window indices of its two values (buffer 0)
+    int cof16, hof16;   // the lane's own / halo pair, window byte offsets
+    int ph;             // the halo pair's index
     int k4[KR];         // the lane's key dwords (clamped), byte offsets
-    double2 st[NK];     // the prefetched plane (registers)
+    double2 st0, st1;   // the prefetched plane's own and halo pair (registers)
     uint32_t kst[KR];
+    uint32_t wmv;       // the prefetched plane's wave masks (uniform)
 
     __device__ static __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
         const uint64_t pl = (uint64_t)(uintptr_t)p;
@@ -673,31 +676,36 @@ struct PlaneMarch {
         return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0,
                                                  (int)__builtin_amdgcn_readfirstlane((uint32_t)bytes), 0x00020000);
     }
-    __host__ __device__ static size_t lds_bytes(int H, int npat) {
-        return (size_t)3 * (kResidPlaneRows + 2 * H) * 8 + (((size_t)3 * KD * 4 + 15) & ~(size_t)15) +
+    __host__ __device__ static size_t lds_bytes(int npat) {
+        return (size_t)3 * BUF * 8 + (((size_t)3 * KD * 4 + 15) & ~(size_t)15) +
                (KM == 0 ? 0 : (size_t)npat * L2 * 8 + (size_t)npat) + 16;
     }
     // the fields are passed one by one from the kernel's by-value PatArgs
     __device__ PlaneMarch(int64_t P_, int H_, int64_t n_, int64_t ld_, const double* x, const void* key,
-                          const double* rzval, const uint8_t* rzmask, int npat, double* lds, int bi, int Z) {
+                          const uint32_t* wavemask, const double* rzval, const uint8_t* rzmask, int npat,
+                          double* lds, int bi, int Z) {
         H = H_;
-        WR = kResidPlaneRows + 2 * H;
-        const int WP = WR / 2;
         tid = threadIdx.x;
         P = (int)P_;
         n = (int)n_;
-        const int nxy = (P + kResidPlaneRows - 1) / kResidPlaneRows;
+        nxy = (P + kPlaneBlockRows - 1) / kPlaneBlockRows;
         const int nz = (n + P - 1) / P;
-        xy0 = (bi % nxy) * kResidPlaneRows;
+        xyb = bi % nxy;
+        xy0 = xyb * kPlaneBlockRows;
         z0 = (bi / nxy) * Z;
         zend = nz - z0 < Z ? nz - z0 : Z;
-        lr = 2 * tid;
-        wi = lr + H;
-        in0 = xy0 + lr < P;
-        in1 = xy0 + lr + 1 < P;
-        full = xy0 + kResidPlaneRows <= P && (int64_t)(z0 + zend) * P <= n_;
+        in0 = xy0 + 2 * tid < P;
+        in1 = xy0 + 2 * tid + 1 < P;
+        full = xy0 + kPlaneBlockRows <= P && (int64_t)(z0 + zend) * P <= n_;
+        wsh = 8 * __builtin_amdgcn_readfirstlane(tid >> 6);
+        pc = tid + H / 2;
+        const int h = tid < H ? tid : H - 1;
+        halo = tid < H;
+        ph = h < H / 2 ? h : h + 256;
+        cof16 = 16 * pc;
+        hof16 = 16 * ph;
         win = lds;
-        keys = reinterpret_cast<uint32_t*>(win + 3 * WR);
+        keys = reinterpret_cast<uint32_t*>(win + 3 * BUF);
         s_rz = reinterpret_cast<double*>(keys + ((3 * KD + 3) & ~3));
         s_rm = reinterpret_cast<uint8_t*>(s_rz + npat * L2);
         if (KM != 0) {
@@ -707,15 +715,24 @@ struct PlaneMarch {
             }
             for (int i = tid; i < npat; i += 256) s_rm[i] = rzmask[i];
         }
-        fullm = (1u << MAXLEN) - 1u;
-#pragma unroll
-        for (int k = 0; k < NK; ++k) pi16[k] = 16 * min(tid + 256 * k, WP - 1);
 #pragma unroll
         for (int k = 0; k < KR; ++k) k4[k] = 4 * min(tid + 256 * k, KD - 1);
         rx = rsrc(x, ld_ * 8);
         // the key arrays carry >= 4 zero bytes past the rows (upload_matrix), so
         // every aligned dword load that reaches a real row lies inside
         rk = rsrc(key, (KB * n_ + 7) & ~(int64_t)3);
+        rw = rsrc(wavemask, (int64_t)(nz + 1) * nxy * 4);
+    }
+    // after ps[] is set: the in-plane slots' window indices.  Rows 2t + H + o,
+    // + 1 are (E, O)[pc + o / 2] for even o, else (O[pc + floor(o / 2)],
+    // E[pc + ceil(o / 2)])
+    __device__ void slots() {
+#pragma unroll
+        for (int e = 0; e < MAXLEN; ++e) {
+            const int o = ps[e];
+            ia[e] = ((o & 1) ? EO : 0) + pc + (o >> 1);
+            ib[e] = ((o & 1) ? 0 : EO) + pc + ((o + 1) >> 1);
+        }
     }
     // 16 B at byte offset off of the column: off < 0 (as 32 bits >= 2^31) or
     // past ld * 8 reads 0.  A load that straddles the descriptor's end returns
@@ -728,62 +745,91 @@ struct PlaneMarch {
                             __builtin_bit_cast(double, ((uint64_t)w.w << 32) | w.z));
     }
     __device__ double2 ld2(int row) const { return ld16(row * 8); }
-    // issue plane z's loads (window + keys) into registers.  Lanes past the
-    // end load (and later store) the last pair / dword again: the same data
-    // to the same place, and no divergent branch.
+    // issue plane z's loads into registers: the lane's own pair, its halo pair
+    // (lanes past H load lane H - 1's again and do not store it), the keys, the
+    // waves' masks.
     __device__ void load(int z) {
         const int g8 = (z * P + xy0 - H) * 8;
-#pragma unroll
-        for (int k = 0; k < NK; ++k) st[k] = ld16(g8 + pi16[k]);
+        st0 = ld16(g8 + cof16);
+        st1 = ld16(g8 + hof16);
         const int al = ((z * P + xy0) * KB) & ~3;
 #pragma unroll
         for (int k = 0; k < KR; ++k) kst[k] = __builtin_amdgcn_raw_buffer_load_b32(rk, al + k4[k], 0, 0);
+        wmv = __builtin_amdgcn_raw_buffer_load_b32(rw, 0, (z * nxy + xyb) * 4, 0);
     }
-    // the prefetched plane into LDS buffer b
-    __device__ void store(int b) {
-        char* wb = reinterpret_cast<char*>(win + b * WR);
-#pragma unroll
-        for (int k = 0; k < NK; ++k) *reinterpret_cast<double2*>(wb + pi16[k]) = st[k];
-        char* kb = reinterpret_cast<char*>(keys + b * KD);
+    // the prefetched plane into LDS buffer B
+    template <int B>
+    __device__ void store() {
+        double* w = win + B * BUF;
+        w[pc] = st0.x;
+        w[EO + pc] = st0.y;
+        if (halo) {
+            w[ph] = st1.x;
+            w[EO + ph] = st1.y;
+        }
+        char* kb = reinterpret_cast<char*>(keys + B * KD);
 #pragma unroll
         for (int k = 0; k < KR; ++k) *reinterpret_cast<uint32_t*>(kb + k4[k]) = kst[k];
     }
-    // The march: plane z0 + j + 2 is loaded into registers at the top of step
-    // j, the step computes plane z0 + j from LDS, then stores the prefetched
-    // plane into buffer (j + 2) % 3 and synchronizes.  f(j, bc, bn) computes
-    // plane z0 + j from buffers bc (current) and bn (next).
-    // xp: the lane's -P pair of the first plane, loaded before the march; it
-    // is pinned once the prologue's stores have waited for the loads (loads
-    // return in order), so the loop's first use does not wait for the
-    // prefetch issued at the top of the step (the compiler otherwise places
-    // a vmcnt(0) there for the value carried in from the preheader).
-    template <typename F>
-    __device__ void march(double2& xp, F&& f) {
-        load(z0);
-        store(0);
-        load(z0 + 1);
-        store(1);
-        asm volatile("" : "+v"(xp.x), "+v"(xp.y));
+    __device__ unsigned wave_bits(uint32_t v) const {
+        return (__builtin_amdgcn_readfirstlane(v) >> wsh) & 0xffu;
+    }
+    // One step of the march on plane z0 + j, whose window is buffer B: plane
+    // z0 + j + 2 is loaded into registers first, f(j, B, xp, xc, xn, wm)
+    // computes plane z0 + j (r[(B + 2) % 3] / r[B] / r[(B + 1) % 3]: the
+    // lane's pair of planes j - 1 / j / j + 1, wm the wave's mask), then the
+    // prefetched plane goes into buffer (B + 2) % 3 and register set
+    // (B + 2) % 3 (plane j - 1's, no longer needed), and the block syncs.
+    template <int B, typename F>
+    __device__ void step(int j, double2 (&r)[3], unsigned (&w)[3], F&& f) {
+        constexpr int BP = (B + 2) % 3, BN = (B + 1) % 3;
+        if (j + 2 <= zend) load(z0 + j + 2);
+        f(j, std::integral_constant<int, B>{}, r[BP], r[B], r[BN], w[B]);
+        // the plane's arithmetic stays ahead of the stores, which wait for
+        // the prefetch (the compiler otherwise sinks it below them).  The
+        // store is unconditional: in the last step it writes the registers
+        // again into the buffer of plane zend - 2, which no step reads any
+        // more.
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("" ::: "memory");
+        store<BP>();
+        r[BP] = st0;
+        w[BP] = wave_bits(wmv);
         __syncthreads();
-        for (int j = 0; j < zend; ++j) {
-            if (j + 2 <= zend) load(z0 + j + 2);
-            f(j, j % 3, (j + 1) % 3);
-            // the plane's arithmetic stays ahead of the stores, which wait for
-            // the prefetch (the compiler otherwise sinks it below them).  The
-            // store is unconditional to keep both in one block: in the last
-            // step it writes the registers again into the buffer of plane
-            // zend - 2, which no step reads any more.
-            __builtin_amdgcn_sched_barrier(0);
-            store((j + 2) % 3);
-            __syncthreads();
+    }
+    // The march, unrolled by three so that the buffer of every access and the
+    // roles of the three register pairs are compile-time.  xp: the lane's pair
+    // of plane z0 - 1, loaded before the march; the pairs are pinned once the
+    // prologue's stores have waited for the loads (loads return in order), so
+    // the loop's first use does not wait for the prefetch issued at the top of
+    // the step.
+    template <typename F>
+    __device__ void march(const double2& xp, F&& f) {
+        double2 r[3];
+        unsigned w[3];
+        load(z0);
+        store<0>();
+        r[0] = st0;
+        w[0] = wave_bits(wmv);
+        load(z0 + 1);
+        store<1>();
+        r[1] = st0;
+        w[1] = wave_bits(wmv);
+        r[2] = xp;
+        w[2] = 0;
+        asm volatile("" : "+v"(r[0].x), "+v"(r[0].y), "+v"(r[1].x), "+v"(r[1].y), "+v"(r[2].x), "+v"(r[2].y));
+        __syncthreads();
+        for (int j = 0; j < zend; j += 3) {
+            step<0>(j, r, w, f);
+            if (j + 1 < zend) step<1>(j + 1, r, w, f);
+            if (j + 2 < zend) step<2>(j + 2, r, w, f);
         }
     }
-    // the lane's centre pair of plane buffer b
-    __device__ double2 centre(int b) const { return *reinterpret_cast<const double2*>(win + b * WR + wi); }
-    // the lane's two row keys of plane z (buffer b)
-    __device__ void row_keys(int b, int z, unsigned& k0, unsigned& k1) const {
+    // the lane's two row keys of plane z (buffer B)
+    template <int B>
+    __device__ void row_keys(int z, unsigned& k0, unsigned& k1) const {
         const int kofs = ((z * P + xy0) * KB) & 3;
-        const uint8_t* kp = reinterpret_cast<const uint8_t*>(keys + b * KD) + kofs + lr * KB;
+        const uint8_t* kp = reinterpret_cast<const uint8_t*>(keys + B * KD) + kofs + 2 * tid * KB;
         if (KB == 1) {
             k0 = kp[0];
             k1 = kp[1];
@@ -792,53 +838,58 @@ struct PlaneMarch {
             k1 = *reinterpret_cast<const uint16_t*>(kp + 2);
         }
     }
-    // the OR of the wave's lanes (DPP row shifts, then the row broadcasts)
-    __device__ static unsigned wave_or(unsigned v) {
-        v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
-        v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
-        v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
-        v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
-        v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-        v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-        return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
-    }
     // x with the row's slot-e bit: x, or +0.0 where the row has no entry
     __device__ static double keep(double x, unsigned m, int e) {
         const unsigned k = 0u - ((m >> e) & 1u);
-        uint2 w = __builtin_bit_cast(uint2, x);
-        w.x &= k;
-        w.y &= k;
-        return __builtin_bit_cast(double, w);
+        uint2 v = __builtin_bit_cast(uint2, x);
+        v.x &= k;
+        v.y &= k;
+        return __builtin_bit_cast(double, v);
     }
-    // y0 / y1: the slot sums of the lane's two rows of plane z (buffer b; bn
-    // the next plane, xp / xc the previous / current plane's centre pair),
+    // y0 / y1: the slot sums of the lane's two rows of plane z (buffer B),
     // each row's own entries in slot (= column) order.  Z0: the sums start
     // from +0.0 (the stored SpMV: a zero sum is +0.0, as in k_spmv); the
     // residual squares its sums and starts from the first product.
-    template <bool Z0>
-    __device__ void sums(int b, int bn, int z, const double2& xp, const double2& xc, double& y0, double& y1) const {
-        unsigned k0, k1;
-        row_keys(b, z, k0, k1);
-        const unsigned m0 = KM == 0 ? k0 : s_rm[k0], m1 = KM == 0 ? k1 : s_rm[k1];
-        const unsigned wm = wave_or(fullm & ~(m0 & m1));
-        const double* w = win + b * WR + wi;
+    template <bool Z0, int B>
+    __device__ void sums(int z, const double2& xp, const double2& xc, const double2& xn, unsigned wm, double& y0,
+                         double& y1) const {
+        const double* w = win + B * BUF;
+        unsigned k0 = 0, k1 = 0, m0 = 0, m1 = 0;
+        if (KM != 0 || wm != 0) {
+            row_keys<B>(z, k0, k1);
+            m0 = KM == 0 ? k0 : s_rm[k0];
+            m1 = KM == 0 ? k1 : s_rm[k1];
+        }
         double lo = 0.0, hi = 0.0;
         if (LN) {
-            lo = w[-1];
-            hi = w[2];
+            lo = w[EO + pc - 1];  // row 2t + H - 1
+            hi = w[pc + 1];       // row 2t + H + 2
         }
 #pragma unroll
         for (int e = 0; e < MAXLEN; ++e) {
             double2 v;
             if (e == 0) v = xp;
-            else if (e == MAXLEN - 1) v = *reinterpret_cast<const double2*>(win + bn * WR + wi);
+            else if (e == MAXLEN - 1) v = xn;
             else if (LN && e == MID - 1) v = make_double2(lo, xc.x);
             else if (LN && e == MID) v = xc;
             else if (LN && e == MID + 1) v = make_double2(xc.y, hi);
-            else v = make_double2(w[ps[e]], w[ps[e] + 1]);
+            else v = make_double2(w[ia[e]], w[ib[e]]);
             if (wm >> e & 1u) {
                 v.x = keep(v.x, m0, e);
                 v.y = keep(v.y, m1, e);
+            }
+            if (NEG1 && e != MID) {  // coefficient -1: y + (-1) x == y - x
+                if (e == 0 && !Z0) {
+                    y0 = -v.x;
+                    y1 = -v.y;
+                } else if (e == 0) {
+                    y0 = 0.0 - v.x;
+                    y1 = 0.0 - v.y;
+                } else {
+                    y0 = y0 - v.x;
+                    y1 = y1 - v.y;
+                }
+                continue;
             }
             const double c0 = KM == 0 ? cv[e] : s_rz[k0 * L2 + e];
             const double c1 = KM == 0 ? cv[e] : s_rz[k1 * L2 + e];
@@ -858,14 +909,16 @@ struct PlaneMarch {
 };
 
 #define CAL_PLANE_MARCH(PM, XPTR, Zv)                                                                          \
-    PlaneMarch<MAXLEN, KM, LN> PM(a.plane_P, a.plane_H, a.n, a.ld, XPTR,                                       \
-                                  KM == 0 ? (const void*)a.rowmask                                            \
-                                          : (KM == 1 ? (const void*)a.rowkey8 : (const void*)a.pat),          \
-                                  a.rzval, a.rzmask, a.npat, lds_plane, xcd_remap(blockIdx.x, gridDim.x), Zv); \
+    PlaneMarch<MAXLEN, KM, LN, NEG1> PM(a.plane_P, a.plane_H, a.n, a.ld, XPTR,                                 \
+                                        KM == 0 ? (const void*)a.rowmask                                      \
+                                                : (KM == 1 ? (const void*)a.rowkey8 : (const void*)a.pat),    \
+                                        a.wavemask, a.rzval, a.rzmask, a.npat, lds_plane,                     \
+                                        xcd_remap(blockIdx.x, gridDim.x), Zv);                                \
     _Pragma("unroll") for (int e_ = 0; e_ < MAXLEN; ++e_) {                                                   \
         PM.ps[e_] = a.pslot[e_];                                                                              \
         PM.cv[e_] = a.cval[e_];                                                                               \
-    }
+    }                                                                                                         \
+    PM.slots();
 
 // SpMV (with the Newton shift) on the plane march, bit-identical to k_spmv /
 // k_spmv_pair.  One 16-B store per row pair (8-B aligned on the odd planes
@@ -877,19 +930,19 @@ __device__ __forceinline__ double2 ld16g(const double* p) {
     return v;
 }
 
-template <int MODE, int MAXLEN, int Z, int KM, bool LN>
+template <int MODE, int MAXLEN, int Z, int KM, bool LN, bool NEG1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_spmv_planes(PatArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds_plane[];
     CAL_PLANE_MARCH(pm, a.x, Z)
-    double2 xp = pm.ld2((pm.z0 - 1) * pm.P + pm.xy0 + pm.lr);
+    const double2 xp0 = pm.ld2((pm.z0 - 1) * pm.P + pm.xy0 + 2 * pm.tid);
     auto run = [&](auto fullc) {
         constexpr bool FULL = decltype(fullc)::value;
-        pm.march(xp, [&](int j, int bc, int bn) {
-            const int r = (pm.z0 + j) * pm.P + pm.xy0 + pm.lr;
+        pm.march(xp0, [&](int j, auto bc, const double2& xp, const double2& xc, const double2& xn, unsigned wm) {
+            constexpr int B = decltype(bc)::value;
+            const int r = (pm.z0 + j) * pm.P + pm.xy0 + 2 * pm.tid;
             const bool v0 = FULL || (pm.in0 && r < pm.n), v1 = FULL || (pm.in1 && r + 1 < pm.n);
-            const double2 xc = pm.centre(bc);
             double y0, y1;
-            pm.template sums<true>(bc, bn, pm.z0 + j, xp, xc, y0, y1);
+            pm.template sums<true, B>(pm.z0 + j, xp, xc, xn, wm, y0, y1);
             if (MODE != 0) {
                 const double u0 = a.shift * xc.x, u1 = a.shift * xc.y;
                 y0 = y0 - u0;
@@ -905,7 +958,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             }
             if (v0 && v1) st16(a.y + r, make_double2(y0, y1));
             else if (v0) a.y[r] = y0;
-            xp = xc;
         });
     };
     if (pm.full) run(std::true_type{});
@@ -914,12 +966,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
 
 // the plane march applies to a whole single slab (pat_args sets the tables)
 static bool planes_ok(const PatArgs& a) {
-    return a.rzval && a.rzmask && a.plane_P >= 256 && a.plane_H <= 256 && a.pmaxlen >= 2 && a.pmaxlen <= 8 &&
-           a.pcanon && a.gap == 0 && a.xlo == 0 && a.ld >= a.n + 2 && a.ld < ((int64_t)1 << 28) &&
-           (a.cuniform ? a.rowmask != nullptr : (a.npat > 256 || a.rowkey8));
+    return a.rzval && a.rzmask && a.wavemask && a.plane_P >= 256 && a.plane_H <= 256 && a.pmaxlen >= 2 &&
+           a.pmaxlen <= 8 && a.pcanon && a.gap == 0 && a.xlo == 0 && a.ld >= a.n + 2 &&
+           a.ld < ((int64_t)1 << 28) && (a.cuniform ? a.rowmask != nullptr : (a.npat > 256 || a.rowkey8));
 }
 static int planes_blocks(const PatArgs& a, int Z) {
-    const int64_t nxy = (a.plane_P + kResidPlaneRows - 1) / kResidPlaneRows;
+    const int64_t nxy = (a.plane_P + kPlaneBlockRows - 1) / kPlaneBlockRows;
     const int64_t nz = (a.n + a.plane_P - 1) / a.plane_P;
     return (int)(nxy * ((nz + Z - 1) / Z));
 }
@@ -927,9 +979,9 @@ static int planes_blocks(const PatArgs& a, int Z) {
 static int planes_km(const PatArgs& a) { return a.cuniform ? 0 : (a.npat <= 256 ? 1 : 2); }
 static size_t planes_lds(const PatArgs& a) {
     switch (planes_km(a)) {
-        case 0: return PlaneMarch<8, 0, false>::lds_bytes(a.plane_H, a.npat);
-        case 1: return PlaneMarch<8, 1, false>::lds_bytes(a.plane_H, a.npat);
-        default: return PlaneMarch<8, 2, false>::lds_bytes(a.plane_H, a.npat);
+        case 0: return PlaneMarch<8, 0, false, false>::lds_bytes(a.npat);
+        case 1: return PlaneMarch<8, 1, false, false>::lds_bytes(a.npat);
+        default: return PlaneMarch<8, 2, false, false>::lds_bytes(a.npat);
     }
 }
 // slots MID - 1, MID, MID + 1 (MID = L / 2, L odd) are the offsets -1, 0, +1
@@ -937,26 +989,42 @@ static bool planes_ln(const PatArgs& a) {
     const int L = a.pmaxlen, m = L / 2;
     return (L & 1) && L >= 5 && a.pslot[m - 1] == -1 && a.pslot[m] == 0 && a.pslot[m + 1] == 1;
 }
-// dispatch f(MAXLEN, KM, LN) over the plane march's instantiations
+// uniform slot values, -1 at every slot but the middle (the Laplacians)
+static bool planes_neg1(const PatArgs& a) {
+    if (!a.cuniform || !planes_ln(a)) return false;
+    for (int e = 0; e < a.pmaxlen; ++e)
+        if (e != a.pmaxlen / 2 && a.cval[e] != -1.0) return false;
+    return true;
+}
+// dispatch f(MAXLEN, KM, LN, NEG1) over the plane march's instantiations
 template <typename F>
 static void planes_dispatch(const PatArgs& a, F&& f) {
     auto km = [&](auto ml, auto ln) {
         switch (planes_km(a)) {
-            case 0: f(ml, std::integral_constant<int, 0>{}, ln); break;
-            case 1: f(ml, std::integral_constant<int, 1>{}, ln); break;
-            default: f(ml, std::integral_constant<int, 2>{}, ln); break;
+            case 0: f(ml, std::integral_constant<int, 0>{}, ln, std::false_type{}); break;
+            case 1: f(ml, std::integral_constant<int, 1>{}, ln, std::false_type{}); break;
+            default: f(ml, std::integral_constant<int, 2>{}, ln, std::false_type{}); break;
         }
     };
-    const bool ln = planes_ln(a);
+    const bool ln = planes_ln(a), ng = planes_neg1(a);
     using T = std::true_type;
     using N = std::false_type;
+    using K0 = std::integral_constant<int, 0>;
     switch (a.pmaxlen) {
         case 2: km(std::integral_constant<int, 2>{}, N{}); break;
         case 3: km(std::integral_constant<int, 3>{}, N{}); break;
         case 4: km(std::integral_constant<int, 4>{}, N{}); break;
-        case 5: if (ln) km(std::integral_constant<int, 5>{}, T{}); else km(std::integral_constant<int, 5>{}, N{}); break;
+        case 5:
+            if (ng) f(std::integral_constant<int, 5>{}, K0{}, T{}, T{});
+            else if (ln) km(std::integral_constant<int, 5>{}, T{});
+            else km(std::integral_constant<int, 5>{}, N{});
+            break;
         case 6: km(std::integral_constant<int, 6>{}, N{}); break;
-        case 7: if (ln) km(std::integral_constant<int, 7>{}, T{}); else km(std::integral_constant<int, 7>{}, N{}); break;
+        case 7:
+            if (ng) f(std::integral_constant<int, 7>{}, K0{}, T{}, T{});
+            else if (ln) km(std::integral_constant<int, 7>{}, T{});
+            else km(std::integral_constant<int, 7>{}, N{});
+            break;
         default: km(std::integral_constant<int, 8>{}, N{}); break;
     }
 }
@@ -970,10 +1038,10 @@ template <int MODE>
 static hipError_t launch_spmv_planes(const PatArgs& a, hipStream_t st) {
     const size_t lds = planes_lds(a);
     dim3 g((unsigned)planes_blocks(a, kSpmvPlanes)), b(256);
-    planes_dispatch(a, [&](auto ml, auto km, auto ln) {
+    planes_dispatch(a, [&](auto ml, auto km, auto ln, auto ng) {
         constexpr int ML = decltype(ml)::value, KM = decltype(km)::value;
-        constexpr bool LN = decltype(ln)::value;
-        hipLaunchKernelGGL((k_spmv_planes<MODE, ML, kSpmvPlanes, KM, LN>), g, b, lds, st, a);
+        constexpr bool LN = decltype(ln)::value, NEG1 = decltype(ng)::value;
+        hipLaunchKernelGGL((k_spmv_planes<MODE, ML, kSpmvPlanes, KM, LN, NEG1>), g, b, lds, st, a);
     });
     return hipGetLastError();
 }
@@ -1264,7 +1332,7 @@ __global__ __launch_bounds__(256) void k_resid_pairs(PatArgs a, const uint16_t* 
 // l x of each row with the SpMV's bits, then the block's sums of y^2 and,
 // times l^2, of x^2 (||l x||^2 = l^2 ||x||^2: one accumulator less than
 // summing (l x)^2, the same value to rounding).
-template <int MAXLEN, int KM, bool LN>
+template <int MAXLEN, int KM, bool LN, bool NEG1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_resid_planes(
     PatArgs a, const double* __restrict__ X, int64_t ldx, const int* __restrict__ col, const double* __restrict__ lam,
     const int* __restrict__ out, double* __restrict__ partial, int64_t pstride) {
@@ -1273,14 +1341,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     const int i = blockIdx.y;
     CAL_PLANE_MARCH(pm, X + (int64_t)col[i] * ldx, kResidPlanes)
     const double l = lam[i];
-    double2 xp = pm.ld2((pm.z0 - 1) * pm.P + pm.xy0 + pm.lr);
+    const double2 xp0 = pm.ld2((pm.z0 - 1) * pm.P + pm.xy0 + 2 * pm.tid);
     double num = 0.0, den = 0.0;
     auto run = [&](auto fullc) {
         constexpr bool FULL = decltype(fullc)::value;
-        pm.march(xp, [&](int j, int bc, int bn) {
-            const double2 xc = pm.centre(bc);
+        pm.march(xp0, [&](int j, auto bc, const double2& xp, const double2& xc, const double2& xn, unsigned wm) {
+            constexpr int B = decltype(bc)::value;
             double y0, y1;
-            pm.template sums<false>(bc, bn, pm.z0 + j, xp, xc, y0, y1);
+            pm.template sums<false, B>(pm.z0 + j, xp, xc, xn, wm, y0, y1);
             const double u0 = l * xc.x, u1 = l * xc.y;
             y0 = y0 - u0;
             y1 = y1 - u1;
@@ -1290,7 +1358,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
                 den = __builtin_fma(xc.x, xc.x, den);
                 den = __builtin_fma(xc.y, xc.y, den);
             } else {
-                const int r = (pm.z0 + j) * pm.P + pm.xy0 + pm.lr;
+                const int r = (pm.z0 + j) * pm.P + pm.xy0 + 2 * pm.tid;
                 const bool v0 = pm.in0 && r < pm.n, v1 = pm.in1 && r + 1 < pm.n;
                 const double a0 = v0 ? y0 : 0.0, a1 = v1 ? y1 : 0.0;
                 const double b0 = v0 ? xc.x : 0.0, b1 = v1 ? xc.y : 0.0;
@@ -1299,7 +1367,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
                 den = __builtin_fma(b0, b0, den);
                 den = __builtin_fma(b1, b1, den);
             }
-            xp = xc;
+            // the sums before the step's LDS stores (PlaneMarch::step)
+            asm volatile("" : "+v"(num), "+v"(den));
         });
     };
     if (pm.full) run(std::true_type{});
@@ -1343,10 +1412,10 @@ hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64
     if (planes_ok(a)) {
         const size_t lds = planes_lds(a);
         dim3 g(blocks, npr), bl(256);
-        planes_dispatch(a, [&](auto ml, auto km, auto ln) {
+        planes_dispatch(a, [&](auto ml, auto km, auto ln, auto ng) {
             constexpr int ML = decltype(ml)::value, KM = decltype(km)::value;
-            constexpr bool LN = decltype(ln)::value;
-            hipLaunchKernelGGL((k_resid_planes<ML, KM, LN>), g, bl, lds, st, a, X, ldx, col, lam, out, partial,
+            constexpr bool LN = decltype(ln)::value, NEG1 = decltype(ng)::value;
+            hipLaunchKernelGGL((k_resid_planes<ML, KM, LN, NEG1>), g, bl, lds, st, a, X, ldx, col, lam, out, partial,
                                pstride);
         });
         return hipGetLastError();

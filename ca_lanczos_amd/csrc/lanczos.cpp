@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <future>
 #include <string>
 #include <vector>
 
@@ -47,6 +48,8 @@ struct DiagJob {
     int k = 0;  // outer iteration described; 0: empty
     std::vector<RitzPair> pairs;  // MATLAB's descending sort
     std::vector<double> V;        // eigenvectors of T_k (sk x sk)
+    std::vector<double> Tk;       // T(1:sk,1:sk), the eig's input
+    std::future<int> eig;         // the eig on a host worker thread (diag_prepare)
     struct OeChunk {
         int a0, na, b0, nb, ldc;
         size_t off;  // doubles into the result region
@@ -364,15 +367,12 @@ static void matlab_sort_desc(std::vector<RitzPair>& v, bool cplx) {
     });
 }
 
-static int diag_prepare(cal_ctx* c, LanczosState& L, DiagJob& J) {
-    const int sk = L.s * L.k;
-    std::vector<double> Tk((size_t)sk * sk), wr(sk), wi(sk);
-    for (int j = 0; j < sk; ++j)
-        for (int i = 0; i < sk; ++i) Tk[i + (size_t)j * sk] = L.T[i + (size_t)j * L.Tld];
+// [Vp,Dp] = eig(T(1:s*k,1:s*k)) (ca_lanczos.m:229) and the sort, on J's own
+// copy of T_k: runs on a host worker thread (touches nothing but J)
+static int diag_eig(DiagJob& J, int sk) {
+    std::vector<double> wr(sk), wi(sk);
     J.V.assign((size_t)sk * sk, 0.0);
-    // [Vp,Dp] = eig(T(1:s*k,1:s*k)) (ca_lanczos.m:229)
-    if (cal_eig(sk, Tk.data(), sk, wr.data(), wi.data(), J.V.data()) != 0)
-        return set_error(c, CAL_ERR_NUMERIC, "eig(T) did not converge");
+    if (cal_eig(sk, J.Tk.data(), sk, wr.data(), wi.data(), J.V.data()) != 0) return CAL_ERR_NUMERIC;
     J.pairs.clear();
     bool cplx = false;
     for (int j = 0; j < sk; ++j) {
@@ -387,7 +387,33 @@ static int diag_prepare(cal_ctx* c, LanczosState& L, DiagJob& J) {
         }
     }
     matlab_sort_desc(J.pairs, cplx);
+    return 0;
+}
+
+// Step k's job: T_k copied, its eig started on a worker thread.  The eig is
+// O((sk)^3) (10 ms at sk = 120 on one core) and used to run on the calling
+// thread between two steps, where at large k it outlasted the GPU work queued
+// behind it; now it overlaps the next step too, and diag_join waits for it
+// right before the job's kernels are launched (one step later).
+static int diag_prepare(cal_ctx* c, LanczosState& L, DiagJob& J) {
+    (void)c;
+    const int sk = L.s * L.k;
+    J.Tk.resize((size_t)sk * sk);
+    for (int j = 0; j < sk; ++j)
+        for (int i = 0; i < sk; ++i) J.Tk[i + (size_t)j * sk] = L.T[i + (size_t)j * L.Tld];
     J.k = L.k;
+    DiagJob* jp = &J;
+    J.eig = std::async(std::launch::async, [jp, sk]() { return diag_eig(*jp, sk); });
+    return 0;
+}
+
+// wait for a job's eig (before anything moves or reads J)
+static int diag_join(cal_ctx* c, DiagJob& J) {
+    if (!J.eig.valid()) return 0;
+    if (J.eig.get() != 0) {
+        J.k = 0;
+        return set_error(c, CAL_ERR_NUMERIC, "eig(T) did not converge");
+    }
     return 0;
 }
 
@@ -429,25 +455,56 @@ struct StreamScope {
 // chunk's residuals overlap the next chunk's apply, measured slower: lap3d_215,
 // 15 iterations, 130.5 outer-it/s on one stream, 125.3 on two, 117-120 with
 // two chunks -- the residual blocks take LDS and CU slots from the apply's.)
+// the orthogonality-error Gram chunks of an iteration with sk columns
+// (compute_orth_err(Q(:,1:sk+1), s): Q(:,1:j-s-1)'Q(:,j-s:j) for j > s+1,
+// else Q'Q - I; chunks of 128 x 16 columns, gram_async): wa, the chunks from
+// result offset 2 sk on, the result size and the largest partial
+static int diag_oe_layout(const LanczosState& L, int64_t n, int sk, std::vector<DiagJob::OeChunk>* oe,
+                          size_t* dres_need, size_t* oe_part) {
+    const int s = L.s, jq = sk + 1;
+    const int wa = jq > s + 1 ? jq - s - 1 : s + 1;
+    size_t off = (size_t)2 * sk, part = 0;
+    if (oe) oe->clear();
+    for (int a0 = 0; a0 < (L.oe_defer ? 0 : wa); a0 += 128)
+        for (int b0 = 0; b0 < s + 1; b0 += 16) {
+            const int na = std::min(128, wa - a0), nb = std::min(16, s + 1 - b0);
+            const GramPlan pl = gram_plan(na, nb, n);
+            if (oe) oe->push_back({a0, na, b0, nb, 16 * pl.nta, off});
+            off += (size_t)pl.entries;
+            part = std::max(part, (size_t)pl.blocks * pl.entries);
+        }
+    *dres_need = off;
+    *oe_part = part;
+    return wa;
+}
+
+// The job buffers sized once for the last iteration (each growth of a pinned
+// buffer frees and allocates: a device synchronisation plus a pinned
+// allocation, ~0.5 ms of idle GPU per growth in the early iterations)
+static int diag_reserve(cal_ctx* c, LanczosState& L) {
+    const int64_t n = c->A.n_local;
+    const int skm = L.s * L.max_outer;
+    size_t dres = 0, oe_part = 0;
+    diag_oe_layout(L, n, skm, nullptr, &dres, &oe_part);
+    const size_t din = (size_t)skm * skm + skm + 2 * (size_t)((skm + 1) / 2);
+    const int nbp = spmv_resid_pair_multi_blocks(c);
+    const int nbr = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (n + 255) / 256));
+    const size_t dpart = (nbp > 0 ? (size_t)2 * skm * nbp : 0) + (size_t)2 * skm * nbr + oe_part;
+    CAL_TRY(grow_pinned(c, &L.d_dres, &L.h_dres, &L.dres_cap, dres));
+    CAL_TRY(grow_pinned(c, &L.d_din, &L.h_din, &L.din_cap, din));
+    CAL_TRY(grow_pinned_dev(c, &L.d_dpart, &L.dpart_cap, dpart));
+    return 0;
+}
+
 static int diag_launch(cal_ctx* c, LanczosState& L, DiagJob& J) {
     const int s = L.s, sk = s * J.k;
     const int64_t n = c->A.n_local, ld = c->A.ld;
     const hipStream_t main = c->stream, aux = c->stream;
-    // compute_orth_err(Q(:,1:sk+1), s): Q(:,1:j-s-1)'Q(:,j-s:j) for j > s+1,
-    // else Q'Q - I; Grams in chunks of 128 x 16 columns (gram_async)
+    if (L.dres_cap == 0) CAL_TRY(diag_reserve(c, L));
+    size_t off = 0, oe_part = 0;
+    J.wa = diag_oe_layout(L, n, sk, &J.oe, &off, &oe_part);
     const int jq = sk + 1;
-    J.wa = jq > s + 1 ? jq - s - 1 : s + 1;
     const int bcol = jq > s + 1 ? J.wa : 0;
-    J.oe.clear();
-    size_t off = (size_t)2 * sk, oe_part = 0;
-    for (int a0 = 0; a0 < (L.oe_defer ? 0 : J.wa); a0 += 128)
-        for (int b0 = 0; b0 < s + 1; b0 += 16) {
-            const int na = std::min(128, J.wa - a0), nb = std::min(16, s + 1 - b0);
-            const GramPlan pl = gram_plan(na, nb, n);
-            J.oe.push_back({a0, na, b0, nb, 16 * pl.nta, off});
-            off += (size_t)pl.entries;
-            oe_part = std::max(oe_part, (size_t)pl.blocks * pl.entries);
-        }
     CAL_TRY(grow_pinned(c, &L.d_dres, &L.h_dres, &L.dres_cap, off));
     // the Ritz vectors (one column chunk; the chunked form is kept for the
     // pair grouping below)
@@ -649,6 +706,7 @@ static int oe_flush(cal_ctx* c, LanczosState& L) {
 // everything still deferred: the stream is drained
 static int diag_flush(cal_ctx* c, LanczosState& L) {
     if (L.pending.k) CAL_TRY(diag_collect(c, L, L.pending));
+    CAL_TRY(diag_join(c, L.ready));
     if (L.ready.k) {
         std::swap(L.pending, L.ready);
         CAL_TRY(diag_launch(c, L, L.pending));
@@ -659,6 +717,7 @@ static int diag_flush(cal_ctx* c, LanczosState& L) {
 
 static void diag_free(LanczosState& L) {
     for (DiagJob* J : {&L.ready, &L.pending}) {
+        if (J->eig.valid()) J->eig.wait();
         if (J->ev) hipEventDestroy(J->ev);
         for (hipEvent_t e : J->evc) hipEventDestroy(e);
     }
@@ -1044,6 +1103,7 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
     // the stream before periodic_update rewrites Q(:,(k-1)s+1:ks+1)
     double td = now_ms();
     if (L.pending.k) CAL_TRY(diag_collect(c, L, L.pending));
+    CAL_TRY(diag_join(c, L.ready));
     if (L.ready.k) {
         std::swap(L.pending, L.ready);
         CAL_TRY(diag_launch(c, L, L.pending));
@@ -1053,7 +1113,7 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
     if (L.mode == 3) CAL_TRY(selective_update(c, L));
     td = now_ms();
     if (diagnostics) {
-        CAL_TRY(diag_prepare(c, L, L.ready));  // eig(T_k) on the host, GPU busy
+        CAL_TRY(diag_prepare(c, L, L.ready));  // eig(T_k) on a host thread, GPU busy
         if (k == L.max_outer) CAL_TRY(diag_flush(c, L));
     }
     const double t2 = now_ms();

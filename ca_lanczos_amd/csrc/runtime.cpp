@@ -174,6 +174,7 @@ static void free_matrix(cal_ctx* c) {
     if (A.rzmask) hipFree(A.rzmask);
     if (A.rowkey8) hipFree(A.rowkey8);
     if (A.rowmask) hipFree(A.rowmask);
+    if (A.wavemask) hipFree(A.wavemask);
     A = DevMatrix();
     if (c->d_work) hipFree(c->d_work);
     c->d_work = nullptr;
@@ -460,6 +461,29 @@ int upload_matrix(cal_ctx* c, int64_t n_rows, int64_t ext_off, int64_t n_local, 
                         }
                         A.plane_P = A.pslot[L - 1];
                         A.plane_H = H;
+                        // the waves' missing-slot masks (cal_internal.hpp DevMatrix::wavemask)
+                        {
+                            const int64_t P = A.plane_P;
+                            const int64_t nxy = (P + kPlaneBlockRows - 1) / kPlaneBlockRows;
+                            const int64_t nz = (n_rows + P - 1) / P;
+                            const unsigned full = (1u << L) - 1u;
+                            std::vector<uint32_t> wm((size_t)(nz + 1) * nxy, 0u);
+                            for (int64_t z = 0; z < nz; ++z)
+                                for (int64_t b = 0; b < nxy; ++b) {
+                                    uint32_t v = 0;
+                                    for (int w = 0; w < 4; ++w) {
+                                        unsigned m = 0;
+                                        const int64_t r0 = z * P + b * kPlaneBlockRows + 128 * w;
+                                        for (int64_t r = r0; r < r0 + 128; ++r)
+                                            m |= r < n_rows ? full & ~(unsigned)rm[pat[(size_t)r]] : full;
+                                        v |= (uint32_t)m << (8 * w);
+                                    }
+                                    wm[(size_t)(z * nxy + b)] = v;
+                                }
+                            CAL_HIP(c, hipMalloc((void**)&A.wavemask, wm.size() * sizeof(uint32_t)));
+                            CAL_HIP(c, hipMemcpy(A.wavemask, wm.data(), wm.size() * sizeof(uint32_t),
+                                                 hipMemcpyHostToDevice));
+                        }
                     }
                 }
             }
@@ -537,6 +561,7 @@ static PatArgs pat_args(const DevMatrix& A, int64_t o, int64_t len, const double
         p.rzmask = A.rzmask;
         p.rowkey8 = A.rowkey8;
         p.rowmask = A.rowmask;
+        p.wavemask = A.wavemask;
         p.cuniform = A.cuniform ? 1 : 0;
         for (int k = 0; k < 8; ++k) p.cval[k] = A.cval[k];
         p.plane_P = A.plane_P;
