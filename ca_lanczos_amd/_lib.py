@@ -16,9 +16,12 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # CAL_LIBRARY=testhooks loads the test build (libcalanczos_testhooks.so: the
 # same sources with -DCAL_TEST_HOOKS, csrc/Makefile), which alone carries the
-# result-altering test hooks; the production library has none compiled in
-LIB_PATH = os.path.join(_HERE, "libcalanczos_testhooks.so" if os.environ.get("CAL_LIBRARY") == "testhooks"
-                        else "libcalanczos.so")
+# result-altering test hooks; the production library has none compiled in.
+# CAL_LIBRARY=variant_X loads libcalanczos_variant_X.so, a kernel-tuning build
+# (`make -C ca_lanczos_amd/csrc variant V=X VFLAGS=...`, measurement only).
+_which = os.environ.get("CAL_LIBRARY", "")
+LIB_PATH = os.path.join(_HERE, "libcalanczos_testhooks.so" if _which == "testhooks"
+                        else ("libcalanczos_%s.so" % _which if _which.startswith("variant_") else "libcalanczos.so"))
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

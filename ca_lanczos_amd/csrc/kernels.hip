@@ -44,7 +44,10 @@ constexpr int kSpmvThreads = 256;
 constexpr int kSpmvNnz = 2048;  // LDS-staged nonzeros per row block (16 KiB)
 // the plane march (k_spmv_planes, k_resid_planes): planes per block of the
 // residual kernel (rows of a plane per block: kPlaneBlockRows)
-constexpr int kResidPlanes = 32;
+#ifndef CAL_RESID_PLANES
+#define CAL_RESID_PLANES 32
+#endif
+constexpr int kResidPlanes = CAL_RESID_PLANES;
 
 // Column c of a panel.  The segment table is taken by value and read with
 // static indices only: binding a reference to a by-value kernel argument
@@ -930,8 +933,19 @@ __device__ __forceinline__ double2 ld16g(const double* p) {
     return v;
 }
 
+// waves per SIMD the plane-march kernels are compiled for: 5 (96 VGPRs, no
+// spills) measured faster than the 6 the LDS (26 KB per block) would allow
+// (80 VGPRs with spill reloads in the loop): lap3d_215 in the loop 40.4-41.0
+// -> 37.9-38.0 us per SpMV, 845-848 -> 862 outer-it/s (profiles/r05/ab/)
+#ifndef CAL_SPMV_WPE
+#define CAL_SPMV_WPE 5
+#endif
+#ifndef CAL_RESID_WPE
+#define CAL_RESID_WPE 5
+#endif
+
 template <int MODE, int MAXLEN, int Z, int KM, bool LN, bool NEG1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_spmv_planes(PatArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CAL_SPMV_WPE))) void k_spmv_planes(PatArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds_plane[];
     CAL_PLANE_MARCH(pm, a.x, Z)
     const double2 xp0 = pm.ld2((pm.z0 - 1) * pm.P + pm.xy0 + 2 * pm.tid);
@@ -1032,7 +1046,10 @@ static void planes_dispatch(const PatArgs& a, F&& f) {
 // planes per block of the plane-march SpMV (round 4, lap3d_215 in the loop:
 // 16 -> 40.5 us per SpMV, 32.8 back to back; 8 -> 40.3 / 34.3; 32 -> 47.7 /
 // 42.1; the row-pair kernel 41.4 / 34.5)
-constexpr int kSpmvPlanes = 16;
+#ifndef CAL_SPMV_PLANES
+#define CAL_SPMV_PLANES 8
+#endif
+constexpr int kSpmvPlanes = CAL_SPMV_PLANES;
 
 template <int MODE>
 static hipError_t launch_spmv_planes(const PatArgs& a, hipStream_t st) {
@@ -1333,7 +1350,7 @@ __global__ __launch_bounds__(256) void k_resid_pairs(PatArgs a, const uint16_t* 
 // times l^2, of x^2 (||l x||^2 = l^2 ||x||^2: one accumulator less than
 // summing (l x)^2, the same value to rounding).
 template <int MAXLEN, int KM, bool LN, bool NEG1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_resid_planes(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CAL_RESID_WPE))) void k_resid_planes(
     PatArgs a, const double* __restrict__ X, int64_t ldx, const int* __restrict__ col, const double* __restrict__ lam,
     const int* __restrict__ out, double* __restrict__ partial, int64_t pstride) {
     extern __shared__ __attribute__((aligned(16))) double lds_plane[];
