@@ -184,7 +184,7 @@ def usable_cpus():
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
-def cpu_baseline(wl, s, iters, basis="newton"):
+def cpu_baseline(wl, s, iters, basis="newton", reps=3):
     """The C/OpenMP restatement (oracle/c/ca_lanczos_omp.c) timed on this host
     with one thread per usable CPU (affinity and cgroup quota, usable_cpus();
     SURVEY §8d "OMP_NUM_THREADS = nproc"): Newton prologue excluded, `iters`
@@ -207,12 +207,18 @@ def cpu_baseline(wl, s, iters, basis="newton"):
         omp.ca_lanczos_local(A, q, Bk, s, iters, basis == "newton")
         return omp.loop_seconds(), time.perf_counter() - t0, omp.threads()
 
-    dt, dt_call, th = timed(cpus["usable"])
-    out = {"value": iters / dt, "unit": "outer-iters/s", "cores": th, "kind": "port",
+    # three runs, the median reported (box-to-box and run-to-run spread of
+    # a shared host: VERDICT r04 weak #7)
+    runs = [timed(cpus["usable"]) for _ in range(reps)]
+    rates = sorted(iters / r[0] for r in runs)
+    dt, dt_call, th = sorted(runs)[len(runs) // 2]
+    out = {"value": rates[len(rates) // 2], "unit": "outer-iters/s", "cores": th, "kind": "port",
+           "runs": len(runs), "min": rates[0], "max": rates[-1],
            "sample": "oracle/c/ca_lanczos_omp.c (C/OpenMP, %d threads = the usable CPUs): %d outer iterations "
                      "(k=1..%d, s=%d, Newton, 'local', Householder TSQR normalize, diagnostics off) on the same "
-                     "%s matrix; outer loop %.1f s (buffers allocated and first-touched in parallel before it, as "
-                     "the GPU's are resident; whole call %.1f s)" % (th, iters, iters, s, wl.name, dt, dt_call),
+                     "%s matrix, %d runs, the median reported; outer loop %.1f s (buffers allocated and "
+                     "first-touched in parallel before it, as the GPU's are resident; whole call %.1f s)"
+                     % (th, iters, iters, s, wl.name, len(runs), dt, dt_call),
            "cpus": cpus}
     if cpus["usable"] > 16:
         dt16, _, th16 = timed(16)
@@ -270,11 +276,16 @@ def cpu_baseline_irl(wl, s, max_lanczos, nw):
                       % (nb, s, m, wl.name, dt)}
 
 
-def setup(args):
-    """Ranks, context, communicator and the resident matrix slab."""
+def setup(args, wd=None):
+    """Ranks, context, communicator and the resident matrix slab (each stage
+    under the watchdog wd of a multi-rank run)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    def stage(name):
+        if wd is not None:
+            wd.enter(name, stage_limit(name))
     wl = Workload(args.workload, args.matrix)
     n = wl.n
 
@@ -284,7 +295,9 @@ def setup(args):
     dist = None
     if world > 1:
         import torch.distributed as dist
+        stage("init_process_group")
         dist.init_process_group("gloo", init_method="env://")
+        stage("comm_init")
 
     ndev = ctypes.c_int(0)
     cal._lib.lib.cal_device_count(ctypes.byref(ndev))
@@ -300,7 +313,12 @@ def setup(args):
             t = torch.from_numpy(a)
             dist.all_reduce(t)
 
+        hang = os.environ.get("CAL_BENCH_TEST_HANG_RANK")
+
         def exchange(peer, send, recv):
+            if hang is not None and int(hang) == rank:  # tests: a rank whose exchange never returns
+                while True:
+                    time.sleep(3600)
             reqs = []
             if send.size:
                 reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(send)), peer))
@@ -325,6 +343,7 @@ def setup(args):
         ctx.comm_init_rccl(world, rank, bytes(t.tolist()))
     import scipy.sparse as sp
     if world > 1:
+        stage("matrix_setup")
         Aloc = sp.csr_matrix((val, col, rowptr), shape=(r1 - r0, n))
         ctx.set_matrix_slab(n, r0, Aloc)
     else:
@@ -383,6 +402,66 @@ def emit(line):
         os.write(_JSON_FD, data)
 
 
+class Watchdog:
+    """Per-rank stage watchdog of a multi-rank run (the first 8-GPU SCALE
+    run is the first RCCL run with more than one rank): every stage has a
+    time limit; when one is exceeded the rank prints its rank and stage to
+    stderr, rank 0 also emits the JSON line with "error" and "stage", and the
+    process leaves with os._exit(3) (no re-exec, no cleanup that could block
+    on the hung collective).  enter() starts a stage, done() stops watching."""
+
+    def __init__(self, rank, world, enabled=True, poll=0.5):
+        import threading
+        self.rank, self.world = rank, world
+        self.stage, self.limit, self.t0 = "start", None, time.monotonic()
+        self.history = []
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self._poll = poll
+        if enabled:
+            self._th = threading.Thread(target=self._run, daemon=True)
+            self._th.start()
+
+    def enter(self, stage, limit_s):
+        with self._lock:
+            now = time.monotonic()
+            if self.limit is not None:
+                self.history.append((self.stage, round(now - self.t0, 3)))
+            self.stage, self.limit, self.t0 = stage, float(limit_s), now
+
+    def done(self):
+        self._stop.set()
+
+    def _run(self):
+        while not self._stop.wait(self._poll):
+            with self._lock:
+                stage, limit, el = self.stage, self.limit, time.monotonic() - self.t0
+            if limit is not None and el > limit:
+                msg = "bench.py rank %d/%d: stage '%s' exceeded %.0f s (%.1f s)" % (self.rank, self.world, stage,
+                                                                                 limit, el)
+                sys.stderr.write(msg + "\n")
+                sys.stderr.flush()
+                if self.rank == 0:
+                    try:
+                        emit({"metric": "CA-Lanczos outer-iters/sec (n~10M, s=8)", "value": None,
+                              "error": msg, "stage": stage, "rank": self.rank, "n_gpus": self.world,
+                              "stages_done_s": self.history})
+                    except Exception:  # pragma: no cover
+                        pass
+                os._exit(3)
+
+
+# per-stage limits (s) of a multi-rank run; the driver's own limit is 600 s
+STAGE_LIMITS = {"init_process_group": 120, "comm_init": 120, "matrix_setup": 240, "lanczos_begin": 120,
+                "first_outer_step": 60, "warmup": 120, "timed": 240, "legs": 240, "finalize": 60}
+
+
+def stage_limit(name):
+    """STAGE_LIMITS, or every stage CAL_BENCH_STAGE_LIMIT seconds (tests)."""
+    v = os.environ.get("CAL_BENCH_STAGE_LIMIT")
+    return float(v) if v else STAGE_LIMITS[name]
+
+
 def _free_port():
     import socket
     s = socket.socket()
@@ -418,9 +497,16 @@ def main():
         sys.stderr.write("bench.py: --gpus %d but WORLD_SIZE=%s\n" % (args.gpus, world_env))
         return 2
     _quiet_stdout()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    wd = Watchdog(int(os.environ.get("RANK", "0")), world) if world > 1 else None
+
+    def stage(name):
+        if wd is not None:
+            wd.enter(name, stage_limit(name))
+
     if args.driver == "irl":
-        return main_irl(args)
-    E = setup(args)
+        return main_irl(args, wd)
+    E = setup(args, wd)
     world, rank, local, wl, cal, dist, ctx = (E[k] for k in ("world", "rank", "local", "wl", "cal", "dist", "ctx"))
     r0, r1, nnz_local, nnz_total = E["r0"], E["r1"], E["nnz_local"], E["nnz_total"]
     n = wl.n
@@ -448,12 +534,25 @@ def main():
         ctx.lanczos_step(False)
         ep["left"] -= 1
 
-    for _ in range(W):
+    # the first begin (normest / Newton prologue: the first RCCL all-reduces)
+    # and the first outer step (the first deep halo exchange) under their own
+    # watchdog stages, synchronised so that a hang is seen where it happens
+    stage("lanczos_begin")
+    ctx.lanczos_begin(r_full[r0:r1], s, t_epoch, args.basis, args.orth)
+    ep["left"], ep["begun"] = t_epoch, True
+    ctx.synchronize()
+    stage("first_outer_step")
+    if W > 0:
+        step()
+        ctx.synchronize()
+    stage("warmup")
+    for _ in range(max(W - 1, 0)):
         step()
     ctx.synchronize()
     if dist is not None:
         dist.barrier()
     ctx.synchronize()
+    stage("timed")
     t0 = time.perf_counter()
     for _ in range(K):
         step()
@@ -464,13 +563,18 @@ def main():
     elapsed = t1 - t0
     ctx.timer_enable(True)
     ctx.timer_reset()
+    ctx.comm_stats(reset=True)
     for _ in range(KT):
         step()
     ctx.synchronize()
     spmv_cnt, spmv_ms = ctx.timer_read("spmv")
     gram_cnt, gram_ms = ctx.timer_read("gram")
     apply_cnt, apply_ms = ctx.timer_read("apply")
+    ar_cnt, ar_ms = ctx.timer_read("allreduce")
+    halo_cnt, halo_ms = ctx.timer_read("halo")
+    cstats = ctx.comm_stats(reset=True)
     ctx.timer_enable(False)
+    stage("legs")
     T, _, _, flags, info = ctx.lanczos_get()
     flags = np.concatenate([np.asarray(ep["flags"], dtype=flags.dtype), flags])
     elapsed, spmv_avg_ms = max_over_ranks(dist, [elapsed, spmv_ms / max(spmv_cnt, 1)])
@@ -486,6 +590,8 @@ def main():
     pat_spmv = None
     csr_leg = None
     lap2d_leg = None
+    cfg2_leg = None
+    full_leg = None
     irl_leg = None
     # the same outer iteration with the Householder TSQR normalize (tsqr.m,
     # BASELINE configs 3/4: "TSQR" / "RCCL TSQR tree"), every rank
@@ -505,6 +611,15 @@ def main():
             except cal.CalError:
                 pass
         ctx.set_normalize(args.normalize)
+    if world == 1 and not args.no_legs and args.orth == "local":
+        # ca_lanczos.m:191-197 'full': the new block projected against all of Q
+        # (one wide Gram and one wide apply sweep per step, f1)
+        try:
+            full_leg = timed_leg(ctx, r_full[r0:r1], s, min(K, 10), min(W, 2), args.basis, "full", dist)
+            fmt0, _, _ = ctx.spmv_format()
+            leg_roofline(full_leg, fmt0, ctx.spmv_pair_info()[0], r1 - r0, nnz_local, s)
+        except cal.CalError as e:
+            full_leg = {"error": str(e)}
     if world == 1 and rank == 0 and ctx.spmv_format()[0] == "pattern":
         # the bench's own SpMV kernel back to back on one x / y pair (the
         # Infinity Cache holds both): the kernel's rate outside the loop
@@ -527,6 +642,16 @@ def main():
                     lap2d_leg = workload_leg(cal, local, "lap2d_3162", s, min(K, 15), min(W, 2), args.basis)
                 except cal.CalError as e:
                     lap2d_leg = {"error": str(e)}
+            # BASELINE config 2 (lap2d_1000, n = 1e6, CholQR): a step of ~0.17 ms,
+            # so 100 timed steps, and the timed kernels' share of the step (the
+            # rest is launch boundaries and small kernels: SURVEY §8d's
+            # cache-resident caveat)
+            if wl.name != "lap2d_1000":
+                try:
+                    cfg2_leg = workload_leg(cal, local, "lap2d_1000", s, 100, 5, args.basis)
+                    cfg2_leg["normalize"] = "CholQR2 fused into the sweeps (the CholQR of config 2)"
+                except cal.CalError as e:
+                    cfg2_leg = {"error": str(e)}
             try:
                 irl_leg = irl_workload_leg(cal, local, "circuit_1259", s, args.basis)
             except cal.CalError as e:
@@ -539,8 +664,25 @@ def main():
             ctx.spmv(v)
         host_rt_ms = (time.perf_counter() - t_h) / 3 * 1e3
         del v
+    # per-rank communication figures of the KT timed steps (max over ranks)
+    comm_line = None
+    if world > 1:
+        red_rows = cstats["spmv_rows"] / KT - s * (r1 - r0)
+        mx = max_over_ranks(dist, [ar_ms / KT * 1e3, ar_cnt / KT, halo_ms / KT * 1e3, halo_cnt / KT, red_rows,
+                                   cstats["halo_doubles"] * 8.0 / KT])
+        comm_line = {"allreduce_us_per_step": mx[0], "allreduces_per_step": mx[1],
+                     "halo_us_per_step": mx[2], "halo_exchanges_per_step": mx[3],
+                     "mpk_redundant_rows_per_step": mx[4], "halo_bytes_per_step": mx[5],
+                     "rccl_comm_count": cstats["rccl_count"], "comm_kind": {0: "none", 1: "rccl", 2: "host"}.get(
+                         cstats["kind"], "?"),
+                     "what": "max over ranks of the KT event-timed steps: RCCL all-reduce and halo-exchange time "
+                             "(timed on the streams they run on; the halo overlaps the interior powers), counts, "
+                             "SpMV rows computed beyond the slab (CA matrix-powers ghost zone)"}
+    stage("finalize")
     if rank != 0:
         dist.barrier()
+        if wd is not None:
+            wd.done()
         return
 
     n_loc = r1 - r0
@@ -639,6 +781,10 @@ def main():
         line["csr_step"] = csr_leg
     if lap2d_leg is not None:
         line["lap2d_3162_step"] = lap2d_leg
+    if cfg2_leg is not None:
+        line["lap2d_1000_step"] = cfg2_leg
+    if full_leg is not None:
+        line["full_step"] = full_leg
     if irl_leg is not None:
         line["irl"] = irl_leg
     if csr_spmv is not None:
@@ -646,6 +792,8 @@ def main():
                                    "gbps": b_csr / (csr_spmv[0] * 1e-3) / 1e9, "bytes_per_launch": b_csr}
     if host_rt_ms is not None:
         line["spmv_host_roundtrip_ms"] = host_rt_ms
+    if comm_line is not None:
+        line["comm"] = comm_line
     line["host"] = host_info()
     if world == 1 and args.orth == "local":
         line["diagnostics_on"] = diagnostics_run(ctx, r_full[r0:r1], s, args)
@@ -655,6 +803,8 @@ def main():
     emit(line)
     if dist is not None:
         dist.barrier()
+    if wd is not None:
+        wd.done()
 
 
 def timed_leg(ctx, r, s, K, W, basis, orth, dist):
@@ -681,6 +831,7 @@ def timed_leg(ctx, r, s, K, W, basis, orth, dist):
         ctx.lanczos_step(False)
     ctx.synchronize()
     tm = {k: ctx.timer_read(k) for k in ("spmv", "gram", "apply", "other")}
+    tb = {k: ctx.timer_bytes(k) for k in ("spmv", "gram", "apply")}
     ctx.timer_enable(False)
     flags = ctx.lanczos_get()[3]
     ctx.lanczos_end()
@@ -690,11 +841,18 @@ def timed_leg(ctx, r, s, K, W, basis, orth, dist):
     per = {k: v[1] / KT for k, v in tm.items()}
     lpp = max(1, ctx.powers_launches())
     per["spmv"] = tm["spmv"][1] / max(tm["spmv"][0], 1) * lpp
+    ksum = sum(v[1] for v in tm.values()) / KT
     return {"outer_iters_per_s": K / elapsed, "ms_per_step": 1e3 * elapsed / K, "steps": K,
             "reorth_passes": "%d/%d" % (int(np.sum(flags[W:W + K])), K),
             "kernel_ms_per_step": per,
             "kernel_avg_launch_us": {k: 1e3 * v[1] / max(v[0], 1) for k, v in tm.items()},
             "kernel_launches": {k: v[0] for k, v in tm.items()},
+            # algorithmic bytes of the timed launches / their summed duration
+            # (the library states each launch's bytes, cal_timer_bytes)
+            "kernel_gbps": {k: tb[k] / (tm[k][1] * 1e-3) / 1e9 if tm[k][1] > 0 else None for k in tb},
+            # the timed kernels' share of the step (the rest: launch boundaries,
+            # small untimed kernels, host time the GPU waits on)
+            "kernel_share": ksum / (1e3 * elapsed / K),
             "spmv_launches_per_step": lpp}
 
 
@@ -711,19 +869,23 @@ def spmv_launch_bytes(fmt, npairpat, n_loc, s, lpp, b_csr):
 
 
 def leg_roofline(leg, fmt, npairpat, n_loc, nnz_loc, s):
-    """SpMV GB/s and the roofline of the leg's dominant kernel class, from its
-    HIP-event per-launch averages (the algorithmic bytes of DESIGN.md §3)."""
+    """SpMV GB/s and the roofline of the leg's dominant kernel class: the
+    algorithmic bytes the library states for that class's timed launches
+    (cal_timer_bytes) over their summed HIP-event durations,
+    i.e. bytes per launch / average launch time for fixed-shape launches
+    ('local'), and the right average for the growing widths of 'full'."""
     lpp = leg["spmv_launches_per_step"]
     b_spmv = spmv_launch_bytes(fmt, npairpat, n_loc, s, lpp, 12 * nnz_loc + 20 * n_loc + 4)
-    bytes_per = {"spmv": b_spmv, "gram": (2 * s + 1) * 8 * n_loc, "apply": (3 * s + 1) * 8 * n_loc}
     avg = leg["kernel_avg_launch_us"]
-    per = {k: leg["kernel_ms_per_step"][k] for k in bytes_per}
+    per = {k: leg["kernel_ms_per_step"][k] for k in ("spmv", "gram", "apply")}
     dom = max(per, key=per.get)
     leg["spmv_gbps"] = b_spmv / (avg["spmv"] * 1e-6) / 1e9
     leg["spmv_frac"] = leg["spmv_gbps"] / HBM_PEAK_GBS
-    ach = bytes_per[dom] / (avg[dom] * 1e-6) / 1e9
+    ach = leg["kernel_gbps"][dom]
+    nl = max(leg["kernel_launches"][dom], 1)
     leg["roofline"] = {"bound": "hbm", "kernel_class": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                       "frac": ach / HBM_PEAK_GBS, "bytes_per_launch": bytes_per[dom], "avg_launch_us": avg[dom]}
+                       "frac": ach / HBM_PEAK_GBS, "bytes_per_launch": ach * 1e9 * avg[dom] * 1e-6,
+                       "avg_launch_us": avg[dom], "launches": nl}
     return leg
 
 
@@ -775,11 +937,12 @@ def irl_workload_leg(cal, local, name, s, basis, ml=64, nw=8, tol=1.0e-8):
             "max_lanczos": ml, "n_wanted_eigs": nw, "m": M["m"], "s": s, "orth": "full", "tol": tol,
             "num_restarts": M["out"]["num_restarts"], "converged": M["out"]["converged"],
             "blocks_per_s": M["blocks"] / M["elapsed"], "spmv_format": fmt,
-            "kernel_ms_per_solve": {"spmv": t[1], "gram": t[3], "apply": t[5]},
+            "kernel_ms_per_solve": {"spmv": t[1], "gram": t[3], "apply": t[5], "other": M["other_ms"]},
             "kernel_launches_per_solve": {"spmv": t[0], "gram": t[2], "apply": t[4]},
-            "roofline": {"bound": "hbm", "kernel": "SpMV (%s) inside the solve" % fmt, "achieved": ach,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                         "bytes_per_launch": b_spmv, "avg_launch_us": M["spmv_avg_ms"] * 1e3}}
+            "roofline": irl_roofline(M)[0], "time_split": irl_roofline(M)[1],
+            "spmv_roofline": {"bound": "hbm", "kernel": "SpMV (%s) inside the solve" % fmt, "achieved": ach,
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                              "bytes_per_launch": b_spmv, "avg_launch_us": M["spmv_avg_ms"] * 1e3}}
 
 
 def diagnostics_run(ctx, r, s, args, t=15):
@@ -846,19 +1009,43 @@ def irl_measure(cal, ctx, r_loc, ml, nw, s, basis, tol, K, W, dist):
     timers = []
     for kind in ("spmv", "gram", "apply"):
         timers += list(ctx.timer_read(kind))
+    other_ms = ctx.timer_read("other")[1]
+    tbytes = {k: ctx.timer_bytes(k) for k in ("spmv", "gram", "apply")}
     ctx.timer_enable(False)
     t_q = time.perf_counter()
     solve(return_Q=True)
     solve_q_ms = (time.perf_counter() - t_q) * 1e3
     elapsed, spmv_avg_ms = max_over_ranks(dist, [elapsed, timers[1] / max(timers[0], 1)])
     return {"k": k, "p": p, "m": m, "out": out, "elapsed": elapsed, "spmv_avg_ms": spmv_avg_ms,
-            "timers": timers, "blocks": blocks, "solve_q_ms": solve_q_ms, "K": K}
+            "timers": timers, "other_ms": other_ms, "bytes": tbytes, "blocks": blocks, "solve_q_ms": solve_q_ms,
+            "K": K}
 
 
-def main_irl(args):
+def irl_roofline(M):
+    """The IRL solve's dominant kernel class (by time per solve) and its
+    roofline: the library's algorithmic bytes of that class's launches
+    (cal_timer_bytes: (a + b) 8 n per Gram of a x b columns, (p + y) 8 n per
+    apply, 12 nnz + 20 n + 4 per CSR SpMV) over their summed duration; and
+    the share of the solve the timed kernels do not cover (host work and
+    the GPU's waits on it, launch boundaries, the small untimed kernels)."""
+    t = M["timers"]
+    ms = {"spmv": t[1], "gram": t[3], "apply": t[5]}
+    dom = max(ms, key=ms.get)
+    ach = M["bytes"][dom] / (ms[dom] * 1e-3) / 1e9
+    solve_ms = 1e3 * M["elapsed"] / M["K"]
+    kern = t[1] + t[3] + t[5] + M["other_ms"]
+    return ({"bound": "hbm", "kernel_class": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": ach / HBM_PEAK_GBS, "bytes_per_solve": M["bytes"][dom], "ms_per_solve": ms[dom],
+             "gbps_by_class": {k: M["bytes"][k] / (ms[k] * 1e-3) / 1e9 if ms[k] > 0 else None for k in ms}},
+            {"kernel_ms_per_solve": kern, "solve_ms": solve_ms, "untimed_share": max(0.0, 1.0 - kern / solve_ms)})
+
+
+def main_irl(args, wd=None):
     """BASELINE config 5: whole impl_restarted_ca_lanczos solves (normest,
     Newton prologue, CA blocks, shifts, compression) on resident A."""
-    E = setup(args)
+    E = setup(args, wd)
+    if wd is not None:
+        wd.enter("timed", stage_limit("timed"))
     world, rank, wl, cal, dist, ctx = (E[k] for k in ("world", "rank", "wl", "cal", "dist", "ctx"))
     r0, r1, nnz_local, nnz_total = E["r0"], E["r1"], E["nnz_local"], E["nnz_total"]
     n = wl.n
@@ -871,8 +1058,12 @@ def main_irl(args):
     elapsed, spmv_avg_ms = M["elapsed"], M["spmv_avg_ms"]
     spmv_cnt, spmv_ms, gram_cnt, gram_ms, apply_cnt, apply_ms = M["timers"]
     blocks, solve_q_ms = M["blocks"], M["solve_q_ms"]
+    if wd is not None:
+        wd.enter("finalize", stage_limit("finalize"))
     if rank != 0:
         dist.barrier()
+        if wd is not None:
+            wd.done()
         return
     fmt, _, _ = ctx.spmv_format()
     n_loc = r1 - r0
@@ -901,12 +1092,14 @@ def main_irl(args):
         "blocks_per_s": blocks / elapsed,
         "solve_with_q_conv_download_ms": solve_q_ms,
         "spmv_format": fmt,
-        "kernel_ms_per_solve": {"spmv": spmv_ms, "gram": gram_ms, "apply": apply_ms},
+        "kernel_ms_per_solve": {"spmv": spmv_ms, "gram": gram_ms, "apply": apply_ms, "other": M["other_ms"]},
         "kernel_launches_per_solve": {"spmv": spmv_cnt, "gram": gram_cnt, "apply": apply_cnt},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_for(args, wl, world, "spmv"),
-                     "kernel": "SpMV (%s) inside the IRL" % fmt, "bytes_per_launch": b_spmv,
-                     "avg_launch_us": spmv_avg_ms * 1e3},
+        "roofline": dict(irl_roofline(M)[0], traffic=None),
+        "time_split": irl_roofline(M)[1],
+        "spmv_roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_for(args, wl, world, "spmv"),
+                          "kernel": "SpMV (%s) inside the IRL" % fmt, "bytes_per_launch": b_spmv,
+                          "avg_launch_us": spmv_avg_ms * 1e3},
     }
     line["host"] = host_info()
     if world == 1 and not args.no_cpu_baseline:
@@ -914,6 +1107,8 @@ def main_irl(args):
     emit(line)
     if dist is not None:
         dist.barrier()
+    if wd is not None:
+        wd.done()
 
 
 if __name__ == "__main__":

@@ -74,6 +74,8 @@ SIGNATURES = [
     ("cal_synchronize", c_int, [c_void_p]),
     ("cal_timer_enable", c_int, [c_void_p, c_int]),
     ("cal_timer_read", c_int, [c_void_p, c_char_p, POINTER(c_int64), dp]),
+    ("cal_timer_bytes", c_int, [c_void_p, c_char_p, dp]),
+    ("cal_comm_stats", c_int, [c_void_p, POINTER(c_int64), c_int, c_int]),
     ("cal_timer_reset", c_int, [c_void_p]),
     ("cal_set_matrix_csc", c_int, [c_void_p, c_int64, POINTER(c_int64), POINTER(c_int64), dp]),
     ("cal_set_matrix_csr", c_int, [c_void_p, c_int64, POINTER(c_int64), POINTER(c_int32), dp]),

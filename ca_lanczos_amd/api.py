@@ -202,6 +202,22 @@ class Context:
     def timer_reset(self):
         check(self.h, lib.cal_timer_reset(self.h))
 
+    def comm_stats(self, reset=False):
+        """Communicator counters (cal_comm_stats): ranks, kind, RCCL comm
+        count, all-reduces and their doubles, halo exchanges and their
+        doubles, SpMV rows computed."""
+        v = (ctypes.c_int64 * 8)()
+        check(self.h, lib.cal_comm_stats(self.h, v, 8, 1 if reset else 0))
+        keys = ("nranks", "kind", "rccl_count", "allreduce_calls", "allreduce_doubles", "halo_calls",
+                "halo_doubles", "spmv_rows")
+        return dict(zip(keys, [int(x) for x in v]))
+
+    def timer_bytes(self, kind="spmv"):
+        """Algorithmic HBM bytes of the timed launches of `kind`."""
+        b = ctypes.c_double()
+        check(self.h, lib.cal_timer_bytes(self.h, kind.encode(), ctypes.byref(b)))
+        return b.value
+
     def timer_read(self, kind="spmv"):
         cnt = ctypes.c_int64()
         tot = ctypes.c_double()

@@ -117,7 +117,7 @@ static int gram_host16(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, do
         const Panel As = panel_slice(A, k.c0, k.nc);
         const GramPlan pl = gram_plan(k.nc, wb, n);
         CAL_TRY(ensure_partial(c, (size_t)pl.blocks * pl.entries));
-        const int t = timer_begin(c, 1);
+        const int t = timer_begin(c, 1, 8.0 * n * (k.nc + wb));
         CAL_HIP(c, launch_gram(As, B, n, pl, c->d_partial, c->stream));
         timer_end(c, t);
         CAL_HIP(c, launch_reduce(c->d_partial, pl.blocks, pl.entries, c->d_red + k.off, c->stream));
@@ -143,7 +143,7 @@ int apply_dev(cal_ctx* c, int64_t n, const Panel& P, const double* dM, int wy, c
     for (int y0 = 0; y0 < wy; y0 += cw_max) {
         const int cw = std::min(cw_max, wy - y0);
         const ApplyPlan pl = apply_plan(wp, cw, n, false, 0);
-        const int t = timer_begin(c, 2);
+        const int t = timer_begin(c, 2, 8.0 * n * (wp + cw));
         CAL_HIP(c, launch_apply(P, dM + (size_t)y0 * wp, wp, cw, panel_out_slice(Y, y0, cw), true, 0, n, pl,
                                 c->d_partial, c->stream));
         timer_end(c, t);
@@ -172,7 +172,7 @@ int apply_host(cal_ctx* c, int64_t n, const Panel& P, const double* M, int wy, c
         PanelOut Ys{};
         if (Y) Ys = panel_out_slice(*Y, y0, cw);
         if (want) CAL_TRY(ensure_partial(c, (size_t)pl.blocks * pl.entries));
-        const int t = timer_begin(c, 2);
+        const int t = timer_begin(c, 2, 8.0 * n * (wp + (Y ? cw : 0)));
         CAL_HIP(c, launch_apply(P, c->d_small + (size_t)y0 * wp, wp, cw, Ys, Y != nullptr, gramp ? wq : 0, n, pl,
                                 c->d_partial, c->stream));
         timer_end(c, t);
@@ -221,7 +221,7 @@ static int tilegram_host(cal_ctx* c, int64_t n, const Panel& T, const double* E,
     int64_t blocks = (n + 255) / 256;
     blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, kRowGramBlocks));
     CAL_TRY(ensure_partial(c, (size_t)blocks * 272));
-    const int t = timer_begin(c, 1);
+    const int t = timer_begin(c, 1, 8.0 * n * (nt + (E ? 1 : 0)));
     CAL_HIP(c, launch_rowgram(cl, nt, E != nullptr, n, (int)blocks, c->d_partial, c->stream));
     timer_end(c, t);
     return fetch_tile(c, (int)blocks, G16, e16);
@@ -267,7 +267,8 @@ static int rowapply_host(cal_ctx* c, int64_t n, const Panel& P, const double* M,
     if (gram) blocks = std::min<int64_t>(blocks, kRowGramBlocks);
     blocks = std::max<int64_t>(1, blocks);
     if (gram) CAL_TRY(ensure_partial(c, (size_t)blocks * 272));
-    const int t = timer_begin(c, kind == 2 ? 1 : 2);  // Gram-only sweeps count as "gram"
+    // bytes: P read; Y stored except by the Gram-only sweep (kind 2)
+    const int t = timer_begin(c, kind == 2 ? 1 : 2, 8.0 * n * (wp + (kind == 2 ? 0 : m)));  // Gram-only sweeps count as "gram"
     CAL_HIP(c, launch_rowapply(cl, c->d_small, wp, m, ol, kind, wq, n, (int)blocks, c->d_partial, c->stream));
     timer_end(c, t);
     if (!gram) return 0;
@@ -470,7 +471,7 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
         const int nt = T.total;
         for (int cc = 0; cc < 16; ++cc) ct.p[cc] = panel_slice(T, cc < nt ? cc : nt - 1, 1).ptr[0];
         ct.p[16] = w == 9 ? panel_slice(Qp, 8, 1).ptr[0] : ct.p[0];
-        const int t = timer_begin(c, 1);
+        const int t = timer_begin(c, 1, 8.0 * n * (nt + (w == 9 ? 1 : 0)));
         CAL_HIP(c, launch_rowgram(ct, nt, w == 9, n, (int)blocks, c->d_partial, c->stream));
         timer_end(c, t);
     }
@@ -495,14 +496,14 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
     for (int j = 0; j < 16; ++j) ol.p[j] = panel_out_slice(Qout, j < m ? j : 0, 1).ptr[0];
     // pass A: Grams of Q1 = W M1, nothing stored
     {
-        const int t = timer_begin(c, 1);
+        const int t = timer_begin(c, 1, 8.0 * n * wp);
         CAL_HIP(c, launch_rowapply(cw, d_mbuf, wp, m, ol, 2, w, n, (int)blocks, c->d_partial, c->stream));
         timer_end(c, t);
     }
     CAL_TRY(coef(1, 0));
     // pass B: Q = [Qp | W M1] M2, one store
     {
-        const int t = timer_begin(c, 2);
+        const int t = timer_begin(c, 2, 8.0 * n * (wp + m));
         CAL_HIP(c, launch_rowapply(cw, d_mbuf, wp, m, ol, 3, w, n, (int)((n + 255) / 256), c->d_partial, c->stream));
         timer_end(c, t);
     }
@@ -701,7 +702,7 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
         const int nt = T.total;
         for (int cc = 0; cc < 16; ++cc) ct.p[cc] = panel_slice(T, cc < nt ? cc : nt - 1, 1).ptr[0];
         ct.p[16] = w == 9 ? panel_slice(Qp, 8, 1).ptr[0] : ct.p[0];
-        const int t = timer_begin(c, 1);
+        const int t = timer_begin(c, 1, 8.0 * n * (nt + (w == 9 ? 1 : 0)));
         CAL_HIP(c, launch_rowgram(ct, nt, w == 9, n, (int)gblocks, c->d_partial, c->stream));
         timer_end(c, t);
     }
@@ -713,7 +714,8 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
     for (int k = 0; k < 9; ++k) cu.p[k] = k < w ? panel_slice(Qp, k, 1).ptr[0] : x0;
     for (int j = 0; j < 8; ++j) cu.p[9 + j] = j < m ? panel_slice(X, j, 1).ptr[0] : x0;
     {
-        const int t = timer_begin(c, 1);
+        // [Qp | X] read, the factored tiles (m columns) stored
+        const int t = timer_begin(c, 1, 8.0 * n * (w + 2 * m));
         CAL_HIP(c, launch_fold_up(cu, fa, c->stream));
         timer_end(c, t);
     }
@@ -784,7 +786,8 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
     OutList qo{};
     for (int j = 0; j < 16; ++j) qo.p[j] = panel_out_slice(Qout, j < m ? j : 0, 1).ptr[0];
     {
-        const int t = timer_begin(c, 2);
+        // the tiles and Qp read, Q stored
+        const int t = timer_begin(c, 2, 8.0 * n * (w + 2 * m));
         CAL_HIP(c, launch_fold_down(cu, qo, fa, c->stream));
         timer_end(c, t);
     }
@@ -1138,7 +1141,7 @@ int gram_async(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* d_
         CAL_TRY(ensure_partial(c, (size_t)pl.blocks * pl.entries));
         part = c->d_partial;
     }
-    const int t = timer_begin(c, 1);
+    const int t = timer_begin(c, 1, 8.0 * n * (A.total + B.total));
     CAL_HIP(c, launch_gram(A, B, n, pl, part, c->stream));
     timer_end(c, t);
     CAL_HIP(c, launch_reduce(part, pl.blocks, pl.entries, d_dst, c->stream));

@@ -412,8 +412,9 @@ hipError_t launch_fold_down(const ColList& P, const OutList& Q, const FoldArgs& 
 
 // Per-launch kernel timer (HIP events on the launching stream).
 struct CalTimerRec {
-    int kind;  // 0 spmv, 1 gram, 2 apply, 3 other
+    int kind;  // 0 spmv, 1 gram, 2 apply, 3 other, 4 allreduce (RCCL), 5 halo exchange (RCCL)
     hipEvent_t a, b;
+    double bytes;  // the launch's algorithmic HBM bytes, 0 if not stated
 };
 
 struct cal_ctx {
@@ -423,6 +424,7 @@ struct cal_ctx {
     std::string err;
     cal::DevMatrix A;
     bool has_A = false;
+    int64_t stat_spmv_rows = 0;  // rows computed by SpMV launches (cal_comm_stats)
 
     // reduction scratch
     double* d_partial = nullptr;
@@ -545,7 +547,10 @@ int ensure_work(cal_ctx* c, int cols, int64_t ld);
 double* work_col(cal_ctx* c, int j);
 
 // timer bracket: returns an index, -1 if timing is off
-int timer_begin(cal_ctx* c, int kind);
+int timer_begin(cal_ctx* c, int kind, double bytes = 0.0);
+// the same on another stream (the halo exchange on the communicator's stream)
+int timer_begin_on(cal_ctx* c, int kind, hipStream_t st);
+void timer_end_on(cal_ctx* c, int idx, hipStream_t st);
 void timer_end(cal_ctx* c, int idx);
 
 // Device block operations (blockorth.cpp).  All matrices column-major; n is

@@ -44,8 +44,12 @@ void comm_destroy(cal_ctx* c) {
 int allreduce_sum(cal_ctx* c, double* d_buf, int64_t count) {
     Comm* m = c->comm;
     if (!m || m->nranks <= 1 || count <= 0) return 0;
+    m->n_allreduce++;
+    m->d_allreduce += count;
     if (m->kind == 1) {
+        const int t = timer_begin(c, 4);
         CAL_NCCL(c, ncclAllReduce(d_buf, d_buf, (size_t)count, ncclDouble, ncclSum, m->nccl, c->stream));
+        timer_end(c, t);
         return 0;
     }
     CAL_TRY(ensure_stage(c, count));
@@ -82,9 +86,12 @@ int halo_exchange(cal_ctx* c, double* x) {
     DevMatrix& A = c->A;
     if (!m || m->nranks <= 1 || A.peers.empty()) return 0;
     CAL_HIP(c, launch_gather(A.send_buf, x, A.send_idx, A.send_total, c->stream));
+    m->n_halo++;
+    m->d_halo += A.send_total + A.nghost;
     // each peer's halo lands contiguously at x + recv_off[p] (origin-relative;
     // negative for the left neighbour in the window layout)
     if (m->kind == 1) {
+        const int t = timer_begin(c, 5);
         CAL_NCCL(c, ncclGroupStart());
         for (size_t p = 0; p < A.peers.size(); ++p) {
             if (A.send_cnt[p] > 0)
@@ -95,6 +102,7 @@ int halo_exchange(cal_ctx* c, double* x) {
                                      c->stream));
         }
         CAL_NCCL(c, ncclGroupEnd());
+        timer_end(c, t);
         return 0;
     }
     const size_t need = (size_t)A.send_total + (size_t)A.nghost;
@@ -155,13 +163,17 @@ int halo_exchange_deep(cal_ctx* c, double* x, int d, hipStream_t hs_st) {
         rtot += rc;
     }
     if (pieces.empty()) return 0;
+    m->n_halo++;
+    m->d_halo += stot + rtot;
     if (m->kind == 1) {
+        const int t = timer_begin_on(c, 5, hs_st);
         CAL_NCCL(c, ncclGroupStart());
         for (const Piece& p : pieces) {
             if (p.s_cnt > 0) CAL_NCCL(c, ncclSend(x + p.s_off, (size_t)p.s_cnt, ncclDouble, p.peer, m->nccl, hs_st));
             if (p.r_cnt > 0) CAL_NCCL(c, ncclRecv(x + p.r_off, (size_t)p.r_cnt, ncclDouble, p.peer, m->nccl, hs_st));
         }
         CAL_NCCL(c, ncclGroupEnd());
+        timer_end_on(c, t, hs_st);
         return 0;
     }
     // host-staged: the copies run on hs_st (the compute stream, or the
@@ -279,6 +291,23 @@ int cal_comm_init_rccl(cal_ctx* c, int nranks, int rank, const void* id128) {
     }
     CAL_TRY(comm_make_halo_stream(c, m));
     c->comm = m;
+    return 0;
+}
+
+int cal_comm_stats(cal_ctx* c, int64_t* stats, int nstats, int reset) {
+    if (!c || (nstats > 0 && !stats)) return CAL_ERR_ARG;
+    Comm* m = c->comm;
+    int64_t v[8] = {m ? m->nranks : 1, m ? m->kind : 0, -1, m ? m->n_allreduce : 0, m ? m->d_allreduce : 0,
+                    m ? m->n_halo : 0, m ? m->d_halo : 0, c->stat_spmv_rows};
+    if (m && m->kind == 1 && m->nccl) {
+        int cnt = 0;
+        if (ncclCommCount(m->nccl, &cnt) == ncclSuccess) v[2] = cnt;
+    }
+    for (int i = 0; i < nstats && i < 8; ++i) stats[i] = v[i];
+    if (reset) {
+        if (m) m->n_allreduce = m->d_allreduce = m->n_halo = m->d_halo = 0;
+        c->stat_spmv_rows = 0;
+    }
     return 0;
 }
 

@@ -30,6 +30,9 @@ struct Comm {
     // matrix powers (runtime.cpp powers_dev); ev_q: q ready, ev_halo: received
     hipStream_t stream = nullptr;
     hipEvent_t ev_q = nullptr, ev_halo = nullptr;
+    // counters since the last cal_comm_stats(reset): collectives issued and
+    // the doubles they carry (the multi-rank bench line)
+    int64_t n_allreduce = 0, d_allreduce = 0, n_halo = 0, d_halo = 0;
 };
 
 void comm_destroy(cal_ctx* c);

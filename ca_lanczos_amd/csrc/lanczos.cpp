@@ -571,7 +571,7 @@ static int diag_launch(cal_ctx* c, LanczosState& L, DiagJob& J) {
         const int c0 = q * cw, c1 = q + 1 == nch ? sk : std::min(sk, c0 + cw);
         // X(:, c0:c1) = Q(:,1:sk) * Vp(:, c0:c1) (ca_lanczos.m:93)
         if (mt) {
-            const int t = timer_begin(c, 2);
+            const int t = timer_begin(c, 2, 8.0 * n * (sk + (c1 - c0)));
             hipError_t e = launch_apply_mt(L.col(0), ld, L.d_din + (size_t)c0 * sk, sk, c1 - c0, X + (int64_t)c0 * ld,
                                            ld, n, main);
             timer_end(c, t);

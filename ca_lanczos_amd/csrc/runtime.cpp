@@ -103,10 +103,11 @@ int ensure_work(cal_ctx* c, int cols, int64_t ld) {
 
 double* work_col(cal_ctx* c, int j) { return c->d_work + (size_t)j * c->work_ld; }
 
-int timer_begin(cal_ctx* c, int kind) {
+int timer_begin(cal_ctx* c, int kind, double bytes) {
     if (!c->timing) return -1;
     CalTimerRec r;
     r.kind = kind;
+    r.bytes = bytes;
     if (c->event_pool.size() >= 2) {
         r.a = c->event_pool.back();
         c->event_pool.pop_back();
@@ -124,6 +125,19 @@ int timer_begin(cal_ctx* c, int kind) {
 void timer_end(cal_ctx* c, int idx) {
     if (idx < 0) return;
     hipEventRecord(c->timers[idx].b, c->stream);
+}
+
+int timer_begin_on(cal_ctx* c, int kind, hipStream_t st) {
+    const hipStream_t saved = c->stream;
+    c->stream = st;
+    const int t = timer_begin(c, kind);
+    c->stream = saved;
+    return t;
+}
+
+void timer_end_on(cal_ctx* c, int idx, hipStream_t st) {
+    if (idx < 0) return;
+    hipEventRecord(c->timers[idx].b, st);
 }
 
 // Split rows into CSR-stream blocks: <= kRowBlockRows rows and <= kRowBlockNnz
@@ -570,13 +584,21 @@ static PatArgs pat_args(const DevMatrix& A, int64_t o, int64_t len, const double
     return p;
 }
 
+// algorithmic bytes of a row-pattern SpMV over len rows: the key (1 B per row
+// with pair patterns / the plane march's keys, 2 B otherwise), x, y, and
+// the previous power for MODE 2
+static double pat_spmv_bytes(const DevMatrix& A, int64_t len, int mode) {
+    return (double)len * ((A.use_pair ? 1 : 2) + 16 + (mode == 2 ? 8 : 0));
+}
+
 int spmv_range(cal_ctx* c, int64_t o, int64_t len, const double* x, double* y, int mode, double shift, double im2,
                const double* xprev) {
     const DevMatrix& A = c->A;
     if (o < 0 || (o & 1) || len < 0 || o + len > A.n_rows)
         return set_error(c, CAL_ERR_ARG, "spmv_range: bad stored-row range");
     const PatArgs p = pat_args(A, o, len, x, y, mode, shift, im2, xprev);
-    const int t = timer_begin(c, 0);
+    c->stat_spmv_rows += len;
+    const int t = timer_begin(c, 0, pat_spmv_bytes(A, len, mode));
     CAL_HIP(c, launch_spmv_pat(p, c->stream));
     timer_end(c, t);
     return 0;
@@ -632,7 +654,8 @@ int spmv_range2(cal_ctx* c, int64_t o1, int64_t len1, int64_t o2, int64_t len2, 
     PatArgs p = pat_args(A, o1, len1 + len2, x, y, mode, shift, im2, xprev);
     p.gap_at = len1 / 2;
     p.gap = (o2 - o1) / 2 - p.gap_at;
-    const int t = timer_begin(c, 0);
+    c->stat_spmv_rows += len1 + len2;
+    const int t = timer_begin(c, 0, pat_spmv_bytes(A, len1 + len2, mode));
     CAL_HIP(c, launch_spmv_pat(p, c->stream));
     timer_end(c, t);
     return 0;
@@ -656,7 +679,9 @@ int spmv_dev(cal_ctx* c, const double* x, double* y, int mode, double shift, dou
     a.mode = mode | (c->A.nit << 8);
     // col + val of the stored rows against the 256 MB Infinity Cache
     a.nt = (int64_t)12 * c->A.nnz > ((int64_t)256 << 20) ? 1 : 0;
-    const int t = timer_begin(c, 0);
+    c->stat_spmv_rows += c->A.n_local;
+    // 12 nnz + 20 n + 4 (+ 8 n for the previous power, MODE 2)
+    const int t = timer_begin(c, 0, 12.0 * c->A.nnz + 20.0 * c->A.n_local + 4.0 + (mode == 2 ? 8.0 * c->A.n_local : 0.0));
     CAL_HIP(c, launch_spmv(a, c->stream));
     timer_end(c, t);
     return 0;
@@ -882,6 +907,23 @@ int cal_timer_reset(cal_ctx* c) {
     return 0;
 }
 
+int cal_timer_bytes(cal_ctx* c, const char* kind, double* bytes) {
+    if (!c || !kind || !bytes) return CAL_ERR_ARG;
+    int k = -1;
+    if (!strcmp(kind, "spmv")) k = 0;
+    else if (!strcmp(kind, "gram")) k = 1;
+    else if (!strcmp(kind, "apply")) k = 2;
+    else if (!strcmp(kind, "other")) k = 3;
+    else if (!strcmp(kind, "allreduce")) k = 4;
+    else if (!strcmp(kind, "halo")) k = 5;
+    else if (strcmp(kind, "all")) return set_error(c, CAL_ERR_ARG, "unknown timer kind");
+    double b = 0.0;
+    for (auto& r : c->timers)
+        if (k < 0 || r.kind == k) b += r.bytes;
+    *bytes = b;
+    return 0;
+}
+
 int cal_timer_read(cal_ctx* c, const char* kind, int64_t* count, double* total_ms) {
     if (!c || !kind) return CAL_ERR_ARG;
     int k = -1;
@@ -889,6 +931,8 @@ int cal_timer_read(cal_ctx* c, const char* kind, int64_t* count, double* total_m
     else if (!strcmp(kind, "gram")) k = 1;
     else if (!strcmp(kind, "apply")) k = 2;
     else if (!strcmp(kind, "other")) k = 3;
+    else if (!strcmp(kind, "allreduce")) k = 4;
+    else if (!strcmp(kind, "halo")) k = 5;
     else if (strcmp(kind, "all")) return set_error(c, CAL_ERR_ARG, "unknown timer kind");
     CAL_HIP(c, hipStreamSynchronize(c->stream));
     int64_t cnt = 0;

@@ -51,10 +51,15 @@ void cal_destroy(cal_ctx* ctx);
 const char* cal_last_error(const cal_ctx* ctx);
 int cal_synchronize(cal_ctx* ctx);
 /* Kernel-duration timer (HIP events on the context stream).  kind: "spmv",
- * "gram", "apply", "all".  Returns the number of launches timed and their
- * summed duration since the last reset. */
+ * "gram", "apply", "other", "allreduce", "halo" (the RCCL calls), "all".
+ * Returns the number of launches timed and their summed duration since the
+ * last reset. */
 int cal_timer_enable(cal_ctx* ctx, int on);
 int cal_timer_read(cal_ctx* ctx, const char* kind, int64_t* count, double* total_ms);
+/* The algorithmic HBM bytes of the timed launches of a kind
+ * since the last reset (the roofline's numerator; 0 for launches that state
+ * none). */
+int cal_timer_bytes(cal_ctx* ctx, const char* kind, double* bytes);
 int cal_timer_reset(cal_ctx* ctx);
 
 /* ---- the sparse matrix A ------------------------------------------------ */
@@ -271,6 +276,14 @@ int cal_impl_restarted_ca_lanczos(cal_ctx* ctx, const double* r, int max_lanczos
 /* 128-byte RCCL unique id; broadcast it out of band (e.g. torch.distributed). */
 int cal_comm_unique_id(void* id128);
 int cal_comm_init_rccl(cal_ctx* ctx, int nranks, int rank, const void* id128);
+/* Communicator statistics since the last reset (reset != 0 zeroes them after
+ * reading): stats[0] ranks, [1] kind (0 none, 1 RCCL, 2 host-staged), [2]
+ * ncclCommCount (-1 unless RCCL), [3] all-reduces issued, [4] doubles they
+ * carried, [5] halo exchanges, [6] doubles exchanged (sent + received), [7]
+ * rows computed by SpMV launches (with the CA matrix powers: the slab's rows
+ * plus the shrinking ghost-zone ranges).  nstats <= 8.  The timer kinds
+ * "allreduce" and "halo" time the RCCL calls (cal_timer_read). */
+int cal_comm_stats(cal_ctx* ctx, int64_t* stats, int nstats, int reset);
 /* Host-staged communicator (tests, CPU rendezvous): device buffers are
  * staged through pinned host memory and handed to these callbacks.  The
  * callbacks run on the caller's thread, except with the opt-in overlapped

@@ -96,3 +96,26 @@ def test_bench_rejects_mismatched_world():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=120)
     assert p.returncode != 0 and p.stdout.strip() == ""
+
+
+def test_bench_watchdog_hung_rank_exits_with_stage():
+    """a rank whose halo exchange never returns (host-staged
+    communicator, CAL_BENCH_TEST_HANG_RANK=1) ends the 2-rank run non-zero
+    within the stage limit (CAL_BENCH_STAGE_LIMIT=20 s), with the rank and
+    stage on stderr and, when rank 0's watchdog fires before the launcher
+    tears the job down, an "error" line naming the stage."""
+    import time
+    env = dict(os.environ, CAL_BENCH_TEST_HANG_RANK="1", CAL_BENCH_STAGE_LIMIT="20")
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup",
+                        "1", "--workload", "lap3d_40", "--comm", "host", "--no-legs"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=240)
+    el = time.monotonic() - t0
+    assert p.returncode != 0
+    assert el < 200
+    assert "stage '" in p.stderr and "exceeded 20 s" in p.stderr, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) <= 1
+    if lines:
+        d = json.loads(lines[0])
+        assert d["value"] is None and d["stage"] in p.stderr and "error" in d
