@@ -1188,6 +1188,11 @@ __global__ __launch_bounds__(256) void k_resid_pairs(PatArgs a, const uint16_t* 
                                                     double* __restrict__ partial, int64_t pstride) {
     extern __shared__ __attribute__((aligned(16))) double lds_pair[];
     double2* s_pz = reinterpret_cast<double2*>(lds_pair);
+    // per pair pattern: bit e set when row 2t or 2t+1 uses slot e; a slot
+    // neither row uses is loaded at an offset past the descriptor's range
+    // (it reads 0), so a padding or non-received ghost position is never
+    // read, whatever it holds
+    uint32_t* s_um = reinterpret_cast<uint32_t*>(s_pz + a.npent);
     __shared__ double ws[CPB][2][4];
     const int tid = threadIdx.x;
     const int64_t npairs = (a.n + 1) >> 1;
@@ -1196,6 +1201,11 @@ __global__ __launch_bounds__(256) void k_resid_pairs(PatArgs a, const uint16_t* 
         const int code = ppoff[i];
         const double2 v = ppval[i];
         s_pz[i] = make_double2((code & 1) ? v.x : 0.0, (code & 2) ? v.y : 0.0);
+    }
+    for (int q = tid; q < a.nppat; q += 256) {
+        uint32_t um = 0;
+        for (int e = 0; e < MAXLEN; ++e) um |= (ppoff[q * MAXLEN + e] & 3) ? (1u << e) : 0u;
+        s_um[q] = um;
     }
     const int i0 = blockIdx.y * CPB;
     const int nq = npairs_ritz - i0 < CPB ? npairs_ritz - i0 : CPB;  // uniform over the block
@@ -1229,8 +1239,10 @@ __global__ __launch_bounds__(256) void k_resid_pairs(PatArgs a, const uint16_t* 
         const bool pairpath = id != kPairSplit && r0 + 1 < a.n;
         const int base = pairpath ? id * MAXLEN : 0;
         uint32_t off[MAXLEN];
+        const uint32_t um = pairpath ? s_um[id] : 0xFFFFFFFFu;
 #pragma unroll
-        for (int e = 0; e < MAXLEN; ++e) off[e] = (uint32_t)(r0 + a.pslot[e] - a.xlo) * 8u;
+        for (int e = 0; e < MAXLEN; ++e)
+            off[e] = ((um >> e) & 1u) ? (uint32_t)(r0 + a.pslot[e] - a.xlo) * 8u : 0xFFFFFFF0u;
         const uint32_t offc = (uint32_t)(r0 - a.xlo) * 8u;
         double2 z[MAXLEN];
 #pragma unroll
@@ -1437,7 +1449,7 @@ hipError_t launch_spmv_pair_resid_multi(const PatArgs& a, const double* X, int64
         });
         return hipGetLastError();
     }
-    const size_t lds = (size_t)a.npent * 16 + 16;
+    const size_t lds = (size_t)a.npent * 16 + (size_t)a.nppat * 4 + 16;
     const bool mid = (a.pmaxlen & 1) && a.pslot[a.pmaxlen / 2] == 0;
     const bool lane = mid && a.pmaxlen >= 3 && a.pslot[a.pmaxlen / 2 - 1] == -1 &&
                       a.pslot[a.pmaxlen / 2 + 1] == 1;

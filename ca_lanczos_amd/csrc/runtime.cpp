@@ -1092,6 +1092,12 @@ int cal_tsqr_fold_stats(cal_ctx* c, long long* runs, long long* declined, double
 int cal_set_tsqr_fold_tol(cal_ctx* c, double tol) {
     if (!c) return CAL_ERR_ARG;
     if (std::isnan(tol)) return set_error(c, CAL_ERR_ARG, "cal_set_tsqr_fold_tol: tol is NaN");
+    // only lowering it keeps the orthogonality guarantee (more declines, each
+    // redone on the explicit-Z path); a larger tol would accept folds whose
+    // loss-of-orthogonality estimate the default declines
+    if (tol > kFoldTol)
+        return set_error(c, CAL_ERR_ARG, "cal_set_tsqr_fold_tol: tol above the default 1e-14 would weaken the "
+                                         "orthogonality guarantee");
     c->fold_tol = tol;
     return 0;
 }

@@ -64,6 +64,9 @@ constexpr int kProbe = FOLD_PROBE;  // bit 1: no Gram, 2: no tile QR, 3: no tile
 #endif
 #ifndef FOLD_DOWN_WPE
 #define FOLD_DOWN_WPE 3  // k_fold_down waves per SIMD (150 VGPRs)
+#ifndef CAL_FOLD_DOWN_NT
+#define CAL_FOLD_DOWN_NT 1  // non-temporal Q stores in k_fold_down (tuning switch)
+#endif
 #endif
 
 __device__ __forceinline__ fd4 fmfma(double a, double b, fd4 c) {
@@ -77,13 +80,23 @@ __device__ __forceinline__ void fwsync() {
 }
 
 // factored register tile <-> lane-contiguous storage (64 doubles per lane slot)
+#ifndef CAL_FOLD_TILE_NT
+// bit 0: non-temporal stores of the factored tiles (up), bit 1: their loads
+// (down): the tiles (636 MB at n = 9.94 M) outgrow the Infinity Cache before
+// the down pass reads them back in the same order (707/708 -> 711/718
+// outer-it/s on the TSQR headline, same box, profiles/r05/ab/)
+#define CAL_FOLD_TILE_NT 3
+#endif
 template <int RPL>
 __device__ __forceinline__ void fstore_tile(double* V, int lane, const double (&x)[RPL][FM]) {
     double* vt = V + lane;
 #pragma unroll
     for (int i = 0; i < RPL; ++i)
 #pragma unroll
-        for (int c = 0; c < FM; ++c) vt[(i * FM + c) * 64] = x[i][c];
+        for (int c = 0; c < FM; ++c) {
+            if (CAL_FOLD_TILE_NT & 1) __builtin_nontemporal_store(x[i][c], &vt[(i * FM + c) * 64]);
+            else vt[(i * FM + c) * 64] = x[i][c];
+        }
 }
 template <int RPL>
 __device__ __forceinline__ void fload_tile(const double* V, int lane, double (&x)[RPL][FM]) {
@@ -91,7 +104,8 @@ __device__ __forceinline__ void fload_tile(const double* V, int lane, double (&x
 #pragma unroll
     for (int i = 0; i < RPL; ++i)
 #pragma unroll
-        for (int c = 0; c < FM; ++c) x[i][c] = vt[(i * FM + c) * 64];
+        for (int c = 0; c < FM; ++c)
+            x[i][c] = (CAL_FOLD_TILE_NT & 2) ? __builtin_nontemporal_load(&vt[(i * FM + c) * 64]) : vt[(i * FM + c) * 64];
 }
 __device__ __forceinline__ void fstore_tb(double* tb, int lane, const double (&tau)[FM], const double (&beta)[FM]) {
 #pragma unroll
@@ -837,11 +851,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FOLD_DOWN_W
         }
         const int64_t r = base + lane + 64 * i;
         if (r < n) {
-            // (plain stores: non-temporal ones, as pass B's, measured 704/707/703
-            // against 705/703/704 outer-it/s on the TSQR leg, profiles/r04/passb_nt/)
+            // (non-temporal, as pass B's: Q is read again only after the next
+            // step's matrix powers; with the round-5 plane-march SpMV 694-697
+            // -> 706-707 outer-it/s on the TSQR headline, same box,
+            // profiles/r05/ab/; round 4 had measured no difference)
 #pragma unroll
             for (int cc = 0; cc < FM; ++cc)
-                if (cc < m) Q.p[cc][r] = o[cc];
+                if (cc < m) {
+                    if (CAL_FOLD_DOWN_NT) __builtin_nontemporal_store(o[cc], &Q.p[cc][r]);
+                    else Q.p[cc][r] = o[cc];
+                }
         }
     }
 }

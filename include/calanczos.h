@@ -133,11 +133,12 @@ int cal_get_normalize(cal_ctx* ctx, int* kind);
  * and the last block's estimate.  Any pointer may be null. */
 int cal_tsqr_fold_stats(cal_ctx* ctx, long long* runs, long long* declined, double* last_est);
 /* The fused TSQR's acceptance threshold on its loss-of-orthogonality estimate
- * (default 1e-14): a block whose estimate exceeds it is declined and redone
- * on the explicit-Z path (projectAndNormalize.m:63-64 literally), so the
- * results stay within the bars either way.  0 declines every block that
- * takes the second projection, a negative tol every block (the fallback's
- * test hooks); NaN is an error. */
+ * (default 1e-14, also the maximum): a block whose estimate exceeds it is
+ * declined and redone on the explicit-Z path (projectAndNormalize.m:63-64
+ * literally), so lowering it keeps the results within the bars.  0 declines
+ * every block that takes the second projection, a negative tol every block
+ * (the fallback's test hooks); NaN or a tol above 1e-14 (which would accept
+ * folds the default declines) is an error. */
 int cal_set_tsqr_fold_tol(cal_ctx* ctx, double tol);
 /* Device-resident SpMV timing: `reps` launches of y = (A - shift I) x on
  * HBM-resident vectors (x = ones), HIP events around each launch on the

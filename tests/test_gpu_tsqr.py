@@ -132,3 +132,16 @@ def test_tsqr_fold_declined_fallback(cal, ref, orth, tol):
     assert abs(w[-1] - we[-1]) <= 1e-10 * nA and abs(w[0] - we[0]) <= 1e-10 * nA
     if orth == "full":
         assert np.max(out.orth_err) < 1e-12
+
+
+def test_tsqr_fold_tol_cannot_be_raised(cal):
+    """the fold's acceptance threshold may only be lowered (more
+    declines, each redone on the explicit-Z path); a tol above the default
+    1e-14 would accept folds the default declines and is rejected."""
+    ctx = cal.Context(normalize="tsqr")
+    ctx.set_tsqr_fold_tol(1e-15)
+    ctx.set_tsqr_fold_tol(1e-14)
+    for bad in (1e-13, 1.0, float("inf"), float("nan")):
+        with pytest.raises(cal.CalError):
+            ctx.set_tsqr_fold_tol(bad)
+    ctx.close()
