@@ -368,6 +368,35 @@ def max_over_ranks(dist, vals):
     return [float(x) for x in tt]
 
 
+MFMA_PMC_JSON = os.path.join(ROOT, "profiles", "r05", "pmc", "mfma_summary.json")
+
+
+def gram_mfma(n_loc, gram_avg_ms, b_gram, wname, world):
+    """MFMA utilisation of the Gram step (BASELINE north_star): 512 n f64
+    flops per sweep of n rows over the live HIP-event average, against the
+    f64 matrix peak, with the counter evidence of the current kernels
+    (profiles/r05/pmc/mfma_summary.json, tools/gpu_r05_pmc_mfma.sh: rocprofv3
+    SQ_INSTS_VALU_MFMA_MOPS_F64 x 512 and SQ_VALU_MFMA_BUSY_CYCLES per
+    launch of P1 and pass A on lap3d_215) when this is that workload."""
+    flops = 512.0 * n_loc
+    out = {"flops_per_launch": flops, "tflops": flops / (gram_avg_ms * 1e-3) / 1e12, "peak_tflops": MFMA_F64_PEAK_TF,
+           "frac": flops / (gram_avg_ms * 1e-3) / 1e12 / MFMA_F64_PEAK_TF,
+           "bound_by_hbm_tflops": 512.0 / b_gram * n_loc * 6.29}
+    try:
+        pm = json.load(open(MFMA_PMC_JSON))
+        if wname == "lap3d_215" and world == 1:
+            ev = {}
+            for k, d in pm.items():
+                if k.startswith("void cal::k_rowapply<17, 4, true") or k.startswith("void cal::k_rowapply<17, 8, true"):
+                    ev["P1" if "<17, 4," in k else "pass_A"] = {
+                        "pmc_flops_per_launch": d["mfma_f64_flops_per_launch"],
+                        "mfma_busy_share": d.get("mfma_busy_share"), "launches_counted": d["launches"]}
+            out["pmc"] = dict(ev, source="profiles/r05/pmc/mfma_summary.json")
+    except (OSError, ValueError, KeyError):
+        pass
+    return out
+
+
 def traffic_for(args, wl, world, cls):
     if not os.path.exists(args.traffic_json):
         return None
@@ -754,13 +783,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": dom[2], "bytes_per_launch": dom[0], "avg_launch_us": dom[1] * 1e3},
-        # the Gram sweeps' matrix-core work: one 16x16 f64 tile Gram per row
-        # (v_mfma_f64_16x16x4f64; rocprofv3 SQ_INSTS_VALU_MFMA_MOPS_F64 x 512
-        # = 512 n per launch, profiles/r01/pmc/bench_mfma_counters_v11.csv)
-        "gram_mfma": {"flops_per_launch": 512 * n_loc, "tflops": 512 * n_loc / (gram_avg_ms * 1e-3) / 1e12,
-                      "peak_tflops": MFMA_F64_PEAK_TF,
-                      "frac": 512 * n_loc / (gram_avg_ms * 1e-3) / 1e12 / MFMA_F64_PEAK_TF,
-                      "bound_by_hbm_tflops": 512.0 / b_gram * n_loc * 6.29},
+        # the Gram sweeps' matrix-core work: one 16x16 f64 tile Gram per 4
+        # rows (v_mfma_f64_16x16x4f64), 512 n flops per launch
+        "gram_mfma": gram_mfma(n_loc, gram_avg_ms, b_gram, wl.name, world),
     }
     if pat_spmv is not None:
         line["spmv_kernel_back_to_back"] = {"avg_us": pat_spmv[0] * 1e3, "min_us": pat_spmv[1] * 1e3,

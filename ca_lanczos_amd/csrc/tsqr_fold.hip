@@ -728,10 +728,34 @@ __global__ __launch_bounds__(64 * UW) void k_fold_root(FoldArgs a, const double*
     tile_geqr2_blk<FM, URPL, UW>(x, tau, beta, m, lane, wave, xlds);
     if (wave == 0) fput_R(Rl, lane, m, x[0]);
     fstore_tile<URPL>(a.Vu[L - 1] + (int64_t)wave * URPL * FM * 64, lane, x);
+    // the WY matrix's Gram shares first (every wave), then the s x s algebra
+    // and the publish on wave 0 while wave 1 sums the Gram and writes M: the
+    // algebra no longer waits for wave 0's Gram share and M is off the
+    // critical path (fold_wy_blk's work, split over two waves)
+    fv_tile<URPL>(x, (int64_t)wave * 64 * URPL + lane, m);
+    wave_gram<URPL>(x, scr[wave], gw[wave], lane);
+    if (wave == 0 && lane < FM) {
+#pragma unroll
+        for (int c = 0; c < FM; ++c) Vt[lane + FM * c] = x[0][c];
+    }
     __syncthreads();
-    if (wave == 0) fold_coef1_body(T1, G, Rl, FM, out, Sbuf, Sm, Kbuf, w, m, doreorth, nglob, a.tol, nullptr, lane);
-    fold_wy_blk<URPL, UW>(x, tau, m, lane, wave, gw, scr, Vt, a.Mu[L - 1]);
-    if (wave == 0 && hout) fold_publish(out, w, m, hout, hseq, seq, lane);
+    if (wave == 0) {
+        fold_coef1_body(T1, G, Rl, FM, out, Sbuf, Sm, Kbuf, w, m, doreorth, nglob, a.tol, nullptr, lane);
+        if (hout) fold_publish(out, w, m, hout, hseq, seq, lane);
+    } else if (wave == 1) {
+        double sum = gw[0][lane];
+#pragma unroll
+        for (int v = 1; v < UW; ++v) sum = sum + gw[v][lane];
+        fwsync();
+        gw[0][lane] = sum;
+        fwsync();
+        if (lane < FM) {
+            double mrow[FM];
+            fwy_row(gw[0], Vt, tau, m, lane, mrow);
+#pragma unroll
+            for (int j = 0; j < FM; ++j) a.Mu[L - 1][lane + FM * j] = mrow[j];
+        }
+    }
 }
 
 // Level 0: Q = Q_tile S - Qp K, one store.  Q: output columns (slots >= m
