@@ -1713,13 +1713,145 @@ __global__ __launch_bounds__(256) void k_gram_lds(Panel A, Panel B, int64_t n, d
     }
 }
 
+// The narrow Grams (A <= 32 columns, B <= 16: the block projections and the
+// s + 1-column normalisations of every outer iteration) with all columns of a
+// round staged at once: per round a block loads R = 16 RUN rows of B's 16 and
+// A's 16 NTA columns, one column per wave instruction (R contiguous doubles:
+// 512 B per wave), into LDS [row][col] (odd leading dimension), one barrier,
+// then lane (c16, g) of wave w feeds MFMA m of tile t with row
+// w*4RUN + g*RUN + m of A column 16t + c16 and of B column c16.  k_gram's
+// row-group loads touch 64 cache lines per wave instruction (16 columns x 4
+// row groups) and ran the IRL's narrow Grams at 3-3.5 TB/s.  Two rounds of
+// loads are in flight (register slots 0/1, the loop unrolled by two), the LDS
+// double buffered: buffer b was last read by round r - 2's MFMAs, which every
+// wave finished before passing round r - 1's barrier.  The row order within
+// a block's MFMAs differs from k_gram<NTA, 16>'s (RUN = 4 vs 16), so the
+// Grams differ from k_gram's in the last bits; the kernel itself is
+// deterministic (fixed rounds per block, fixed block reduction).  Taken up to
+// 64 A columns (NTA 4: 83 KB of LDS, one block per CU); 512 blocks.  IRL
+// driver (circuit_1259, n = 1.58 M, A 4..48 x B 8 columns): Gram class
+// 3.29 -> 4.27 TB/s, 31.3 -> 34.5 solves/s (profiles/r05/ab_gram).
+#ifndef CAL_GRAM_ROWS
+#define CAL_GRAM_ROWS 1
+#endif
+#ifndef CAL_GRAM_ROWS_RUN
+#define CAL_GRAM_ROWS_RUN 4
+#endif
+#ifndef CAL_GRAM_ROWS_BLOCKS
+#define CAL_GRAM_ROWS_BLOCKS 512
+#endif
+#ifndef CAL_GRAM_ROWS_MAXNTA
+#define CAL_GRAM_ROWS_MAXNTA 4
+#endif
+template <int NTA, int RUN>
+__global__ __launch_bounds__(256) void k_gram_rows(Panel A, Panel B, int64_t n, double* __restrict__ partial) {
+    constexpr int R = 16 * RUN;         // rows per round
+    constexpr int NC = 16 * (NTA + 1);  // staged columns: B's 16, then A's
+    constexpr int LD = NC + 1;
+    constexpr int CPI = 256 / R;        // columns per block-wide load instruction
+    constexpr int PER = NC / CPI;       // loads per thread and round
+    static_assert(R >= 64 && 256 % R == 0 && NC % CPI == 0, "k_gram_rows geometry");
+    extern __shared__ __attribute__((aligned(16))) double lds_gr[];  // [2][R][LD], then the partials
+    auto red = reinterpret_cast<double (*)[NTA][64][4]>(lds_gr);      // [3][NTA][64][4]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, c16 = lane & 15, g = lane >> 4;
+    const int lrow = tid % R, lcol0 = __builtin_amdgcn_readfirstlane(tid / R);
+    // column q of this thread: lcol0 + CPI q (wave-uniform); absent columns
+    // are not loaded (zeros staged), rows past n read row 0 and are zeroed
+    const double* pc[PER];
+    bool on[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int cc = lcol0 + CPI * q;
+        if (cc < 16) {
+            on[q] = cc < B.total;
+            pc[q] = pcol(B, on[q] ? cc : 0);
+        } else {
+            on[q] = cc - 16 < A.total;
+            pc[q] = pcol(A, on[q] ? cc - 16 : 0);
+        }
+    }
+    d4 acc[NTA];
+#pragma unroll
+    for (int t = 0; t < NTA; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+    const int orow = wave * 4 * RUN + g * RUN;
+    const int64_t stride = (int64_t)gridDim.x * R;
+    double v[2][PER];
+    bool vin[2] = {false, false};
+    auto load = [&](auto S, int64_t rb) {
+        const int64_t rr = rb + lrow;
+        vin[S] = rr < n;
+        const int64_t ro = vin[S] ? rr : 0;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) v[S][q] = on[q] ? pc[q][ro] : 0.0;  // on[q] wave-uniform
+    };
+    auto round = [&](auto S, int64_t rb) {
+        double* s = lds_gr + S * (R * LD);
+#pragma unroll
+        for (int q = 0; q < PER; ++q) s[lrow * LD + lcol0 + CPI * q] = vin[S] ? v[S][q] : 0.0;
+        if (rb + 2 * stride < n) load(S, rb + 2 * stride);
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < RUN; ++m) {
+            const double* row = s + (orow + m) * LD + c16;
+            const double b = row[0];
+#pragma unroll
+            for (int t = 0; t < NTA; ++t) acc[t] = mfma64(row[16 + 16 * t], b, acc[t]);
+        }
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    int64_t rb = (int64_t)blockIdx.x * R;
+    if (rb < n) load(S0{}, rb);
+    if (rb + stride < n) load(S1{}, rb + stride);
+    while (rb < n) {
+        round(S0{}, rb);
+        rb += stride;
+        if (rb >= n) break;
+        round(S1{}, rb);
+        rb += stride;
+    }
+    __syncthreads();  // the staging buffers become the partials
+    if (wave > 0) {
+#pragma unroll
+        for (int t = 0; t < NTA; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[wave - 1][t][lane][r] = acc[t][r];
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const int ldc = 16 * NTA;
+        double* out = partial + blockIdx.x;
+        const int64_t nb = gridDim.x;
+#pragma unroll
+        for (int t = 0; t < NTA; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                double x = acc[t][r];
+                x = x + red[0][t][lane][r];
+                x = x + red[1][t][lane][r];
+                x = x + red[2][t][lane][r];
+                const int i = t * 16 + g + 4 * r, j = c16;
+                out[(int64_t)(j * ldc + i) * nb] = x;
+            }
+    }
+}
+
+template <int NTA>
+static void launch_gram_rows(const Panel& A, const Panel& B, int64_t n, int blocks, double* partial, hipStream_t st) {
+    constexpr int RUN = CAL_GRAM_ROWS_RUN, R = 16 * RUN, LD = 16 * (NTA + 1) + 1;
+    const size_t lds = std::max((size_t)2 * R * LD, (size_t)3 * NTA * 64 * 4) * sizeof(double);
+    hipLaunchKernelGGL((k_gram_rows<NTA, RUN>), dim3(blocks), dim3(256), lds, st, A, B, n, partial);
+}
+
 GramPlan gram_plan(int wa, int wb, int64_t n) {
     (void)wb;
     GramPlan p;
     p.nta = (wa + 15) / 16;
     if (p.nta < 1) p.nta = 1;
-    const int run = p.nta <= 2 ? 16 : (p.nta <= 4 ? 8 : 4);
+    const bool rows = CAL_GRAM_ROWS && p.nta <= CAL_GRAM_ROWS_MAXNTA;
+    const int run = rows ? CAL_GRAM_ROWS_RUN : (p.nta <= 2 ? 16 : (p.nta <= 4 ? 8 : 4));
     int64_t blocks = (n + 16 * run - 1) / (16 * run);
+    if (rows && blocks > CAL_GRAM_ROWS_BLOCKS) blocks = CAL_GRAM_ROWS_BLOCKS;
     if (blocks > 2048) blocks = 2048;
     if (blocks < 1) blocks = 1;
     p.blocks = (int)blocks;
@@ -1882,9 +2014,25 @@ hipError_t launch_gram_wide(const double* Q, int64_t ld, int w, int64_t n, doubl
 hipError_t launch_gram(const Panel& A, const Panel& B, int64_t n, const GramPlan& pl, double* partial,
                        hipStream_t st) {
     dim3 g(pl.blocks), b(256);
+    static const bool log_shapes = getenv("CAL_LOG_GRAM_SHAPES") != nullptr;  // tuning aid
+    if (log_shapes) fprintf(stderr, "gram %d %d %lld\n", A.total, B.total, (long long)n);
     // the staged loads pay from 33 A columns on (tools/gram_probe.hip: +5-15 %
     // at 48-128 columns; RUN = 16 stages 256-row blocks in 70 KB of LDS and
     // loses to the direct loads at <= 32 columns)
+    if (CAL_GRAM_ROWS && pl.nta <= CAL_GRAM_ROWS_MAXNTA) {
+        switch (pl.nta) {
+            case 1: launch_gram_rows<1>(A, B, n, pl.blocks, partial, st); break;
+            case 2: launch_gram_rows<2>(A, B, n, pl.blocks, partial, st); break;
+#if CAL_GRAM_ROWS_MAXNTA >= 3
+            case 3: launch_gram_rows<3>(A, B, n, pl.blocks, partial, st); break;
+#endif
+#if CAL_GRAM_ROWS_MAXNTA >= 4
+            case 4: launch_gram_rows<4>(A, B, n, pl.blocks, partial, st); break;
+#endif
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     if (pl.nta >= 3) {
         switch (pl.nta) {
             case 3: launch_gram_lds<3, 8>(A, B, n, pl.blocks, partial, st); break;

@@ -323,9 +323,28 @@ def _pn_worker(rank, world, port, heights, out_q):
         t = torch.from_numpy(a)
         dist.all_reduce(t)
 
-    def exchange(peer, send, recv):  # no halo exchange in this test
-        raise RuntimeError("unexpected exchange")
+    def exchange(peer, send, recv):  # the slab's halo setup
+        reqs = []
+        if send.size:
+            reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(send)), peer))
+        rt = torch.zeros(recv.size, dtype=torch.float64)
+        if recv.size:
+            reqs.append(dist.irecv(rt, peer))
+        for r in reqs:
+            r.wait()
+        if recv.size:
+            recv[:] = rt.numpy()
 
+    try:
+        _pn_run(cal, rank, world, heights, out_q, allreduce, exchange)
+    except Exception as e:  # reported, so the parent does not wait out its timeout
+        out_q.put((rank, "error", repr(e), None, None))
+        raise
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _pn_run(cal, rank, world, heights, out_q, allreduce, exchange):
     A = cal.matrices.laplacian_2d(200)
     n = A.shape[0]
     b = cal.matrices.slab_bounds(n, world, 200)
@@ -343,8 +362,6 @@ def _pn_worker(rank, world, port, heights, out_q):
                                                 ctx=ctx)
     out_q.put((rank, QZ, RZ, re, rk))
     ctx.close()
-    dist.barrier()
-    dist.destroy_process_group()
 
 
 def test_tier1_project_and_normalize_mismatched_heights(cal, ref):
@@ -361,7 +378,8 @@ def test_tier1_project_and_normalize_mismatched_heights(cal, ref):
     procs = [mpc.Process(target=_pn_worker, args=(r, world, port, heights, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+    res = sorted([q.get(timeout=100) for _ in range(world)], key=lambda t: t[0])
+    assert not any(isinstance(r[1], str) for r in res), res
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -490,11 +490,17 @@ def test_restarted_ca_lanczos(cal, ref):
     r = ones, max_lanczos 60, 10 wanted, s = 4, newton, 'full', tol 1e-8).
     Known answer: the 10 largest diagonal entries; the oracle's eigenvalues;
     the converged vectors orthonormal eigenvectors.  The restart count is
-    ill-conditioned here (ten wanted eigenvalues 2 apart at tol 1e-8): the
-    oracle itself takes 93, 106, 120 and 96 restarts for r = ones perturbed
-    by 0, +-1e-15 and 3e-15 relative (times cos(i)), so the bar is that
-    measured spread, [93, 120], not equality; the oracle's own unperturbed
-    count is pinned at 93."""
+    ill-conditioned here (ten wanted eigenvalues 2 apart at tol 1e-8): over
+    98 start vectors ones .* (1 + 1e-15 randn) the oracle takes 90..122
+    restarts (median 95; tests/golden/restart_spread_diag5000.json, made by
+    make_restart_spread.py), and its own count for r = ones moves with the
+    BLAS thread count (93 / 94).  So the count is held as a distribution:
+    the device's median over the first 12 of those start vectors lies within
+    the oracle's 10..90 % range, and every device count (r = ones included)
+    within [80, 170] (the device, like the oracle, has rare short and long
+    runs: 82..125 over 32 seeds with either Gram kernel)."""
+    import json
+    import os
     import scipy.sparse as sp
     a = ref.matlab_linspace(1.0, 1.0e4, 5000)
     A = sp.csr_matrix(sp.diags(a))
@@ -502,10 +508,8 @@ def test_restarted_ca_lanczos(cal, ref):
     exp = ref.restarted_ca_lanczos(A, r, 60, 10, 4, "newton", "full", 1.0e-8)
     out = cal.restarted_ca_lanczos(A, r, 60, 10, 4, "newton", "full", 1.0e-8)
     assert out["converged"] and exp["converged"]
-    print("restarts: device %d, oracle %d (oracle spread under 1e-15 perturbations of r: 93..120)"
-          % (out["num_restarts"], exp["num_restarts"]))
-    assert exp["num_restarts"] == 93
-    assert 93 <= out["num_restarts"] <= 120
+    assert exp["num_restarts"] in (93, 94)
+    assert 80 <= out["num_restarts"] <= 170
     eref = a[::-1][:10]
     assert np.max(np.abs(out["conv_eigs"] - eref)) <= 1e-8 * 1.0e4
     assert np.max(np.abs(out["conv_eigs"] - exp["conv_eigs"])) <= 1e-9 * 1.0e4
@@ -514,6 +518,21 @@ def test_restarted_ca_lanczos(cal, ref):
     res = np.linalg.norm(A @ V - V * out["conv_eigs"], axis=0) / np.abs(out["conv_eigs"])
     assert np.max(res) < 1e-6
     assert np.max(out["orth_err"]) < 1e-10
+    spread = np.array(json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                                  "restart_spread_diag5000.json")))["counts"])
+    dev = []
+    for seed in range(12):
+        rng = np.random.RandomState(seed)
+        o = cal.restarted_ca_lanczos(A, np.ones(5000) * (1 + 1e-15 * rng.randn(5000)), 60, 10, 4, "newton", "full",
+                                     1.0e-8)
+        assert o["converged"]
+        assert np.max(np.abs(o["conv_eigs"] - eref)) <= 1e-8 * 1.0e4
+        dev.append(o["num_restarts"])
+    lo, hi = np.percentile(spread, [10, 90])
+    print("restarts: device %d (r = ones), %s (perturbed; median %.1f), oracle %d, oracle 10..90 %%: %.1f..%.1f"
+          % (out["num_restarts"], dev, np.median(dev), exp["num_restarts"], lo, hi))
+    assert lo <= np.median(dev) <= hi
+    assert all(80 <= d <= 170 for d in dev)
 
 
 def test_restarted_ca_lanczos_local_lap2d(cal, ref):

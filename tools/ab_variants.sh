@@ -11,6 +11,12 @@ for v in $VARIANTS; do
     CAL_LIBRARY=$L timeout -k 10 300 python bench.py --no-cpu-baseline --no-legs --steps ${STEPS:-20} $BENCH_ARGS > $O/$v.$rep.json 2> $O/$v.$rep.err || exit $?
     python3 -c "
 import json; d=json.load(open('$O/$v.$rep.json'))
-print('%-8s'%'$v', round(d['value'],1), 'spmv', round(d['spmv_avg_us'],1), 'b2b', round(d['spmv_kernel_back_to_back']['avg_us'],1), 'diag', round(d['diagnostics_on']['outer_iters_per_s'],1), {k: round(x*1e3,1) for k,x in d['kernel_ms_per_step'].items()})"
+ks = d.get('kernel_ms_per_step') or d.get('kernel_ms_per_solve') or {}
+ex = ''
+if 'spmv_avg_us' in d:
+    ex = 'spmv %.1f b2b %.1f diag %.1f' % (d['spmv_avg_us'], d['spmv_kernel_back_to_back']['avg_us'], d['diagnostics_on']['outer_iters_per_s'])
+elif 'roofline' in d:
+    ex = 'gbps %s split %s' % ({k: round(x) for k, x in d['roofline'].get('gbps_by_class', {}).items()}, d.get('time_split'))
+print('%-8s'%'$v', round(d['value'],2), ex, {k: round(x*1e3,1) for k,x in ks.items()})"
 done
 done
