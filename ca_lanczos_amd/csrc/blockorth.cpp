@@ -1134,19 +1134,22 @@ static bool async_ok(int nb, const int* widths, int m) {
 // Gram A'B (A <= 128 columns, B <= 16) reduced (and all-reduced) into d_dst
 // (ld *ldc) and copied to h_dst; nothing waits.
 int gram_async(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* d_dst, double* h_dst, int* ldc,
-               double* part) {
+               double* part, bool bb) {
     if (B.total > 16 || A.total > 128) return set_error(c, CAL_ERR_ARG, "gram_async: A <= 128, B <= 16 columns");
+    if (bb && !gram_bb_ok(A.total, B.total)) return set_error(c, CAL_ERR_ARG, "gram_async: no fused B'B here");
     const GramPlan pl = gram_plan(A.total, B.total, n);
+    const int64_t ne = pl.entries + (bb ? 256 : 0);
     if (!part) {
-        CAL_TRY(ensure_partial(c, (size_t)pl.blocks * pl.entries));
+        CAL_TRY(ensure_partial(c, (size_t)pl.blocks * ne));
         part = c->d_partial;
     }
     const int t = timer_begin(c, 1, 8.0 * n * (A.total + B.total));
-    CAL_HIP(c, launch_gram(A, B, n, pl, part, c->stream));
+    if (bb) CAL_HIP(c, launch_gram_bb(A, B, n, pl, part, c->stream));
+    else CAL_HIP(c, launch_gram(A, B, n, pl, part, c->stream));
     timer_end(c, t);
-    CAL_HIP(c, launch_reduce(part, pl.blocks, pl.entries, d_dst, c->stream));
-    CAL_TRY(allreduce_sum(c, d_dst, pl.entries));
-    CAL_HIP(c, hipMemcpyAsync(h_dst, d_dst, pl.entries * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    CAL_HIP(c, launch_reduce(part, pl.blocks, ne, d_dst, c->stream));
+    CAL_TRY(allreduce_sum(c, d_dst, ne));
+    CAL_HIP(c, hipMemcpyAsync(h_dst, d_dst, ne * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     *ldc = 16 * pl.nta;
     return 0;
 }
@@ -1155,12 +1158,19 @@ int gram_async(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* d_
 // region r of d_red / h_red holds block r's Gram; ldc[r] its leading dimension.
 // dSrc (optional): the input block when it is not dX; the first projection
 // reads it and writes dX (no separate copy of X into the work block).
+// bb_first: the first block's Gram also forms X'X (the norms before of
+// projectAndNormalize.m:17-22) in the same pass, at region + 16 ldc (ld 16).
 static int project_blocks_async(cal_ctx* c, int64_t n, int64_t ld, int nb, const std::vector<double*>& dQ,
                                 const int* widths, int m, double* dX, int region0, std::vector<int>& ldc,
-                                const double* dSrc = nullptr) {
+                                const double* dSrc = nullptr, bool bb_first = false) {
     const PanelOut Xo = panel_out(dX, ld, m);
     const double* cur = dSrc ? dSrc : dX;  // where X currently is
     ldc.assign(nb, 0);
+    // the update of block i and the Gram of block i + 1 share one pass over
+    // the rows (k_apply_gram) where the shapes allow; CAL_APPLY_GRAM_OFF=1
+    // keeps them apart (A/B measurements)
+    static const bool fuse = getenv("CAL_APPLY_GRAM_OFF") == nullptr;
+    bool first = true, have_R = false;  // have_R: block i's Gram already enqueued (fused step)
     for (int i = 0; i < nb; ++i) {
         const int w = widths[i];
         if (w <= 0) continue;
@@ -1168,13 +1178,36 @@ static int project_blocks_async(cal_ctx* c, int64_t n, int64_t ld, int nb, const
         Panel Qi = panel(), X = panel();
         panel_add(Qi, dQ[i], ld, w);
         panel_add(X, cur, ld, m);
-        CAL_TRY(gram_async(c, n, Qi, X, c->d_red + off, c->h_red + off, &ldc[i]));  // R{i} = Q{i}'*X
+        if (!have_R)
+            CAL_TRY(gram_async(c, n, Qi, X, c->d_red + off, c->h_red + off, &ldc[i], nullptr,
+                               bb_first && first));  // R{i} = Q{i}'*X
+        first = false;
         double* dM = c->d_red + off + 4096;
         CAL_HIP(c, launch_form_projM(c->d_red + off, ldc[i], w, m, dM, c->stream));
         Panel W = panel();
         panel_add(W, dQ[i], ld, w);
         panel_add(W, cur, ld, m);
-        CAL_TRY(apply_dev(c, n, W, dM, m, Xo));  // X = X - Q{i}*R{i}
+        int nx = i + 1;
+        while (nx < nb && widths[nx] <= 0) ++nx;
+        have_R = fuse && nx < nb && apply_gram_ok(w + m, m, widths[nx]);
+        if (have_R) {
+            // X = X - Q{i}*R{i} and R{i+1} = Q{i+1}'*X in one pass
+            const size_t offn = kAsyncBase + (size_t)(region0 + nx) * kAsyncRegion;
+            Panel Qn = panel();
+            panel_add(Qn, dQ[nx], ld, widths[nx]);
+            const int blocks = apply_gram_blocks(n);
+            CAL_TRY(ensure_partial(c, (size_t)blocks * 256));
+            const int t = timer_begin(c, 2, 8.0 * n * (w + 2 * m + widths[nx]));
+            CAL_HIP(c, launch_apply_gram(W, dM, w + m, m, Xo, Qn, n, c->d_partial, c->stream));
+            timer_end(c, t);
+            CAL_HIP(c, launch_reduce(c->d_partial, blocks, 256, c->d_red + offn, c->stream));
+            CAL_TRY(allreduce_sum(c, c->d_red + offn, 256));
+            CAL_HIP(c, hipMemcpyAsync(c->h_red + offn, c->d_red + offn, 256 * sizeof(double), hipMemcpyDeviceToHost,
+                                      c->stream));
+            ldc[nx] = 16;
+        } else {
+            CAL_TRY(apply_dev(c, n, W, dM, m, Xo));  // X = X - Q{i}*R{i}
+        }
         cur = dX;
     }
     if (cur != dX) CAL_HIP(c, copy_cols(c, dX, cur, ld, n, m));  // no block to project against
@@ -1207,14 +1240,23 @@ int project_and_normalize_blocks_dev(cal_ctx* c, int64_t n, int64_t ld, int nblo
     if (async) {
         // (the regions lie above everything the synchronous paths stage in h_red)
         CAL_TRY(ensure_red(c, kAsyncBase + (size_t)(nblocks + 1) * kAsyncRegion));
-        Panel Xp = panel();
-        panel_add(Xp, dX, ld, m);
-        int ldx = 0;
-        const size_t offx = kAsyncBase + (size_t)nblocks * kAsyncRegion;
-        CAL_TRY(gram_async(c, n, Xp, Xp, c->d_red + offx, c->h_red + offx, &ldx));  // norms before (:17-22)
+        // norms before (:17-22): X'X rides on the first block's Gram (same
+        // pass over X) when that Gram is the row-staged kernel, else its own
+        int b0 = -1;
+        for (int i = 0; i < nblocks && b0 < 0; ++i)
+            if (widths[i] > 0) b0 = i;
+        const bool fused = b0 >= 0 && gram_bb_ok(widths[b0], m);
+        int ldx = 16;
+        size_t offx = kAsyncBase + (size_t)nblocks * kAsyncRegion;
+        if (!fused) {
+            Panel Xp = panel();
+            panel_add(Xp, dX, ld, m);
+            CAL_TRY(gram_async(c, n, Xp, Xp, c->d_red + offx, c->h_red + offx, &ldx));
+        }
         std::vector<int> ldc;
-        CAL_TRY(project_blocks_async(c, n, ld, nblocks, dQ, widths, m, dY, 0, ldc, dX));  // :25 (Y from X)
-        CAL_TRY(normalize_dev(c, n, Yp, Qout, R, 1.0e-8, &rk, &sh));                   // :26 (waits)
+        CAL_TRY(project_blocks_async(c, n, ld, nblocks, dQ, widths, m, dY, 0, ldc, dX, fused));  // :25 (Y from X)
+        if (fused) offx = kAsyncBase + (size_t)b0 * kAsyncRegion + 16 * (size_t)ldc[b0];
+        CAL_TRY(normalize_dev(c, n, Yp, Qout, R, 1.0e-8, &rk, &sh));  // :26 (waits)
         for (int i = 0; i < m; ++i) before[i] = std::sqrt(c->h_red[offx + i + (size_t)i * ldx]);
         read_async_R(c, nblocks, widths, m, 0, ldc, RY);
     } else {

@@ -224,6 +224,11 @@ struct GramPlan {
 GramPlan gram_plan(int wa, int wb, int64_t n);
 hipError_t launch_gram(const Panel& A, const Panel& B, int64_t n, const GramPlan& pl, double* partial,
                        hipStream_t st);
+// A'B and B'B in one pass (the row-staged Gram with B'B as an extra tile):
+// pl.entries + 256 partial entries per block, B'B (ld 16) after A'B's
+bool gram_bb_ok(int wa, int wb);
+hipError_t launch_gram_bb(const Panel& A, const Panel& B, int64_t n, const GramPlan& pl, double* partial,
+                          hipStream_t st);
 struct ApplyPlan {
     int nty;
     int run;
@@ -236,6 +241,12 @@ struct ApplyPlan {
 ApplyPlan apply_plan(int wp, int wy, int64_t n, bool gram, int wq);
 int apply_rows_max_wy(int wp);  // widest output chunk of the row-parallel store-only apply
 bool apply_rows_ok(int wp, int wy);
+// Y = P M (stored) and the Gram Qn'Y (partials of apply_gram_blocks(n) blocks
+// x 256 entries, ldc 16) in one pass: wp <= 32, wy <= 16, Qn <= 16 columns
+bool apply_gram_ok(int wp, int wy, int wq);
+int apply_gram_blocks(int64_t n);
+hipError_t launch_apply_gram(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y, const Panel& Qn,
+                             int64_t n, double* partial, hipStream_t st);
 hipError_t launch_apply(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y, bool store,
                         int wq, int64_t n, const ApplyPlan& pl, double* partial, hipStream_t st);
 hipError_t launch_reduce(const double* partial, int nparts, int64_t nent, double* out, hipStream_t st);
@@ -282,6 +293,15 @@ hipError_t launch_axpy_sub(double* y, const double* x, double a, int64_t n, hipS
 hipError_t launch_div(double* y, const double* x, double b, int64_t n, hipStream_t st);      // y = x / b
 hipError_t launch_form_projM(const double* G, int ldg, int w, int m, double* M, hipStream_t st);
 // y -= a * x, a = *pa (take_sqrt: sqrt(*pa)) read on the device
+// one step of the Newton prologue's recurrence, single rank (kernels.hip
+// k_pro_*): r -= sqrt(*pb_prev) qprev (qprev may be null), alpha = r'q ->
+// *d_alpha, r -= alpha q, beta^2 = r'r -> *d_beta2, qnext = r / beta; part:
+// 2 dot_blocks(n) doubles
+// normest's iteration tail, single rank: dst[0] = x'x, dst[1] = y'y, x /= sqrt(x'x)
+// (part: 2 dot_blocks(n) doubles)
+hipError_t launch_normest_norms(double* x, const double* y, int64_t n, double* part, double* dst, hipStream_t st);
+hipError_t launch_pro_step(double* r, const double* qprev, const double* pb_prev, const double* q, double* qnext,
+                           int64_t n, double* part, double* d_alpha, double* d_beta2, hipStream_t st);
 hipError_t launch_axpy_sub_dev(double* y, const double* x, const double* pa, bool take_sqrt, int64_t n,
                                hipStream_t st);
 hipError_t launch_div_sqrt(double* y, const double* x, const double* nn, int64_t n, hipStream_t st);  // y = x / sqrt(*nn)
@@ -291,8 +311,9 @@ hipError_t launch_gather(double* dst, const double* src, const int* idx, int64_t
 // Gram A'B (A <= 128 columns, B <= 16) reduced, all-reduced and copied to
 // h_dst (ld *ldc) asynchronously: valid after the stream's next wait
 // (part: the block partials' scratch, gram_plan blocks x entries doubles; default c->d_partial)
+// bb: B'B too (gram_bb_ok), 256 entries (ld 16) at d_dst / h_dst + 16 *ldc * 16 (after A'B)
 int gram_async(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* d_dst, double* h_dst, int* ldc,
-               double* part = nullptr);
+               double* part = nullptr, bool bb = false);
 int spmv_pair_resid_blocks(const PatArgs& a);
 hipError_t launch_spmv_pair_resid(const PatArgs& a, double lr, double* partial, hipStream_t st);
 // the same for npr real Ritz pairs in one launch: x_i = X + col[i] * ldx,

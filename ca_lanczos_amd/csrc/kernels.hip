@@ -1051,14 +1051,26 @@ static void planes_dispatch(const PatArgs& a, F&& f) {
 #endif
 constexpr int kSpmvPlanes = CAL_SPMV_PLANES;
 
+// Small grids (few planes of few blocks: lap2d_1000 has 2 blocks per plane,
+// 250 blocks at 8 planes each, a quarter of the chip) march 2 planes per
+// block instead, at the price of re-reading 2 halo planes of x per 2.
+#ifndef CAL_SPMV_PLANES_MIN_BLOCKS
+#define CAL_SPMV_PLANES_MIN_BLOCKS 1024
+#endif
+static int spmv_planes_z(const PatArgs& a) {
+    return planes_blocks(a, kSpmvPlanes) >= CAL_SPMV_PLANES_MIN_BLOCKS ? kSpmvPlanes : 2;
+}
+
 template <int MODE>
 static hipError_t launch_spmv_planes(const PatArgs& a, hipStream_t st) {
     const size_t lds = planes_lds(a);
-    dim3 g((unsigned)planes_blocks(a, kSpmvPlanes)), b(256);
+    const int z = spmv_planes_z(a);
+    dim3 g((unsigned)planes_blocks(a, z)), b(256);
     planes_dispatch(a, [&](auto ml, auto km, auto ln, auto ng) {
         constexpr int ML = decltype(ml)::value, KM = decltype(km)::value;
         constexpr bool LN = decltype(ln)::value, NEG1 = decltype(ng)::value;
-        hipLaunchKernelGGL((k_spmv_planes<MODE, ML, kSpmvPlanes, KM, LN, NEG1>), g, b, lds, st, a);
+        if (z == kSpmvPlanes) hipLaunchKernelGGL((k_spmv_planes<MODE, ML, kSpmvPlanes, KM, LN, NEG1>), g, b, lds, st, a);
+        else hipLaunchKernelGGL((k_spmv_planes<MODE, ML, 2, KM, LN, NEG1>), g, b, lds, st, a);
     });
     return hipGetLastError();
 }
@@ -1743,7 +1755,7 @@ __global__ __launch_bounds__(256) void k_gram_lds(Panel A, Panel B, int64_t n, d
 #ifndef CAL_GRAM_ROWS_MAXNTA
 #define CAL_GRAM_ROWS_MAXNTA 4
 #endif
-template <int NTA, int RUN>
+template <int NTA, int RUN, bool BB>
 __global__ __launch_bounds__(256) void k_gram_rows(Panel A, Panel B, int64_t n, double* __restrict__ partial) {
     constexpr int R = 16 * RUN;         // rows per round
     constexpr int NC = 16 * (NTA + 1);  // staged columns: B's 16, then A's
@@ -1752,7 +1764,8 @@ __global__ __launch_bounds__(256) void k_gram_rows(Panel A, Panel B, int64_t n, 
     constexpr int PER = NC / CPI;       // loads per thread and round
     static_assert(R >= 64 && 256 % R == 0 && NC % CPI == 0, "k_gram_rows geometry");
     extern __shared__ __attribute__((aligned(16))) double lds_gr[];  // [2][R][LD], then the partials
-    auto red = reinterpret_cast<double (*)[NTA][64][4]>(lds_gr);      // [3][NTA][64][4]
+    constexpr int NT = NTA + (BB ? 1 : 0);                             // output tiles (B'B last)
+    auto red = reinterpret_cast<double (*)[NT][64][4]>(lds_gr);        // [3][NT][64][4]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, c16 = lane & 15, g = lane >> 4;
     const int lrow = tid % R, lcol0 = __builtin_amdgcn_readfirstlane(tid / R);
     // column q of this thread: lcol0 + CPI q (wave-uniform); absent columns
@@ -1770,9 +1783,9 @@ __global__ __launch_bounds__(256) void k_gram_rows(Panel A, Panel B, int64_t n, 
             pc[q] = pcol(A, on[q] ? cc - 16 : 0);
         }
     }
-    d4 acc[NTA];
+    d4 acc[NT];
 #pragma unroll
-    for (int t = 0; t < NTA; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int t = 0; t < NT; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
     const int orow = wave * 4 * RUN + g * RUN;
     const int64_t stride = (int64_t)gridDim.x * R;
     double v[2][PER];
@@ -1796,6 +1809,7 @@ __global__ __launch_bounds__(256) void k_gram_rows(Panel A, Panel B, int64_t n, 
             const double b = row[0];
 #pragma unroll
             for (int t = 0; t < NTA; ++t) acc[t] = mfma64(row[16 + 16 * t], b, acc[t]);
+            if constexpr (BB) acc[NTA] = mfma64(b, b, acc[NTA]);
         }
     };
     using S0 = std::integral_constant<int, 0>;
@@ -1813,7 +1827,7 @@ __global__ __launch_bounds__(256) void k_gram_rows(Panel A, Panel B, int64_t n, 
     __syncthreads();  // the staging buffers become the partials
     if (wave > 0) {
 #pragma unroll
-        for (int t = 0; t < NTA; ++t)
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) red[wave - 1][t][lane][r] = acc[t][r];
     }
@@ -1823,24 +1837,46 @@ __global__ __launch_bounds__(256) void k_gram_rows(Panel A, Panel B, int64_t n, 
         double* out = partial + blockIdx.x;
         const int64_t nb = gridDim.x;
 #pragma unroll
-        for (int t = 0; t < NTA; ++t)
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 double x = acc[t][r];
                 x = x + red[0][t][lane][r];
                 x = x + red[1][t][lane][r];
                 x = x + red[2][t][lane][r];
-                const int i = t * 16 + g + 4 * r, j = c16;
-                out[(int64_t)(j * ldc + i) * nb] = x;
+                const int i = g + 4 * r, j = c16;
+                // A'B entry (16t + i, j) at j ldc + 16t + i; B'B (i, j) after
+                // them at 16 ldc + j 16 + i
+                const int e = t < NTA ? j * ldc + 16 * t + i : 16 * ldc + j * 16 + i;
+                out[(int64_t)e * nb] = x;
             }
     }
 }
 
-template <int NTA>
+template <int NTA, bool BB = false>
 static void launch_gram_rows(const Panel& A, const Panel& B, int64_t n, int blocks, double* partial, hipStream_t st) {
     constexpr int RUN = CAL_GRAM_ROWS_RUN, R = 16 * RUN, LD = 16 * (NTA + 1) + 1;
-    const size_t lds = std::max((size_t)2 * R * LD, (size_t)3 * NTA * 64 * 4) * sizeof(double);
-    hipLaunchKernelGGL((k_gram_rows<NTA, RUN>), dim3(blocks), dim3(256), lds, st, A, B, n, partial);
+    const size_t lds = std::max((size_t)2 * R * LD, (size_t)3 * (NTA + 1) * 64 * 4) * sizeof(double);
+    hipLaunchKernelGGL((k_gram_rows<NTA, RUN, BB>), dim3(blocks), dim3(256), lds, st, A, B, n, partial);
+}
+
+bool gram_bb_ok(int wa, int wb) { return CAL_GRAM_ROWS && wb <= 16 && wa >= 1 && (wa + 15) / 16 <= CAL_GRAM_ROWS_MAXNTA; }
+
+hipError_t launch_gram_bb(const Panel& A, const Panel& B, int64_t n, const GramPlan& pl, double* partial,
+                          hipStream_t st) {
+    if (!gram_bb_ok(A.total, B.total)) return hipErrorInvalidValue;
+    switch (pl.nta) {
+        case 1: launch_gram_rows<1, true>(A, B, n, pl.blocks, partial, st); break;
+        case 2: launch_gram_rows<2, true>(A, B, n, pl.blocks, partial, st); break;
+#if CAL_GRAM_ROWS_MAXNTA >= 3
+        case 3: launch_gram_rows<3, true>(A, B, n, pl.blocks, partial, st); break;
+#endif
+#if CAL_GRAM_ROWS_MAXNTA >= 4
+        case 4: launch_gram_rows<4, true>(A, B, n, pl.blocks, partial, st); break;
+#endif
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 GramPlan gram_plan(int wa, int wb, int64_t n) {
@@ -2227,6 +2263,12 @@ ApplyPlan apply_plan(int wp, int wy, int64_t n, bool gram, int wq) {
 // staged row-major in LDS for broadcast reads.  y_j = fma(p_c, M(c,j), y_j)
 // over c ascending.  Y may alias columns of P: a lane reads all of its row
 // before it writes it.
+#ifndef CAL_APPLY_ROWS_G
+#define CAL_APPLY_ROWS_G 8
+#endif
+#ifndef CAL_APPLY_ROWS_GRID
+#define CAL_APPLY_ROWS_GRID 0  // blocks cap (grid-stride rows); 0: one 256-row tile per block
+#endif
 template <int WY>
 __global__ __launch_bounds__(256) void k_apply_rows(Panel P, const double* __restrict__ M, int wp, int wy,
                                                     PanelOut Y, int64_t n) {
@@ -2236,8 +2278,6 @@ __global__ __launch_bounds__(256) void k_apply_rows(Panel P, const double* __res
         Mr[e] = j < wy ? M[(int64_t)j * wp + c] : 0.0;
     }
     __syncthreads();
-    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= n) return;
     // segment tables copied field by field with static indices (a reference
     // to the by-value kernel argument would copy it to scratch per thread)
     const double* sp[kMaxSeg];
@@ -2250,30 +2290,6 @@ __global__ __launch_bounds__(256) void k_apply_rows(Panel P, const double* __res
         sl[q] = P.ld[q];
         sb[q + 1] = sb[q] + (q < P.nseg ? P.ncol[q] : 0);
     }
-    auto colp = [&](int c) {
-        const double* res = sp[0] + r;
-#pragma unroll
-        for (int q = 0; q < kMaxSeg; ++q)
-            if (c >= sb[q] && c < sb[q + 1]) res = sp[q] + (int64_t)(c - sb[q]) * sl[q] + r;
-        return res;
-    };
-    double y[WY];
-#pragma unroll
-    for (int j = 0; j < WY; ++j) y[j] = 0.0;
-    constexpr int G = 8;  // columns whose loads are in flight together
-    for (int c0 = 0; c0 < wp; c0 += G) {
-        double p[G];
-#pragma unroll
-        for (int u = 0; u < G; ++u) p[u] = *colp(c0 + u < wp ? c0 + u : c0);
-#pragma unroll
-        for (int u = 0; u < G; ++u) {
-            if (c0 + u < wp) {
-                const double* mrow = Mr + (c0 + u) * WY;
-#pragma unroll
-                for (int j = 0; j < WY; ++j) y[j] = __builtin_fma(p[u], mrow[j], y[j]);
-            }
-        }
-    }
     double* yp[kMaxSeg];
     int64_t yl[kMaxSeg];
     int yb[kMaxSeg + 1];
@@ -2284,20 +2300,213 @@ __global__ __launch_bounds__(256) void k_apply_rows(Panel P, const double* __res
         yl[q] = Y.ld[q];
         yb[q + 1] = yb[q] + (q < Y.nseg ? Y.ncol[q] : 0);
     }
-#pragma unroll
-    for (int j = 0; j < WY; ++j) {
-        if (j < wy) {
-            double* dst = yp[0] + r;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += stride) {
+        auto colp = [&](int c) {
+            const double* res = sp[0] + r;
 #pragma unroll
             for (int q = 0; q < kMaxSeg; ++q)
-                if (j >= yb[q] && j < yb[q + 1]) dst = yp[q] + (int64_t)(j - yb[q]) * yl[q] + r;
-            *dst = y[j];
+                if (c >= sb[q] && c < sb[q + 1]) res = sp[q] + (int64_t)(c - sb[q]) * sl[q] + r;
+            return res;
+        };
+        double y[WY];
+#pragma unroll
+        for (int j = 0; j < WY; ++j) y[j] = 0.0;
+        constexpr int G = CAL_APPLY_ROWS_G;  // columns whose loads are in flight together
+        for (int c0 = 0; c0 < wp; c0 += G) {
+            double p[G];
+#pragma unroll
+            for (int u = 0; u < G; ++u) p[u] = *colp(c0 + u < wp ? c0 + u : c0);
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                if (c0 + u < wp) {
+                    const double* mrow = Mr + (c0 + u) * WY;
+#pragma unroll
+                    for (int j = 0; j < WY; ++j) y[j] = __builtin_fma(p[u], mrow[j], y[j]);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < WY; ++j) {
+            if (j < wy) {
+                double* dst = yp[0] + r;
+#pragma unroll
+                for (int q = 0; q < kMaxSeg; ++q)
+                    if (j >= yb[q] && j < yb[q + 1]) dst = yp[q] + (int64_t)(j - yb[q]) * yl[q] + r;
+                *dst = y[j];
+            }
         }
     }
 }
 
 // the row-parallel store-only apply: <= 16 outputs for any panel up to 256
 // columns, wider output chunks (32, 64) while M fits 64 KB of LDS
+// One block-MGS step of project.m fused with the next block's Gram:
+//   Y = P M (P = [Q{i} | X], M = [-R{i}; I]: X - Q{i} R{i}, stored), and
+//   G = Qn' Y (Qn = Q{i+1}: the next step's R{i+1}), in one pass over the rows.
+// Staged like k_gram_rows: per round a block loads 64 rows of P's and Qn's
+// columns, one column per wave instruction (lane = row, 512 B), into LDS
+// [row][col] (the loads of the next round in flight across the round);
+// barrier; thread (row = lane, wave w) forms y_j = fma(p_c, M(c,j), y_j) over
+// c ascending for its WY/4 columns j (k_apply_rows' order: the same Y bits),
+// stores them (lane = row again) and parks them in LDS; barrier; lane (c16,
+// g) of wave w feeds MFMA m with row w*16 + g*4 + m of Qn column c16 and of
+// Y column c16.  Buffer b is rewritten two rounds on, after both barriers of
+// the round between.  GRAM = false is the plain staged apply (one barrier).
+// The four waves' accumulators are added in order at the end (entry-major
+// partials as k_gram's: A = Qn, B = Y, ldc = 16).  Replaces apply (read P,
+// write Y) + Gram (read Qn, re-read Y): 8 n (wp + wq) read and 8 n wy written
+// instead of 8 n (wp + wq + wy) read and 8 n wy written, and one launch.
+template <int WY, int NCP, bool GRAM>
+__global__ __launch_bounds__(256) void k_apply_stage(Panel P, const double* __restrict__ M, int wp, int wy,
+                                                     PanelOut Y, Panel Qn, int64_t n, double* __restrict__ partial) {
+    constexpr int R = 64;
+    constexpr int NQ = GRAM ? 16 : 0;
+    constexpr int NS = NCP + NQ;             // staged global columns
+    constexpr int PER = NS / 4;              // loads per thread and round
+    constexpr int LD = NS + (GRAM ? WY : 0) + 1;
+    constexpr int JW = WY / 4;               // y columns per thread
+    static_assert(NS % 4 == 0 && WY % 4 == 0, "k_apply_stage geometry");
+    extern __shared__ __attribute__((aligned(16))) double lds_as[];
+    double* Mr = lds_as;                     // [NCP][WY]
+    double* buf = lds_as + NCP * WY;         // [2][R][LD]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, c16 = lane & 15, g = lane >> 4;
+    for (int e = tid; e < NCP * WY; e += 256) {
+        const int c = e / WY, j = e % WY;
+        Mr[e] = (j < wy && c < wp) ? M[(int64_t)j * wp + c] : 0.0;
+    }
+    const int wq = GRAM ? Qn.total : 0;
+    // loader: column wave + 4 q (wave-uniform), row lane
+    const double* pc[PER];
+    bool on[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int cc = wave + 4 * q;
+        if (cc < NCP) {
+            on[q] = cc < wp;
+            pc[q] = pcol(P, on[q] ? cc : 0);
+        } else {
+            on[q] = cc - NCP < wq;
+            pc[q] = pcol(Qn, on[q] ? cc - NCP : 0);
+        }
+    }
+    double* yc[JW];
+    bool yon[JW];
+#pragma unroll
+    for (int u = 0; u < JW; ++u) {
+        const int j = wave * JW + u;
+        yon[u] = j < wy;
+        yc[u] = pcol_out(Y, yon[u] ? j : 0);
+    }
+    d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+    const int64_t stride = (int64_t)gridDim.x * R;
+    double v[PER];
+    bool vin = false;
+    auto load = [&](int64_t rb) {
+        const int64_t rr = rb + lane;
+        vin = rr < n;
+        const int64_t ro = vin ? rr : 0;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) v[q] = on[q] ? pc[q][ro] : 0.0;
+    };
+    int64_t rb = (int64_t)blockIdx.x * R;
+    if (rb < n) load(rb);
+    __syncthreads();  // Mr
+    for (int b = 0; rb < n; rb += stride, b ^= 1) {
+        double* sb = buf + b * (R * LD);
+        const bool in = vin;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) sb[lane * LD + wave + 4 * q] = in ? v[q] : 0.0;
+        if (rb + stride < n) load(rb + stride);
+        __syncthreads();
+        // Y rows: this thread's row `lane`, columns wave*JW + u
+        double y[JW];
+#pragma unroll
+        for (int u = 0; u < JW; ++u) y[u] = 0.0;
+        const double* prow = sb + lane * LD;
+        for (int c = 0; c < wp; ++c) {
+            const double pv = prow[c];
+#pragma unroll
+            for (int u = 0; u < JW; ++u) y[u] = __builtin_fma(pv, Mr[c * WY + wave * JW + u], y[u]);
+        }
+        const int64_t r = rb + lane;
+#pragma unroll
+        for (int u = 0; u < JW; ++u)
+            if (yon[u] && r < n) yc[u][r] = y[u];
+        if constexpr (GRAM) {
+#pragma unroll
+            for (int u = 0; u < JW; ++u) sb[lane * LD + NS + wave * JW + u] = (yon[u] && r < n) ? y[u] : 0.0;
+            __syncthreads();
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const double* row = sb + (wave * 16 + g * 4 + m) * LD;
+                const double yb = c16 < WY ? row[NS + (c16 < WY ? c16 : 0)] : 0.0;
+                acc = mfma64(row[NCP + c16], yb, acc);
+            }
+        }
+    }
+    if constexpr (GRAM) {
+        __syncthreads();  // the staging buffers become the partials
+        auto red = reinterpret_cast<double (*)[64][4]>(buf);  // [3][64][4]
+        if (wave > 0)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) red[wave - 1][lane][q] = acc[q];
+        __syncthreads();
+        if (wave == 0) {
+            double* out = partial + blockIdx.x;
+            const int64_t nb = gridDim.x;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                double x = acc[q];
+                x = x + red[0][lane][q];
+                x = x + red[1][lane][q];
+                x = x + red[2][lane][q];
+                const int i = g + 4 * q, j = c16;
+                out[(int64_t)(j * 16 + i) * nb] = x;
+            }
+        }
+    }
+}
+
+#ifndef CAL_APPLY_GRAM_BLOCKS
+#define CAL_APPLY_GRAM_BLOCKS 1024
+#endif
+bool apply_gram_ok(int wp, int wy, int wq) { return wp >= 1 && wp <= 32 && wy >= 1 && wy <= 16 && wq >= 1 && wq <= 16; }
+int apply_gram_blocks(int64_t n) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>(CAL_APPLY_GRAM_BLOCKS, (n + 63) / 64));
+}
+
+template <bool GRAM>
+static hipError_t launch_apply_stage(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y,
+                                     const Panel& Qn, int64_t n, double* partial, hipStream_t st) {
+    const int blocks = apply_gram_blocks(n);
+    auto go = [&](auto WY_, auto NCP_) {
+        constexpr int WY = decltype(WY_)::value, NCP = decltype(NCP_)::value;
+        constexpr int LD = NCP + (GRAM ? 16 + WY : 0) + 1;
+        const size_t lds = sizeof(double) * std::max((size_t)NCP * WY + 2 * 64 * LD, (size_t)3 * 64 * 4);
+        hipLaunchKernelGGL((k_apply_stage<WY, NCP, GRAM>), dim3(blocks), dim3(256), lds, st, P, dM, wp, wy, Y, Qn,
+                           n, partial);
+    };
+    using I8 = std::integral_constant<int, 8>;
+    using I16 = std::integral_constant<int, 16>;
+    using I24 = std::integral_constant<int, 24>;
+    using I32 = std::integral_constant<int, 32>;
+    if (wy <= 8) {
+        if (wp <= 24) go(I8{}, I24{});
+        else go(I8{}, I32{});
+    } else {
+        if (wp <= 24) go(I16{}, I24{});
+        else go(I16{}, I32{});
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_apply_gram(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y, const Panel& Qn,
+                             int64_t n, double* partial, hipStream_t st) {
+    if (!apply_gram_ok(wp, wy, Qn.total)) return hipErrorInvalidValue;
+    return launch_apply_stage<true>(P, dM, wp, wy, Y, Qn, n, partial, st);
+}
+
 int apply_rows_max_wy(int wp) {
     if (wp < 1 || wp > 256) return 0;
     int wy = 16;
@@ -2306,10 +2515,17 @@ int apply_rows_max_wy(int wp) {
 }
 bool apply_rows_ok(int wp, int wy) { return wy >= 1 && wy <= apply_rows_max_wy(wp); }
 
+#ifndef CAL_APPLY_STAGE
+#define CAL_APPLY_STAGE 1  // plain applies (wp <= 32, wy <= 16) on k_apply_stage<GRAM = false>
+#endif
 hipError_t launch_apply(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y, bool store,
                         int wq, int64_t n, const ApplyPlan& pl, double* partial, hipStream_t st) {
+    if (CAL_APPLY_STAGE && store && !pl.gram && !pl.gramp && wp <= 32 && wy <= 16 && wp >= 1 && wy >= 1 && n > 0)
+        return launch_apply_stage<false>(P, dM, wp, wy, Y, Panel{}, n, nullptr, st);
     if (store && !pl.gram && !pl.gramp && apply_rows_ok(wp, wy)) {
-        const dim3 g((unsigned)((n + 255) / 256)), b(256);
+        int64_t nbk = (n + 255) / 256;
+        if (CAL_APPLY_ROWS_GRID > 0 && nbk > CAL_APPLY_ROWS_GRID) nbk = CAL_APPLY_ROWS_GRID;
+        const dim3 g((unsigned)nbk), b(256);
         const int WY = wy <= 1 ? 1 : (wy <= 2 ? 2 : (wy <= 4 ? 4 : (wy <= 8 ? 8 : (wy <= 16 ? 16 : (wy <= 32 ? 32 : 64)))));
         const size_t sh = sizeof(double) * (size_t)wp * WY;
         if (n <= 0) return hipSuccess;
@@ -3371,6 +3587,152 @@ __global__ __launch_bounds__(256) void k_axpy_sub_dev(double* __restrict__ y, co
         const double t = a * x[i];
         y[i] = y[i] - t;
     }
+}
+
+// The Newton prologue's recurrence (lanczos.m:105-110) in three launches
+// instead of seven, single rank: no reduce launches, each kernel sums the
+// block partials of the dot before it itself (every block the same sum, in
+// k_reduce's order; block 0 publishes it), so the bits are those of
+// k_axpy_sub_dev / k_dot / k_reduce / k_div_sqrt:
+//   k_pro_dot     y = y - sqrt(*pb) x (x may be null); partials of y'z
+//   k_pro_update  a = sum(pin) -> dst; y = y - a x; partials of y'y
+//   k_pro_div     b = sum(pin) -> dst; q = y / sqrt(b)
+// The partial-producing kernels run on k_dot's grid (dot_blocks) with its
+// per-thread order.  A kernel's own partials go to a buffer the next kernel
+// reads, never the one it reads itself.
+__device__ __forceinline__ double pro_block_sum(double s, double* ws) {
+    s = wave_sum(s);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __syncthreads();  // ws may still be read by a previous use
+    if (lane == 0) ws[wave] = s;
+    __syncthreads();
+    return ((ws[0] + ws[1]) + ws[2]) + ws[3];
+}
+// k_reduce's sum of np partials, in every block
+__device__ __forceinline__ double pro_reduce(const double* __restrict__ p, int np, double* ws) {
+    double s = 0.0;
+    for (int i = threadIdx.x; i < np; i += 256) s = s + p[i];
+    return pro_block_sum(s, ws);
+}
+// y = y - a x (x non-null), then sum of y z (z null: y y), k_dot's order
+__device__ __forceinline__ double pro_axpy_dot(double* __restrict__ y, const double* __restrict__ x, double a,
+                                               const double* __restrict__ z, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    double s = 0.0;
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + stride < n; i += 2 * stride) {
+        double y0 = y[i], y1 = y[i + stride];
+        const double x0 = x ? x[i] : 0.0, x1 = x ? x[i + stride] : 0.0;
+        const double z0 = z ? z[i] : 0.0, z1 = z ? z[i + stride] : 0.0;
+        if (x) {
+            const double t0 = a * x0, t1 = a * x1;
+            y0 = y0 - t0;
+            y1 = y1 - t1;
+            y[i] = y0;
+            y[i + stride] = y1;
+        }
+        s = s + y0 * (z ? z0 : y0);
+        s = s + y1 * (z ? z1 : y1);
+    }
+    if (i < n) {
+        double yi = y[i];
+        const double zi = z ? z[i] : 0.0;
+        if (x) {
+            const double t = a * x[i];
+            yi = yi - t;
+            y[i] = yi;
+        }
+        s = s + yi * (z ? zi : yi);
+    }
+    return s;
+}
+
+__global__ __launch_bounds__(256) void k_pro_dot(double* __restrict__ y, const double* __restrict__ x,
+                                                 const double* __restrict__ pb, const double* __restrict__ z,
+                                                 int64_t n, double* __restrict__ pout) {
+    __shared__ double ws[4];
+    const double a = x ? sqrt(*pb) : 0.0;
+    const double s = pro_block_sum(pro_axpy_dot(y, x, a, z, n), ws);
+    if (threadIdx.x == 0) pout[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void k_pro_update(double* __restrict__ y, const double* __restrict__ x,
+                                                    const double* __restrict__ pin, int np, double* __restrict__ dst,
+                                                    int64_t n, double* __restrict__ pout) {
+    __shared__ double ws[4];
+    const double a = pro_reduce(pin, np, ws);
+    if (blockIdx.x == 0 && threadIdx.x == 0) dst[0] = a;
+    const double s = pro_block_sum(pro_axpy_dot(y, x, a, nullptr, n), ws);
+    if (threadIdx.x == 0) pout[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void k_pro_div(double* __restrict__ q, const double* __restrict__ y,
+                                                 const double* __restrict__ pin, int np, double* __restrict__ dst,
+                                                 int64_t n) {
+    __shared__ double ws[4];
+    const double b = pro_reduce(pin, np, ws);
+    if (blockIdx.x == 0 && threadIdx.x == 0) dst[0] = b;
+    const double sb = sqrt(b);
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) q[i] = y[i] / sb;
+}
+
+// normest's per-iteration norms (lanczos.cpp normest_dev), single rank: one
+// launch for the partials of x'x and y'y (k_dot's grid and order for each),
+// one that sums them in k_reduce's order (block 0 publishes both) and scales
+// x by 1/sqrt(x'x) (k_div_sqrt's arithmetic) -- four launches fewer per
+// iteration, the same bits.
+__global__ __launch_bounds__(256) void k_norms2(const double* __restrict__ x, const double* __restrict__ y,
+                                                int64_t n, double* __restrict__ px, double* __restrict__ py) {
+    __shared__ double ws[4];
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    double sx = 0.0, sy = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const double a = x[i], b = y[i];
+        sx = sx + a * a;
+        sy = sy + b * b;
+    }
+    sx = pro_block_sum(sx, ws);
+    sy = pro_block_sum(sy, ws);
+    if (threadIdx.x == 0) {
+        px[blockIdx.x] = sx;
+        py[blockIdx.x] = sy;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_nrm_div(double* __restrict__ x, const double* __restrict__ px,
+                                                 const double* __restrict__ py, int np, double* __restrict__ dst,
+                                                 int64_t n) {
+    __shared__ double ws[4];
+    const double xx = pro_reduce(px, np, ws);
+    const double yy = pro_reduce(py, np, ws);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        dst[0] = xx;
+        dst[1] = yy;
+    }
+    const double sx = sqrt(xx);
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) x[i] = x[i] / sx;
+}
+
+hipError_t launch_normest_norms(double* x, const double* y, int64_t n, double* part, double* dst, hipStream_t st) {
+    if (n <= 0) return hipErrorInvalidValue;
+    const int nb = dot_blocks(n);
+    hipLaunchKernelGGL(k_norms2, dim3(nb), dim3(256), 0, st, x, y, n, part, part + nb);
+    hipLaunchKernelGGL(k_nrm_div, dim3(vec_blocks(n)), dim3(256), 0, st, x, part, part + nb, nb, dst, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_pro_step(double* r, const double* qprev, const double* pb_prev, const double* q, double* qnext,
+                           int64_t n, double* part, double* d_alpha, double* d_beta2, hipStream_t st) {
+    if (n <= 0) return hipErrorInvalidValue;
+    const int nb = dot_blocks(n);
+    double* pa = part;       // alpha partials
+    double* pb = part + nb;  // beta^2 partials
+    hipLaunchKernelGGL(k_pro_dot, dim3(nb), dim3(256), 0, st, r, qprev, pb_prev, q, n, pa);
+    hipLaunchKernelGGL(k_pro_update, dim3(nb), dim3(256), 0, st, r, q, pa, nb, d_alpha, n, pb);
+    hipLaunchKernelGGL(k_pro_div, dim3(vec_blocks(n)), dim3(256), 0, st, qnext, r, pb, nb, d_beta2, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_axpy_sub_dev(double* y, const double* x, const double* pa, bool take_sqrt, int64_t n,

@@ -181,12 +181,21 @@ static int normest_dev(cal_ctx* c, double* out) {
     };
     double* d_nrm = c->d_red + kNrm;
     const double* h_nrm = c->h_red + kNrm;
+    // one rank: both norms and the rescale in two launches (the same bits);
+    // CAL_PROLOGUE_FUSED=0 keeps the separate launches
+    const char* pf = std::getenv("CAL_PROLOGUE_FUSED");
+    const bool fused = (!pf || std::atoi(pf) != 0) && (!c->comm || c->comm->nranks <= 1);
+    if (fused) CAL_TRY(ensure_partial(c, 2 * (size_t)nb));
     double e0 = 0.0;
     int cnt = 0;
     for (;;) {
         for (int i = 0; i < kNormestChunk; ++i) {
             CAL_TRY(spmv_dev(c, x, y, 0, 0.0, 0.0, nullptr));  // Sx = S*x
             CAL_TRY(spmv_dev(c, y, x, 0, 0.0, 0.0, nullptr));  // x = S'*Sx
+            if (fused) {
+                CAL_HIP(c, launch_normest_norms(x, y, n, c->d_partial, d_nrm + 2 * i, c->stream));
+                continue;
+            }
             CAL_TRY(dot_dev(x, d_nrm + 2 * i));
             CAL_TRY(dot_dev(y, d_nrm + 2 * i + 1));
             CAL_HIP(c, launch_div_sqrt(x, x, d_nrm + 2 * i, n, c->stream));  // x = x / norm(x)
@@ -287,13 +296,25 @@ static int newton_prologue(cal_ctx* c, LanczosState& L, bool cgs = true) {
         CAL_HIP(c, launch_reduce(c->d_partial, nbd, 1, dst, c->stream));
         return allreduce_sum(c, dst, 1);
     };
+    // one rank: the recurrence in three launches per step (launch_pro_step,
+    // the same bits); several ranks all-reduce each dot before its use.
+    // CAL_PROLOGUE_FUSED=0 (read per run) keeps the separate launches: the
+    // parity test compares both.
+    const char* pf = std::getenv("CAL_PROLOGUE_FUSED");
+    const bool fused = (!pf || std::atoi(pf) != 0) && (!c->comm || c->comm->nranks <= 1);
+    if (fused) CAL_TRY(ensure_partial(c, 2 * (size_t)nbd));
     for (int j = 0; j < m; ++j) {
         CAL_TRY(spmv_dev(c, Qc(j), r, 0, 0.0, 0.0, nullptr));  // :103
-        if (j > 0) CAL_HIP(c, launch_axpy_sub_dev(r, Qc(j - 1), d_ab + m + j - 1, true, n, c->stream));  // :105
-        CAL_TRY(dot_dev(r, Qc(j), d_ab + j));                                                          // :107
-        CAL_HIP(c, launch_axpy_sub_dev(r, Qc(j), d_ab + j, false, n, c->stream));                      // :108
-        CAL_TRY(dot_dev(r, r, d_ab + m + j));                                                          // :109
-        CAL_HIP(c, launch_div_sqrt(Qc(j + 1), r, d_ab + m + j, n, c->stream));                         // :110
+        if (fused) {
+            CAL_HIP(c, launch_pro_step(r, j > 0 ? Qc(j - 1) : nullptr, d_ab + m + j - 1, Qc(j), Qc(j + 1), n,
+                                       c->d_partial, d_ab + j, d_ab + m + j, c->stream));  // :105-110
+        } else {
+            if (j > 0) CAL_HIP(c, launch_axpy_sub_dev(r, Qc(j - 1), d_ab + m + j - 1, true, n, c->stream));  // :105
+            CAL_TRY(dot_dev(r, Qc(j), d_ab + j));                                                          // :107
+            CAL_HIP(c, launch_axpy_sub_dev(r, Qc(j), d_ab + j, false, n, c->stream));                      // :108
+            CAL_TRY(dot_dev(r, r, d_ab + m + j));                                                          // :109
+            CAL_HIP(c, launch_div_sqrt(Qc(j + 1), r, d_ab + m + j, n, c->stream));                         // :110
+        }
         if (!cgs) continue;  // lanczos(...,'local') (restarted_ca_lanczos.m:65)
         // one CGS pass against Q(:,1:j) (lanczos.m:62-66)
         Panel Qj = panel();
@@ -1624,6 +1645,10 @@ namespace {
 // first block is normalised (:371-380), otherwise V(:,2:s+1) is projected
 // against {Q(:,1:nvecs-s), Q(:,nvecs-s+1:nvecs+1)} ('full', :387-392; doreorth
 // true, see oracle/ca_lanczos_ref.irl_lanczos_basic) and T is extended.
+// (Prefetching the next block's powers before the host waits for R, as
+// lanczos_step does, measured neutral here: 34.5-35.1 vs 34.9-35.4 solves/s,
+// the Grams after the prefetched powers lose the Infinity Cache lines of the
+// block they project, 6.74 -> 6.95 ms per solve; not kept.)
 int irl_block(cal_ctx* c, LanczosState& L, int nvecs, double* bprev) {
     const int s = L.s;
     const int64_t n = c->A.n_local, ld = L.ld;

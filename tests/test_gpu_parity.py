@@ -262,6 +262,32 @@ def test_project_and_normalize_two_blocks(cal, ref):
         assert np.max(np.abs(a - b)) < 1e-11
 
 
+@pytest.mark.parametrize("n,widths,m", [(2000, (9, 9, 9), 8), (600001, (9, 9, 12, 5), 8),
+                                          (300007, (20, 9, 16), 12), (70001, (16, 7), 16)])
+def test_project_and_normalize_blocks_fused(cal, ref, n, widths, m):
+    """Block MGS over several blocks (project.m): the update of block i and
+    the Gram of block i + 1 run as one pass (k_apply_gram: [Q{i} | X] up to
+    32 columns, X up to 16, Q{i+1} up to 16); heights past one grid stride of
+    the kernel (262144 rows) and not a multiple of 64, the 8- and 16-column X
+    layouts, 24- and 32-column P.  R blocks within 1e-11 of the oracle's,
+    QZ within 1e-10, the same reorth decision."""
+    rng = np.random.RandomState(len(widths) * 7 + m)
+    Qs = []
+    for w in widths:
+        Q = rng.randn(n, w)
+        for P in Qs:
+            Q = Q - P @ (P.T @ Q)
+        Qs.append(np.linalg.qr(Q)[0])
+    X = sum(P @ rng.randn(P.shape[1], m) for P in Qs) * 3 + rng.randn(n, m)
+    QZ, RZ, re, _ = cal.projectAndNormalize_ex(Qs, X)
+    QZr, RZr, info = ref.projectAndNormalize_ex(Qs, X)
+    assert re == info.reorth
+    for a, b in zip(RZ, RZr):
+        assert np.max(np.abs(a - b)) < 1e-11 * max(1.0, np.max(np.abs(b)))
+    assert np.max(np.abs(QZ - QZr)) < 1e-10
+    assert np.max(np.abs(QZ.T @ QZ - np.eye(m))) < 1e-13
+
+
 # ---------------------------------------------------------------- a10 - a14
 def _compare_lanczos(out, exp, normA, check_rn=True, t_blocks=None):
     """T is compared within 1e-9 ||A|| on its leading t_blocks x t_blocks
@@ -345,6 +371,52 @@ def test_orth_err_deferred_wide_gram(cal, ref, monkeypatch, N, orth):
         assert np.all(np.abs(a.orth_err - b.orth_err) <= 1e-15 + 1e-9 * b.orth_err), (a.orth_err, b.orth_err)
     if orth == "full":
         assert np.max(a.orth_err) < 1e-12
+
+
+@pytest.mark.parametrize("N,s", [(40, 8), (23, 4), (70, 16)])
+def test_newton_prologue_fused_bitexact(cal, ref, monkeypatch, N, s):
+    """The Newton prologue's recurrence (lanczos.m:103-110) with each update
+    and the dot after it in one launch (k_axpy_dot: k_dot's grid and order,
+    the partials summed by the last block in k_reduce's order) against the
+    separate axpy / dot / reduce launches (CAL_PROLOGUE_FUSED=0): the same
+    bits in T, Q's Ritz residual norms and the orthogonality errors; rows not
+    a multiple of the 256-thread blocks (23^3, 70^3 = 343000 > one grid
+    stride of 1024 blocks)."""
+    A = cal.matrices.laplacian_3d(N)
+    r = ref.matlab_rand(A.shape[0])
+    monkeypatch.delenv("CAL_PROLOGUE_FUSED", raising=False)
+    a = cal.ca_lanczos_ex(A, r, s, 4 * s, "newton", "full")
+    monkeypatch.setenv("CAL_PROLOGUE_FUSED", "0")
+    b = cal.ca_lanczos_ex(A, r, s, 4 * s, "newton", "full")
+    assert np.array_equal(a.T, b.T)
+    assert np.array_equal(a.ritz_rnorm, b.ritz_rnorm)
+    assert np.array_equal(a.orth_err, b.orth_err)
+
+
+def test_normest_and_irl_fused_bitexact(cal, ref, monkeypatch):
+    """normest (MATLAB built-in, ca_lanczos.m:258) with both norms and the
+    rescale fused (k_norms2 + k_nrm_div) against the separate dot / reduce /
+    div launches (CAL_PROLOGUE_FUSED=0): 'periodic' CA-Lanczos (which takes
+    normest(A) for its omega recurrence) and a whole implicit-restart solve
+    (normest, the Newton prologue, every restart) give the same bits."""
+    A = cal.matrices.circuit_like(60, seed=3)
+    r = ref.matlab_rand(A.shape[0])
+    outs = []
+    for env in (None, "0"):
+        if env is None:
+            monkeypatch.delenv("CAL_PROLOGUE_FUSED", raising=False)
+        else:
+            monkeypatch.setenv("CAL_PROLOGUE_FUSED", env)
+        p = cal.ca_lanczos_ex(A, r, 4, 40, "newton", "periodic")
+        irl = cal.impl_restarted_ca_lanczos(A, r, 40, 6, 4, "newton", "full", 1e-8)
+        outs.append((p, irl))
+    (p0, i0), (p1, i1) = outs
+    assert p0.info["norm_A"] == p1.info["norm_A"] and p0.info["norm_A"] > 0
+    assert i0["norm_A"] == i1["norm_A"]
+    assert np.array_equal(p0.T, p1.T)
+    assert i0["num_restarts"] == i1["num_restarts"]
+    assert np.array_equal(i0["conv_eigs"], i1["conv_eigs"])
+    assert np.array_equal(i0["Q_conv"], i1["Q_conv"])
 
 
 def test_ca_lanczos_bad_args(cal):
