@@ -932,6 +932,10 @@ def workload_leg(cal, local, name, s, K, W, basis):
         leg["workload"] = wl2.desc % (wl2.n, nnz)
         leg["spmv_format"] = ("%s (%d pair patterns, %d split pairs)" % (fmt, npairpat, nsplit)
                               if fmt == "pattern" else fmt)
+        pP, pH, pmode = c.spmv_plane_info()
+        if pP > 0:
+            leg["spmv_format"] = "pattern (plane march: plane stride %d, in-plane reach %d, key mode %d)" % (
+                pP, pH, pmode)
         leg_roofline(leg, fmt, npairpat, wl2.n, nnz, s)
         if fmt == "pattern":
             b2b = c.bench_spmv(20, 1.0)

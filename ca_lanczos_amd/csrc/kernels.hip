@@ -2491,12 +2491,15 @@ static hipError_t launch_apply_stage(const Panel& P, const double* dM, int wp, i
     using I16 = std::integral_constant<int, 16>;
     using I24 = std::integral_constant<int, 24>;
     using I32 = std::integral_constant<int, 32>;
+    using I64 = std::integral_constant<int, 64>;
     if (wy <= 8) {
         if (wp <= 24) go(I8{}, I24{});
-        else go(I8{}, I32{});
+        else if (wp <= 32 || GRAM) go(I8{}, I32{});
+        else go(I8{}, I64{});
     } else {
         if (wp <= 24) go(I16{}, I24{});
-        else go(I16{}, I32{});
+        else if (wp <= 32 || GRAM) go(I16{}, I32{});
+        else go(I16{}, I64{});
     }
     return hipGetLastError();
 }
@@ -2516,11 +2519,15 @@ int apply_rows_max_wy(int wp) {
 bool apply_rows_ok(int wp, int wy) { return wy >= 1 && wy <= apply_rows_max_wy(wp); }
 
 #ifndef CAL_APPLY_STAGE
-#define CAL_APPLY_STAGE 1  // plain applies (wp <= 32, wy <= 16) on k_apply_stage<GRAM = false>
+#define CAL_APPLY_STAGE 1  // plain applies (wp <= CAL_APPLY_STAGE_WP, wy <= 16) on k_apply_stage<GRAM = false>
+#endif
+#ifndef CAL_APPLY_STAGE_WP
+#define CAL_APPLY_STAGE_WP 32
 #endif
 hipError_t launch_apply(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y, bool store,
                         int wq, int64_t n, const ApplyPlan& pl, double* partial, hipStream_t st) {
-    if (CAL_APPLY_STAGE && store && !pl.gram && !pl.gramp && wp <= 32 && wy <= 16 && wp >= 1 && wy >= 1 && n > 0)
+    if (CAL_APPLY_STAGE && store && !pl.gram && !pl.gramp && wp <= CAL_APPLY_STAGE_WP && wy <= 16 && wp >= 1 &&
+        wy >= 1 && n > 0)
         return launch_apply_stage<false>(P, dM, wp, wy, Y, Panel{}, n, nullptr, st);
     if (store && !pl.gram && !pl.gramp && apply_rows_ok(wp, wy)) {
         int64_t nbk = (n + 255) / 256;

@@ -376,7 +376,11 @@ int upload_matrix(cal_ctx* c, int64_t n_rows, int64_t ext_off, int64_t n_local, 
     A.nnz = rowptr[n_rows];
     A.nnz_loc = rowptr[ext_off + n_local] - rowptr[ext_off];
     A.lpad = ((lpad + 63) / 64) * 64;
-    A.ld = ((A.lpad + n_local + rext + 63) / 64) * 64;
+    // two rows of slack past the data: the plane march reads row pairs up
+    // to n + 1 (planes_ok needs ld >= n + 2; with n a multiple of 64 the
+    // row-pair kernel ran instead: lap2d_1000 5905-6022 -> 6112-6234
+    // outer-it/s with the slack, profiles/r05/ld_slack/)
+    A.ld = ((A.lpad + n_local + rext + 2 + 63) / 64) * 64;
     if (A.ld == 0) A.ld = 64;
     // storage format: row patterns when the table is small (auto) or forced
     if (c->spmv_format != 1) {
