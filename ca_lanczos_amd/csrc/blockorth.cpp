@@ -288,7 +288,7 @@ static int rank_from_R(int m, const double* R, double tol) {
     dense::singular_values(m, R, m, sv.data());
     const double abs_tol = tol * sv[0];
     for (int i = 0; i < m; ++i)
-        if (sv[i] <= abs_tol) return i;  // normalize.m:19-24
+        if (!(sv[i] > abs_tol)) return i;  // normalize.m:19-24 (a non-finite R counts as deficient)
     return m;
 }
 

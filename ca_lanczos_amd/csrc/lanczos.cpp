@@ -764,6 +764,11 @@ static int extend_T_first(cal_ctx* c, LanczosState& L, const std::vector<double>
         return CAL_WARN_BREAKDOWN;
     }
     dense::rdiv_upper(s1, s, RB.data(), s1, R11.data(), s);
+    for (const double v : RB)
+        if (!std::isfinite(v)) {  // the reference divides on (Inf/NaN in T, a MATLAB warning): flagged here
+            L.breakdown = true;
+            return CAL_WARN_BREAKDOWN;
+        }
     for (int j = 0; j < s; ++j)
         for (int i = 0; i < s1; ++i) L.T[i + (size_t)j * L.Tld] = RB[i + (size_t)j * s1];
     L.b.assign(1, RB[s + (size_t)(s - 1) * s1]);  // b(1) = T(s+1,s)
@@ -831,7 +836,10 @@ static int extend_T(cal_ctx* c, LanczosState& L, const std::vector<double>& Rkk_
     std::vector<double> Tk;
     double bnew = 0.0;
     const double bprev = L.b[k - 2];
-    if (block_T(L.Bk, L.s, bprev, Rkk_s, Rk_s, Tk, &bnew) != 0) {
+    bool finite = true;
+    const int bt = block_T(L.Bk, L.s, bprev, Rkk_s, Rk_s, Tk, &bnew);
+    for (const double v : Tk) finite = finite && std::isfinite(v);
+    if (bt != 0 || !finite || !std::isfinite(bnew)) {  // non-finite: the reference's Inf/NaN T, flagged
         L.breakdown = true;
         return CAL_WARN_BREAKDOWN;
     }
@@ -1687,8 +1695,10 @@ int irl_block(cal_ctx* c, LanczosState& L, int nvecs, double* bprev) {
     if (ro && rk < s) L.info.n_rank_deficient++;
     std::vector<double> Tk;
     double bnew = 0.0;
-    if (block_T(L.Bk, s, *bprev, RZ.back(), R, Tk, &bnew) != 0)
-        return set_error(c, CAL_WARN_BREAKDOWN, "IRL: CA-Lanczos breakdown (rho_t = 0)");
+    const int bt = block_T(L.Bk, s, *bprev, RZ.back(), R, Tk, &bnew);
+    bool finite = std::isfinite(bnew);
+    for (const double v : Tk) finite = finite && std::isfinite(v);
+    if (bt != 0 || !finite) return set_error(c, CAL_WARN_BREAKDOWN, "IRL: CA-Lanczos breakdown (rho_t = 0)");
     place_T(L, nvecs, Tk, *bprev, bnew);
     *bprev = bnew;
     return 0;

@@ -753,7 +753,7 @@ def test_ca_lanczos_exhausted_krylov_space(cal, ref, s, basis, start):
     except cal.CalError as e:
         assert e.status < 0
         return
-    assert out.info["n_rank_deficient"] >= 1 or out.info["breakdown"] == 1
+    assert out.info["n_rank_deficient"] >= 1 or out.info["breakdown"] == 1, (out.info, np.isfinite(out.T).all())
 
 
 @pytest.mark.parametrize("basis", ["newton", "monomial"])
