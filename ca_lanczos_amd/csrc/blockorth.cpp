@@ -452,8 +452,11 @@ static int wait_published(cal_ctx* c, const unsigned long long* h_seq, unsigned 
     }
 }
 
+// p1_blocks > 0 (Qp empty): P1's partials (X'X, the rowgram tile layout) were
+// already written to d_partial by that many blocks of the kernel that formed X
+// (k_apply_stage<..., 2>, the last block-MGS step): P1 is not launched.
 static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, bool doreorth, const PanelOut& Qout,
-                       double* Rq, double* R, bool* reorth) {
+                       double* Rq, double* R, bool* reorth, int p1_blocks = 0) {
     const int w = Qp.total, m = X.total, nq = w < 8 ? w : 8, wp = w + m;
     const int WP = rowapply_wpmax(wp), MO = rowapply_mout(m);
     const Panel W = panel_concat(Qp, X);
@@ -466,7 +469,10 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
     CAL_TRY(ensure_partial(c, (size_t)blocks * 272));
     // P1: [Qp(0:nq) | X]' X (+ Qp column 8 as the extra column)
     ColList ct{};
-    {
+    if (p1_blocks > 0 && w == 0) {
+        // formed with X
+    } else {
+        p1_blocks = 0;
         const Panel T = panel_concat(panel_slice(W, 0, nq), X);
         const int nt = T.total;
         for (int cc = 0; cc < 16; ++cc) ct.p[cc] = panel_slice(T, cc < nt ? cc : nt - 1, 1).ptr[0];
@@ -483,7 +489,8 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
     // reduce the Gram partials, all-reduce the tile over the ranks, then the
     // s x s algebra; phase 1 publishes R / RY / flags to h_out
     auto coef = [&](int phase, int dore) -> int {
-        CAL_HIP(c, launch_reduce(c->d_partial, (int)blocks, 272, d_tile, c->stream));
+        const int np = phase == 0 && p1_blocks > 0 ? p1_blocks : (int)blocks;
+        CAL_HIP(c, launch_reduce(c->d_partial, np, 272, d_tile, c->stream));
         CAL_TRY(allreduce_sum(c, d_tile, 272));
         CAL_HIP(c, launch_orth_coef(phase, d_tile, d_st, d_mbuf, d_out, w, m, WP, MO, dore,
                                     phase == 1 ? c->d_pub : nullptr, d_seq, seq, c->stream));
@@ -524,7 +531,7 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
 }
 
 int normalize_dev(cal_ctx* c, int64_t n, const Panel& X, const PanelOut& Qout, double* R, double tol, int* rank,
-                  bool* shifted) {
+                  bool* shifted, int p1_blocks) {
     const int m = X.total;
     if (use_tsqr(c, m, c->tier1)) {  // tsqr.m: Householder TSQR
         CAL_TRY(tsqr_dev(c, n, X, nullptr, m, Qout, R));
@@ -542,7 +549,7 @@ int normalize_dev(cal_ctx* c, int64_t n, const Panel& X, const PanelOut& Qout, d
     if (m < 1 || m > 16) return set_error(c, CAL_ERR_ARG, "normalize: 1..32 columns supported");
     if (orth_device_ok(c, panel(), X)) {
         bool ro = false;
-        const int st = orth_device(c, n, panel(), X, false, Qout, nullptr, R, &ro);
+        const int st = orth_device(c, n, panel(), X, false, Qout, nullptr, R, &ro, p1_blocks);
         CAL_TRY(st);
         if (st == 0) {
             if (shifted) *shifted = false;
@@ -1160,9 +1167,13 @@ int gram_async(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* d_
 // reads it and writes dX (no separate copy of X into the work block).
 // bb_first: the first block's Gram also forms X'X (the norms before of
 // projectAndNormalize.m:17-22) in the same pass, at region + 16 ldc (ld 16).
+// self_blocks (optional): the last step's update also forms X'X for the
+// normalize that follows (normalize_dev's p1_blocks; 0 when it did not).
 static int project_blocks_async(cal_ctx* c, int64_t n, int64_t ld, int nb, const std::vector<double*>& dQ,
                                 const int* widths, int m, double* dX, int region0, std::vector<int>& ldc,
-                                const double* dSrc = nullptr, bool bb_first = false) {
+                                const double* dSrc = nullptr, bool bb_first = false, int* self_blocks = nullptr) {
+    static const bool self_off = getenv("CAL_SELFGRAM_OFF") != nullptr;  // A/B
+    if (self_blocks) *self_blocks = 0;
     const PanelOut Xo = panel_out(dX, ld, m);
     const double* cur = dSrc ? dSrc : dX;  // where X currently is
     ldc.assign(nb, 0);
@@ -1205,6 +1216,12 @@ static int project_blocks_async(cal_ctx* c, int64_t n, int64_t ld, int nb, const
             CAL_HIP(c, hipMemcpyAsync(c->h_red + offn, c->d_red + offn, 256 * sizeof(double), hipMemcpyDeviceToHost,
                                       c->stream));
             ldc[nx] = 16;
+        } else if (self_blocks && !self_off && nx == nb && apply_selfgram_ok(w + m, m)) {
+            // the last step: X = X - Q{i}*R{i} and X'X (the normalize's P1) in one pass
+            CAL_TRY(ensure_partial(c, (size_t)std::max<int64_t>(apply_gram_blocks(n), (n + 255) / 256) * 272));
+            const int t = timer_begin(c, 2, 8.0 * n * (w + 2 * m));
+            CAL_HIP(c, launch_apply_selfgram(W, dM, w + m, m, Xo, n, c->d_partial, self_blocks, c->stream));
+            timer_end(c, t);
         } else {
             CAL_TRY(apply_dev(c, n, W, dM, m, Xo));  // X = X - Q{i}*R{i}
         }
@@ -1254,9 +1271,10 @@ int project_and_normalize_blocks_dev(cal_ctx* c, int64_t n, int64_t ld, int nblo
             CAL_TRY(gram_async(c, n, Xp, Xp, c->d_red + offx, c->h_red + offx, &ldx));
         }
         std::vector<int> ldc;
-        CAL_TRY(project_blocks_async(c, n, ld, nblocks, dQ, widths, m, dY, 0, ldc, dX, fused));  // :25 (Y from X)
+        int p1 = 0;
+        CAL_TRY(project_blocks_async(c, n, ld, nblocks, dQ, widths, m, dY, 0, ldc, dX, fused, &p1));  // :25
         if (fused) offx = kAsyncBase + (size_t)b0 * kAsyncRegion + 16 * (size_t)ldc[b0];
-        CAL_TRY(normalize_dev(c, n, Yp, Qout, R, 1.0e-8, &rk, &sh));  // :26 (waits)
+        CAL_TRY(normalize_dev(c, n, Yp, Qout, R, 1.0e-8, &rk, &sh, p1));  // :26 (waits)
         for (int i = 0; i < m; ++i) before[i] = std::sqrt(c->h_red[offx + i + (size_t)i * ldx]);
         read_async_R(c, nblocks, widths, m, 0, ldc, RY);
     } else {
@@ -1285,8 +1303,9 @@ int project_and_normalize_blocks_dev(cal_ctx* c, int64_t n, int64_t ld, int nblo
         for (int i = 0; i < nblocks; ++i) R2[i].assign((size_t)std::max(widths[i], 0) * m, 0.0);
         if (async) {
             std::vector<int> ldc;
-            CAL_TRY(project_blocks_async(c, n, ld, nblocks, dQ, widths, m, dY, 0, ldc));
-            CAL_TRY(normalize_dev(c, n, Yp, Qout, R, 1.0e-8, &rk, &sh));
+            int p1 = 0;
+            CAL_TRY(project_blocks_async(c, n, ld, nblocks, dQ, widths, m, dY, 0, ldc, nullptr, false, &p1));
+            CAL_TRY(normalize_dev(c, n, Yp, Qout, R, 1.0e-8, &rk, &sh, p1));
             read_async_R(c, nblocks, widths, m, 0, ldc, R2);
         } else {
             CAL_TRY(project_blocks(c, n, ld, nblocks, dQ, widths, m, dY, false, R2));

@@ -247,6 +247,11 @@ bool apply_gram_ok(int wp, int wy, int wq);
 int apply_gram_blocks(int64_t n);
 hipError_t launch_apply_gram(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y, const Panel& Qn,
                              int64_t n, double* partial, hipStream_t st);
+// Y = P M (stored) and Y'Y as the 272-entry tile partials of the rowgram
+// (P1 of orth_device) over *blocks blocks: wp <= 32, wy <= 16
+bool apply_selfgram_ok(int wp, int wy);
+hipError_t launch_apply_selfgram(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y, int64_t n,
+                                 double* partial, int* blocks, hipStream_t st);
 hipError_t launch_apply(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y, bool store,
                         int wq, int64_t n, const ApplyPlan& pl, double* partial, hipStream_t st);
 hipError_t launch_reduce(const double* partial, int nparts, int64_t nent, double* out, hipStream_t st);
@@ -591,8 +596,9 @@ struct PNResult {
     bool chol_shifted = false;
 };
 // CholQR2 normalise of the n x m panel X into Qout, R (m x m) on host.
+// p1_blocks: X'X's tile partials already in d_partial (blockorth.cpp orth_device)
 int normalize_dev(cal_ctx* c, int64_t n, const Panel& X, const PanelOut& Qout, double* R, double tol, int* rank,
-                  bool* shifted);
+                  bool* shifted, int p1_blocks = 0);
 // projectAndNormalize of X (n x m) against one block Qp (n x w): QZ into Qout,
 // Rq (w x m) and R (m x m) on host.  Mirrors projectAndNormalize.m:3-90.
 int project_and_normalize_dev(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, bool doreorth,

@@ -2339,8 +2339,6 @@ __global__ __launch_bounds__(256) void k_apply_rows(Panel P, const double* __res
     }
 }
 
-// the row-parallel store-only apply: <= 16 outputs for any panel up to 256
-// columns, wider output chunks (32, 64) while M fits 64 KB of LDS
 // One block-MGS step of project.m fused with the next block's Gram:
 //   Y = P M (P = [Q{i} | X], M = [-R{i}; I]: X - Q{i} R{i}, stored), and
 //   G = Qn' Y (Qn = Q{i+1}: the next step's R{i+1}), in one pass over the rows.
@@ -2357,11 +2355,14 @@ __global__ __launch_bounds__(256) void k_apply_rows(Panel P, const double* __res
 // partials as k_gram's: A = Qn, B = Y, ldc = 16).  Replaces apply (read P,
 // write Y) + Gram (read Qn, re-read Y): 8 n (wp + wq) read and 8 n wy written
 // instead of 8 n (wp + wq + wy) read and 8 n wy written, and one launch.
-template <int WY, int NCP, bool GRAM>
+// GRAM: 0 none, 1 Qn'Y as above, 2 Y'Y (the last MGS step fused with the
+// normalize's first Gram sweep, P1 of blockorth.cpp orth_device: its 272-entry
+// tile layout, the extra column's 16 entries zero).
+template <int WY, int NCP, int GRAM>
 __global__ __launch_bounds__(256) void k_apply_stage(Panel P, const double* __restrict__ M, int wp, int wy,
                                                      PanelOut Y, Panel Qn, int64_t n, double* __restrict__ partial) {
     constexpr int R = 64;
-    constexpr int NQ = GRAM ? 16 : 0;
+    constexpr int NQ = GRAM == 1 ? 16 : 0;
     constexpr int NS = NCP + NQ;             // staged global columns
     constexpr int PER = NS / 4;              // loads per thread and round
     constexpr int LD = NS + (GRAM ? WY : 0) + 1;
@@ -2375,7 +2376,7 @@ __global__ __launch_bounds__(256) void k_apply_stage(Panel P, const double* __re
         const int c = e / WY, j = e % WY;
         Mr[e] = (j < wy && c < wp) ? M[(int64_t)j * wp + c] : 0.0;
     }
-    const int wq = GRAM ? Qn.total : 0;
+    const int wq = GRAM == 1 ? Qn.total : 0;
     // loader: column wave + 4 q (wave-uniform), row lane
     const double* pc[PER];
     bool on[PER];
@@ -2441,7 +2442,7 @@ __global__ __launch_bounds__(256) void k_apply_stage(Panel P, const double* __re
             for (int m = 0; m < 4; ++m) {
                 const double* row = sb + (wave * 16 + g * 4 + m) * LD;
                 const double yb = c16 < WY ? row[NS + (c16 < WY ? c16 : 0)] : 0.0;
-                acc = mfma64(row[NCP + c16], yb, acc);
+                acc = mfma64(GRAM == 1 ? row[NCP + c16] : yb, yb, acc);
             }
         }
     }
@@ -2464,6 +2465,7 @@ __global__ __launch_bounds__(256) void k_apply_stage(Panel P, const double* __re
                 const int i = g + 4 * q, j = c16;
                 out[(int64_t)(j * 16 + i) * nb] = x;
             }
+            if (GRAM == 2 && g == 0) out[(int64_t)(256 + c16) * nb] = 0.0;
         }
     }
 }
@@ -2476,13 +2478,13 @@ int apply_gram_blocks(int64_t n) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(CAL_APPLY_GRAM_BLOCKS, (n + 63) / 64));
 }
 
-template <bool GRAM>
+template <int GRAM>
 static hipError_t launch_apply_stage(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y,
                                      const Panel& Qn, int64_t n, double* partial, hipStream_t st) {
     const int blocks = apply_gram_blocks(n);
     auto go = [&](auto WY_, auto NCP_) {
         constexpr int WY = decltype(WY_)::value, NCP = decltype(NCP_)::value;
-        constexpr int LD = NCP + (GRAM ? 16 + WY : 0) + 1;
+        constexpr int LD = NCP + (GRAM == 1 ? 16 : 0) + (GRAM ? WY : 0) + 1;
         const size_t lds = sizeof(double) * std::max((size_t)NCP * WY + 2 * 64 * LD, (size_t)3 * 64 * 4);
         hipLaunchKernelGGL((k_apply_stage<WY, NCP, GRAM>), dim3(blocks), dim3(256), lds, st, P, dM, wp, wy, Y, Qn,
                            n, partial);
@@ -2507,9 +2509,20 @@ static hipError_t launch_apply_stage(const Panel& P, const double* dM, int wp, i
 hipError_t launch_apply_gram(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y, const Panel& Qn,
                              int64_t n, double* partial, hipStream_t st) {
     if (!apply_gram_ok(wp, wy, Qn.total)) return hipErrorInvalidValue;
-    return launch_apply_stage<true>(P, dM, wp, wy, Y, Qn, n, partial, st);
+    return launch_apply_stage<1>(P, dM, wp, wy, Y, Qn, n, partial, st);
 }
 
+bool apply_selfgram_ok(int wp, int wy) { return wp >= 1 && wp <= 32 && wy >= 1 && wy <= 16; }
+
+hipError_t launch_apply_selfgram(const Panel& P, const double* dM, int wp, int wy, const PanelOut& Y, int64_t n,
+                                 double* partial, int* blocks, hipStream_t st) {
+    if (!apply_selfgram_ok(wp, wy)) return hipErrorInvalidValue;
+    *blocks = apply_gram_blocks(n);
+    return launch_apply_stage<2>(P, dM, wp, wy, Y, Panel{}, n, partial, st);
+}
+
+// the row-parallel store-only apply: <= 16 outputs for any panel up to 256
+// columns, wider output chunks (32, 64) while M fits 64 KB of LDS
 int apply_rows_max_wy(int wp) {
     if (wp < 1 || wp > 256) return 0;
     int wy = 16;
@@ -2528,7 +2541,7 @@ hipError_t launch_apply(const Panel& P, const double* dM, int wp, int wy, const 
                         int wq, int64_t n, const ApplyPlan& pl, double* partial, hipStream_t st) {
     if (CAL_APPLY_STAGE && store && !pl.gram && !pl.gramp && wp <= CAL_APPLY_STAGE_WP && wy <= 16 && wp >= 1 &&
         wy >= 1 && n > 0)
-        return launch_apply_stage<false>(P, dM, wp, wy, Y, Panel{}, n, nullptr, st);
+        return launch_apply_stage<0>(P, dM, wp, wy, Y, Panel{}, n, nullptr, st);
     if (store && !pl.gram && !pl.gramp && apply_rows_ok(wp, wy)) {
         int64_t nbk = (n + 255) / 256;
         if (CAL_APPLY_ROWS_GRID > 0 && nbk > CAL_APPLY_ROWS_GRID) nbk = CAL_APPLY_ROWS_GRID;
