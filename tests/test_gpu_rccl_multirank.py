@@ -1,0 +1,176 @@
+"""The RCCL communicator with several ranks (comm.cpp's kind == 1 branches:
+ncclAllReduce of the Gram tiles, ncclSend/ncclRecv of the halo and the deep
+ghost zone, ncclAllGather of the TSQR roots, the exchange on the
+communicator's own stream overlapped with the interior powers).
+
+The test box has one GPU and RCCL refuses two ranks on one device of one
+host ("Duplicate GPU detected").  Each rank therefore states its own host id
+(NCCL_HOSTID), so RCCL sees P one-GPU hosts and connects them over its socket
+transport on the loopback interface.  The transport differs from xGMI; the
+library's calls, their order, their buffers, offsets and streams are the ones
+an 8-GPU node runs.  Every result is checked against the single-rank run or
+the oracle's bits, as the host-staged tests in test_gpu_distributed.py do."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rccl_env(rank):
+    # one "host" per rank, sockets over loopback; set before RCCL initialises
+    os.environ.update(NCCL_HOSTID="cal-rank-%d" % rank, NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1",
+                      NCCL_DEBUG=os.environ.get("NCCL_DEBUG", "WARN"))
+
+
+def _worker(rank, world, port, case, out_q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    _rccl_env(rank)
+    try:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import ctypes
+        import ca_lanczos_amd as cal
+        from ca_lanczos_amd._lib import check, lib, ptr
+        from oracle import ca_lanczos_ref as ref
+
+        uid = bytearray(128)
+        if rank == 0:
+            buf = ctypes.create_string_buffer(128)
+            check(None, lib.cal_comm_unique_id(buf))
+            uid = bytearray(buf.raw)
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        dist.broadcast(t, 0)
+        uid = bytes(t.tolist())
+
+        kind, dim, N, s, it, orth, normalize = case
+        A = cal.matrices.laplacian_2d(N) if dim == 2 else cal.matrices.laplacian_3d(N)
+        n = A.shape[0]
+        b = cal.matrices.slab_bounds(n, world, N ** (dim - 1))
+        r0, r1 = b[rank], b[rank + 1]
+        ctx = cal.Context(0, mpk_depth=8, normalize=normalize)
+        ctx.comm_init_rccl(world, rank, uid)
+        ctx.set_matrix_slab(n, r0, A[r0:r1])
+        res = dict(r0=r0, r1=r1, info=ctx.matrix_info(), mpk=ctx.mpk_info())
+        x = ref.matlab_rand(n, seed=5)
+        xl = np.ascontiguousarray(x[r0:r1])
+        y = np.zeros(r1 - r0)
+        check(ctx.h, lib.cal_spmv(ctx.h, ptr(xl), ptr(y)))
+        res["spmv"] = y
+        if kind == "lanczos":
+            v = ref.matlab_rand(n, seed=7)[r0:r1]
+            lam = np.array([7.5, 0.5, 3.0, 11.0, 1.5, 5.0, 9.0, 2.5])[:s]
+            res["Vn"] = cal.matrix_powers_newton(None, v, s, lam, 1, ctx=ctx)
+            res["schedule"] = ctx.mpk_schedule()
+            out = cal.ca_lanczos_ex(A, ref.matlab_rand(n)[r0:r1], s, it, "newton", orth, diagnostics=True, ctx=ctx)
+            res.update(T=out.T, rn=out.ritz_rnorm, oe=out.orth_err, flags=list(out.reorth),
+                       brk=(out.info.get("n_orth_breaks"), out.info.get("n_ritz_locked")))
+            if normalize == "tsqr":
+                res["fold"] = ctx.tsqr_fold_stats()
+        else:  # the implicit restart (config 5's driver)
+            r = ref.matlab_rand(n, seed=2)[r0:r1]
+            res["irl"] = cal.impl_restarted_ca_lanczos(None, r, 48, 8, 8, "newton", "full", 1.0e-8, ctx=ctx)
+        res["stats"] = ctx.comm_stats()
+        ctx.close()
+        out_q.put((rank, res))
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:  # reported, so the parent does not wait out its timeout
+        out_q.put((rank, "error: %r" % (e,)))
+        raise
+
+
+def _run(world, case):
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    procs = [mpc.Process(target=_worker, args=(r, world, port, case, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.exitcode is None:
+                p.kill()
+    errs = [r for r in res if isinstance(r[1], str)]
+    assert not errs, errs
+    for p in procs:
+        assert p.exitcode == 0
+    return [r[1] for r in res]
+
+
+CASES = [
+    # world, (kind, dim, N, s, iters, orth, normalize)
+    # lap3d 40 in 2 slabs of 20 planes: > 2s planes, so the exchange overlaps
+    # the interior powers on the RCCL stream (schedule 2)
+    (2, ("lanczos", 3, 40, 8, 40, "local", "auto")),
+    # 3 slabs of 3-4 planes: the 8-deep ghost zone spans two ranks, clipped
+    # at the domain ends; 'full' orth; TSQR normalize with the all-gathered root
+    (3, ("lanczos", 3, 10, 8, 32, "full", "tsqr")),
+    # 4 slabs of lap2d 64 rows: the fused TSQR fold's rank-uniform vote
+    (4, ("lanczos", 2, 64, 6, 36, "local", "tsqr")),
+    (2, ("irl", 2, 40, 8, 0, "full", "auto")),
+]
+
+
+@pytest.mark.parametrize("world,case", CASES)
+def test_rccl_ranks_match_single(cal, ref, world, case):
+    res = _run(world, case)
+    kind, dim, N, s, it, orth, normalize = case
+    A = cal.matrices.laplacian_2d(N) if dim == 2 else cal.matrices.laplacian_3d(N)
+    n = A.shape[0]
+    normA = 4.0 * dim
+    x = ref.matlab_rand(n, seed=5)
+    y = A @ x
+    for rank, rr in enumerate(res):
+        st = rr["stats"]
+        assert st["nranks"] == world and st["kind"] == 1 and st["rccl_count"] == world, st
+        assert st["allreduce_calls"] > 0 and st["halo_calls"] > 0, st
+        assert rr["mpk"]["depth"] == 8
+        assert np.array_equal(rr["spmv"], y[rr["r0"]:rr["r1"]]), rank
+    if kind == "lanczos":
+        v = ref.matlab_rand(n, seed=7)
+        lam = np.array([7.5, 0.5, 3.0, 11.0, 1.5, 5.0, 9.0, 2.5])[:s]
+        Vn = ref.matrix_powers_newton(A, v, s, lam, 1)
+        ctx1 = cal.Context(0, normalize=normalize).set_matrix(A)
+        single = cal.ca_lanczos_ex(A, ref.matlab_rand(n), s, it, "newton", orth, diagnostics=True, ctx=ctx1)
+        for rank, rr in enumerate(res):
+            print("world %d case %s rank %d: schedule %d, stats %s" % (world, case, rank, rr["schedule"], rr["stats"]))
+            assert np.array_equal(rr["Vn"], Vn[rr["r0"]:rr["r1"]]), rank   # the oracle's bits
+            assert rr["flags"] == list(single.reorth)
+            assert rr["brk"] == (single.info.get("n_orth_breaks"), single.info.get("n_ritz_locked"))
+            assert np.max(np.abs(rr["T"] - single.T)) <= 1e-9 * normA
+            big = single.ritz_rnorm > 1e-10
+            dev = np.abs(rr["rn"][big] / single.ritz_rnorm[big] - 1.0)
+            assert np.all(dev <= 1e-8), dev.max()
+            assert np.array_equal(rr["T"], res[0]["T"])            # every rank holds the same T
+        if world == 2 and dim == 3 and N == 40:
+            assert all(rr["schedule"] == 2 for rr in res), [rr["schedule"] for rr in res]
+        ctx1.close()
+    else:
+        eref = ref.laplacian_2d_eigs(N)[::-1]
+        outs = [rr["irl"] for rr in res]
+        assert all(o["converged"] for o in outs)
+        assert outs[0]["num_restarts"] == outs[1]["num_restarts"]
+        assert np.array_equal(outs[0]["conv_eigs"], outs[1]["conv_eigs"])
+        ev = outs[0]["conv_eigs"]
+        assert np.max(np.min(np.abs(ev[:, None] - eref[None, :]), axis=1)) <= 1e-10 * normA
+        V = np.vstack([o["Q_conv"] for o in outs])
+        assert np.max(np.abs(V.T @ V - np.eye(V.shape[1]))) < 1e-9
