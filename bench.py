@@ -333,6 +333,13 @@ def setup(args, wd=None):
         ctx.comm_init_host(world, rank, allreduce, exchange)
     elif world > 1:
         import torch
+        if os.environ.get("CAL_RCCL_HOSTID_PER_RANK") == "1":
+            # one-GPU rehearsal of the RCCL line: RCCL refuses two ranks on one
+            # device of one host, so each rank states a host of its own and the
+            # ranks connect over sockets (tests/test_gpu_rccl_multirank.py)
+            os.environ["NCCL_HOSTID"] = "cal-rank-%d" % rank
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+            os.environ.setdefault("NCCL_IB_DISABLE", "1")
         uid = bytearray(128)
         if rank == 0:
             buf = ctypes.create_string_buffer(128)
@@ -583,7 +590,9 @@ def main():
     # basis (about 300 outer iterations of lap3d_215 on one GPU) continues in
     # epochs: a new epoch restarts the Krylov space from the same vector, and
     # its Newton prologue is timed when it falls inside the timed region.
-    t_epoch = min(W + K + KT, max(4, int(args.basis_gb * 1e9 / ((r1 - r0) * 8.0 * (s + 1)))))
+    # (+1: the run's last step prefetches no matrix powers, so one step more
+    # keeps the KT window at one powers call per step, as the timed K steps are)
+    t_epoch = min(W + K + KT + 1, max(4, int(args.basis_gb * 1e9 / ((r1 - r0) * 8.0 * (s + 1)))))
     ep = {"left": 0, "flags": []}
 
     def step():

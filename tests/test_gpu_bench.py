@@ -90,6 +90,29 @@ def test_bench_gpus_flag_launches_ranks():
     assert d["tsqr_step"]["reorth_passes"] == d["reorth_passes"].replace("/3", "/3")
 
 
+def test_bench_gpus_flag_rccl_line():
+    """The driver's SCALE command (`bench.py --gpus N`, RCCL) rehearsed on the
+    one-GPU box: CAL_RCCL_HOSTID_PER_RANK=1 gives each rank its own RCCL host
+    id (RCCL refuses two ranks on one device of one host), so the ranks talk
+    over RCCL's socket transport.  One line, the RCCL communicator counted on
+    every rank, all-reduces and the one deep halo exchange per step."""
+    env = dict(os.environ, CAL_RCCL_HOSTID_PER_RANK="1")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup",
+                        "1", "--workload", "lap3d_40"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    print(json.dumps({k: d.get(k) for k in ("value", "ms_per_step", "comm", "config")}))
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["comm"] == "rccl"
+    c = d["comm"]
+    assert c["comm_kind"] == "rccl" and c["rccl_comm_count"] == 2
+    assert c["allreduces_per_step"] >= 2 and abs(c["halo_exchanges_per_step"] - 1.0) < 1e-9
+    assert c["mpk_redundant_rows_per_step"] > 0
+    assert "overlapped" in d["config"]["halo"]
+
+
 def test_bench_rejects_mismatched_world():
     """--gpus N under a launcher with another WORLD_SIZE exits non-zero."""
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")

@@ -1,0 +1,208 @@
+// Probe: P1's Gram ([Qp(0:8) | X]'[Qp(0:8) | X] + Qp column 8 as the extra
+// column; lap3d_215, n = 9,938,375, 17 columns) with the MFMA operands loaded
+// straight from HBM in the MFMA's own layout, no LDS transpose:
+// lane (c16, g) loads 16 B of column c16 at rows base + 8 i + 2 g (i = 0..7),
+// so one wave instruction reads 64 contiguous bytes of each of the 16 columns,
+// and each of the two doubles is the k = g operand of one
+// v_mfma_f64_16x16x4f64 (A = B: a Gram sums over rows in any order).
+// Against the library's row Gram sweep (k_rowapply<17,4,Gram-only>, one lane
+// per row, LDS transpose) and a bare read of the same bytes, back to back.
+//   hipcc -O3 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -Iinclude \
+//         -Ica_lanczos_amd/csrc tools/direct_gram_probe.hip -o tools/direct_gram_probe
+#include "../ca_lanczos_amd/csrc/kernels.hip"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+namespace cal {
+
+template <int WPE, int U, bool NTL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_gram_direct(
+    ColList P, int64_t n, double* __restrict__ partial) {
+    __shared__ double red[3 * 64 * 5];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int c16 = lane & 15, g = lane >> 4;
+    const double* __restrict__ col = P.p[c16];
+    const double* __restrict__ ext = P.p[16];
+    d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+    double eacc = 0.0;
+    const int64_t nfull = n / 64;  // full 64-row chunks
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    int64_t ci = (int64_t)blockIdx.x * 4 + wave;
+    auto ld2 = [&](const double* p) -> d2 {
+        if constexpr (NTL) return __builtin_nontemporal_load(reinterpret_cast<const d2*>(p));
+        else return *reinterpret_cast<const d2*>(p);
+    };
+    for (; ci + (U - 1) * nw < nfull; ci += U * nw) {
+        d2 v[U][8], e[U][8];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t base = (ci + u * nw) * 64 + 2 * g;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[u][i] = ld2(col + base + 8 * i);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) e[u][i] = ld2(ext + base + 8 * i);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                acc = mfma64(v[u][i][0], v[u][i][0], acc);
+                acc = mfma64(v[u][i][1], v[u][i][1], acc);
+                eacc = eacc + e[u][i][0] * v[u][i][0];
+                eacc = eacc + e[u][i][1] * v[u][i][1];
+            }
+    }
+    for (; ci < nfull; ci += nw) {
+        const int64_t base = ci * 64 + 2 * g;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const d2 v = ld2(col + base + 8 * i), e = ld2(ext + base + 8 * i);
+            acc = mfma64(v[0], v[0], acc);
+            acc = mfma64(v[1], v[1], acc);
+            eacc = eacc + e[0] * v[0];
+            eacc = eacc + e[1] * v[1];
+        }
+    }
+    // the ragged tail (< 64 rows): the last wave of the grid, guarded loads
+    if (ci == nfull && nfull * 64 < n) {
+        const int64_t base = nfull * 64 + 2 * g;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int64_t r = base + 8 * i + h;
+                const double v = r < n ? col[r] : 0.0, e = r < n ? ext[r] : 0.0;
+                acc = mfma64(v, v, acc);
+                eacc = eacc + e * v;
+            }
+    }
+    if (wave > 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[((wave - 1) * 64 + lane) * 5 + r] = acc[r];
+        red[((wave - 1) * 64 + lane) * 5 + 4] = eacc;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const int64_t nb = gridDim.x;
+        double* out = partial + blockIdx.x;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            double v = acc[r];
+            v = v + red[(0 * 64 + lane) * 5 + r];
+            v = v + red[(1 * 64 + lane) * 5 + r];
+            v = v + red[(2 * 64 + lane) * 5 + r];
+            out[(int64_t)(c16 * 16 + g + 4 * r) * nb] = v;
+        }
+        double e = eacc;
+        e = e + red[(0 * 64 + lane) * 5 + 4];
+        e = e + red[(1 * 64 + lane) * 5 + 4];
+        e = e + red[(2 * 64 + lane) * 5 + 4];
+        const double e1 = __shfl(e, c16 + 16, 64), e2 = __shfl(e, c16 + 32, 64), e3 = __shfl(e, c16 + 48, 64);
+        if (g == 0) out[(int64_t)(256 + c16) * nb] = ((e + e1) + e2) + e3;
+    }
+}
+
+// a bare read of the same 17 columns (d2 per lane, 64 contiguous B per column per instruction)
+__global__ __launch_bounds__(256) void k_read17(ColList P, int64_t n, double* __restrict__ sink) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int c16 = lane & 15, g = lane >> 4;
+    const double* col = P.p[c16];
+    const double* ext = P.p[16];
+    double s = 0.0;
+    const int64_t nfull = n / 64, nw = (int64_t)gridDim.x * 4;
+    for (int64_t ci = (int64_t)blockIdx.x * 4 + wave; ci < nfull; ci += nw) {
+        const int64_t base = ci * 64 + 2 * g;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const d2 v = *reinterpret_cast<const d2*>(col + base + 8 * i);
+            const d2 e = *reinterpret_cast<const d2*>(ext + base + 8 * i);
+            s += v[0] + v[1] + e[0] + e[1];
+        }
+    }
+    if (s == 12345.678) sink[0] = s;
+}
+
+}  // namespace cal
+
+int main() {
+    using namespace cal;
+    const int64_t n = 9938375, ld = (n + 2 + 63) / 64 * 64;
+    const int w = 9, m = 8;
+    double* buf;
+    CK(hipMalloc(&buf, (size_t)(w + m) * ld * 8));
+    {
+        std::vector<double> h((size_t)ld);
+        for (int c = 0; c < w + m; ++c) {
+            for (int64_t i = 0; i < ld; ++i) h[i] = ((i * 7919 + c * 104729) % 2003) / 1001.0 - 1.0;
+            CK(hipMemcpy(buf + (size_t)c * ld, h.data(), ld * 8, hipMemcpyHostToDevice));
+        }
+    }
+    double* part;
+    CK(hipMalloc(&part, (size_t)(272) * 8192 * 8));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    auto time = [&](auto launch) -> double {
+        for (int i = 0; i < 3; ++i) launch();
+        CK(hipEventRecord(a));
+        const int reps = 20;
+        for (int i = 0; i < reps; ++i) launch();
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms = 0.f;
+        CK(hipEventElapsedTime(&ms, a, b));
+        return ms * 1e3 / reps;
+    };
+    // reduce the entry-major partials on the host (272 entries)
+    auto sums = [&](int nb) {
+        std::vector<double> h((size_t)272 * nb), s(272, 0.0);
+        CK(hipMemcpy(h.data(), part, h.size() * 8, hipMemcpyDeviceToHost));
+        for (int e = 0; e < 272; ++e)
+            for (int p = 0; p < nb; ++p) s[e] += h[(size_t)e * nb + p];
+        return s;
+    };
+    const double gb = 8.0 * n * (w + m) / 1e3;
+    ColList ct{};
+    for (int cc = 0; cc < 16; ++cc) ct.p[cc] = buf + (size_t)(cc < 8 ? cc : cc + 1) * ld;
+    ct.p[16] = buf + (size_t)8 * ld;
+    printf("{\"n\": %lld", (long long)n);
+    double* sink = part;
+    for (int blocks : {1024, 2048, 4096}) {
+        const double us = time([&] { hipLaunchKernelGGL(k_read17, dim3(blocks), dim3(256), 0, 0, ct, n, sink); });
+        printf(", \"read17_b%d_us\": %.1f", blocks, us);
+    }
+    std::vector<double> ref;
+    for (int blocks : {1024, 2048}) {
+        const double us = time([&] { launch_rowgram(ct, 16, true, n, blocks, part, 0); });
+        printf(", \"rowgram_b%d_us\": %.1f, \"rowgram_b%d_GBps\": %.0f", blocks, us, blocks, gb / us);
+        CK(hipDeviceSynchronize());
+        if (ref.empty()) ref = sums(blocks);
+    }
+    auto check = [&](int nb) {
+        CK(hipDeviceSynchronize());
+        std::vector<double> s = sums(nb);
+        double md = 0.0;
+        for (int e = 0; e < 272; ++e) md = std::max(md, std::fabs(s[e] - ref[e]) / std::max(1.0, std::fabs(ref[e])));
+        return md;
+    };
+#define RUN_DIRECT(WPE, U, NTL, NAME)                                                                          \
+    for (int blocks : {1024, 2048, 4096}) {                                                                    \
+        const double us = time([&] {                                                                           \
+            hipLaunchKernelGGL((k_gram_direct<WPE, U, NTL>), dim3(blocks), dim3(256), 0, 0, ct, n, part);       \
+        });                                                                                                    \
+        printf(", \"" NAME "_b%d_us\": %.1f, \"" NAME "_b%d_GBps\": %.0f, \"" NAME "_b%d_relerr\": %.1e", blocks, \
+               us, blocks, gb / us, blocks, check(blocks));                                                    \
+    }
+    RUN_DIRECT(4, 1, false, "direct_w4_u1")
+    RUN_DIRECT(6, 1, false, "direct_w6_u1")
+    RUN_DIRECT(8, 1, false, "direct_w8_u1")
+    RUN_DIRECT(4, 2, false, "direct_w4_u2")
+    RUN_DIRECT(6, 1, true, "direct_w6_u1_nt")
+    printf("}\n");
+    return 0;
+}
