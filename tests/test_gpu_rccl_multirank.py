@@ -85,6 +85,7 @@ def _worker(rank, world, port, case, out_q):
         else:  # the implicit restart (config 5's driver)
             r = ref.matlab_rand(n, seed=2)[r0:r1]
             res["irl"] = cal.impl_restarted_ca_lanczos(None, r, 48, 8, 8, "newton", "full", 1.0e-8, ctx=ctx)
+            res["erl"] = cal.restarted_ca_lanczos(None, r, 48, 4, 8, "newton", "full", 1.0e-8, ctx=ctx)
         res["stats"] = ctx.comm_stats()
         ctx.close()
         out_q.put((rank, res))
@@ -166,11 +167,15 @@ def test_rccl_ranks_match_single(cal, ref, world, case):
         ctx1.close()
     else:
         eref = ref.laplacian_2d_eigs(N)[::-1]
-        outs = [rr["irl"] for rr in res]
-        assert all(o["converged"] for o in outs)
-        assert outs[0]["num_restarts"] == outs[1]["num_restarts"]
-        assert np.array_equal(outs[0]["conv_eigs"], outs[1]["conv_eigs"])
-        ev = outs[0]["conv_eigs"]
-        assert np.max(np.min(np.abs(ev[:, None] - eref[None, :]), axis=1)) <= 1e-10 * normA
-        V = np.vstack([o["Q_conv"] for o in outs])
-        assert np.max(np.abs(V.T @ V - np.eye(V.shape[1]))) < 1e-9
+        for key, nw in (("irl", 8), ("erl", 4)):   # the implicit (f3) and explicit (f2) restarts
+            outs = [rr[key] for rr in res]
+            assert all(o["converged"] for o in outs)
+            assert outs[0]["num_restarts"] == outs[1]["num_restarts"]
+            assert np.array_equal(outs[0]["conv_eigs"], outs[1]["conv_eigs"])
+            ev = outs[0]["conv_eigs"]
+            assert np.max(np.min(np.abs(ev[:, None] - eref[None, :]), axis=1)) <= 1e-10 * normA
+            if key == "erl":
+                assert np.max(np.abs(ev - eref[:nw])) <= 1e-10 * normA
+            V = np.vstack([o["Q_conv"] for o in outs])
+            assert V.shape == (n, nw)
+            assert np.max(np.abs(V.T @ V - np.eye(nw))) < 1e-9
