@@ -276,6 +276,52 @@ def cpu_baseline_irl(wl, s, max_lanczos, nw):
                       % (nb, s, m, wl.name, dt)}
 
 
+def rank_comm(cal, ctx, args, world, rank, dist):
+    """The rank's communicator on ctx: the host-staged gloo callbacks
+    (--comm host) or RCCL, whose unique id rank 0 broadcasts over the gloo
+    group (every context of a rank gets a communicator of its own)."""
+    import torch
+    if args.comm == "host":
+        def allreduce(a):
+            t = torch.from_numpy(a)
+            dist.all_reduce(t)
+
+        hang = os.environ.get("CAL_BENCH_TEST_HANG_RANK")
+
+        def exchange(peer, send, recv):
+            if hang is not None and int(hang) == rank:  # tests: a rank whose exchange never returns
+                while True:
+                    time.sleep(3600)
+            reqs = []
+            if send.size:
+                reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(send)), peer))
+            rt = torch.zeros(recv.size, dtype=torch.float64)
+            if recv.size:
+                reqs.append(dist.irecv(rt, peer))
+            for q in reqs:
+                q.wait()
+            if recv.size:
+                recv[:] = rt.numpy()
+
+        ctx.comm_init_host(world, rank, allreduce, exchange)
+        return
+    if os.environ.get("CAL_RCCL_HOSTID_PER_RANK") == "1":
+        # one-GPU rehearsal of the RCCL line: RCCL refuses two ranks on one
+        # device of one host, so each rank states a host of its own and the
+        # ranks connect over sockets (tests/test_gpu_rccl_multirank.py)
+        os.environ["NCCL_HOSTID"] = "cal-rank-%d" % rank
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
+    uid = bytearray(128)
+    if rank == 0:
+        buf = ctypes.create_string_buffer(128)
+        cal._lib.check(None, cal._lib.lib.cal_comm_unique_id(buf))
+        uid = bytearray(buf.raw)
+    t = torch.tensor(list(uid), dtype=torch.uint8)
+    dist.broadcast(t, 0)
+    ctx.comm_init_rccl(world, rank, bytes(t.tolist()))
+
+
 def setup(args, wd=None):
     """Ranks, context, communicator and the resident matrix slab (each stage
     under the watchdog wd of a multi-rank run)."""
@@ -306,48 +352,8 @@ def setup(args, wd=None):
     r0, r1 = bounds[rank], bounds[rank + 1]
     rowptr, col, val = wl.rows(r0, r1)
     nnz_local = int(rowptr[-1])
-    if world > 1 and args.comm == "host":
-        import torch
-
-        def allreduce(a):
-            t = torch.from_numpy(a)
-            dist.all_reduce(t)
-
-        hang = os.environ.get("CAL_BENCH_TEST_HANG_RANK")
-
-        def exchange(peer, send, recv):
-            if hang is not None and int(hang) == rank:  # tests: a rank whose exchange never returns
-                while True:
-                    time.sleep(3600)
-            reqs = []
-            if send.size:
-                reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(send)), peer))
-            rt = torch.zeros(recv.size, dtype=torch.float64)
-            if recv.size:
-                reqs.append(dist.irecv(rt, peer))
-            for q in reqs:
-                q.wait()
-            if recv.size:
-                recv[:] = rt.numpy()
-
-        ctx.comm_init_host(world, rank, allreduce, exchange)
-    elif world > 1:
-        import torch
-        if os.environ.get("CAL_RCCL_HOSTID_PER_RANK") == "1":
-            # one-GPU rehearsal of the RCCL line: RCCL refuses two ranks on one
-            # device of one host, so each rank states a host of its own and the
-            # ranks connect over sockets (tests/test_gpu_rccl_multirank.py)
-            os.environ["NCCL_HOSTID"] = "cal-rank-%d" % rank
-            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
-            os.environ.setdefault("NCCL_IB_DISABLE", "1")
-        uid = bytearray(128)
-        if rank == 0:
-            buf = ctypes.create_string_buffer(128)
-            cal._lib.check(None, cal._lib.lib.cal_comm_unique_id(buf))
-            uid = bytearray(buf.raw)
-        t = torch.tensor(list(uid), dtype=torch.uint8)
-        dist.broadcast(t, 0)
-        ctx.comm_init_rccl(world, rank, bytes(t.tolist()))
+    if world > 1:
+        rank_comm(cal, ctx, args, world, rank, dist)
     import scipy.sparse as sp
     if world > 1:
         stage("matrix_setup")
@@ -508,6 +514,11 @@ class Watchdog:
                 msg = "bench.py rank %d/%d: stage '%s' exceeded %.0f s (%.1f s)" % (self.rank, self.world, stage,
                                                                                  limit, el)
                 sys.stderr.write(msg + "\n")
+                try:  # where every thread of the rank stands
+                    import faulthandler
+                    faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+                except Exception:  # pragma: no cover
+                    pass
                 sys.stderr.flush()
                 if self.rank == 0:
                     try:
@@ -681,6 +692,13 @@ def main():
             except cal.CalError:
                 pass
         ctx.set_normalize(args.normalize)
+    if world > 1 and not args.no_legs and args.comm == "rccl" and args.orth == "local":
+        # BASELINE config 5 names 8 GPUs: the implicit restart on every rank's
+        # row slab of the G3_circuit stand-in (compact halo, RCCL)
+        try:
+            irl_leg = irl_workload_leg(cal, ctx.device, "circuit_1259", s, args.basis, dist=dist, args=args)
+        except cal.CalError as e:
+            irl_leg = {"error": str(e)}
     if world == 1 and not args.no_legs and args.orth == "local":
         # ca_lanczos.m:191-197 'full': the new block projected against all of Q
         # (one wide Gram and one wide apply sweep per step, f1)
@@ -988,25 +1006,42 @@ def workload_leg(cal, local, name, s, K, W, basis):
     return leg
 
 
-def irl_workload_leg(cal, local, name, s, basis, ml=64, nw=8, tol=1.0e-8):
+def irl_workload_leg(cal, local, name, s, basis, ml=64, nw=8, tol=1.0e-8, dist=None, args=None):
     """BASELINE config 5's driver as a leg of the default line: whole
     impl_restarted_ca_lanczos solves on the resident G3_circuit stand-in
-    (CSR SpMV), solves/s and the SpMV's roofline inside the solve."""
+    (CSR SpMV), solves/s and the SpMV's roofline inside the solve.  With
+    dist (a multi-rank line: config 5 names 8 GPUs) every rank holds a row
+    slab of the matrix on a context with a communicator of its own; the
+    solve time is the max over ranks, the SpMV figures are rank 0's."""
     wl2 = Workload(name)
+    world = dist.get_world_size() if dist is not None else 1
+    rank = dist.get_rank() if dist is not None else 0
     c = cal.Context(device=local)
     try:
-        c.set_matrix(wl2.full())
         r = np.random.RandomState(5489).random_sample(wl2.n)
-        M = irl_measure(cal, c, r, ml, nw, s, basis, tol, 3, 1, None)
+        if world > 1:
+            from ca_lanczos_amd.matrices import slab_bounds
+            import scipy.sparse as sp
+            rank_comm(cal, c, args, world, rank, dist)
+            b = slab_bounds(wl2.n, world, wl2.plane)
+            r0, r1 = b[rank], b[rank + 1]
+            rowptr, col, val = wl2.rows(r0, r1)
+            c.set_matrix_slab(wl2.n, r0, sp.csr_matrix((val, col, rowptr), shape=(r1 - r0, wl2.n)))
+            r = r[r0:r1]
+        else:
+            r0, r1 = 0, wl2.n
+            c.set_matrix(wl2.full())
+        M = irl_measure(cal, c, r, ml, nw, s, basis, tol, 3, 1, dist)
         fmt = c.spmv_format()[0]
         nnz = c.matrix_info()["nnz_local"]
     finally:
         c.close()
-    b_spmv = (12 * nnz + 20 * wl2.n + 4) if fmt == "csr" else 18 * wl2.n
+    n_loc = r1 - r0
+    b_spmv = (12 * nnz + 20 * n_loc + 4) if fmt == "csr" else 18 * n_loc
     ach = b_spmv / (M["spmv_avg_ms"] * 1e-3) / 1e9
     t = M["timers"]
     return {"solves_per_s": M["K"] / M["elapsed"], "ms_per_solve": 1e3 * M["elapsed"] / M["K"], "solves": M["K"],
-            "workload": wl2.desc % (wl2.n, nnz), "driver": "impl_restarted_ca_lanczos",
+            "n_ranks": world, "workload": wl2.desc % (wl2.n, wl2.full().nnz), "driver": "impl_restarted_ca_lanczos",
             "max_lanczos": ml, "n_wanted_eigs": nw, "m": M["m"], "s": s, "orth": "full", "tol": tol,
             "num_restarts": M["out"]["num_restarts"], "converged": M["out"]["converged"],
             "blocks_per_s": M["blocks"] / M["elapsed"], "spmv_format": fmt,

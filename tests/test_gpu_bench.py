@@ -111,6 +111,10 @@ def test_bench_gpus_flag_rccl_line():
     assert c["allreduces_per_step"] >= 2 and abs(c["halo_exchanges_per_step"] - 1.0) < 1e-9
     assert c["mpk_redundant_rows_per_step"] > 0
     assert "overlapped" in d["config"]["halo"]
+    # BASELINE config 5 on the ranks' slabs of the G3_circuit stand-in
+    irl = d["irl"]
+    assert "error" not in irl, irl
+    assert irl["n_ranks"] == 2 and irl["converged"] and irl["solves_per_s"] > 0
 
 
 def test_bench_rejects_mismatched_world():

@@ -35,11 +35,19 @@ def _rccl_env(rank):
                       NCCL_DEBUG=os.environ.get("NCCL_DEBUG", "WARN"))
 
 
+def _matrix(cal, dim, N):
+    if dim == 0:
+        return cal.matrices.circuit_like(N)
+    return cal.matrices.laplacian_2d(N) if dim == 2 else cal.matrices.laplacian_3d(N)
+
+
 def _worker(rank, world, port, case, out_q):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     _rccl_env(rank)
+    import faulthandler
+    faulthandler.dump_traceback_later(150, exit=True)  # a hung rank names its call
     try:
         import torch
         import torch.distributed as dist
@@ -59,11 +67,12 @@ def _worker(rank, world, port, case, out_q):
         uid = bytes(t.tolist())
 
         kind, dim, N, s, it, orth, normalize = case
-        A = cal.matrices.laplacian_2d(N) if dim == 2 else cal.matrices.laplacian_3d(N)
+        A = _matrix(cal, dim, N)
         n = A.shape[0]
-        b = cal.matrices.slab_bounds(n, world, N ** (dim - 1))
+        b = cal.matrices.slab_bounds(n, world, N ** (dim - 1) if dim else 1)
         r0, r1 = b[rank], b[rank + 1]
-        ctx = cal.Context(0, mpk_depth=8, normalize=normalize)
+        # config 5's topology (dim 0): the irregular stand-in in CSR, compact ghosts
+        ctx = cal.Context(0, mpk_depth=8, normalize=normalize, spmv_format="csr" if dim == 0 else None)
         ctx.comm_init_rccl(world, rank, uid)
         ctx.set_matrix_slab(n, r0, A[r0:r1])
         res = dict(r0=r0, r1=r1, info=ctx.matrix_info(), mpk=ctx.mpk_info())
@@ -82,6 +91,9 @@ def _worker(rank, world, port, case, out_q):
                        brk=(out.info.get("n_orth_breaks"), out.info.get("n_ritz_locked")))
             if normalize == "tsqr":
                 res["fold"] = ctx.tsqr_fold_stats()
+        elif kind == "circuit":  # config 5's driver on the irregular matrix
+            r = ref.matlab_rand(n, seed=2)[r0:r1]
+            res["irl"] = cal.impl_restarted_ca_lanczos(None, r, 64, 8, 8, "newton", "full", 1.0e-8, ctx=ctx)
         else:  # the implicit restart (config 5's driver)
             r = ref.matlab_rand(n, seed=2)[r0:r1]
             res["irl"] = cal.impl_restarted_ca_lanczos(None, r, 48, 8, 8, "newton", "full", 1.0e-8, ctx=ctx)
@@ -128,6 +140,10 @@ CASES = [
     # 4 slabs of lap2d 64 rows: the fused TSQR fold's rank-uniform vote
     (4, ("lanczos", 2, 64, 6, 36, "local", "tsqr")),
     (2, ("irl", 2, 40, 8, 0, "full", "auto")),
+    # config 5's topology: circuit_like(200) in CSR, ghost columns scattered
+    # over the peer's rows (compact layout, gather kernel, one exchange per SpMV)
+    (2, ("circuit", 0, 200, 8, 0, "full", "auto")),
+    (3, ("circuit", 0, 200, 8, 0, "full", "auto")),
 ]
 
 
@@ -135,16 +151,16 @@ CASES = [
 def test_rccl_ranks_match_single(cal, ref, world, case):
     res = _run(world, case)
     kind, dim, N, s, it, orth, normalize = case
-    A = cal.matrices.laplacian_2d(N) if dim == 2 else cal.matrices.laplacian_3d(N)
+    A = _matrix(cal, dim, N)
     n = A.shape[0]
-    normA = 4.0 * dim
+    normA = 4.0 * dim if dim else float(abs(A).sum(axis=1).max())
     x = ref.matlab_rand(n, seed=5)
     y = A @ x
     for rank, rr in enumerate(res):
         st = rr["stats"]
         assert st["nranks"] == world and st["kind"] == 1 and st["rccl_count"] == world, st
         assert st["allreduce_calls"] > 0 and st["halo_calls"] > 0, st
-        assert rr["mpk"]["depth"] == 8
+        assert rr["mpk"]["depth"] == (8 if dim else 1)   # compact ghosts: one exchange per SpMV
         assert np.array_equal(rr["spmv"], y[rr["r0"]:rr["r1"]]), rank
     if kind == "lanczos":
         v = ref.matlab_rand(n, seed=7)
@@ -165,6 +181,22 @@ def test_rccl_ranks_match_single(cal, ref, world, case):
         if world == 2 and dim == 3 and N == 40:
             assert all(rr["schedule"] == 2 for rr in res), [rr["schedule"] for rr in res]
         ctx1.close()
+    elif kind == "circuit":
+        c1 = cal.Context(0, spmv_format="csr").set_matrix(A)
+        irl1 = cal.impl_restarted_ca_lanczos(A, ref.matlab_rand(n, seed=2), 64, 8, 8, "newton", "full", 1.0e-8,
+                                             ctx=c1)
+        c1.close()
+        outs = [rr["irl"] for rr in res]
+        print("circuit_%d x%d over RCCL: restarts %s (single %d)" % (N, world, [o["num_restarts"] for o in outs],
+                                                                     irl1["num_restarts"]))
+        assert irl1["converged"] and all(o["converged"] for o in outs)
+        assert all(o["num_restarts"] == outs[0]["num_restarts"] for o in outs)
+        assert abs(outs[0]["num_restarts"] - irl1["num_restarts"]) <= 1
+        assert all(np.array_equal(o["conv_eigs"], outs[0]["conv_eigs"]) for o in outs)
+        ev = outs[0]["conv_eigs"]
+        assert np.max(np.abs(ev - irl1["conv_eigs"]) / np.abs(irl1["conv_eigs"])) <= 1e-10
+        V = np.vstack([o["Q_conv"] for o in outs])
+        assert np.max(np.abs(V.T @ V - np.eye(V.shape[1]))) < 1e-9
     else:
         eref = ref.laplacian_2d_eigs(N)[::-1]
         for key, nw in (("irl", 8), ("erl", 4)):   # the implicit (f3) and explicit (f2) restarts
