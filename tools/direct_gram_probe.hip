@@ -198,11 +198,33 @@ int main() {
         printf(", \"" NAME "_b%d_us\": %.1f, \"" NAME "_b%d_GBps\": %.0f, \"" NAME "_b%d_relerr\": %.1e", blocks, \
                us, blocks, gb / us, blocks, check(blocks));                                                    \
     }
+    // the library's pass A (Gram of [Qp(0:8) | Q1], Q1 = [Qp | X] M1 in registers, nothing stored)
+    // and pass B (chained apply, 8 columns stored non-temporally), back to back
+    {
+        std::vector<double> hm((size_t)17 * 8 * 2 + 64);
+        for (size_t i = 0; i < hm.size(); ++i) hm[i] = 0.01 * (double)((i * 37) % 11) - 0.05;
+        double* dM;
+        CK(hipMalloc(&dM, hm.size() * 8));
+        CK(hipMemcpy(dM, hm.data(), hm.size() * 8, hipMemcpyHostToDevice));
+        double* out;
+        CK(hipMalloc(&out, (size_t)8 * ld * 8));
+        ColList cp{};
+        for (int c = 0; c < 17; ++c) cp.p[c] = buf + (size_t)c * ld;
+        OutList ol{};
+        for (int j = 0; j < 16; ++j) ol.p[j] = out + (size_t)(j < 8 ? j : 7) * ld;
+        for (int blocks : {768, 1024}) {
+            const double us = time([&] { launch_rowapply(cp, dM, 17, 8, ol, 2, 9, n, blocks, part, 0); });
+            printf(", \"passA_b%d_us\": %.1f, \"passA_b%d_GBps\": %.0f", blocks, us, blocks, gb / us);
+        }
+        const int bb = (int)((n + 255) / 256);
+        const double usb = time([&] { launch_rowapply(cp, dM, 17, 8, ol, 3, 9, n, bb, part, 0); });
+        printf(", \"passB_us\": %.1f, \"passB_GBps\": %.0f", usb, (gb + 8.0 * n * 8 / 1e3) / usb);
+        // P1 again after the others (same box, same state)
+        const double up1 = time([&] { launch_rowgram(ct, 16, true, n, 1024, part, 0); });
+        printf(", \"rowgram_again_b1024_us\": %.1f", up1);
+    }
     RUN_DIRECT(4, 1, false, "direct_w4_u1")
-    RUN_DIRECT(6, 1, false, "direct_w6_u1")
     RUN_DIRECT(8, 1, false, "direct_w8_u1")
-    RUN_DIRECT(4, 2, false, "direct_w4_u2")
-    RUN_DIRECT(6, 1, true, "direct_w6_u1_nt")
     printf("}\n");
     return 0;
 }
