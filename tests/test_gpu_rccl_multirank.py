@@ -139,6 +139,10 @@ CASES = [
     (3, ("lanczos", 3, 10, 8, 32, "full", "tsqr")),
     # 4 slabs of lap2d 64 rows: the fused TSQR fold's rank-uniform vote
     (4, ("lanczos", 2, 64, 6, 36, "local", "tsqr")),
+    # 'periodic' (omega recurrence, normest over the all-reduced dots) and
+    # 'selective' (locked Ritz vectors in the projection)
+    (2, ("lanczos", 2, 24, 8, 64, "periodic", "auto")),
+    (2, ("lanczos", 2, 24, 8, 64, "selective", "auto")),
     (2, ("irl", 2, 40, 8, 0, "full", "auto")),
     # config 5's topology: circuit_like(200) in CSR, ghost columns scattered
     # over the peer's rows (compact layout, gather kernel, one exchange per SpMV)
