@@ -62,3 +62,46 @@ def test_watchdog_stage_limits_cover_every_stage():
     for st in ("init_process_group", "comm_init", "matrix_setup", "lanczos_begin", "first_outer_step", "warmup",
                "timed", "legs", "finalize"):
         assert 0 < bench.stage_limit(st) < 600
+
+
+_CHILD_LEGS = r"""
+import os, sys, time, json
+sys.path.insert(0, %(root)r)
+import bench
+import torch, torch.distributed as dist
+rank, world = int(sys.argv[1]), 2
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=sys.argv[2])
+bench._quiet_stdout()
+wd = bench.Watchdog(rank, world, poll=0.1)
+wd.enter("init_process_group", 60)
+dist.init_process_group("gloo", rank=rank, world_size=world)
+wd.enter("timed", 60)
+t = torch.ones(1)
+dist.all_reduce(t)            # the headline's max over ranks
+wd.fallback = {"metric": "m", "value": 123.0, "n_gpus": world}
+wd.enter("legs", 2.0)
+if rank == 1:
+    time.sleep(3600)          # a secondary leg that never returns
+dist.all_reduce(t)            # rank 0 blocks in the leg's collective
+print("unreachable")
+"""
+
+
+def test_watchdog_keeps_the_headline_when_a_leg_hangs(tmp_path):
+    """A secondary leg that hangs after the headline was measured (e.g. a
+    multi-rank leg over a slow transport) ends the ranks with exit code 0 and
+    rank 0's one line carries the measured value plus "legs_error"."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = str(s.getsockname()[1])
+    s.close()
+    src = tmp_path / "child_legs.py"
+    src.write_text(_CHILD_LEGS % {"root": ROOT})
+    procs = [subprocess.Popen([sys.executable, str(src), str(r), port], stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = [p.communicate(timeout=120) for p in procs]
+    assert [p.returncode for p in procs] == [0, 0], [o[1][-800:] for o in outs]
+    lines = [ln for ln in outs[0][0].splitlines() if ln.strip()]
+    assert len(lines) == 1 and outs[1][0].strip() == ""
+    d = json.loads(lines[0])
+    assert d["value"] == 123.0 and "stage 'legs' exceeded" in d["legs_error"]
