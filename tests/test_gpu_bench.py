@@ -112,9 +112,13 @@ def test_bench_gpus_flag_rccl_line():
     assert c["mpk_redundant_rows_per_step"] > 0
     assert "overlapped" in d["config"]["halo"]
     # BASELINE config 5 on the ranks' slabs of the G3_circuit stand-in
+    # (skipped only when this box's socket all-reduces exceed IRL_MAX_ALLREDUCE_US; ~0.1 ms measured)
     irl = d["irl"]
     assert "error" not in irl, irl
-    assert irl["n_ranks"] == 2 and irl["converged"] and irl["solves_per_s"] > 0
+    if "skipped" not in irl:
+        assert irl["n_ranks"] == 2 and irl["converged"] and irl["solves_per_s"] > 0
+    else:
+        assert c["allreduce_us_per_step"] / c["allreduces_per_step"] > 1000.0, irl
 
 
 def test_bench_rejects_mismatched_world():
