@@ -3187,6 +3187,18 @@ static unsigned vec_blocks(int64_t n) {
     return (unsigned)b;
 }
 
+// Vector kernels whose every block first sums the previous dot's partials
+// (k_nrm_div, k_pro_div: up to 2 x 1024 doubles per block): at most 1024
+// blocks, so the partials are read 1024 times, not 4096.  The per-block sum
+// and the elementwise update are unchanged: the same bits.
+#ifndef CAL_REDVEC_BLOCKS
+#define CAL_REDVEC_BLOCKS 1024
+#endif
+static unsigned redvec_blocks(int64_t n) {
+    const unsigned b = vec_blocks(n);
+    return b > CAL_REDVEC_BLOCKS ? CAL_REDVEC_BLOCKS : b;
+}
+
 hipError_t launch_axpy_sub(double* y, const double* x, double a, int64_t n, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_axpy_sub, dim3(vec_blocks(n)), dim3(256), 0, st, y, x, a, n);
@@ -3739,7 +3751,7 @@ hipError_t launch_normest_norms(double* x, const double* y, int64_t n, double* p
     if (n <= 0) return hipErrorInvalidValue;
     const int nb = dot_blocks(n);
     hipLaunchKernelGGL(k_norms2, dim3(nb), dim3(256), 0, st, x, y, n, part, part + nb);
-    hipLaunchKernelGGL(k_nrm_div, dim3(vec_blocks(n)), dim3(256), 0, st, x, part, part + nb, nb, dst, n);
+    hipLaunchKernelGGL(k_nrm_div, dim3(redvec_blocks(n)), dim3(256), 0, st, x, part, part + nb, nb, dst, n);
     return hipGetLastError();
 }
 
@@ -3751,7 +3763,7 @@ hipError_t launch_pro_step(double* r, const double* qprev, const double* pb_prev
     double* pb = part + nb;  // beta^2 partials
     hipLaunchKernelGGL(k_pro_dot, dim3(nb), dim3(256), 0, st, r, qprev, pb_prev, q, n, pa);
     hipLaunchKernelGGL(k_pro_update, dim3(nb), dim3(256), 0, st, r, q, pa, nb, d_alpha, n, pb);
-    hipLaunchKernelGGL(k_pro_div, dim3(vec_blocks(n)), dim3(256), 0, st, qnext, r, pb, nb, d_beta2, n);
+    hipLaunchKernelGGL(k_pro_div, dim3(redvec_blocks(n)), dim3(256), 0, st, qnext, r, pb, nb, d_beta2, n);
     return hipGetLastError();
 }
 
