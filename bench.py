@@ -933,7 +933,9 @@ def timed_leg(ctx, r, s, K, W, basis, orth, dist):
     timed outer iterations (barrier + synchronize on both sides, max over
     ranks), then one more with the per-kernel HIP-event timers."""
     KT = 3
-    ctx.lanczos_begin(r, s, W + K + KT, basis, orth)
+    # (+1: the run's last step prefetches no matrix powers; one step more keeps
+    # the timed window at one powers call per step)
+    ctx.lanczos_begin(r, s, W + K + KT + 1, basis, orth)
     for _ in range(W):
         ctx.lanczos_step(False)
     ctx.synchronize()
