@@ -1756,7 +1756,8 @@ __global__ __launch_bounds__(256) void k_gram_lds(Panel A, Panel B, int64_t n, d
 #define CAL_GRAM_ROWS_MAXNTA 4
 #endif
 template <int NTA, int RUN, bool BB>
-__global__ __launch_bounds__(256) void k_gram_rows(Panel A, Panel B, int64_t n, double* __restrict__ partial) {
+__global__ __launch_bounds__(256) void k_gram_rows(Panel A, Panel B, int64_t n, double* __restrict__ partial,
+                                                   int ldc_out, int a_off) {
     constexpr int R = 16 * RUN;         // rows per round
     constexpr int NC = 16 * (NTA + 1);  // staged columns: B's 16, then A's
     constexpr int LD = NC + 1;
@@ -1833,7 +1834,7 @@ __global__ __launch_bounds__(256) void k_gram_rows(Panel A, Panel B, int64_t n, 
     }
     __syncthreads();
     if (wave == 0) {
-        const int ldc = 16 * NTA;
+        const int ldc = ldc_out;  // 16 NTA, or the whole Gram's when A is one column range of it
         double* out = partial + blockIdx.x;
         const int64_t nb = gridDim.x;
 #pragma unroll
@@ -1845,19 +1846,60 @@ __global__ __launch_bounds__(256) void k_gram_rows(Panel A, Panel B, int64_t n, 
                 x = x + red[1][t][lane][r];
                 x = x + red[2][t][lane][r];
                 const int i = g + 4 * r, j = c16;
-                // A'B entry (16t + i, j) at j ldc + 16t + i; B'B (i, j) after
-                // them at 16 ldc + j 16 + i
-                const int e = t < NTA ? j * ldc + 16 * t + i : 16 * ldc + j * 16 + i;
+                // A'B entry (a_off + 16t + i, j) at j ldc + a_off + 16t + i;
+                // B'B (i, j) after them at 16 ldc + j 16 + i
+                const int e = t < NTA ? j * ldc + a_off + 16 * t + i : 16 * ldc + j * 16 + i;
                 out[(int64_t)e * nb] = x;
             }
     }
 }
 
 template <int NTA, bool BB = false>
-static void launch_gram_rows(const Panel& A, const Panel& B, int64_t n, int blocks, double* partial, hipStream_t st) {
+static void launch_gram_rows(const Panel& A, const Panel& B, int64_t n, int blocks, double* partial, hipStream_t st,
+                             int ldc_out = 16 * NTA, int a_off = 0) {
     constexpr int RUN = CAL_GRAM_ROWS_RUN, R = 16 * RUN, LD = 16 * (NTA + 1) + 1;
     const size_t lds = std::max((size_t)2 * R * LD, (size_t)3 * (NTA + 1) * 64 * 4) * sizeof(double);
-    hipLaunchKernelGGL((k_gram_rows<NTA, RUN, BB>), dim3(blocks), dim3(256), lds, st, A, B, n, partial);
+    hipLaunchKernelGGL((k_gram_rows<NTA, RUN, BB>), dim3(blocks), dim3(256), lds, st, A, B, n, partial, ldc_out,
+                       a_off);
+}
+
+// Columns c0 .. c0 + nc - 1 of a panel (host side)
+static Panel gram_panel_slice(const Panel& P, int c0, int nc) {
+    Panel out = panel();
+    int base = 0;
+    for (int q = 0; q < P.nseg; ++q) {
+        const int lo = std::max(c0, base), hi = std::min(c0 + nc, base + P.ncol[q]);
+        if (hi > lo) panel_add(out, P.ptr[q] + (int64_t)(lo - base) * P.ld[q], P.ld[q], hi - lo);
+        base += P.ncol[q];
+    }
+    return out;
+}
+
+// A'B for 65 .. 128 A columns on the row-staged kernel: A's first 64 columns
+// and the rest in two launches writing their column ranges of one partial
+// layout (ldc = 16 nta, the layout of k_gram_lds), reduced as one Gram.  B
+// is read twice (<= 16 of 80 .. 144 columns).  Used when CAL_GRAM_ROWS_SPLIT.
+#ifndef CAL_GRAM_ROWS_SPLIT
+#define CAL_GRAM_ROWS_SPLIT 1
+#endif
+static hipError_t launch_gram_rows_split(const Panel& A, const Panel& B, int64_t n, const GramPlan& pl,
+                                         double* partial, hipStream_t st) {
+    constexpr int W0 = 16 * CAL_GRAM_ROWS_MAXNTA;
+    const int ldc = 16 * pl.nta, nta2 = pl.nta - CAL_GRAM_ROWS_MAXNTA;
+    const Panel A0 = gram_panel_slice(A, 0, W0), A1 = gram_panel_slice(A, W0, A.total - W0);
+    launch_gram_rows<CAL_GRAM_ROWS_MAXNTA>(A0, B, n, pl.blocks, partial, st, ldc, 0);
+    switch (nta2) {
+        case 1: launch_gram_rows<1>(A1, B, n, pl.blocks, partial, st, ldc, W0); break;
+        case 2: launch_gram_rows<2>(A1, B, n, pl.blocks, partial, st, ldc, W0); break;
+#if CAL_GRAM_ROWS_MAXNTA >= 3
+        case 3: launch_gram_rows<3>(A1, B, n, pl.blocks, partial, st, ldc, W0); break;
+#endif
+#if CAL_GRAM_ROWS_MAXNTA >= 4
+        case 4: launch_gram_rows<4>(A1, B, n, pl.blocks, partial, st, ldc, W0); break;
+#endif
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 bool gram_bb_ok(int wa, int wb) { return CAL_GRAM_ROWS && wb <= 16 && wa >= 1 && (wa + 15) / 16 <= CAL_GRAM_ROWS_MAXNTA; }
@@ -1880,11 +1922,11 @@ hipError_t launch_gram_bb(const Panel& A, const Panel& B, int64_t n, const GramP
 }
 
 GramPlan gram_plan(int wa, int wb, int64_t n) {
-    (void)wb;
     GramPlan p;
     p.nta = (wa + 15) / 16;
     if (p.nta < 1) p.nta = 1;
-    const bool rows = CAL_GRAM_ROWS && p.nta <= CAL_GRAM_ROWS_MAXNTA;
+    const bool rows = CAL_GRAM_ROWS && (p.nta <= CAL_GRAM_ROWS_MAXNTA ||
+                                        (CAL_GRAM_ROWS_SPLIT && wb <= 16 && p.nta <= 2 * CAL_GRAM_ROWS_MAXNTA));
     const int run = rows ? CAL_GRAM_ROWS_RUN : (p.nta <= 2 ? 16 : (p.nta <= 4 ? 8 : 4));
     int64_t blocks = (n + 16 * run - 1) / (16 * run);
     if (rows && blocks > CAL_GRAM_ROWS_BLOCKS) blocks = CAL_GRAM_ROWS_BLOCKS;
@@ -2069,6 +2111,8 @@ hipError_t launch_gram(const Panel& A, const Panel& B, int64_t n, const GramPlan
         }
         return hipGetLastError();
     }
+    if (CAL_GRAM_ROWS && CAL_GRAM_ROWS_SPLIT && B.total <= 16 && pl.nta <= 2 * CAL_GRAM_ROWS_MAXNTA)
+        return launch_gram_rows_split(A, B, n, pl, partial, st);
     if (pl.nta >= 3) {
         switch (pl.nta) {
             case 3: launch_gram_lds<3, 8>(A, B, n, pl.blocks, partial, st); break;

@@ -95,7 +95,7 @@ int main() {
                 auto go = [&](auto NTA_, auto RUN_) {
                     constexpr int NTA = decltype(NTA_)::value, RUN = decltype(RUN_)::value;
                     const size_t lds = std::max((size_t)2 * 16 * RUN * (16 * (NTA + 1) + 1), (size_t)3 * NTA * 64 * 4) * 8;
-                    hipLaunchKernelGGL((k_gram_rows<NTA, RUN, false>), dim3(blocks), dim3(256), lds, 0, A, B, n, p1);
+                    hipLaunchKernelGGL((k_gram_rows<NTA, RUN, false>), dim3(blocks), dim3(256), lds, 0, A, B, n, p1, 16 * NTA, 0);
                 };
                 using I1 = std::integral_constant<int, 1>;
                 using I2 = std::integral_constant<int, 2>;

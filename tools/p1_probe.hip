@@ -59,7 +59,7 @@ int main() {
     for (int blocks : {512, 1024, 2048}) {
         const double us = time([&] {
             const size_t lds = std::max((size_t)2 * 64 * 33, (size_t)3 * 2 * 64 * 4) * 8;
-            hipLaunchKernelGGL((k_gram_rows<1, 4, true>), dim3(blocks), dim3(256), lds, 0, A, B, n, part);
+            hipLaunchKernelGGL((k_gram_rows<1, 4, true>), dim3(blocks), dim3(256), lds, 0, A, B, n, part, 16, 0);
         });
         printf(", \"gram_rows_bb_b%d_us\": %.1f, \"gram_rows_bb_b%d_GBps\": %.0f", blocks, us, blocks, gb / us);
     }
