@@ -394,9 +394,9 @@ def launch_boundaries(leg):
     kernels' sum exceed the step (with default events, which fence the
     caches at record, the SpMV averaged 11.4 us timed against 7.1 us back to
     back); the library's timing events now skip that fence (5.9 vs 5.5 us,
-    kernel share 0.88 against rocprof's 0.87-0.89 busy share), and the share
-    is withheld only if the timed SpMV still exceeds 1.3x its back-to-back
-    time.  The busy share comes from a rocprofv3 kernel trace of the timed
+    kernel share 0.88 against rocprof's 0.87-0.89 busy share, on one box;
+    7.7-12.8 us on others), and the share is withheld whenever the timed SpMV
+    exceeds 1.3x its back-to-back time.  The busy share comes from a rocprofv3 kernel trace of the timed
     steps and the HIP-graph A/B of the matrix powers
     (profiles/r05/graph_powers/summary.json, tools/gpu_r05_lap2d.sh,
     tools/gpu_r05_graph.sh)."""
