@@ -1882,22 +1882,27 @@ static Panel gram_panel_slice(const Panel& P, int c0, int nc) {
 #ifndef CAL_GRAM_ROWS_SPLIT
 #define CAL_GRAM_ROWS_SPLIT 1
 #endif
+#ifndef CAL_GRAM_SPLIT_NTA
+#define CAL_GRAM_SPLIT_NTA CAL_GRAM_ROWS_MAXNTA  // A columns per launch / 16
+#endif
 static hipError_t launch_gram_rows_split(const Panel& A, const Panel& B, int64_t n, const GramPlan& pl,
                                          double* partial, hipStream_t st) {
-    constexpr int W0 = 16 * CAL_GRAM_ROWS_MAXNTA;
-    const int ldc = 16 * pl.nta, nta2 = pl.nta - CAL_GRAM_ROWS_MAXNTA;
-    const Panel A0 = gram_panel_slice(A, 0, W0), A1 = gram_panel_slice(A, W0, A.total - W0);
-    launch_gram_rows<CAL_GRAM_ROWS_MAXNTA>(A0, B, n, pl.blocks, partial, st, ldc, 0);
-    switch (nta2) {
-        case 1: launch_gram_rows<1>(A1, B, n, pl.blocks, partial, st, ldc, W0); break;
-        case 2: launch_gram_rows<2>(A1, B, n, pl.blocks, partial, st, ldc, W0); break;
+    constexpr int W0 = 16 * CAL_GRAM_SPLIT_NTA;
+    const int ldc = 16 * pl.nta;
+    for (int a0 = 0; a0 < A.total; a0 += W0) {
+        const int na = std::min(W0, A.total - a0), nt = (na + 15) / 16;
+        const Panel As = gram_panel_slice(A, a0, na);
+        switch (nt) {
+            case 1: launch_gram_rows<1>(As, B, n, pl.blocks, partial, st, ldc, a0); break;
+            case 2: launch_gram_rows<2>(As, B, n, pl.blocks, partial, st, ldc, a0); break;
 #if CAL_GRAM_ROWS_MAXNTA >= 3
-        case 3: launch_gram_rows<3>(A1, B, n, pl.blocks, partial, st, ldc, W0); break;
+            case 3: launch_gram_rows<3>(As, B, n, pl.blocks, partial, st, ldc, a0); break;
 #endif
 #if CAL_GRAM_ROWS_MAXNTA >= 4
-        case 4: launch_gram_rows<4>(A1, B, n, pl.blocks, partial, st, ldc, W0); break;
+            case 4: launch_gram_rows<4>(As, B, n, pl.blocks, partial, st, ldc, a0); break;
 #endif
-        default: return hipErrorInvalidValue;
+            default: return hipErrorInvalidValue;
+        }
     }
     return hipGetLastError();
 }
