@@ -288,7 +288,10 @@ hipError_t launch_orth_coef(int phase, const double* tile, double* st, double* m
                             unsigned long long seq, hipStream_t stream);
 // Grid of the row-parallel Gram sweeps (k_rowapply with GRAM): 4 blocks of
 // 38 KB LDS per CU on 256 CUs.
-constexpr int kRowGramBlocks = 1024;
+#ifndef CAL_ROWGRAM_BLOCKS
+#define CAL_ROWGRAM_BLOCKS 1024
+#endif
+constexpr int kRowGramBlocks = CAL_ROWGRAM_BLOCKS;
 hipError_t launch_rowgram(const ColList& P, int nt, bool has_extra, int64_t n, int blocks, double* partial,
                           hipStream_t st);
 hipError_t launch_dot(const double* x, const double* y, int64_t n, double* partial, int blocks,
