@@ -465,7 +465,12 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
     double* d_st = c->d_red + 1024;
     double* d_mbuf = c->d_red + 2048;
     double* d_out = c->d_red + 3072;
-    int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, kRowGramBlocks));
+    // sweeps the Infinity Cache holds (17 columns in <= 160 MB: config 2's
+    // n = 1e6) run on half the grid: lap2d_1000 6050-6225 -> 6216-6334
+    // outer-it/s, while lap3d_215 loses 0.8 % with 512 blocks and the IRL
+    // (n = 1.58 M) is unchanged (same-box A/B, profiles/r05/rg/)
+    const int64_t rg_cap = (int64_t)n * 8 * 17 <= ((int64_t)160 << 20) ? kRowGramBlocks / 2 : kRowGramBlocks;
+    int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, rg_cap));
     CAL_TRY(ensure_partial(c, (size_t)blocks * 272));
     // P1: [Qp(0:nq) | X]' X (+ Qp column 8 as the extra column)
     ColList ct{};
