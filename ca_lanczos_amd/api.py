@@ -306,15 +306,26 @@ def default_context() -> Context:
     return _default_ctx
 
 
+def _evict(key, ref) -> None:
+    """Close the context of a matrix that died (its weakref's callback):
+    the device copy of A and the work buffers go with it."""
+    hit = _matrix_ctx.get(key)
+    if hit is not None and hit[0] is ref:
+        del _matrix_ctx[key]
+        hit[1].close()
+
+
 def context_for(A) -> Context:
     key = id(A)
     hit = _matrix_ctx.get(key)
     if hit is not None and hit[0]() is A:
         return hit[1]
+    if hit is not None:  # a dead matrix's id, reused before its callback ran
+        _evict(key, hit[0])
     ctx = Context().set_matrix(A)
     try:
-        ref = weakref.ref(A)
-    except TypeError:  # pragma: no cover
+        ref = weakref.ref(A, lambda r, key=key: _evict(key, r))
+    except TypeError:  # pragma: no cover  (not weak-referenceable: kept for the process)
         ref = lambda: A  # noqa: E731
     _matrix_ctx[key] = (ref, ctx)
     return ctx

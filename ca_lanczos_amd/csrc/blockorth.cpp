@@ -465,6 +465,15 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
     double* d_st = c->d_red + 1024;
     double* d_mbuf = c->d_red + 2048;
     double* d_out = c->d_red + 3072;
+#ifdef CAL_TEST_HOOKS
+    // the test build poisons this block's coefficient scratch: whatever the
+    // sweeps read that the coefficient steps did not write is NaN
+    CAL_HIP(c, hipMemsetAsync(c->d_red, 0xFF, 4096 * sizeof(double), c->stream));
+#endif
+    // pass B stores only if neither Cholesky failed (out flags [512], [513]):
+    // on a failure the host redoes the block from X, and X may share storage
+    // with Qout (ca_lanczos.m:176, q = Q(:,1) in the first block)
+    const double* gate = test_switch("CAL_TEST_NO_PASSB_GATE") ? nullptr : d_out + 512;
     // sweeps the Infinity Cache holds (17 columns in <= 160 MB: config 2's
     // n = 1e6) run on half the grid: lap2d_1000 6050-6225 -> 6216-6334
     // outer-it/s, while lap3d_215 loses 0.8 % with 512 blocks and the IRL
@@ -516,7 +525,8 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
     // pass B: Q = [Qp | W M1] M2, one store
     {
         const int t = timer_begin(c, 2, 8.0 * n * (wp + m));
-        CAL_HIP(c, launch_rowapply(cw, d_mbuf, wp, m, ol, 3, w, n, (int)((n + 255) / 256), c->d_partial, c->stream));
+        CAL_HIP(c, launch_rowapply(cw, d_mbuf, wp, m, ol, 3, w, n, (int)((n + 255) / 256), c->d_partial, c->stream,
+                                   gate));
         timer_end(c, t);
     }
     if (c->pre_wait) {  // e.g. the next step's matrix powers (lanczos_step)
@@ -595,7 +605,7 @@ static int ensure_zbuf(cal_ctx* c, int64_t n, int m, double** p, int64_t* ld) {
     if (need > c->zbuf_cap) {
         if (c->d_zbuf) CAL_HIP(c, hipFree(c->d_zbuf));
         c->d_zbuf = nullptr;
-        CAL_HIP(c, hipMalloc((void**)&c->d_zbuf, need * sizeof(double)));
+        CAL_HIP(c, scratch_malloc((void**)&c->d_zbuf, need * sizeof(double)));
         c->zbuf_cap = need;
     }
     *p = c->d_zbuf;
@@ -677,7 +687,7 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
     if (off > c->fold_cap) {
         if (c->d_fold) CAL_HIP(c, hipFree(c->d_fold));
         c->d_fold = nullptr;
-        CAL_HIP(c, hipMalloc((void**)&c->d_fold, off * sizeof(double)));
+        CAL_HIP(c, scratch_malloc((void**)&c->d_fold, off * sizeof(double)));
         c->fold_cap = off;
     }
     double* const F = c->d_fold;
@@ -1177,15 +1187,15 @@ int gram_async(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* d_
 static int project_blocks_async(cal_ctx* c, int64_t n, int64_t ld, int nb, const std::vector<double*>& dQ,
                                 const int* widths, int m, double* dX, int region0, std::vector<int>& ldc,
                                 const double* dSrc = nullptr, bool bb_first = false, int* self_blocks = nullptr) {
-    static const bool self_off = getenv("CAL_SELFGRAM_OFF") != nullptr;  // A/B
+    const bool self_off = test_switch("CAL_TEST_SELFGRAM_OFF");  // A/B (test build)
     if (self_blocks) *self_blocks = 0;
     const PanelOut Xo = panel_out(dX, ld, m);
     const double* cur = dSrc ? dSrc : dX;  // where X currently is
     ldc.assign(nb, 0);
     // the update of block i and the Gram of block i + 1 share one pass over
-    // the rows (k_apply_gram) where the shapes allow; CAL_APPLY_GRAM_OFF=1
-    // keeps them apart (A/B measurements)
-    static const bool fuse = getenv("CAL_APPLY_GRAM_OFF") == nullptr;
+    // the rows (k_apply_gram) where the shapes allow; the test build's
+    // CAL_TEST_APPLY_GRAM_OFF keeps them apart (the fused/unfused parity test)
+    const bool fuse = !test_switch("CAL_TEST_APPLY_GRAM_OFF");
     bool first = true, have_R = false;  // have_R: block i's Gram already enqueued (fused step)
     for (int i = 0; i < nb; ++i) {
         const int w = widths[i];

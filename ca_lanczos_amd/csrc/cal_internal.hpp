@@ -13,6 +13,7 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <functional>
 #include <string>
 #include <vector>
@@ -275,9 +276,10 @@ struct ColList {
 struct OutList {
     double* p[16];
 };
-// kind: 0 store, 1 store + Gram, 2 Gram only (pass A), 3 chained store (pass B)
+// kind: 0 store, 1 store + Gram, 2 Gram only (pass A), 3 chained store (pass B).
+// gate (kind 3): device flags; a nonzero gate[0] or gate[1] skips the store.
 hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, const OutList& Y, int kind, int wq,
-                           int64_t n, int blocks, double* partial, hipStream_t st);
+                           int64_t n, int blocks, double* partial, hipStream_t st, const double* gate = nullptr);
 // s x s coefficients of the two-sweep block orthogonalisation (phase 0 after
 // the P1 Gram, phase 1 after pass A); see kernels.hip k_orth_coef.
 // Phase 1 with hout != nullptr also publishes out (R, RY, flags; 516
@@ -517,6 +519,9 @@ struct cal_ctx {
     long fold_runs = 0, fold_declined = 0;  // fused-TSQR blocks run / declined (explicit-Z path taken)
     double fold_last_est = 0.0;             // the last block's loss-of-orthogonality estimate
     double fold_tol = cal::kFoldTol;        // its acceptance threshold (cal_set_tsqr_fold_tol)
+    // the test build only (CAL_TEST_HOOKS): R of ca_lanczos's first block
+    // (normalize, ca_lanczos.m:176), read back by cal_test_first_block_R
+    std::vector<double> test_R1;
 };
 
 // ---- helpers shared by the host-side translation units -----------------
@@ -568,6 +573,21 @@ inline hipError_t copy_cols(cal_ctx* c, double* dst, const double* src, int64_t 
 }
 // pointer to column j of a vector buffer laid out with A.ld / A.lpad
 inline double* vcol(const cal_ctx* c, double* base, int64_t j) { return base + j * c->A.ld + c->A.lpad; }
+// A/B switches of the test build (libcalanczos_testhooks.so: lanczos.cpp,
+// blockorth.cpp and runtime.cpp compiled -DCAL_TEST_HOOKS), read per call;
+// the production library reads no such variable.
+inline bool test_switch(const char* name) {
+#ifdef CAL_TEST_HOOKS
+    return std::getenv(name) != nullptr;
+#else
+    (void)name;
+    return false;
+#endif
+}
+// Device scratch allocation.  The test build fills every new buffer with NaN
+// (all-ones bytes, then a device sync): a kernel that reads scratch it did
+// not write first returns NaN there instead of a previous allocation's data.
+hipError_t scratch_malloc(void** p, size_t bytes);
 int ensure_partial(cal_ctx* c, size_t doubles);
 int ensure_scratch(cal_ctx* c, size_t doubles);
 int ensure_red(cal_ctx* c, size_t doubles);

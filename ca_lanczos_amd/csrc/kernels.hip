@@ -2097,8 +2097,6 @@ hipError_t launch_gram_wide(const double* Q, int64_t ld, int w, int64_t n, doubl
 hipError_t launch_gram(const Panel& A, const Panel& B, int64_t n, const GramPlan& pl, double* partial,
                        hipStream_t st) {
     dim3 g(pl.blocks), b(256);
-    static const bool log_shapes = getenv("CAL_LOG_GRAM_SHAPES") != nullptr;  // tuning aid
-    if (log_shapes) fprintf(stderr, "gram %d %d %lld\n", A.total, B.total, (long long)n);
     // the staged loads pay from 33 A columns on (tools/gram_probe.hip: +5-15 %
     // at 48-128 columns; RUN = 16 stages 256-row blocks in 70 KB of LDS and
     // loses to the direct loads at <= 32 columns)
@@ -2929,9 +2927,16 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// gate (CHAIN only, may be null): the coefficient step's two failure flags
+// (k_orth_coef out[512..513]); when either is set the sweep stores nothing.
+// A failed Cholesky leaves M1 or M2 unwritten (stale scratch) and the host
+// redoes the block from its input -- which, in ca_lanczos's first block, is
+// the same storage as the output (q = Q(:,1)).
 template <int WPMAX, int MOUT, bool GRAM, bool APPLY = true, bool STORE = true, bool CHAIN = false, bool NTS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_rowapply(ColList P, const double* __restrict__ M, int wp, int m,
-                                                  OutList Y, int wq, int64_t n, double* __restrict__ partial) {
+                                                  OutList Y, int wq, int64_t n, double* __restrict__ partial,
+                                                  const double* __restrict__ gate) {
+    if (CHAIN && gate && (gate[0] != 0.0 || gate[1] != 0.0)) return;  // block-uniform
     constexpr int TLD = 17;  // padded LDS row (doubles)
     constexpr int MSZ = WPMAX * MOUT * (CHAIN ? 2 : 1) + (CHAIN ? MOUT * MOUT : 0);
     // tile: 256 rows x 16 Gram columns, the pad column 16 holds the extra
@@ -3099,7 +3104,7 @@ int rowapply_mout(int m) { return m <= 4 ? 4 : (m <= 8 ? 8 : (m <= 16 ? 16 : 0))
 // 3 chained store (pass B).  Instantiated for the shapes of s = 4 and s = 8
 // ('full' with s = 4 reaches 10..17 projection columns with 4 outputs).
 hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, const OutList& Y, int kind, int wq,
-                           int64_t n, int blocks, double* partial, hipStream_t st) {
+                           int64_t n, int blocks, double* partial, hipStream_t st, const double* gate) {
     const int WP = rowapply_wpmax(wp), MO = rowapply_mout(m);
     dim3 g(blocks), b(256);
     // pass B's block Q is read again only after the next step's matrix powers
@@ -3110,9 +3115,10 @@ hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, co
     // profiles/r04/passb_nt/)
     const bool nts = (int64_t)n * 8 * (wp + m) > ((int64_t)256 << 20);
 #define CAL_RA(W, MM, G, S, C) \
-    hipLaunchKernelGGL((k_rowapply<W, MM, G, true, S, C>), g, b, 0, st, P, dM, wp, m, Y, wq, n, partial)
+    hipLaunchKernelGGL((k_rowapply<W, MM, G, true, S, C>), g, b, 0, st, P, dM, wp, m, Y, wq, n, partial, gate)
 #define CAL_RA_NT(W, MM) \
-    hipLaunchKernelGGL((k_rowapply<W, MM, false, true, true, true, true>), g, b, 0, st, P, dM, wp, m, Y, wq, n, partial)
+    hipLaunchKernelGGL((k_rowapply<W, MM, false, true, true, true, true>), g, b, 0, st, P, dM, wp, m, Y, wq, n, partial, \
+                       gate)
 #define CAL_RA_SHAPE(W, MM)                                  \
     case W * 100 + MM:                                       \
         switch (kind) {                                      \
@@ -3151,7 +3157,7 @@ hipError_t launch_rowgram(const ColList& P, int nt, bool has_extra, int64_t n, i
                           hipStream_t st) {
     OutList none{};
     hipLaunchKernelGGL((k_rowapply<17, 4, true, false>), dim3(blocks), dim3(256), 0, st, P, nullptr, 17, nt, none,
-                       has_extra ? 1 : 0, n, partial);
+                       has_extra ? 1 : 0, n, partial, nullptr);
     return hipGetLastError();
 }
 

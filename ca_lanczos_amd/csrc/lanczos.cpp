@@ -182,9 +182,8 @@ static int normest_dev(cal_ctx* c, double* out) {
     double* d_nrm = c->d_red + kNrm;
     const double* h_nrm = c->h_red + kNrm;
     // one rank: both norms and the rescale in two launches (the same bits);
-    // CAL_PROLOGUE_FUSED=0 keeps the separate launches
-    const char* pf = std::getenv("CAL_PROLOGUE_FUSED");
-    const bool fused = (!pf || std::atoi(pf) != 0) && (!c->comm || c->comm->nranks <= 1);
+    // the test build's CAL_TEST_PROLOGUE_SPLIT keeps the separate launches
+    const bool fused = !test_switch("CAL_TEST_PROLOGUE_SPLIT") && (!c->comm || c->comm->nranks <= 1);
     if (fused) CAL_TRY(ensure_partial(c, 2 * (size_t)nb));
     double e0 = 0.0;
     int cnt = 0;
@@ -298,10 +297,9 @@ static int newton_prologue(cal_ctx* c, LanczosState& L, bool cgs = true) {
     };
     // one rank: the recurrence in three launches per step (launch_pro_step,
     // the same bits); several ranks all-reduce each dot before its use.
-    // CAL_PROLOGUE_FUSED=0 (read per run) keeps the separate launches: the
-    // parity test compares both.
-    const char* pf = std::getenv("CAL_PROLOGUE_FUSED");
-    const bool fused = (!pf || std::atoi(pf) != 0) && (!c->comm || c->comm->nranks <= 1);
+    // the test build's CAL_TEST_PROLOGUE_SPLIT (read per run) keeps the
+    // separate launches: the parity test compares both.
+    const bool fused = !test_switch("CAL_TEST_PROLOGUE_SPLIT") && (!c->comm || c->comm->nranks <= 1);
     if (fused) CAL_TRY(ensure_partial(c, 2 * (size_t)nbd));
     for (int j = 0; j < m; ++j) {
         CAL_TRY(spmv_dev(c, Qc(j), r, 0, 0.0, 0.0, nullptr));  // :103
@@ -444,7 +442,7 @@ static int grow_pinned(cal_ctx* c, double** d, double** h, size_t* cap, size_t n
     if (*h) CAL_HIP(c, hipHostFree(*h));
     *d = *h = nullptr;
     const size_t n = std::max(need, *cap + *cap / 2);
-    CAL_HIP(c, hipMalloc((void**)d, n * sizeof(double)));
+    CAL_HIP(c, scratch_malloc((void**)d, n * sizeof(double)));
     CAL_HIP(c, hipHostMalloc((void**)h, n * sizeof(double), hipHostMallocDefault));
     *cap = n;
     return 0;
@@ -455,7 +453,7 @@ static int grow_pinned_dev(cal_ctx* c, double** d, size_t* cap, size_t need) {
     if (*d) CAL_HIP(c, hipFree(*d));
     *d = nullptr;
     const size_t n = std::max(need, *cap + *cap / 2);
-    CAL_HIP(c, hipMalloc((void**)d, n * sizeof(double)));
+    CAL_HIP(c, scratch_malloc((void**)d, n * sizeof(double)));
     *cap = n;
     return 0;
 }
@@ -849,6 +847,18 @@ static int extend_T(cal_ctx* c, LanczosState& L, const std::vector<double>& Rkk_
 }
 
 #ifdef CAL_TEST_HOOKS  // the test build only (csrc/Makefile libcalanczos_testhooks.so)
+// TEST HOOK: R of the last ca_lanczos run's first block ((s+1) x (s+1),
+// column-major); returns s + 1, or a negative status when there is none.
+extern "C" int cal_test_first_block_R(cal_ctx* c, double* R, int cap) {
+    if (!c || !R) return CAL_ERR_ARG;
+    const size_t m2 = c->test_R1.size();
+    int m = 0;
+    while ((size_t)(m + 1) * (m + 1) <= m2) ++m;
+    if (m == 0 || (size_t)m * m != m2 || (size_t)cap < m2) return CAL_ERR_ARG;
+    std::copy(c->test_R1.begin(), c->test_R1.end(), R);
+    return m;
+}
+
 // TEST HOOK (CAL_TEST_EIG_PAIR set; tests/test_gpu_parity.py): no converged
 // complex Ritz pair arises on the inputs the tests can reach, so the test
 // rewrites every all-real eig(T) the way tests/test_oracle.py's hook rewrites
@@ -1054,6 +1064,9 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
         bool sh = false;
         CAL_TRY(normalize_dev(c, n, X, Qo, Rk.data(), 1.0e-8, &rank, &sh));
         if (rank < s + 1) L.info.n_rank_deficient++;
+#ifdef CAL_TEST_HOOKS
+        c->test_R1 = Rk;
+#endif
         if (L.restart_inner) {
             // [Q(:,1:s+1),R_] = projectAndNormalize({Q_conv},Q_,true) (restarted_ca_lanczos.m:291)
             CAL_TRY(ensure_work(c, s + 1, ld));

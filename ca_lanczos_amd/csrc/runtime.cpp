@@ -34,12 +34,21 @@ int hip_fail(cal_ctx* c, hipError_t e, const char* what) {
     return set_error(c, CAL_ERR_HIP, m);
 }
 
+hipError_t scratch_malloc(void** p, size_t bytes) {
+    hipError_t e = hipMalloc(p, bytes);
+#ifdef CAL_TEST_HOOKS
+    if (e == hipSuccess) e = hipMemset(*p, 0xFF, bytes);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+#endif
+    return e;
+}
+
 static int grow(cal_ctx* c, double** p, size_t* cap, size_t need) {
     if (need <= *cap) return 0;
     if (*p) CAL_HIP(c, hipFree(*p));
     *p = nullptr;
     size_t n = std::max(need, (size_t)4096);
-    CAL_HIP(c, hipMalloc((void**)p, n * sizeof(double)));
+    CAL_HIP(c, scratch_malloc((void**)p, n * sizeof(double)));
     *cap = n;
     return 0;
 }
@@ -54,7 +63,7 @@ int ensure_small(cal_ctx* c, size_t doubles) {
     c->d_small = nullptr;
     c->h_small = nullptr;
     size_t n = std::max(doubles, (size_t)65536);
-    CAL_HIP(c, hipMalloc((void**)&c->d_small, n * sizeof(double)));
+    CAL_HIP(c, scratch_malloc((void**)&c->d_small, n * sizeof(double)));
     CAL_HIP(c, hipHostMalloc((void**)&c->h_small, n * sizeof(double), hipHostMallocDefault));
     c->small_cap = n;
     return 0;
@@ -67,7 +76,7 @@ int ensure_red(cal_ctx* c, size_t doubles) {
     c->d_red = nullptr;
     c->h_red = nullptr;
     size_t n = std::max(doubles, (size_t)65536);
-    CAL_HIP(c, hipMalloc((void**)&c->d_red, n * sizeof(double)));
+    CAL_HIP(c, scratch_malloc((void**)&c->d_red, n * sizeof(double)));
     CAL_HIP(c, hipHostMalloc((void**)&c->h_red, n * sizeof(double), hipHostMallocDefault));
     c->red_cap = n;
     return 0;

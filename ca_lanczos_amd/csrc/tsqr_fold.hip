@@ -64,9 +64,9 @@ constexpr int kProbe = FOLD_PROBE;  // bit 1: no Gram, 2: no tile QR, 3: no tile
 #endif
 #ifndef FOLD_DOWN_WPE
 #define FOLD_DOWN_WPE 3  // k_fold_down waves per SIMD (150 VGPRs)
+#endif
 #ifndef CAL_FOLD_DOWN_NT
 #define CAL_FOLD_DOWN_NT 1  // non-temporal Q stores in k_fold_down (tuning switch)
-#endif
 #endif
 
 __device__ __forceinline__ fd4 fmfma(double a, double b, fd4 c) {

@@ -142,3 +142,58 @@ def test_residency_generation_is_process_wide(cal):
     g0 = lib.cal_residency_generation()
     assert lib.cal_residency_invalidate() == g0 + 1
     assert lib.cal_residency_generation() == g0 + 1
+
+
+HOOK_NAMES = ["CAL_TEST_EIG_PAIR", "CAL_TEST_PROLOGUE_SPLIT", "CAL_TEST_SELFGRAM_OFF", "CAL_TEST_APPLY_GRAM_OFF",
+              "CAL_TEST_NO_PASSB_GATE", "cal_test_first_block_R",
+              # the pre-round-6 spellings of the same switches, and the tuning log
+              "CAL_PROLOGUE_FUSED", "CAL_SELFGRAM_OFF", "CAL_APPLY_GRAM_OFF", "CAL_LOG_GRAM_SHAPES"]
+
+
+def test_production_library_carries_no_test_switches():
+    """The A/B switches and result-altering hooks live in the test build
+    only (csrc/Makefile HOOKED objects, -DCAL_TEST_HOOKS): the production
+    library's image holds none of their names, the test build holds the
+    current ones."""
+    prod = open(os.path.join(ROOT, "ca_lanczos_amd", "libcalanczos.so"), "rb").read()
+    test = open(os.path.join(ROOT, "ca_lanczos_amd", "libcalanczos_testhooks.so"), "rb").read()
+    present = [h for h in HOOK_NAMES if h.encode() in prod]
+    assert not present, present
+    for h in HOOK_NAMES[:6]:
+        assert h.encode() in test, h
+
+
+def test_context_cache_evicts_dead_matrices(cal, monkeypatch):
+    """api.context_for keeps one context per live matrix; when the matrix is
+    collected its context is closed and dropped.  A
+    stand-in Context records set_matrix / close, so no device is needed."""
+    import gc
+
+    import scipy.sparse as sp
+    from ca_lanczos_amd import api
+
+    closed = []
+
+    class FakeCtx:
+        def set_matrix(self, A):
+            self.n = A.shape[0]
+            return self
+
+        def close(self):
+            closed.append(self.n)
+
+    monkeypatch.setattr(api, "Context", FakeCtx)
+    monkeypatch.setattr(api, "_matrix_ctx", {})
+    A = sp.identity(5, format="csr")
+    B = sp.identity(7, format="csr")
+    ca, cb = api.context_for(A), api.context_for(B)
+    assert api.context_for(A) is ca and api.context_for(B) is cb
+    assert len(api._matrix_ctx) == 2
+    del A
+    gc.collect()
+    assert closed == [5] and len(api._matrix_ctx) == 1
+    C = sp.identity(9, format="csr")
+    assert api.context_for(C) is not cb and len(api._matrix_ctx) == 2
+    del B, C, cb
+    gc.collect()
+    assert sorted(closed) == [5, 7, 9] and not api._matrix_ctx

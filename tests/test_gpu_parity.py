@@ -373,52 +373,6 @@ def test_orth_err_deferred_wide_gram(cal, ref, monkeypatch, N, orth):
         assert np.max(a.orth_err) < 1e-12
 
 
-@pytest.mark.parametrize("N,s", [(40, 8), (23, 4), (70, 16)])
-def test_newton_prologue_fused_bitexact(cal, ref, monkeypatch, N, s):
-    """The Newton prologue's recurrence (lanczos.m:103-110) with each update
-    and the dot after it in one launch (k_axpy_dot: k_dot's grid and order,
-    the partials summed by the last block in k_reduce's order) against the
-    separate axpy / dot / reduce launches (CAL_PROLOGUE_FUSED=0): the same
-    bits in T, Q's Ritz residual norms and the orthogonality errors; rows not
-    a multiple of the 256-thread blocks (23^3, 70^3 = 343000 > one grid
-    stride of 1024 blocks)."""
-    A = cal.matrices.laplacian_3d(N)
-    r = ref.matlab_rand(A.shape[0])
-    monkeypatch.delenv("CAL_PROLOGUE_FUSED", raising=False)
-    a = cal.ca_lanczos_ex(A, r, s, 4 * s, "newton", "full")
-    monkeypatch.setenv("CAL_PROLOGUE_FUSED", "0")
-    b = cal.ca_lanczos_ex(A, r, s, 4 * s, "newton", "full")
-    assert np.array_equal(a.T, b.T)
-    assert np.array_equal(a.ritz_rnorm, b.ritz_rnorm)
-    assert np.array_equal(a.orth_err, b.orth_err)
-
-
-def test_normest_and_irl_fused_bitexact(cal, ref, monkeypatch):
-    """normest (MATLAB built-in, ca_lanczos.m:258) with both norms and the
-    rescale fused (k_norms2 + k_nrm_div) against the separate dot / reduce /
-    div launches (CAL_PROLOGUE_FUSED=0): 'periodic' CA-Lanczos (which takes
-    normest(A) for its omega recurrence) and a whole implicit-restart solve
-    (normest, the Newton prologue, every restart) give the same bits."""
-    A = cal.matrices.circuit_like(60, seed=3)
-    r = ref.matlab_rand(A.shape[0])
-    outs = []
-    for env in (None, "0"):
-        if env is None:
-            monkeypatch.delenv("CAL_PROLOGUE_FUSED", raising=False)
-        else:
-            monkeypatch.setenv("CAL_PROLOGUE_FUSED", env)
-        p = cal.ca_lanczos_ex(A, r, 4, 40, "newton", "periodic")
-        irl = cal.impl_restarted_ca_lanczos(A, r, 40, 6, 4, "newton", "full", 1e-8)
-        outs.append((p, irl))
-    (p0, i0), (p1, i1) = outs
-    assert p0.info["norm_A"] == p1.info["norm_A"] and p0.info["norm_A"] > 0
-    assert i0["norm_A"] == i1["norm_A"]
-    assert np.array_equal(p0.T, p1.T)
-    assert i0["num_restarts"] == i1["num_restarts"]
-    assert np.array_equal(i0["conv_eigs"], i1["conv_eigs"])
-    assert np.array_equal(i0["Q_conv"], i1["Q_conv"])
-
-
 def test_ca_lanczos_bad_args(cal):
     A = cal.matrices.laplacian_2d(8)
     with pytest.raises(ValueError):
