@@ -1196,6 +1196,9 @@ int cal_lanczos_begin(cal_ctx* c, const double* r, int s, int max_outer, const c
     if (b != "monomial" && b != "newton") return set_error(c, CAL_ERR_ARG, "ERROR: Unknown basis type: " + b);
     hipSetDevice(c->device);
     cal_lanczos_free_state(c);
+#ifdef CAL_TEST_HOOKS
+    c->test_R1.clear();
+#endif
     LanczosState* L = new LanczosState();
     c->lz = L;
     L->s = s;
