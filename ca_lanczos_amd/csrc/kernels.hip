@@ -1755,15 +1755,36 @@ __global__ __launch_bounds__(256) void k_gram_lds(Panel A, Panel B, int64_t n, d
 #ifndef CAL_GRAM_ROWS_MAXNTA
 #define CAL_GRAM_ROWS_MAXNTA 4
 #endif
-template <int NTA, int RUN, bool BB>
+// NSLOT rounds of loads in flight per thread (register slots), the LDS
+// double buffered: round r loads into slot r % NSLOT, stages into buffer
+// r % 2 and issues round r + NSLOT's loads into the slot it just drained.
+// One block per CU (83 KB at NTA 4), so the bytes in flight per CU are
+// NSLOT x 256 threads x PER x 8 B: 80 KB with 2 slots.
+#ifndef CAL_GRAM_ROWS_NSLOT
+#define CAL_GRAM_ROWS_NSLOT 2
+#endif
+// LDS stage buffers: 2 (one barrier per round) or 1 (a second barrier before
+// the stage is rewritten; half the LDS, so more blocks per CU)
+#ifndef CAL_GRAM_ROWS_LDSBUF
+#define CAL_GRAM_ROWS_LDSBUF 2
+#endif
+// BW: B columns staged (16, or 8 when B has <= 8: the MFMA lanes of B
+// columns 8..15 take zeros without LDS).  With BW = 8 the NTA = 4 stage is
+// 75 KB, so two blocks share a CU: a 64 + 8-column sweep reads at the
+// two-block rate (6.0 against 5.1-5.3 TB/s at lap3d_215's n,
+// tools/wide_read_probe.hip, profiles/r06/wide_read_probe.json).
+template <int NTA, int RUN, bool BB, int BW = 16>
 __global__ __launch_bounds__(256) void k_gram_rows(Panel A, Panel B, int64_t n, double* __restrict__ partial,
                                                    int ldc_out, int a_off) {
+    static_assert(BW == 8 || BW == 16, "k_gram_rows B width");
     constexpr int R = 16 * RUN;         // rows per round
-    constexpr int NC = 16 * (NTA + 1);  // staged columns: B's 16, then A's
+    constexpr int NC = BW + 16 * NTA;   // staged columns: B's BW, then A's
     constexpr int LD = NC + 1;
     constexpr int CPI = 256 / R;        // columns per block-wide load instruction
     constexpr int PER = NC / CPI;       // loads per thread and round
+    constexpr int NS = CAL_GRAM_ROWS_NSLOT;
     static_assert(R >= 64 && 256 % R == 0 && NC % CPI == 0, "k_gram_rows geometry");
+    static_assert(NS >= 2 && NS <= 4, "k_gram_rows slots");
     extern __shared__ __attribute__((aligned(16))) double lds_gr[];  // [2][R][LD], then the partials
     constexpr int NT = NTA + (BB ? 1 : 0);                             // output tiles (B'B last)
     auto red = reinterpret_cast<double (*)[NT][64][4]>(lds_gr);        // [3][NT][64][4]
@@ -1776,12 +1797,12 @@ __global__ __launch_bounds__(256) void k_gram_rows(Panel A, Panel B, int64_t n, 
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const int cc = lcol0 + CPI * q;
-        if (cc < 16) {
+        if (cc < BW) {
             on[q] = cc < B.total;
             pc[q] = pcol(B, on[q] ? cc : 0);
         } else {
-            on[q] = cc - 16 < A.total;
-            pc[q] = pcol(A, on[q] ? cc - 16 : 0);
+            on[q] = cc - BW < A.total;
+            pc[q] = pcol(A, on[q] ? cc - BW : 0);
         }
     }
     d4 acc[NT];
@@ -1789,41 +1810,47 @@ __global__ __launch_bounds__(256) void k_gram_rows(Panel A, Panel B, int64_t n, 
     for (int t = 0; t < NT; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
     const int orow = wave * 4 * RUN + g * RUN;
     const int64_t stride = (int64_t)gridDim.x * R;
-    double v[2][PER];
-    bool vin[2] = {false, false};
-    auto load = [&](auto S, int64_t rb) {
+    double v[NS][PER];
+    bool vin[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) vin[q] = false;
+    // (slot and buffer indices are constants once the loops below unroll)
+    auto load = [&](int S, int64_t rb) {
         const int64_t rr = rb + lrow;
         vin[S] = rr < n;
         const int64_t ro = vin[S] ? rr : 0;
 #pragma unroll
         for (int q = 0; q < PER; ++q) v[S][q] = on[q] ? pc[q][ro] : 0.0;  // on[q] wave-uniform
     };
-    auto round = [&](auto S, int64_t rb) {
-        double* s = lds_gr + S * (R * LD);
+    auto round = [&](int S, int L, int64_t rb) {
+        double* s = lds_gr + (CAL_GRAM_ROWS_LDSBUF == 2 ? L : 0) * (R * LD);
+        if (CAL_GRAM_ROWS_LDSBUF == 1) __syncthreads();  // the previous round's MFMAs read the stage
 #pragma unroll
         for (int q = 0; q < PER; ++q) s[lrow * LD + lcol0 + CPI * q] = vin[S] ? v[S][q] : 0.0;
-        if (rb + 2 * stride < n) load(S, rb + 2 * stride);
+        if (rb + NS * stride < n) load(S, rb + NS * stride);
         __syncthreads();
 #pragma unroll
         for (int m = 0; m < RUN; ++m) {
             const double* row = s + (orow + m) * LD + c16;
-            const double b = row[0];
+            const double b = BW == 16 || c16 < BW ? row[0] : 0.0;
 #pragma unroll
-            for (int t = 0; t < NTA; ++t) acc[t] = mfma64(row[16 + 16 * t], b, acc[t]);
+            for (int t = 0; t < NTA; ++t) acc[t] = mfma64(row[BW + 16 * t], b, acc[t]);
             if constexpr (BB) acc[NTA] = mfma64(b, b, acc[NTA]);
         }
     };
-    using S0 = std::integral_constant<int, 0>;
-    using S1 = std::integral_constant<int, 1>;
+    // rounds of one unrolled pass: slot i % NS, LDS buffer i % 2
+    constexpr int U = NS % 2 == 0 ? NS : 2 * NS;
     int64_t rb = (int64_t)blockIdx.x * R;
-    if (rb < n) load(S0{}, rb);
-    if (rb + stride < n) load(S1{}, rb + stride);
+#pragma unroll
+    for (int i = 0; i < NS; ++i)
+        if (rb + i * stride < n) load(i, rb + i * stride);
     while (rb < n) {
-        round(S0{}, rb);
-        rb += stride;
-        if (rb >= n) break;
-        round(S1{}, rb);
-        rb += stride;
+#pragma unroll
+        for (int i = 0; i < U; ++i) {
+            if (rb >= n) break;
+            round(i % NS, i % 2, rb);
+            rb += stride;
+        }
     }
     __syncthreads();  // the staging buffers become the partials
     if (wave > 0) {
@@ -1857,10 +1884,15 @@ __global__ __launch_bounds__(256) void k_gram_rows(Panel A, Panel B, int64_t n, 
 template <int NTA, bool BB = false>
 static void launch_gram_rows(const Panel& A, const Panel& B, int64_t n, int blocks, double* partial, hipStream_t st,
                              int ldc_out = 16 * NTA, int a_off = 0) {
-    constexpr int RUN = CAL_GRAM_ROWS_RUN, R = 16 * RUN, LD = 16 * (NTA + 1) + 1;
-    const size_t lds = std::max((size_t)2 * R * LD, (size_t)3 * (NTA + 1) * 64 * 4) * sizeof(double);
-    hipLaunchKernelGGL((k_gram_rows<NTA, RUN, BB>), dim3(blocks), dim3(256), lds, st, A, B, n, partial, ldc_out,
-                       a_off);
+    constexpr int RUN = CAL_GRAM_ROWS_RUN, R = 16 * RUN;
+    const int bw = B.total <= 8 ? 8 : 16, LD = bw + 16 * NTA + 1;
+    const size_t lds = std::max((size_t)CAL_GRAM_ROWS_LDSBUF * R * LD, (size_t)3 * (NTA + 1) * 64 * 4) * sizeof(double);
+    if (bw == 8)
+        hipLaunchKernelGGL((k_gram_rows<NTA, RUN, BB, 8>), dim3(blocks), dim3(256), lds, st, A, B, n, partial,
+                           ldc_out, a_off);
+    else
+        hipLaunchKernelGGL((k_gram_rows<NTA, RUN, BB, 16>), dim3(blocks), dim3(256), lds, st, A, B, n, partial,
+                           ldc_out, a_off);
 }
 
 // Columns c0 .. c0 + nc - 1 of a panel (host side)
@@ -1887,7 +1919,12 @@ static Panel gram_panel_slice(const Panel& P, int c0, int nc) {
 #endif
 static hipError_t launch_gram_rows_split(const Panel& A, const Panel& B, int64_t n, const GramPlan& pl,
                                          double* partial, hipStream_t st) {
-    constexpr int W0 = 16 * CAL_GRAM_SPLIT_NTA;
+    // the fewest launches of <= CAL_GRAM_SPLIT_NTA tiles, the tiles spread
+    // evenly over them (72 columns: 48 + 24, not 64 + 8 -- a launch of 8 + 8
+    // columns streams at a fraction of the rate, profiles/r06/gram3)
+    const int tiles = (A.total + 15) / 16;
+    const int nl = (tiles + CAL_GRAM_SPLIT_NTA - 1) / CAL_GRAM_SPLIT_NTA;
+    const int W0 = 16 * ((tiles + nl - 1) / nl);
     const int ldc = 16 * pl.nta;
     for (int a0 = 0; a0 < A.total; a0 += W0) {
         const int na = std::min(W0, A.total - a0), nt = (na + 15) / 16;
