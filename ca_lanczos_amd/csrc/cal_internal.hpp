@@ -84,7 +84,9 @@ struct SpmvArgs {
     const double* xprev;  // modified Newton basis, complex shift
     double shift;         // y = A x - shift * x
     double im2;           //     + im2 * xprev
-    int mode;             // 0: y = A x, 1: shifted, 2: shifted + im2 term
+    int mode;             // 0: y = A x, 1: shifted, 2: shifted + im2 term,
+                          // 3: y = A (x / sqrt(*xnrm)) (normest; each gathered x_j divided)
+    const double* xnrm = nullptr;
     int xcd;              // XCD-contiguous block order (set by launch_spmv)
     int nt = 0;           // col / val loaded non-temporally (matrix larger than the Infinity Cache)
 };
@@ -310,6 +312,9 @@ hipError_t launch_form_projM(const double* G, int ldg, int w, int m, double* M, 
 // normest's iteration tail, single rank: dst[0] = x'x, dst[1] = y'y, x /= sqrt(x'x)
 // (part: 2 dot_blocks(n) doubles)
 hipError_t launch_normest_norms(double* x, const double* y, int64_t n, double* part, double* dst, hipStream_t st);
+// the same norms without rescaling x (the next S*x divides in its gathers: MODE 3)
+hipError_t launch_normest_norms_only(const double* x, const double* y, int64_t n, double* part, double* dst,
+                                     hipStream_t st);
 hipError_t launch_pro_step(double* r, const double* qprev, const double* pb_prev, const double* q, double* qnext,
                            int64_t n, double* part, double* d_alpha, double* d_beta2, hipStream_t st);
 hipError_t launch_axpy_sub_dev(double* y, const double* x, const double* pa, bool take_sqrt, int64_t n,
@@ -638,9 +643,10 @@ int project_and_normalize_blocks_dev(cal_ctx* c, int64_t n, int64_t ld, int nblo
 int normalize_wide_dev(cal_ctx* c, int64_t n, int64_t ld, const double* dX, int m, double* dQ, double* dW);
 // Halo exchange of a column (distributed only; no-op for one rank).
 int halo_exchange(cal_ctx* c, double* x);
-// y = A x (with modes), handling the halo first.
+// y = A x (with modes), handling the halo first.  Mode 3 (CSR only):
+// y = A (x / sqrt(*xnrm)), xnrm a device scalar.
 int spmv_dev(cal_ctx* c, const double* x, double* y, int mode, double shift, double im2,
-             const double* xprev);
+             const double* xprev, const double* xnrm = nullptr);
 int allreduce_sum(cal_ctx* c, double* d_buf, int64_t count);
 // d_recv[p * count + i] = rank p's d_send[i] (in rank order, every rank)
 int allgather(cal_ctx* c, const double* d_send, double* d_recv, int64_t count);

@@ -77,7 +77,7 @@ __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
 // --------------------------------------------------------------------------
 template <int MODE>
 __device__ __forceinline__ double spmv_epilogue(double sum, const SpmvArgs& a, int r) {
-    if (MODE == 0) return sum;
+    if (MODE == 0 || MODE == 3) return sum;
     double t = a.shift * a.x[r];
     double y = sum - t;
     if (MODE == 2) {
@@ -115,6 +115,9 @@ __global__ __launch_bounds__(kSpmvThreads) void k_spmv(SpmvArgs a) {
     const int r0 = a.blk[b], r1 = a.blk[b + 1];
     const int p0 = a.rowptr[r0], p1 = a.rowptr[r1];
     const int cnt = p1 - p0;
+    // MODE 3: normest's S * (x / norm(x)), the division per gathered element
+    // (MATLAB's x = x/normx, then S*x: the same quotients and products)
+    const double sx = MODE == 3 ? sqrt(*a.xnrm) : 1.0;
     if (cnt <= kSpmvNnz) {
         if (cnt > 0) {
             // all loads first (clamped, never branched around: one vmcnt wait
@@ -135,7 +138,10 @@ __global__ __launch_bounds__(kSpmvThreads) void k_spmv(SpmvArgs a) {
 #pragma unroll
             for (int it = 0; it < NI; ++it)
 #pragma unroll
-                for (int u = 0; u < V; ++u) xv[it][u] = a.x[ci[it][u]];
+                for (int u = 0; u < V; ++u) {
+                    xv[it][u] = a.x[ci[it][u]];
+                    if (MODE == 3) xv[it][u] = xv[it][u] / sx;
+                }
 #pragma unroll
             for (int it = 0; it < NI; ++it)
 #pragma unroll
@@ -157,7 +163,11 @@ __global__ __launch_bounds__(kSpmvThreads) void k_spmv(SpmvArgs a) {
         double sum = 0.0;
         for (int c = p0; c < p1; c += kSpmvNnz) {
             const int m = min(kSpmvNnz, p1 - c);
-            for (int q = tid; q < m; q += kSpmvThreads) prod[q] = a.val[c + q] * a.x[a.col[c + q]];
+            for (int q = tid; q < m; q += kSpmvThreads) {
+                double xq = a.x[a.col[c + q]];
+                if (MODE == 3) xq = xq / sx;
+                prod[q] = a.val[c + q] * xq;
+            }
             __syncthreads();
             if (tid == 0)
                 for (int j = 0; j < m; ++j) sum = sum + prod[j];
@@ -204,7 +214,9 @@ hipError_t launch_spmv(const SpmvArgs& a0, hipStream_t st) {
     switch (a.mode & 0xff) {
         case 0: return launch_spmv_mode<0>(a, nit, st);
         case 1: return launch_spmv_mode<1>(a, nit, st);
-        default: return launch_spmv_mode<2>(a, nit, st);
+        case 2: return launch_spmv_mode<2>(a, nit, st);
+        case 3: return a.xnrm ? launch_spmv_mode<3>(a, nit, st) : hipErrorInvalidValue;
+        default: return hipErrorInvalidValue;
     }
 }
 
@@ -3837,6 +3849,26 @@ __global__ __launch_bounds__(256) void k_nrm_div(double* __restrict__ x, const d
     const double sx = sqrt(xx);
     const int64_t stride = (int64_t)gridDim.x * 256;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) x[i] = x[i] / sx;
+}
+
+__global__ __launch_bounds__(256) void k_nrm_pair(const double* __restrict__ px, const double* __restrict__ py, int np,
+                                                  double* __restrict__ dst) {
+    __shared__ double ws[4];
+    const double xx = pro_reduce(px, np, ws);  // k_nrm_div's reduction
+    const double yy = pro_reduce(py, np, ws);
+    if (threadIdx.x == 0) {
+        dst[0] = xx;
+        dst[1] = yy;
+    }
+}
+
+hipError_t launch_normest_norms_only(const double* x, const double* y, int64_t n, double* part, double* dst,
+                                     hipStream_t st) {
+    if (n <= 0) return hipErrorInvalidValue;
+    const int nb = dot_blocks(n);
+    hipLaunchKernelGGL(k_norms2, dim3(nb), dim3(256), 0, st, x, y, n, part, part + nb);
+    hipLaunchKernelGGL(k_nrm_pair, dim3(1), dim3(256), 0, st, part, part + nb, nb, dst);
+    return hipGetLastError();
 }
 
 hipError_t launch_normest_norms(double* x, const double* y, int64_t n, double* part, double* dst, hipStream_t st) {

@@ -20,6 +20,7 @@
 #include <cstring>
 #include <future>
 #include <string>
+#include <system_error>
 #include <vector>
 
 #include "../../include/calanczos_host.h"
@@ -185,12 +186,22 @@ static int normest_dev(cal_ctx* c, double* out) {
     // the test build's CAL_TEST_PROLOGUE_SPLIT keeps the separate launches
     const bool fused = !test_switch("CAL_TEST_PROLOGUE_SPLIT") && (!c->comm || c->comm->nranks <= 1);
     if (fused) CAL_TRY(ensure_partial(c, 2 * (size_t)nb));
+    // CSR: x is never rescaled in memory -- the next Sx = S*x divides each
+    // gathered x_j by the norm (SpMV mode 3): the same quotients, one read
+    // and one write of x fewer per iteration
+    const bool gather_div = fused && !c->A.use_pat;
+    const double* xnrm = nullptr;  // ||x||^2 of the unscaled x (device), after the first iteration
     double e0 = 0.0;
     int cnt = 0;
     for (;;) {
         for (int i = 0; i < kNormestChunk; ++i) {
-            CAL_TRY(spmv_dev(c, x, y, 0, 0.0, 0.0, nullptr));  // Sx = S*x
-            CAL_TRY(spmv_dev(c, y, x, 0, 0.0, 0.0, nullptr));  // x = S'*Sx
+            CAL_TRY(spmv_dev(c, x, y, xnrm ? 3 : 0, 0.0, 0.0, nullptr, xnrm));  // Sx = S*x
+            CAL_TRY(spmv_dev(c, y, x, 0, 0.0, 0.0, nullptr));                  // x = S'*Sx
+            if (gather_div) {
+                CAL_HIP(c, launch_normest_norms_only(x, y, n, c->d_partial, d_nrm + 2 * i, c->stream));
+                xnrm = d_nrm + 2 * i;
+                continue;
+            }
             if (fused) {
                 CAL_HIP(c, launch_normest_norms(x, y, n, c->d_partial, d_nrm + 2 * i, c->stream));
                 continue;
@@ -422,7 +433,13 @@ static int diag_prepare(cal_ctx* c, LanczosState& L, DiagJob& J) {
         for (int i = 0; i < sk; ++i) J.Tk[i + (size_t)j * sk] = L.T[i + (size_t)j * L.Tld];
     J.k = L.k;
     DiagJob* jp = &J;
-    J.eig = std::async(std::launch::async, [jp, sk]() { return diag_eig(*jp, sk); });
+    try {
+        J.eig = std::async(std::launch::async, [jp, sk]() { return diag_eig(*jp, sk); });
+    } catch (const std::system_error&) {  // no thread to be had: the eig on this thread
+        std::promise<int> done;
+        done.set_value(diag_eig(J, sk));
+        J.eig = done.get_future();
+    }
     return 0;
 }
 

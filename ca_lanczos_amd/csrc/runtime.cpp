@@ -678,11 +678,14 @@ int spmv_range2(cal_ctx* c, int64_t o1, int64_t len1, int64_t o2, int64_t len2, 
     return 0;
 }
 
-int spmv_dev(cal_ctx* c, const double* x, double* y, int mode, double shift, double im2, const double* xprev) {
+int spmv_dev(cal_ctx* c, const double* x, double* y, int mode, double shift, double im2, const double* xprev,
+             const double* xnrm) {
     if (!c->has_A) return set_error(c, CAL_ERR_NOMATRIX, "no matrix set on the context");
+    if (mode == 3 && (c->A.use_pat || !xnrm)) return set_error(c, CAL_ERR_ARG, "spmv_dev: mode 3 needs CSR and xnrm");
     CAL_TRY(halo_exchange(c, const_cast<double*>(x)));
     if (c->A.use_pat) return spmv_range(c, c->A.ext_off, c->A.n_local, x, y, mode, shift, im2, xprev);
     SpmvArgs a;
+    a.xnrm = xnrm;
     a.rowptr = c->A.rowptr;
     a.col = c->A.col;
     a.val = c->A.val;
