@@ -120,10 +120,10 @@ static int gram_host16(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, do
         const int t = timer_begin(c, 1, 8.0 * n * (k.nc + wb));
         CAL_HIP(c, launch_gram(As, B, n, pl, c->d_partial, c->stream));
         timer_end(c, t);
-        CAL_HIP(c, launch_reduce(c->d_partial, pl.blocks, pl.entries, c->d_red + k.off, c->stream));
+        CAL_HIP_OTHER(c, launch_reduce(c->d_partial, pl.blocks, pl.entries, c->d_red + k.off, c->stream));
     }
     CAL_TRY(allreduce_sum(c, c->d_red, off));
-    CAL_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, off * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    CAL_HIP_OTHER(c, hipMemcpyAsync(c->h_red, c->d_red, off * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     CAL_HIP(c, hipStreamSynchronize(c->stream));
     c->small_pending = false;
     for (auto& k : ch)
@@ -180,9 +180,9 @@ int apply_host(cal_ctx* c, int64_t n, const Panel& P, const double* M, int wy, c
     }
     if (!want) return 0;
     CAL_TRY(ensure_red(c, last.entries));
-    CAL_HIP(c, launch_reduce(c->d_partial, last.blocks, last.entries, c->d_red, c->stream));
+    CAL_HIP_OTHER(c, launch_reduce(c->d_partial, last.blocks, last.entries, c->d_red, c->stream));
     CAL_TRY(allreduce_sum(c, c->d_red, last.entries));
-    CAL_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, last.entries * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    CAL_HIP_OTHER(c, hipMemcpyAsync(c->h_red, c->d_red, last.entries * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     CAL_HIP(c, hipStreamSynchronize(c->stream));
     c->small_pending = false;
     int base = 0;
@@ -201,9 +201,9 @@ int apply_host(cal_ctx* c, int64_t n, const Panel& P, const double* M, int wy, c
 static int fetch_tile(cal_ctx* c, int blocks, double* G16, double* e16) {
     const int64_t nent = 272;
     CAL_TRY(ensure_red(c, nent));
-    CAL_HIP(c, launch_reduce(c->d_partial, blocks, nent, c->d_red, c->stream));
+    CAL_HIP_OTHER(c, launch_reduce(c->d_partial, blocks, nent, c->d_red, c->stream));
     CAL_TRY(allreduce_sum(c, c->d_red, nent));
-    CAL_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, nent * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    CAL_HIP_OTHER(c, hipMemcpyAsync(c->h_red, c->d_red, nent * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     CAL_HIP(c, hipStreamSynchronize(c->stream));
     c->small_pending = false;
     std::copy(c->h_red, c->h_red + 256, G16);
@@ -504,9 +504,9 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
     // s x s algebra; phase 1 publishes R / RY / flags to h_out
     auto coef = [&](int phase, int dore) -> int {
         const int np = phase == 0 && p1_blocks > 0 ? p1_blocks : (int)blocks;
-        CAL_HIP(c, launch_reduce(c->d_partial, np, 272, d_tile, c->stream));
+        CAL_HIP_OTHER(c, launch_reduce(c->d_partial, np, 272, d_tile, c->stream));
         CAL_TRY(allreduce_sum(c, d_tile, 272));
-        CAL_HIP(c, launch_orth_coef(phase, d_tile, d_st, d_mbuf, d_out, w, m, WP, MO, dore,
+        CAL_HIP_OTHER(c, launch_orth_coef(phase, d_tile, d_st, d_mbuf, d_out, w, m, WP, MO, dore,
                                     phase == 1 ? c->d_pub : nullptr, d_seq, seq, c->stream));
         return 0;
     };
@@ -728,7 +728,7 @@ static int pn_tsqr_fold(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, 
         CAL_HIP(c, launch_rowgram(ct, nt, w == 9, n, (int)gblocks, c->d_partial, c->stream));
         timer_end(c, t);
     }
-    CAL_HIP(c, launch_reduce(c->d_partial, (int)gblocks, 272, F + oT1, c->stream));
+    CAL_HIP_OTHER(c, launch_reduce(c->d_partial, (int)gblocks, 272, F + oT1, c->stream));
     CAL_TRY(allreduce_sum(c, F + oT1, 272));
     // up: Y, the tile QRs and the tree to the local root, Qp'Y
     ColList cu{};
@@ -1169,7 +1169,7 @@ int gram_async(cal_ctx* c, int64_t n, const Panel& A, const Panel& B, double* d_
     if (bb) CAL_HIP(c, launch_gram_bb(A, B, n, pl, part, c->stream));
     else CAL_HIP(c, launch_gram(A, B, n, pl, part, c->stream));
     timer_end(c, t);
-    CAL_HIP(c, launch_reduce(part, pl.blocks, ne, d_dst, c->stream));
+    CAL_HIP_OTHER(c, launch_reduce(part, pl.blocks, ne, d_dst, c->stream));
     CAL_TRY(allreduce_sum(c, d_dst, ne));
     CAL_HIP(c, hipMemcpyAsync(h_dst, d_dst, ne * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     *ldc = 16 * pl.nta;
@@ -1209,7 +1209,7 @@ static int project_blocks_async(cal_ctx* c, int64_t n, int64_t ld, int nb, const
                                bb_first && first));  // R{i} = Q{i}'*X
         first = false;
         double* dM = c->d_red + off + 4096;
-        CAL_HIP(c, launch_form_projM(c->d_red + off, ldc[i], w, m, dM, c->stream));
+        CAL_HIP_OTHER(c, launch_form_projM(c->d_red + off, ldc[i], w, m, dM, c->stream));
         Panel W = panel();
         panel_add(W, dQ[i], ld, w);
         panel_add(W, cur, ld, m);
@@ -1226,9 +1226,9 @@ static int project_blocks_async(cal_ctx* c, int64_t n, int64_t ld, int nb, const
             const int t = timer_begin(c, 2, 8.0 * n * (w + 2 * m + widths[nx]));
             CAL_HIP(c, launch_apply_gram(W, dM, w + m, m, Xo, Qn, n, c->d_partial, c->stream));
             timer_end(c, t);
-            CAL_HIP(c, launch_reduce(c->d_partial, blocks, 256, c->d_red + offn, c->stream));
+            CAL_HIP_OTHER(c, launch_reduce(c->d_partial, blocks, 256, c->d_red + offn, c->stream));
             CAL_TRY(allreduce_sum(c, c->d_red + offn, 256));
-            CAL_HIP(c, hipMemcpyAsync(c->h_red + offn, c->d_red + offn, 256 * sizeof(double), hipMemcpyDeviceToHost,
+            CAL_HIP_OTHER(c, hipMemcpyAsync(c->h_red + offn, c->d_red + offn, 256 * sizeof(double), hipMemcpyDeviceToHost,
                                       c->stream));
             ldc[nx] = 16;
         } else if (self_blocks && !self_off && nx == nb && apply_selfgram_ok(w + m, m)) {

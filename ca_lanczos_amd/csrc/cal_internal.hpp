@@ -540,6 +540,15 @@ int hip_fail(cal_ctx* c, hipError_t e, const char* what);
         hipError_t _e = (expr);                             \
         if (_e != hipSuccess) return cal::hip_fail((ctx), _e, #expr); \
     } while (0)
+// a small launch (reduction, coefficient step, vector op, result copy)
+// bracketed by the "other" kernel timer when timing is on
+#define CAL_HIP_OTHER(ctx, expr)                                            \
+    do {                                                                    \
+        const int _t = cal::timer_begin((ctx), 3);                          \
+        hipError_t _e = (expr);                                             \
+        cal::timer_end((ctx), _t);                                          \
+        if (_e != hipSuccess) return cal::hip_fail((ctx), _e, #expr);       \
+    } while (0)
 #define CAL_TRY(expr)             \
     do {                          \
         int _s = (expr);          \

@@ -121,10 +121,10 @@ static int dot_host(cal_ctx* c, int64_t n, const double* x, const double* y, dou
     const int nb = dot_blocks(n);
     CAL_TRY(ensure_partial(c, nb));
     CAL_TRY(ensure_red(c, 1));
-    CAL_HIP(c, launch_dot(x, y, n, c->d_partial, nb, c->stream));
-    CAL_HIP(c, launch_reduce(c->d_partial, nb, 1, c->d_red, c->stream));
+    CAL_HIP_OTHER(c, launch_dot(x, y, n, c->d_partial, nb, c->stream));
+    CAL_HIP_OTHER(c, launch_reduce(c->d_partial, nb, 1, c->d_red, c->stream));
     CAL_TRY(allreduce_sum(c, c->d_red, 1));
-    CAL_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    CAL_HIP_OTHER(c, hipMemcpyAsync(c->h_red, c->d_red, sizeof(double), hipMemcpyDeviceToHost, c->stream));
     CAL_HIP(c, hipStreamSynchronize(c->stream));
     c->small_pending = false;
     *out = c->h_red[0];
@@ -164,7 +164,7 @@ static int normest_dev(cal_ctx* c, double* out) {
     CAL_TRY(ensure_red(c, kNrm + 2 * kNormestChunk));
     double* x = work_col(c, 0) + c->A.lpad;
     double* y = work_col(c, 1) + c->A.lpad;
-    CAL_HIP(c, launch_abs_rowsum(c->A.rowptr + c->A.ext_off, c->A.val, n, x, c->stream));
+    CAL_HIP_OTHER(c, launch_abs_rowsum(c->A.rowptr + c->A.ext_off, c->A.val, n, x, c->stream));
     double xx = 0.0;
     CAL_TRY(dot_host(c, n, x, x, &xx));
     double e = std::sqrt(xx);
@@ -172,12 +172,12 @@ static int normest_dev(cal_ctx* c, double* out) {
         *out = 0.0;
         return 0;
     }
-    CAL_HIP(c, launch_div(x, x, e, n, c->stream));
+    CAL_HIP_OTHER(c, launch_div(x, x, e, n, c->stream));
     const int nb = dot_blocks(n);
     CAL_TRY(ensure_partial(c, nb));
     auto dot_dev = [&](const double* a, double* dst) -> int {
-        CAL_HIP(c, launch_dot(a, a, n, c->d_partial, nb, c->stream));
-        CAL_HIP(c, launch_reduce(c->d_partial, nb, 1, dst, c->stream));
+        CAL_HIP_OTHER(c, launch_dot(a, a, n, c->d_partial, nb, c->stream));
+        CAL_HIP_OTHER(c, launch_reduce(c->d_partial, nb, 1, dst, c->stream));
         return allreduce_sum(c, dst, 1);
     };
     double* d_nrm = c->d_red + kNrm;
@@ -198,19 +198,19 @@ static int normest_dev(cal_ctx* c, double* out) {
             CAL_TRY(spmv_dev(c, x, y, xnrm ? 3 : 0, 0.0, 0.0, nullptr, xnrm));  // Sx = S*x
             CAL_TRY(spmv_dev(c, y, x, 0, 0.0, 0.0, nullptr));                  // x = S'*Sx
             if (gather_div) {
-                CAL_HIP(c, launch_normest_norms_only(x, y, n, c->d_partial, d_nrm + 2 * i, c->stream));
+                CAL_HIP_OTHER(c, launch_normest_norms_only(x, y, n, c->d_partial, d_nrm + 2 * i, c->stream));
                 xnrm = d_nrm + 2 * i;
                 continue;
             }
             if (fused) {
-                CAL_HIP(c, launch_normest_norms(x, y, n, c->d_partial, d_nrm + 2 * i, c->stream));
+                CAL_HIP_OTHER(c, launch_normest_norms(x, y, n, c->d_partial, d_nrm + 2 * i, c->stream));
                 continue;
             }
             CAL_TRY(dot_dev(x, d_nrm + 2 * i));
             CAL_TRY(dot_dev(y, d_nrm + 2 * i + 1));
-            CAL_HIP(c, launch_div_sqrt(x, x, d_nrm + 2 * i, n, c->stream));  // x = x / norm(x)
+            CAL_HIP_OTHER(c, launch_div_sqrt(x, x, d_nrm + 2 * i, n, c->stream));  // x = x / norm(x)
         }
-        CAL_HIP(c, hipMemcpyAsync(c->h_red + kNrm, d_nrm, 2 * kNormestChunk * sizeof(double), hipMemcpyDeviceToHost,
+        CAL_HIP_OTHER(c, hipMemcpyAsync(c->h_red + kNrm, d_nrm, 2 * kNormestChunk * sizeof(double), hipMemcpyDeviceToHost,
                                   c->stream));
         CAL_HIP(c, hipStreamSynchronize(c->stream));
         c->small_pending = false;
@@ -290,7 +290,7 @@ static int newton_prologue(cal_ctx* c, LanczosState& L, bool cgs = true) {
     // q = r/norm(r) (lanczos.m:47) of the already normalised start vector
     double nrm2 = 0.0;
     CAL_TRY(dot_host(c, n, L.col(0), L.col(0), &nrm2));
-    CAL_HIP(c, launch_div(Qc(0), L.col(0), std::sqrt(nrm2), n, c->stream));
+    CAL_HIP_OTHER(c, launch_div(Qc(0), L.col(0), std::sqrt(nrm2), n, c->stream));
     // the 2s steps run without host round trips: alpha_j and beta_j^2 stay
     // on the device (d_red [kAB, kAB + 2m)) and feed the updates directly; the
     // CGS coefficients become [-R; 1] on the device (k_form_projM).  Same
@@ -302,8 +302,8 @@ static int newton_prologue(cal_ctx* c, LanczosState& L, bool cgs = true) {
     const int nbd = dot_blocks(n);
     CAL_TRY(ensure_partial(c, nbd));
     auto dot_dev = [&](const double* a, const double* b, double* dst) -> int {
-        CAL_HIP(c, launch_dot(a, b, n, c->d_partial, nbd, c->stream));
-        CAL_HIP(c, launch_reduce(c->d_partial, nbd, 1, dst, c->stream));
+        CAL_HIP_OTHER(c, launch_dot(a, b, n, c->d_partial, nbd, c->stream));
+        CAL_HIP_OTHER(c, launch_reduce(c->d_partial, nbd, 1, dst, c->stream));
         return allreduce_sum(c, dst, 1);
     };
     // one rank: the recurrence in three launches per step (launch_pro_step,
@@ -315,14 +315,14 @@ static int newton_prologue(cal_ctx* c, LanczosState& L, bool cgs = true) {
     for (int j = 0; j < m; ++j) {
         CAL_TRY(spmv_dev(c, Qc(j), r, 0, 0.0, 0.0, nullptr));  // :103
         if (fused) {
-            CAL_HIP(c, launch_pro_step(r, j > 0 ? Qc(j - 1) : nullptr, d_ab + m + j - 1, Qc(j), Qc(j + 1), n,
+            CAL_HIP_OTHER(c, launch_pro_step(r, j > 0 ? Qc(j - 1) : nullptr, d_ab + m + j - 1, Qc(j), Qc(j + 1), n,
                                        c->d_partial, d_ab + j, d_ab + m + j, c->stream));  // :105-110
         } else {
-            if (j > 0) CAL_HIP(c, launch_axpy_sub_dev(r, Qc(j - 1), d_ab + m + j - 1, true, n, c->stream));  // :105
+            if (j > 0) CAL_HIP_OTHER(c, launch_axpy_sub_dev(r, Qc(j - 1), d_ab + m + j - 1, true, n, c->stream));  // :105
             CAL_TRY(dot_dev(r, Qc(j), d_ab + j));                                                          // :107
-            CAL_HIP(c, launch_axpy_sub_dev(r, Qc(j), d_ab + j, false, n, c->stream));                      // :108
+            CAL_HIP_OTHER(c, launch_axpy_sub_dev(r, Qc(j), d_ab + j, false, n, c->stream));                      // :108
             CAL_TRY(dot_dev(r, r, d_ab + m + j));                                                          // :109
-            CAL_HIP(c, launch_div_sqrt(Qc(j + 1), r, d_ab + m + j, n, c->stream));                         // :110
+            CAL_HIP_OTHER(c, launch_div_sqrt(Qc(j + 1), r, d_ab + m + j, n, c->stream));                         // :110
         }
         if (!cgs) continue;  // lanczos(...,'local') (restarted_ca_lanczos.m:65)
         // one CGS pass against Q(:,1:j) (lanczos.m:62-66)
@@ -333,10 +333,10 @@ static int newton_prologue(cal_ctx* c, LanczosState& L, bool cgs = true) {
         const GramPlan pl = gram_plan(j + 1, 1, n);
         CAL_TRY(ensure_partial(c, (size_t)pl.blocks * pl.entries));
         CAL_HIP(c, launch_gram(Qj, qn, n, pl, c->d_partial, c->stream));
-        CAL_HIP(c, launch_reduce(c->d_partial, pl.blocks, pl.entries, d_cg, c->stream));
+        CAL_HIP_OTHER(c, launch_reduce(c->d_partial, pl.blocks, pl.entries, d_cg, c->stream));
         CAL_TRY(allreduce_sum(c, d_cg, pl.entries));
         double* dM = d_cg + 1024;
-        CAL_HIP(c, launch_form_projM(d_cg, 16 * pl.nta, j + 1, 1, dM, c->stream));
+        CAL_HIP_OTHER(c, launch_form_projM(d_cg, 16 * pl.nta, j + 1, 1, dM, c->stream));
         Panel W = panel();
         panel_add(W, Qc(0), ld, j + 2);  // [Q(:,1:j) | q_{j+1}] contiguous
         const ApplyPlan ap = apply_plan(j + 2, 1, n, false, 0);
@@ -345,7 +345,7 @@ static int newton_prologue(cal_ctx* c, LanczosState& L, bool cgs = true) {
     }
     std::vector<double> alpha(m), beta(m);
     {
-        CAL_HIP(c, hipMemcpyAsync(c->h_red + kAB, d_ab, 2 * m * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        CAL_HIP_OTHER(c, hipMemcpyAsync(c->h_red + kAB, d_ab, 2 * m * sizeof(double), hipMemcpyDeviceToHost, c->stream));
         CAL_HIP(c, hipStreamSynchronize(c->stream));
         c->small_pending = false;
         for (int j = 0; j < m; ++j) {
@@ -651,11 +651,11 @@ static int diag_launch(cal_ctx* c, LanczosState& L, DiagJob& J) {
             timer_end(c, t);
         }
         if (batched) {
-            if (cnt[nch] > 0) CAL_HIP(c, launch_reduce(L.d_dpart, nbp, 2 * sk, L.d_dres, c->stream));
+            if (cnt[nch] > 0) CAL_HIP_OTHER(c, launch_reduce(L.d_dpart, nbp, 2 * sk, L.d_dres, c->stream));
             for (size_t q = 0; q < J.sep.size(); ++q)
-                CAL_HIP(c, launch_reduce(L.d_dpart + sep0 + q * 2 * nbr, nbr, 2, L.d_dres + 2 * J.sep[q], c->stream));
+                CAL_HIP_OTHER(c, launch_reduce(L.d_dpart + sep0 + q * 2 * nbr, nbr, 2, L.d_dres + 2 * J.sep[q], c->stream));
         } else {
-            CAL_HIP(c, launch_reduce(L.d_dpart, nbr, 2 * sk, L.d_dres, c->stream));
+            CAL_HIP_OTHER(c, launch_reduce(L.d_dpart, nbr, 2 * sk, L.d_dres, c->stream));
         }
         CAL_TRY(allreduce_sum(c, L.d_dres, 2 * sk));
         CAL_HIP(c, hipMemcpyAsync(L.h_dres, L.d_dres, 2 * sk * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -705,7 +705,7 @@ static int oe_flush(cal_ctx* c, LanczosState& L) {
     CAL_TRY(grow_pinned_dev(c, &L.d_dpart, &L.dpart_cap, (size_t)nent * nb));
     CAL_TRY(grow_pinned(c, &L.d_oe, &L.h_oe, &L.oe_cap, (size_t)nent));
     CAL_HIP(c, launch_gram_wide(L.col(0), L.ld, w, n, L.d_dpart, c->stream));
-    CAL_HIP(c, launch_reduce(L.d_dpart, nb, nent, L.d_oe, c->stream));
+    CAL_HIP_OTHER(c, launch_reduce(L.d_dpart, nb, nent, L.d_oe, c->stream));
     CAL_TRY(allreduce_sum(c, L.d_oe, nent));
     CAL_HIP(c, hipMemcpyAsync(L.h_oe, L.d_oe, (size_t)nent * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     CAL_HIP(c, hipStreamSynchronize(c->stream));
@@ -1246,7 +1246,7 @@ int cal_lanczos_begin(cal_ctx* c, const double* r, int s, int max_outer, const c
     CAL_HIP(c, hipMemcpyAsync(L->vcolumn(0), r, L->n * sizeof(double), hipMemcpyHostToDevice, c->stream));
     double rr = 0.0;
     CAL_TRY(dot_host(c, L->n, L->vcolumn(0), L->vcolumn(0), &rr));
-    CAL_HIP(c, launch_div(L->col(0), L->vcolumn(0), std::sqrt(rr), L->n, c->stream));
+    CAL_HIP_OTHER(c, launch_div(L->col(0), L->vcolumn(0), std::sqrt(rr), L->n, c->stream));
     if (L->newton) {
         CAL_TRY(newton_prologue(c, *L));
     } else {  // Bk = I(:,2:s+1) (ca_lanczos.m:63-65)
@@ -1377,7 +1377,7 @@ int cal_compute_ritz_rnorm(cal_ctx* c, const double* Q, int k, const double* Vp,
         if (nbp > 0) {
             CAL_TRY(spmv_resid_pair_multi_dev(c, X, ld, reinterpret_cast<const int*>(din + o_col), din + o_lam,
                                               reinterpret_cast<const int*>(din + o_out), k, dpart, nbp));
-            CAL_HIP(c, launch_reduce(dpart, nbp, 2 * k, dres, c->stream));
+            CAL_HIP_OTHER(c, launch_reduce(dpart, nbp, 2 * k, dres, c->stream));
         } else {
             for (int i = 0; i < k; ++i) {
                 SpmvArgs a{};
@@ -1387,7 +1387,7 @@ int cal_compute_ritz_rnorm(cal_ctx* c, const double* Q, int k, const double* Vp,
                 a.x = X + (int64_t)pairs[i].cr * ld;
                 CAL_HIP(c, launch_spmv_resid(a, nullptr, pairs[i].lr, 0.0, n, dpart + (size_t)2 * i * nbr, nbr,
                                              c->stream));
-                CAL_HIP(c, launch_reduce(dpart + (size_t)2 * i * nbr, nbr, 2, dres + 2 * i, c->stream));
+                CAL_HIP_OTHER(c, launch_reduce(dpart + (size_t)2 * i * nbr, nbr, 2, dres + 2 * i, c->stream));
             }
         }
         CAL_TRY(allreduce_sum(c, dres, 2 * k));
@@ -1434,7 +1434,7 @@ int rel_residual(cal_ctx* c, double* x, double l, double* out) {
     int nbk = 0;
     CAL_TRY(spmv_resid_pair_dev(c, x, l, c->d_partial, &nbk));
     if (nbk > 0) {
-        CAL_HIP(c, launch_reduce(c->d_partial, nbk, 2, c->d_red, c->stream));
+        CAL_HIP_OTHER(c, launch_reduce(c->d_partial, nbk, 2, c->d_red, c->stream));
     } else {
         SpmvArgs a{};
         a.rowptr = c->A.rowptr + c->A.ext_off;  // local rows of a stored slab
@@ -1442,10 +1442,10 @@ int rel_residual(cal_ctx* c, double* x, double l, double* out) {
         a.val = c->A.val;
         a.x = x;
         CAL_HIP(c, launch_spmv_resid(a, nullptr, l, 0.0, n, c->d_partial, nb, c->stream));
-        CAL_HIP(c, launch_reduce(c->d_partial, nb, 2, c->d_red, c->stream));
+        CAL_HIP_OTHER(c, launch_reduce(c->d_partial, nb, 2, c->d_red, c->stream));
     }
     CAL_TRY(allreduce_sum(c, c->d_red, 2));
-    CAL_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    CAL_HIP_OTHER(c, hipMemcpyAsync(c->h_red, c->d_red, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     CAL_HIP(c, hipStreamSynchronize(c->stream));
     c->small_pending = false;
     *out = std::sqrt(c->h_red[0]) / std::sqrt(c->h_red[1]);
@@ -1511,7 +1511,7 @@ int cal_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, int n
     CAL_HIP(c, hipMemcpyAsync(L->vcolumn(0), r, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
     double rr = 0.0;
     CAL_TRY(dot_host(c, n, L->vcolumn(0), L->vcolumn(0), &rr));
-    CAL_HIP(c, launch_div(L->col(0), L->vcolumn(0), std::sqrt(rr), n, c->stream));
+    CAL_HIP_OTHER(c, launch_div(L->col(0), L->vcolumn(0), std::sqrt(rr), n, c->stream));
     if (L->newton) {
         CAL_TRY(newton_prologue(c, *L, false));  // lanczos(A,q,2*s,'local') (:65)
     } else {
@@ -1644,7 +1644,7 @@ int cal_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, int n
             CAL_TRY(apply_host(c, n, Qn, V.data() + (size_t)l * m, 1, &X1, nullptr, 0, nullptr));
             double xx = 0.0;
             CAL_TRY(dot_host(c, n, x, x, &xx));
-            CAL_HIP(c, launch_div(L->col(0), x, std::sqrt(xx), n, c->stream));
+            CAL_HIP_OTHER(c, launch_div(L->col(0), x, std::sqrt(xx), n, c->stream));
         }
     }
     // sort descending, keep n_wanted (or all, if not converged) (:180-196)
@@ -1810,7 +1810,7 @@ int cal_impl_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, 
     CAL_HIP(c, hipMemcpyAsync(L->vcolumn(0), r, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
     double rr = 0.0;
     CAL_TRY(dot_host(c, n, L->vcolumn(0), L->vcolumn(0), &rr));
-    CAL_HIP(c, launch_div(L->col(0), L->vcolumn(0), std::sqrt(rr), n, c->stream));  // :53
+    CAL_HIP_OTHER(c, launch_div(L->col(0), L->vcolumn(0), std::sqrt(rr), n, c->stream));  // :53
     if (L->newton) {
         CAL_TRY(newton_prologue(c, *L, true));  // lanczos(A,q,2*s,'full') (:229-234)
     } else {
@@ -1858,7 +1858,7 @@ int cal_impl_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, 
         CAL_TRY(dot_host(c, n, L->col(k), L->col(k), &rk2));
         const double bk = std::sqrt(rk2);
         if (!(bk > 0.0) || !std::isfinite(bk)) return set_error(c, CAL_ERR_NUMERIC, "IRL: zero restart residual");
-        CAL_HIP(c, launch_div(L->col(k), L->col(k), bk, n, c->stream));
+        CAL_HIP_OTHER(c, launch_div(L->col(k), L->col(k), bk, n, c->stream));
         std::fill(L->T.begin(), L->T.end(), 0.0);
         for (int j = 0; j < k; ++j)
             for (int i = 0; i < k; ++i) L->T[i + (size_t)j * L->Tld] = H[i + (size_t)j * m];

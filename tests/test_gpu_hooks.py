@@ -128,21 +128,28 @@ print(json.dumps(dict(T=bool(np.array_equal(a.T, b.T)), rn=bool(np.array_equal(a
     assert res == dict(T=True, rn=True, oe=True, t=4), res
 
 
-def test_normest_and_irl_fused_bitexact():
-    """normest (MATLAB built-in, ca_lanczos.m:258) with both norms and the
-    rescale fused (k_norms2 + k_nrm_div) against the separate dot / reduce /
-    div launches (CAL_TEST_PROLOGUE_SPLIT): 'periodic' CA-Lanczos (which
-    takes normest(A) for its omega recurrence) and a whole implicit-restart
-    solve (normest, the Newton prologue, every restart) give the same bits."""
+@pytest.mark.parametrize("fmt", ["auto", "csr"])
+def test_normest_and_irl_fused_bitexact(fmt):
+    """normest (MATLAB built-in, ca_lanczos.m:258) with both norms fused
+    (k_norms2 + k_nrm_div; on CSR the rescale of x folded into the next
+    SpMV's gathers, mode 3) against the separate dot / reduce / div launches
+    (CAL_TEST_PROLOGUE_SPLIT): 'periodic' CA-Lanczos (which takes normest(A)
+    for its omega recurrence) and a whole implicit-restart solve (normest,
+    the Newton prologue, every restart) give the same bits, in the matrix's
+    own SpMV format and forced to CSR."""
     res = run_testhooks(r"""
 A = cal.matrices.circuit_like(60, seed=3)
 r = ref.matlab_rand(A.shape[0])
+fmt = %r
 outs = []
 for split in (False, True):
     if split:
         os.environ["CAL_TEST_PROLOGUE_SPLIT"] = "1"
-    p = cal.ca_lanczos_ex(A, r, 4, 40, "newton", "periodic")
-    irl = cal.impl_restarted_ca_lanczos(A, r, 40, 6, 4, "newton", "full", 1e-8)
+    ctx = cal.Context(spmv_format=None if fmt == "auto" else fmt).set_matrix(A)
+    assert fmt == "auto" or ctx.spmv_format()[0] == "csr"
+    p = cal.ca_lanczos_ex(A, r, 4, 40, "newton", "periodic", ctx=ctx)
+    irl = cal.impl_restarted_ca_lanczos(A, r, 40, 6, 4, "newton", "full", 1e-8, ctx=ctx)
+    ctx.close()
     outs.append((p, irl))
 (p0, i0), (p1, i1) = outs
 print(json.dumps(dict(na=bool(p0.info["norm_A"] == p1.info["norm_A"] and p0.info["norm_A"] > 0),
@@ -150,7 +157,7 @@ print(json.dumps(dict(na=bool(p0.info["norm_A"] == p1.info["norm_A"] and p0.info
                       nr=bool(i0["num_restarts"] == i1["num_restarts"]),
                       e=bool(np.array_equal(i0["conv_eigs"], i1["conv_eigs"])),
                       q=bool(np.array_equal(i0["Q_conv"], i1["Q_conv"])))))
-""")
+""" % fmt)
     assert all(res.values()), res
 
 
