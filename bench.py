@@ -382,6 +382,7 @@ def max_over_ranks(dist, vals):
 
 
 MFMA_PMC_JSON = os.path.join(ROOT, "profiles", "r05", "pmc", "mfma_summary.json")
+PERSISTENT_JSON = os.path.join(ROOT, "profiles", "r06", "config2", "persistent_powers_probe.json")
 
 
 BOUNDARY_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05", "graph_powers",
@@ -398,8 +399,11 @@ def launch_boundaries(leg):
     7.7-12.8 us on others), and the share is withheld whenever the timed SpMV
     exceeds 1.3x its back-to-back time.  The busy share comes from a rocprofv3 kernel trace of the timed
     steps and the HIP-graph A/B of the matrix powers
-    (profiles/r05/graph_powers/summary.json, tools/gpu_r05_lap2d.sh,
-    tools/gpu_r05_graph.sh)."""
+    (profiles/r05/graph_powers/summary.json; round 5's command files are in
+    git history), and the persistent-launch A/B of round 6: the eight powers
+    as one launch with grid barriers between them against eight launches
+    (profiles/r06/config2/persistent_powers_probe.json,
+    tools/persistent_powers_probe.hip)."""
     out = {}
     b2b = leg.get("spmv_kernel_back_to_back", {}).get("avg_us")
     timed = leg.get("kernel_avg_launch_us", {}).get("spmv")
@@ -416,6 +420,17 @@ def launch_boundaries(leg):
         out["source"] = "profiles/r05/graph_powers/summary.json"
     except (OSError, ValueError, KeyError):
         pass
+    try:
+        for ln in open(PERSISTENT_JSON):
+            d = json.loads(ln)
+            if d.get("N") == 1000:
+                out["persistent_powers"] = {
+                    "eight_launches_us": d["eight_launches_us"],
+                    "one_persistent_launch_us": min(d[k] for k in d if k.startswith("persistent_")),
+                    "grid_barrier_us": d["barriers_only_1percu_us"] / 7.0,
+                    "kept": False, "source": "profiles/r06/config2/persistent_powers_probe.json"}
+    except (OSError, ValueError, KeyError):
+        pass
     return out
 
 
@@ -423,7 +438,7 @@ def gram_mfma(n_loc, gram_avg_ms, b_gram, wname, world):
     """MFMA utilisation of the Gram step (BASELINE north_star): 512 n f64
     flops per sweep of n rows over the live HIP-event average, against the
     f64 matrix peak, with the counter evidence of the current kernels
-    (profiles/r05/pmc/mfma_summary.json, tools/gpu_r05_pmc_mfma.sh: rocprofv3
+    (profiles/r05/pmc/mfma_summary.json, tools/pmc_mfma.sh: rocprofv3
     SQ_INSTS_VALU_MFMA_MOPS_F64 x 512 and SQ_VALU_MFMA_BUSY_CYCLES per
     launch of P1 and pass A on lap3d_215) when this is that workload."""
     flops = 512.0 * n_loc

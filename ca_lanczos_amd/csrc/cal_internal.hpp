@@ -524,6 +524,14 @@ struct cal_ctx {
     long fold_runs = 0, fold_declined = 0;  // fused-TSQR blocks run / declined (explicit-Z path taken)
     double fold_last_est = 0.0;             // the last block's loss-of-orthogonality estimate
     double fold_tol = cal::kFoldTol;        // its acceptance threshold (cal_set_tsqr_fold_tol)
+    // the asynchronous normest (lanczos.cpp normest_async_*): its stream,
+    // completion event, device scratch (x, Sx, partials, norms) and pinned
+    // norms, grown to the matrix once and reused by every solve
+    hipStream_t nest_stream = nullptr;
+    hipEvent_t nest_event = nullptr;
+    double* d_nest = nullptr;
+    double* h_nest = nullptr;
+    size_t nest_cap = 0;
     // the test build only (CAL_TEST_HOOKS): R of ca_lanczos's first block
     // (normalize, ca_lanczos.m:176), read back by cal_test_first_block_R
     std::vector<double> test_R1;
@@ -656,6 +664,9 @@ int halo_exchange(cal_ctx* c, double* x);
 // y = A (x / sqrt(*xnrm)), xnrm a device scalar.
 int spmv_dev(cal_ctx* c, const double* x, double* y, int mode, double shift, double im2,
              const double* xprev, const double* xnrm = nullptr);
+// y = A x (mode 0, or 3 on CSR) on stream st without timers or statistics
+// (one rank; the asynchronous normest)
+hipError_t spmv_on_stream(const cal_ctx* c, const double* x, double* y, int mode, const double* xnrm, hipStream_t st);
 int allreduce_sum(cal_ctx* c, double* d_buf, int64_t count);
 // d_recv[p * count + i] = rank p's d_send[i] (in rank order, every rank)
 int allgather(cal_ctx* c, const double* d_send, double* d_recv, int64_t count);

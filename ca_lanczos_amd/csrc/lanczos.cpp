@@ -227,6 +227,129 @@ static int normest_dev(cal_ctx* c, double* out) {
     }
 }
 
+// ---- normest on its own stream (one rank) ----------------------------------
+// The same iteration as normest_dev -- the same kernels in the same order, so
+// the same e to the bit -- enqueued on the context's normest stream in chunks
+// of kNestChunk iterations, so that it runs beside whatever the caller
+// enqueues next on the solver's stream (the IRL's Newton prologue and first CA
+// blocks: normest(A) is needed only at the first convergence test,
+// impl_restarted_ca_lanczos.m:37-40,127-143).  The host never waits on it
+// until normest_async_finish: normest_async_poll (non-blocking) replays
+// MATLAB's stopping test over a finished chunk and enqueues the next one.
+// x, Sx and the partials are the normest's own scratch (c->d_nest), nothing
+// the solver's stream touches.
+namespace {
+constexpr int kNestChunk = 16;
+struct NormestAsync {
+    bool active = false, done = false;
+    bool gather_div = false;   // CSR: x rescaled in the next SpMV's gathers (mode 3)
+    double e = 0.0, e0 = 0.0;  // MATLAB's e, e0
+    int cnt = 0;               // iterations replayed
+    int chunk = 0;             // chunks enqueued
+    const double* xnrm = nullptr;
+    double result = 0.0;
+};
+}  // namespace
+
+static int normest_async_enqueue_chunk(cal_ctx* c, NormestAsync& J) {
+    const int64_t n = c->A.n_local;
+    const int nb = dot_blocks(n);
+    double* x = c->d_nest;
+    double* y = x + n;
+    double* part = y + n;
+    double* d_nrm = part + 2 * (size_t)nb;  // [0] = x0'x0, then 2 per iteration of the chunk
+    const hipStream_t st = c->nest_stream;
+    for (int i = 0; i < kNestChunk; ++i) {
+        CAL_HIP(c, spmv_on_stream(c, x, y, J.xnrm ? 3 : 0, J.xnrm, st));  // Sx = S*x
+        CAL_HIP(c, spmv_on_stream(c, y, x, 0, nullptr, st));              // x = S'*Sx
+        double* dst = d_nrm + 1 + 2 * i;
+        if (J.gather_div) {
+            CAL_HIP(c, launch_normest_norms_only(x, y, n, part, dst, st));
+            J.xnrm = dst;
+        } else {
+            CAL_HIP(c, launch_normest_norms(x, y, n, part, dst, st));
+        }
+    }
+    CAL_HIP(c, hipMemcpyAsync(c->h_nest, d_nrm, (1 + 2 * kNestChunk) * sizeof(double), hipMemcpyDeviceToHost, st));
+    CAL_HIP(c, hipEventRecord(c->nest_event, st));
+    J.chunk++;
+    return 0;
+}
+
+static int normest_async_begin(cal_ctx* c, NormestAsync& J) {
+    J = NormestAsync();
+    const int64_t n = c->A.n_local;
+    const int nb = dot_blocks(n);
+    const size_t need = 2 * (size_t)n + 2 * (size_t)nb + 1 + 2 * kNestChunk;
+    if (!c->nest_stream) CAL_HIP(c, hipStreamCreateWithFlags(&c->nest_stream, hipStreamNonBlocking));
+    if (!c->nest_event) CAL_HIP(c, hipEventCreateWithFlags(&c->nest_event, hipEventDisableTiming));
+    if (need > c->nest_cap) {
+        if (c->d_nest) CAL_HIP(c, hipFree(c->d_nest));
+        c->d_nest = nullptr;
+        CAL_HIP(c, scratch_malloc((void**)&c->d_nest, need * sizeof(double)));
+        if (!c->h_nest)
+            CAL_HIP(c, hipHostMalloc((void**)&c->h_nest, (1 + 2 * kNestChunk) * sizeof(double), hipHostMallocDefault));
+        c->nest_cap = need;
+    }
+    double* x = c->d_nest;
+    double* part = x + 2 * n;
+    double* d_nrm = part + 2 * (size_t)nb;
+    const hipStream_t st = c->nest_stream;
+    // the matrix must be on the device before the normest stream reads it
+    CAL_HIP(c, hipEventRecord(c->nest_event, c->stream));
+    CAL_HIP(c, hipStreamWaitEvent(st, c->nest_event, 0));
+    // x = sum(abs(S))', e = norm(x) (kept on the device), x = x/e
+    CAL_HIP(c, launch_abs_rowsum(c->A.rowptr + c->A.ext_off, c->A.val, n, x, st));
+    CAL_HIP(c, launch_dot(x, x, n, part, nb, st));
+    CAL_HIP(c, launch_reduce(part, nb, 1, d_nrm, st));
+    CAL_HIP(c, launch_div_sqrt(x, x, d_nrm, n, st));
+    J.gather_div = !c->A.use_pat;
+    J.active = true;
+    return normest_async_enqueue_chunk(c, J);
+}
+
+// The finished chunk's norms: MATLAB's stopping test replayed (normest_dev's
+// loop); enqueue the next chunk if it did not stop.  wait: block on the chunk.
+static int normest_async_poll(cal_ctx* c, NormestAsync& J, bool wait) {
+    while (J.active && !J.done) {
+        if (wait) CAL_HIP(c, hipEventSynchronize(c->nest_event));
+        else {
+            const hipError_t q = hipEventQuery(c->nest_event);
+            if (q == hipErrorNotReady) return 0;
+            CAL_HIP(c, q);
+        }
+        const double* h = c->h_nest;
+        if (J.chunk == 1) {
+            J.e = std::sqrt(h[0]);
+            if (J.e == 0.0) {  // normest of a zero matrix
+                J.result = 0.0;
+                J.done = true;
+                return 0;
+            }
+        }
+        for (int i = 0; i < kNestChunk; ++i) {
+            if (!(std::fabs(J.e - J.e0) > 1.0e-6 * J.e && J.cnt <= 100)) {
+                J.result = J.e;
+                J.done = true;
+                return 0;
+            }
+            J.e0 = J.e;
+            J.e = std::sqrt(h[1 + 2 * i]) / std::sqrt(h[2 + 2 * i]);
+            ++J.cnt;
+        }
+        CAL_TRY(normest_async_enqueue_chunk(c, J));
+        if (!wait) return 0;
+    }
+    return 0;
+}
+
+static int normest_async_finish(cal_ctx* c, NormestAsync& J, double* out) {
+    CAL_TRY(normest_async_poll(c, J, true));
+    J.active = false;
+    *out = J.result;
+    return 0;
+}
+
 // ---- periodic: the omega recurrence (ca_lanczos.m:464-549) -----------------
 static void update_omega(LanczosState& L, const std::vector<double>& alpha, const std::vector<double>& beta) {
     const int s = L.s;
@@ -1805,14 +1928,31 @@ int cal_impl_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, 
     L->Tld = (int)qcols;
     L->T.assign((size_t)L->Tld * L->Tld, 0.0);
     double norm_A = 0.0;
-    CAL_TRY(normest_dev(c, &norm_A));  // :37-40
-    tol = tol * norm_A;
+    // normest(A) (:37-40) on its own stream beside the prologue and the first
+    // CA blocks (one rank); it is first needed by the convergence test
+    NormestAsync nest;
+    struct NestGuard {  // an early return leaves no normest running
+        cal_ctx* c;
+        NormestAsync* J;
+        ~NestGuard() {
+            if (J->active) hipStreamSynchronize(c->nest_stream);
+            J->active = false;
+        }
+    } nest_guard{c, &nest};
+    const double tol_rel = tol;
+    if (!c->comm || c->comm->nranks <= 1) {
+        CAL_TRY(normest_async_begin(c, nest));
+    } else {
+        CAL_TRY(normest_dev(c, &norm_A));
+        tol = tol_rel * norm_A;
+    }
     CAL_HIP(c, hipMemcpyAsync(L->vcolumn(0), r, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
     double rr = 0.0;
     CAL_TRY(dot_host(c, n, L->vcolumn(0), L->vcolumn(0), &rr));
     CAL_HIP_OTHER(c, launch_div(L->col(0), L->vcolumn(0), std::sqrt(rr), n, c->stream));  // :53
     if (L->newton) {
         CAL_TRY(newton_prologue(c, *L, true));  // lanczos(A,q,2*s,'full') (:229-234)
+        if (nest.active) CAL_TRY(normest_async_poll(c, nest, false));
     } else {
         L->Bk.assign((size_t)(s + 1) * s, 0.0);
         for (int j = 0; j < s; ++j) L->Bk[(j + 1) + (size_t)j * (s + 1)] = 1.0;
@@ -1826,7 +1966,14 @@ int cal_impl_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, 
         ++it;
         // extend to m vectors (:85-94)
         double bprev = it == 1 ? 0.0 : L->T[k + (size_t)(k - 1) * L->Tld];
-        for (int nv = it == 1 ? 0 : k; nv < m; nv += s) CAL_TRY(irl_block(c, *L, nv, &bprev));
+        for (int nv = it == 1 ? 0 : k; nv < m; nv += s) {
+            if (nest.active) CAL_TRY(normest_async_poll(c, nest, false));
+            CAL_TRY(irl_block(c, *L, nv, &bprev));
+        }
+        if (nest.active) {
+            CAL_TRY(normest_async_finish(c, nest, &norm_A));
+            tol = tol_rel * norm_A;
+        }
         const double beta_m = L->T[m + (size_t)(m - 1) * L->Tld];
         // exact shifts: the p smallest-modulus Ritz values of T_m (:96-107)
         std::vector<double> H((size_t)m * m), W((size_t)m * m, 0.0), w, Ym;

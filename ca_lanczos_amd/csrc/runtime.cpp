@@ -621,6 +621,33 @@ int spmv_range(cal_ctx* c, int64_t o, int64_t len, const double* x, double* y, i
     return 0;
 }
 
+// y = A x on stream st, no timer and no statistics: the asynchronous normest
+// (lanczos.cpp) on its own stream beside the solver's.  One rank (no halo).
+// Mode 0, or 3 on CSR (y = A (x / sqrt(*xnrm))).
+hipError_t spmv_on_stream(const cal_ctx* c, const double* x, double* y, int mode, const double* xnrm, hipStream_t st) {
+    const DevMatrix& A = c->A;
+    if (mode != 0 && mode != 3) return hipErrorInvalidValue;
+    if (A.use_pat) {
+        if (mode != 0) return hipErrorInvalidValue;
+        return launch_spmv_pat(pat_args(A, A.ext_off, A.n_local, x, y, 0, 0.0, 0.0, nullptr), st);
+    }
+    SpmvArgs a;
+    a.rowptr = A.rowptr;
+    a.col = A.col;
+    a.val = A.val;
+    a.blk = A.blk;
+    a.nblk = A.nblk;
+    a.x = x;
+    a.y = y;
+    a.xprev = nullptr;
+    a.shift = 0.0;
+    a.im2 = 0.0;
+    a.xnrm = xnrm;
+    a.mode = mode | (A.nit << 8);
+    a.nt = (int64_t)12 * A.nnz > ((int64_t)256 << 20) ? 1 : 0;
+    return launch_spmv(a, st);
+}
+
 int spmv_resid_pair_blocks(cal_ctx* c) {
     const DevMatrix& A = c->A;
     if (!c->has_A || !A.use_pat || !A.use_pair) return 0;
@@ -876,6 +903,7 @@ void cal_destroy(cal_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
+    if (c->nest_stream) hipStreamSynchronize(c->nest_stream);
     cal_lanczos_free_state(c);
     cal::comm_destroy(c);
     free_matrix(c);
@@ -897,6 +925,10 @@ void cal_destroy(cal_ctx* c) {
     if (c->d_fold) hipFree(c->d_fold);
     if (c->h_pub) hipHostFree(c->h_pub);
     if (c->aux_stream) hipStreamDestroy(c->aux_stream);
+    if (c->d_nest) hipFree(c->d_nest);
+    if (c->h_nest) hipHostFree(c->h_nest);
+    if (c->nest_event) hipEventDestroy(c->nest_event);
+    if (c->nest_stream) hipStreamDestroy(c->nest_stream);
 
     hipStreamDestroy(c->stream);
     delete c;

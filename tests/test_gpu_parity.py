@@ -1091,3 +1091,28 @@ def test_production_library_has_no_test_hooks(cal, ref):
     p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-2000:]
     assert p.stdout.strip().splitlines()[-1] == "0"
+
+
+@pytest.mark.parametrize("fmt", ["auto", "csr"])
+def test_impl_restart_normest_async_matches_sync(cal, ref, fmt):
+    """The implicit restart runs normest(A) on its own stream beside the
+    Newton prologue and the first CA blocks (lanczos.cpp normest_async_*);
+    'periodic' CA-Lanczos runs the synchronous normest_dev.  Same kernels in
+    the same order: the same norm to the bit, in the matrix's own SpMV format
+    and forced to CSR (the rescale in the gathers, mode 3); and the restart
+    still matches the oracle's normest-scaled convergence (same restart count
+    and eigenvalues as with the synchronous normest's value)."""
+    A = cal.matrices.circuit_like(60, seed=3)
+    r = ref.matlab_rand(A.shape[0])
+    ctx = cal.Context(spmv_format=None if fmt == "auto" else fmt).set_matrix(A)
+    p = cal.ca_lanczos_ex(A, r, 4, 40, "newton", "periodic", ctx=ctx)
+    irl = cal.impl_restarted_ca_lanczos(A, r, 40, 6, 4, "newton", "full", 1e-8, ctx=ctx)
+    irl2 = cal.impl_restarted_ca_lanczos(A, r, 40, 6, 4, "newton", "full", 1e-8, ctx=ctx)
+    ctx.close()
+    assert p.info["norm_A"] > 0 and irl["norm_A"] == p.info["norm_A"], (irl["norm_A"], p.info["norm_A"])
+    assert irl2["norm_A"] == irl["norm_A"] and irl2["num_restarts"] == irl["num_restarts"]
+    assert np.array_equal(irl2["conv_eigs"], irl["conv_eigs"])
+    exp = ref.impl_restarted_ca_lanczos(A, r, 40, 6, 4, "newton", "full", 1.0e-8)
+    assert abs(irl["norm_A"] - exp["norm_A"]) <= 1e-12 * exp["norm_A"]
+    assert irl["num_restarts"] == exp["num_restarts"]
+    assert np.max(np.abs(irl["conv_eigs"] - exp["conv_eigs"])) <= 1e-10 * exp["norm_A"]
