@@ -248,6 +248,7 @@ struct NormestAsync {
     int chunk = 0;             // chunks enqueued
     const double* xnrm = nullptr;
     double result = 0.0;
+    int timer = -1;  // the span on the normest stream (timer kind "normest")
 };
 }  // namespace
 
@@ -271,6 +272,7 @@ static int normest_async_enqueue_chunk(cal_ctx* c, NormestAsync& J) {
         }
     }
     CAL_HIP(c, hipMemcpyAsync(c->h_nest, d_nrm, (1 + 2 * kNestChunk) * sizeof(double), hipMemcpyDeviceToHost, st));
+    timer_end_on(c, J.timer, st);  // re-recorded per chunk: the last one ends the span
     CAL_HIP(c, hipEventRecord(c->nest_event, st));
     J.chunk++;
     return 0;
@@ -298,6 +300,7 @@ static int normest_async_begin(cal_ctx* c, NormestAsync& J) {
     // the matrix must be on the device before the normest stream reads it
     CAL_HIP(c, hipEventRecord(c->nest_event, c->stream));
     CAL_HIP(c, hipStreamWaitEvent(st, c->nest_event, 0));
+    J.timer = timer_begin_on(c, 6, st);
     // x = sum(abs(S))', e = norm(x) (kept on the device), x = x/e
     CAL_HIP(c, launch_abs_rowsum(c->A.rowptr + c->A.ext_off, c->A.val, n, x, st));
     CAL_HIP(c, launch_dot(x, x, n, part, nb, st));
@@ -1940,7 +1943,7 @@ int cal_impl_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, 
         }
     } nest_guard{c, &nest};
     const double tol_rel = tol;
-    if (!c->comm || c->comm->nranks <= 1) {
+    if ((!c->comm || c->comm->nranks <= 1) && !test_switch("CAL_TEST_NORMEST_SYNC")) {
         CAL_TRY(normest_async_begin(c, nest));
     } else {
         CAL_TRY(normest_dev(c, &norm_A));

@@ -968,6 +968,7 @@ int cal_timer_bytes(cal_ctx* c, const char* kind, double* bytes) {
     else if (!strcmp(kind, "other")) k = 3;
     else if (!strcmp(kind, "allreduce")) k = 4;
     else if (!strcmp(kind, "halo")) k = 5;
+    else if (!strcmp(kind, "normest")) k = 6;
     else if (strcmp(kind, "all")) return set_error(c, CAL_ERR_ARG, "unknown timer kind");
     double b = 0.0;
     for (auto& r : c->timers)
@@ -985,6 +986,7 @@ int cal_timer_read(cal_ctx* c, const char* kind, int64_t* count, double* total_m
     else if (!strcmp(kind, "other")) k = 3;
     else if (!strcmp(kind, "allreduce")) k = 4;
     else if (!strcmp(kind, "halo")) k = 5;
+    else if (!strcmp(kind, "normest")) k = 6;
     else if (strcmp(kind, "all")) return set_error(c, CAL_ERR_ARG, "unknown timer kind");
     CAL_HIP(c, hipStreamSynchronize(c->stream));
     int64_t cnt = 0;

@@ -51,7 +51,8 @@ void cal_destroy(cal_ctx* ctx);
 const char* cal_last_error(const cal_ctx* ctx);
 int cal_synchronize(cal_ctx* ctx);
 /* Kernel-duration timer (HIP events on the context stream).  kind: "spmv",
- * "gram", "apply", "other", "allreduce", "halo" (the RCCL calls), "all".
+ * "gram", "apply", "other", "allreduce", "halo" (the RCCL calls), "normest"
+ * (the span of the implicit restart's normest on its own stream), "all".
  * Returns the number of launches timed and their summed duration since the
  * last reset. */
 int cal_timer_enable(cal_ctx* ctx, int on);
