@@ -522,8 +522,36 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
         timer_end(c, t);
     }
     CAL_TRY(coef(1, 0));
-    // pass B: Q = [Qp | W M1] M2, one store
-    {
+    // pass B: Q = [Qp | W M1] M2, one store -- with the 'full' projection's
+    // Gram [Qp | Q | Qold]' Q when the caller asked for it (k_passb_wide)
+    const bool pbw = c->pbw.want && w == 9 && m == 8 && WP == 17 && MO == 8 &&
+                     passb_wide_tiles(c->pbw.qold.total) <= kPassbWideMaxTiles && Qp.nseg == 1;
+    c->pbw.want = false;
+    c->pbw.ready = false;
+    if (pbw) {
+        const int ntw = passb_wide_tiles(c->pbw.qold.total);
+        const size_t ent = (size_t)128 * ntw;
+        const int pblocks = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, kRowGramBlocks));
+        CAL_TRY(ensure_partial(c, (size_t)pblocks * ent));
+        if (ent > c->pbw.cap) {
+            if (c->pbw.d) CAL_HIP(c, hipFree(c->pbw.d));
+            if (c->pbw.h) CAL_HIP(c, hipHostFree(c->pbw.h));
+            c->pbw.d = c->pbw.h = nullptr;
+            c->pbw.cap = 0;
+            CAL_HIP(c, scratch_malloc((void**)&c->pbw.d, ent * sizeof(double)));
+            CAL_HIP(c, hipHostMalloc((void**)&c->pbw.h, ent * sizeof(double), hipHostMallocDefault));
+            c->pbw.cap = ent;
+        }
+        if (!c->pbw.ev) CAL_HIP(c, hipEventCreateWithFlags(&c->pbw.ev, hipEventDisableTiming));
+        // bytes: pass B's, plus the Qold columns the Gram reads
+        const int t = timer_begin(c, 2, 8.0 * n * (wp + m + c->pbw.qold.total));
+        CAL_HIP(c, launch_passb_wide(cw, d_mbuf, ol, c->pbw.qold, n, pblocks, c->d_partial, gate, c->stream));
+        timer_end(c, t);
+        CAL_HIP_OTHER(c, launch_reduce(c->d_partial, pblocks, (int64_t)ent, c->pbw.d, c->stream));
+        CAL_HIP_OTHER(c, hipMemcpyAsync(c->pbw.h, c->pbw.d, ent * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        CAL_HIP(c, hipEventRecord(c->pbw.ev, c->stream));
+        c->pbw.ntw = ntw;
+    } else {
         const int t = timer_begin(c, 2, 8.0 * n * (wp + m));
         CAL_HIP(c, launch_rowapply(cw, d_mbuf, wp, m, ol, 3, w, n, (int)((n + 255) / 256), c->d_partial, c->stream,
                                    gate));
@@ -538,7 +566,8 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
     // pass B): poll the sequence word; if the stream drains without it, the
     // kernels failed -- report the stream's error
     CAL_TRY(wait_published(c, h_seq, seq));
-    if (h_out[512] != 0.0 || h_out[513] != 0.0) return 1;
+    if (h_out[512] != 0.0 || h_out[513] != 0.0) return 1;  // (pass B and its Gram skipped: pbw stays not ready)
+    c->pbw.ready = pbw;
     std::copy(h_out, h_out + (size_t)m * m, R);
     std::copy(h_out + 256, h_out + 256 + (size_t)w * m, Rq);
     *reorth = h_out[514] != 0.0;
@@ -953,7 +982,7 @@ static int pn_tsqr(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, bool 
 }
 
 int project_and_normalize_dev(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, bool doreorth,
-                              const PanelOut& Qout, double* Rq, double* R, PNResult* res) {
+                              const PanelOut& Qout, double* Rq, double* R, PNResult* res, const double* G1_pre) {
     const int w = Qp.total, m = X.total;
     if (Qp.nseg + X.nseg > kMaxSeg) return set_error(c, CAL_ERR_ARG, "projectAndNormalize: too many segments");
     if (use_tsqr(c, m, c->tier1) || (m > 16 && tsqr_ok(m))) return pn_tsqr(c, n, Qp, X, doreorth, Qout, Rq, R, res);
@@ -994,7 +1023,8 @@ int project_and_normalize_dev(cal_ctx* c, int64_t n, const Panel& Qp, const Pane
         }
     } else {
         std::vector<double> G1((size_t)wp * m);
-        CAL_TRY(gram_host(c, n, W, X, G1.data()));
+        if (G1_pre) std::copy(G1_pre, G1_pre + (size_t)wp * m, G1.begin());  // formed with X (k_passb_wide)
+        else CAL_TRY(gram_host(c, n, W, X, G1.data()));
         for (int j = 0; j < m; ++j) {
             for (int i = 0; i < w; ++i) C[i + (size_t)j * w] = G1[i + (size_t)j * wp];
             for (int i = 0; i < m; ++i) GZ[i + (size_t)j * m] = G1[w + i + (size_t)j * wp];

@@ -298,6 +298,13 @@ hipError_t launch_orth_coef(int phase, const double* tile, double* st, double* m
 constexpr int kRowGramBlocks = CAL_ROWGRAM_BLOCKS;
 hipError_t launch_rowgram(const ColList& P, int nt, bool has_extra, int64_t n, int blocks, double* partial,
                           hipStream_t st);
+// pass B (w = 9, m = 8) fused with G = [Qp | Q_new | Qold]' Q_new (kernels.hip
+// k_passb_wide): passb_wide_tiles(wold) 16-column groups, at most
+// kPassbWideMaxTiles; partial entries j (16 tiles) + a, j < 8
+constexpr int kPassbWideMaxTiles = 12;
+int passb_wide_tiles(int wold);
+hipError_t launch_passb_wide(const ColList& P, const double* dM, const OutList& Y, const Panel& Qold, int64_t n,
+                             int blocks, double* partial, const double* gate, hipStream_t st);
 hipError_t launch_dot(const double* x, const double* y, int64_t n, double* partial, int blocks,
                       hipStream_t st);
 int dot_blocks(int64_t n);
@@ -499,6 +506,19 @@ struct cal_ctx {
     // set by lanczos_step: work to enqueue after a block orthogonalisation is
     // enqueued and before the host waits for its R (orth_device)
     std::function<int()> pre_wait;
+    // 'full' orthogonalisation (lanczos_step): the local block's pass B also
+    // forms the next projection's Gram [Qp | Q_new | Qold]' Q_new
+    // (k_passb_wide); want/qold set by the caller, ready once the reduced
+    // Gram's copy to h_pbw is enqueued (pbw_event after it)
+    struct {
+        bool want = false, ready = false;
+        cal::Panel qold{};
+        int ntw = 0;
+        double* d = nullptr;
+        double* h = nullptr;
+        size_t cap = 0;
+        hipEvent_t ev = nullptr;
+    } pbw;
     bool orth_redone = false;  // the last block was redone on the host path
     hipEvent_t orth_event = nullptr;
     // device-coefficient block orthogonalisation: the pinned host-mapped
@@ -646,8 +666,11 @@ int normalize_dev(cal_ctx* c, int64_t n, const Panel& X, const PanelOut& Qout, d
                   bool* shifted, int p1_blocks = 0);
 // projectAndNormalize of X (n x m) against one block Qp (n x w): QZ into Qout,
 // Rq (w x m) and R (m x m) on host.  Mirrors projectAndNormalize.m:3-90.
+// G1_pre (optional, wide Qp only): [Qp | X]' X ((w+m) x m), already formed
+// (the local block's k_passb_wide): the Gram sweep is skipped.
 int project_and_normalize_dev(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, bool doreorth,
-                              const PanelOut& Qout, double* Rq, double* R, PNResult* res);
+                              const PanelOut& Qout, double* Rq, double* R, PNResult* res,
+                              const double* G1_pre = nullptr);
 // project.m:7-58 on device blocks (block MGS across blocks, CGS within); X in place.
 int project_blocks(cal_ctx* c, int64_t n, int64_t ld, int nb, const std::vector<double*>& dQ, const int* widths,
                    int m, double* dX, bool doreorth, std::vector<std::vector<double>>& R);

@@ -3200,6 +3200,226 @@ hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, co
     return hipGetLastError();
 }
 
+// k_passb_wide: pass B of the s = 8 block orthogonalisation (k_rowapply<17,
+// 8, CHAIN>: the same FMA sequence, so the same Q bits) fused with the Gram
+// the 'full' orthogonalisation needs next (ca_lanczos.m:197:
+// projectAndNormalize({Q(:,1:(k-1)s+1)}, Q_new)): G = A' Q_new with
+// A = [Qp (9) | Q_new (8) | Qold (wold)] -- the block's own columns from
+// registers, only Qold = Q(:,1:(k-2)s) loaded -- so the wide Gram sweep no
+// longer re-reads Qp and Q_new.  One row per lane, grid-stride; per 64-row
+// wave group the 16-column A groups go through the wave's LDS rows onto
+// v_mfma_f64_16x16x4f64 with B = Q_new (columns 8..15 zero), the next
+// group's Qold loads in flight during the current group's MFMAs.  Partials
+// entry-major: entry j (16 NTW) + a (a = A column, j < 8) of block b at
+// partial[entry * nblocks + b].  gate: as k_rowapply's.
+#ifndef CAL_PBW_PREFETCH
+#define CAL_PBW_PREFETCH 0
+#endif
+template <int NTW, bool NTS>
+__global__ __launch_bounds__(256) void k_passb_wide(ColList P, const double* __restrict__ M, OutList Y, Panel Qold,
+                                                    int64_t n, double* __restrict__ partial,
+                                                    const double* __restrict__ gate) {
+    constexpr int WPMAX = 17, MOUT = 8, WQ = 9;
+    constexpr int MSZ = WPMAX * MOUT * 2 + MOUT * MOUT;
+    constexpr int TLD = 17;
+    constexpr int WTILE = 64 * TLD;  // a wave's rows: Q_new (for B), then each A group
+    constexpr int RT = 4;            // tiles per step of the cross-wave reduction (3 x RT x 256 <= 4 WTILE)
+    constexpr int LDSZ = 4 * WTILE;  // 35 KB: four blocks per CU
+    if (gate && (gate[0] != 0.0 || gate[1] != 0.0)) return;  // block-uniform
+    __shared__ __attribute__((aligned(16))) double Ms[MSZ];
+    __shared__ double lds[LDSZ];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, c16 = lane & 15, g = lane >> 4;
+    for (int e = tid; e < MSZ; e += 256) Ms[e] = M[e];
+    __syncthreads();
+    double* const tw = lds + wave * WTILE;
+    const int wold = Qold.total;
+    d4 acc[NTW];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+    const double* const* pc = P.p;
+    double* const* yc = Y.p;
+    const int64_t nch = (n + 255) / 256;
+#if CAL_PBW_PREFETCH
+    // the next chunk's W row loads fly during this chunk's Gram groups
+    double pn[WPMAX];
+    {
+        const int64_t r0 = (int64_t)blockIdx.x * 256 + tid;
+        const int64_t rr0 = r0 < n ? r0 : n - 1;
+#pragma unroll
+        for (int c = 0; c < WPMAX; ++c) pn[c] = pc[c][rr0];
+    }
+#endif
+    for (int64_t ci = blockIdx.x; ci < nch; ci += gridDim.x) {
+        asm volatile("" ::: "memory");
+        const int64_t r = ci * 256 + tid;
+        const bool in = r < n;
+        const int64_t rr = in ? r : n - 1;
+        double p[WPMAX];
+#if CAL_PBW_PREFETCH
+#pragma unroll
+        for (int c = 0; c < WPMAX; ++c) p[c] = pn[c];
+        if (ci + gridDim.x < nch) {
+            const int64_t r1 = (ci + gridDim.x) * 256 + tid;
+            const int64_t rr1 = r1 < n ? r1 : n - 1;
+#pragma unroll
+            for (int c = 0; c < WPMAX; ++c) pn[c] = pc[c][rr1];
+        }
+#else
+#pragma unroll
+        for (int c = 0; c < WPMAX; ++c) p[c] = pc[c][rr];
+#endif
+#pragma unroll
+        for (int c = 0; c < WPMAX; ++c) p[c] = in ? p[c] : 0.0;
+        // Q1 = P M1, then Q_new = [P(0:9) | Q1] [M2p; M2y] (k_rowapply CHAIN)
+        double y[MOUT];
+#pragma unroll
+        for (int j = 0; j < MOUT; ++j) y[j] = 0.0;
+#pragma unroll
+        for (int c = 0; c < WPMAX; ++c) {
+#pragma unroll
+            for (int j = 0; j < MOUT; ++j) asm volatile("" : "+v"(y[j])::"memory");
+            double mrow[MOUT];
+#pragma unroll
+            for (int j = 0; j < MOUT; j += 2) {
+                const d2 t = *reinterpret_cast<const d2*>(&Ms[c * MOUT + j]);
+                mrow[j] = t[0];
+                mrow[j + 1] = t[1];
+            }
+#pragma unroll
+            for (int j = 0; j < MOUT; ++j) y[j] = __builtin_fma(p[c], mrow[j], y[j]);
+        }
+        {
+            const double* M2p = Ms + WPMAX * MOUT;
+            const double* M2y = Ms + 2 * WPMAX * MOUT;
+            double y2[MOUT];
+#pragma unroll
+            for (int j = 0; j < MOUT; ++j) y2[j] = 0.0;
+#pragma unroll
+            for (int c = 0; c < WPMAX + MOUT; ++c) {
+#pragma unroll
+                for (int j = 0; j < MOUT; ++j) asm volatile("" : "+v"(y2[j])::"memory");
+                const double src = c < WPMAX ? p[c < WPMAX ? c : 0] : y[c >= WPMAX ? c - WPMAX : 0];
+                const double* row = c < WPMAX ? M2p + c * MOUT : M2y + (c - WPMAX) * MOUT;
+                double mrow[MOUT];
+#pragma unroll
+                for (int j = 0; j < MOUT; j += 2) {
+                    const d2 t = *reinterpret_cast<const d2*>(&row[j]);
+                    mrow[j] = t[0];
+                    mrow[j + 1] = t[1];
+                }
+#pragma unroll
+                for (int j = 0; j < MOUT; ++j) y2[j] = __builtin_fma(src, mrow[j], y2[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < MOUT; ++j) y[j] = y2[j];
+        }
+        if (in) {
+#pragma unroll
+            for (int j = 0; j < MOUT; ++j) {
+                if constexpr (NTS) __builtin_nontemporal_store(y[j], &yc[j][r]);
+                else yc[j][r] = y[j];
+            }
+        }
+        // the Gram: Q_new rows (B) through the wave's rows, then the A groups
+        // [Qp | Q_new | Qold] through the same rows
+#pragma unroll
+        for (int j = 0; j < MOUT; ++j) tw[lane * TLD + j] = y[j];
+        double nxt[2][16];  // the next two groups' Qold values (group t in slot t & 1)
+        auto load_old = [&](int t) {
+            if (t >= NTW) return;
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+                const int k = 16 * t + c - (WQ + MOUT);  // Qold column
+                nxt[t & 1][c] = (k >= 0 && k < wold && in) ? pcol(Qold, k)[rr] : 0.0;
+            }
+        };
+        load_old(1);
+        load_old(2);
+        wave_lds_sync();
+        double bv[16];
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) bv[kk] = c16 < MOUT ? tw[(4 * kk + g) * TLD + c16] : 0.0;
+        wave_lds_sync();
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) {
+            double a[16];
+            if (t == 0) {  // [Qp (9) | Q_new (0:7)]
+#pragma unroll
+                for (int c = 0; c < 16; ++c) a[c] = c < WQ ? p[c < WQ ? c : 0] : y[c >= WQ ? c - WQ : 0];
+            } else {
+#pragma unroll
+                for (int c = 0; c < 16; ++c) a[c] = nxt[t & 1][c];
+                load_old(t + 2);
+            }
+            if (t == 1) a[0] = y[7];  // column 16 = Q_new(:, 7)
+#pragma unroll
+            for (int c = 0; c < 16; ++c) tw[lane * TLD + c] = a[c];
+            wave_lds_sync();
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk) acc[t] = mfma64(tw[(4 * kk + g) * TLD + c16], bv[kk], acc[t]);
+            wave_lds_sync();
+        }
+    }
+    // the block's partials, RT tiles at a time through the tiles' LDS
+    auto red = reinterpret_cast<double (*)[RT][64][4]>(lds);  // [3][RT][64][4]
+    const int64_t nb = gridDim.x;
+    double* out = partial + blockIdx.x;
+#pragma unroll
+    for (int t0 = 0; t0 < NTW; t0 += RT) {
+        __syncthreads();  // the tiles (or the previous step's partials) are read
+        if (wave > 0) {
+#pragma unroll
+            for (int t = t0; t < (t0 + RT < NTW ? t0 + RT : NTW); ++t)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) red[wave - 1][t - t0][lane][q] = acc[t][q];
+        }
+        __syncthreads();
+        if (wave == 0 && c16 < MOUT) {
+#pragma unroll
+            for (int t = t0; t < (t0 + RT < NTW ? t0 + RT : NTW); ++t)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    double v = acc[t][q];
+                    v = v + red[0][t - t0][lane][q];
+                    v = v + red[1][t - t0][lane][q];
+                    v = v + red[2][t - t0][lane][q];
+                    const int a = 16 * t + g + 4 * q, j = c16;
+                    out[(int64_t)(j * 16 * NTW + a) * nb] = v;
+                }
+        }
+    }
+}
+
+int passb_wide_tiles(int wold) { return (9 + 8 + wold + 15) / 16; }
+
+hipError_t launch_passb_wide(const ColList& P, const double* dM, const OutList& Y, const Panel& Qold, int64_t n,
+                             int blocks, double* partial, const double* gate, hipStream_t st) {
+    const int ntw = passb_wide_tiles(Qold.total);
+    const bool nts = (int64_t)n * 8 * (17 + 8) > ((int64_t)256 << 20);  // as launch_rowapply's pass B
+    dim3 g(blocks), b(256);
+#define CAL_PBW(T)                                                                                              \
+    case T:                                                                                                     \
+        if (nts) hipLaunchKernelGGL((k_passb_wide<T, true>), g, b, 0, st, P, dM, Y, Qold, n, partial, gate);  \
+        else hipLaunchKernelGGL((k_passb_wide<T, false>), g, b, 0, st, P, dM, Y, Qold, n, partial, gate);     \
+        break;
+    switch (ntw) {
+        CAL_PBW(2)
+        CAL_PBW(3)
+        CAL_PBW(4)
+        CAL_PBW(5)
+        CAL_PBW(6)
+        CAL_PBW(7)
+        CAL_PBW(8)
+        CAL_PBW(9)
+        CAL_PBW(10)
+        CAL_PBW(11)
+        CAL_PBW(12)
+        default: return hipErrorInvalidValue;
+    }
+#undef CAL_PBW
+    return hipGetLastError();
+}
+
 // Row-parallel tile Gram: tile = P.p[0..nt) (nt <= 16), extra = P.p[16] if
 // has_extra.  Same partial layout as k_tilegram.
 hipError_t launch_rowgram(const ColList& P, int nt, bool has_extra, int64_t n, int blocks, double* partial,

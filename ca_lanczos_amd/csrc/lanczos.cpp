@@ -1247,7 +1247,16 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
             res.reorth = ro;
             res.rank = rk;
         } else {
+            // 'full' (ca_lanczos.m:197): this block's pass B also forms the
+            // projection's Gram [Q(:,1:(k-1)s+1) | Q_new]' Q_new below, reading
+            // only Q(:,1:(k-2)s) beyond its own columns (k_passb_wide)
+            if (L.full && !L.restart_inner && k >= 3 && !test_switch("CAL_TEST_PASSB_WIDE_OFF")) {
+                c->pbw.want = true;
+                c->pbw.qold = panel();
+                panel_add(c->pbw.qold, L.col(0), ld, (k - 2) * s);
+            }
             CAL_TRY(project_and_normalize_dev(c, n, Qp, X, true, Qo, Rq.data(), R.data(), &res));
+            c->pbw.want = false;
         }
         L.reorth.push_back(res.reorth ? 1 : 0);
         if (res.reorth) L.info.n_reorth++;
@@ -1269,11 +1278,24 @@ int lanczos_step(cal_ctx* c, int diagnostics) {
                                                      &ro, &rk));
         } else if (L.full) {  // ca_lanczos.m:197
             Panel Qall = panel(), Xn = panel();
-            panel_add(Qall, L.col(0), ld, (k - 1) * s + 1);
+            const int wall = (k - 1) * s + 1;
+            panel_add(Qall, L.col(0), ld, wall);
             panel_add(Xn, L.col((k - 1) * s + 1), ld, s);
-            std::vector<double> Rq2((size_t)((k - 1) * s + 1) * s), R2((size_t)s * s);
+            std::vector<double> Rq2((size_t)wall * s), R2((size_t)s * s);
             PNResult res2;
-            CAL_TRY(project_and_normalize_dev(c, n, Qall, Xn, true, Qo, Rq2.data(), R2.data(), &res2));
+            std::vector<double> G1;
+            if (c->pbw.ready) {
+                // [Qp | Q_new | Qold]' Q_new (k_passb_wide's order) -> [Qall | Q_new]' Q_new
+                CAL_HIP(c, hipEventSynchronize(c->pbw.ev));
+                const int wold = c->pbw.qold.total, wp = wall + s, lda = 16 * c->pbw.ntw;
+                G1.assign((size_t)wp * s, 0.0);
+                for (int j = 0; j < s; ++j)
+                    for (int a = 0; a < wold + 17; ++a)
+                        G1[(a < 17 ? wold + a : a - 17) + (size_t)j * wp] = c->pbw.h[a + (size_t)j * lda];
+            }
+            c->pbw.ready = false;
+            CAL_TRY(project_and_normalize_dev(c, n, Qall, Xn, true, Qo, Rq2.data(), R2.data(), &res2,
+                                              G1.empty() ? nullptr : G1.data()));
         }
         status = extend_T(c, L, Rq, R);
     }
@@ -1631,8 +1653,25 @@ int cal_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, int n
         }
     } free_qc{dQc};
     double norm_A = 0.0;
-    CAL_TRY(normest_dev(c, &norm_A));  // :35
-    tol = tol * norm_A;                // :39
+    // normest(A) (:35) on its own stream beside the prologue and the first
+    // inner run (one rank; cal_impl_restarted_ca_lanczos does the same); tol is
+    // first used by the first restart's convergence test (:39, :114)
+    NormestAsync nest;
+    struct NestGuard {
+        cal_ctx* c;
+        NormestAsync* J;
+        ~NestGuard() {
+            if (J->active) hipStreamSynchronize(c->nest_stream);
+            J->active = false;
+        }
+    } nest_guard{c, &nest};
+    const double tol_rel = tol;
+    if ((!c->comm || c->comm->nranks <= 1) && !test_switch("CAL_TEST_NORMEST_SYNC")) {
+        CAL_TRY(normest_async_begin(c, nest));
+    } else {
+        CAL_TRY(normest_dev(c, &norm_A));
+        tol = tol_rel * norm_A;
+    }
     // q = r/norm(r) (:56)
     CAL_HIP(c, hipMemcpyAsync(L->vcolumn(0), r, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
     double rr = 0.0;
@@ -1640,6 +1679,7 @@ int cal_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, int n
     CAL_HIP_OTHER(c, launch_div(L->col(0), L->vcolumn(0), std::sqrt(rr), n, c->stream));
     if (L->newton) {
         CAL_TRY(newton_prologue(c, *L, false));  // lanczos(A,q,2*s,'local') (:65)
+        if (nest.active) CAL_TRY(normest_async_poll(c, nest, false));
     } else {
         L->Bk.assign((size_t)(s + 1) * s, 0.0);
         for (int j = 0; j < s; ++j) L->Bk[(j + 1) + (size_t)j * (s + 1)] = 1.0;
@@ -1661,9 +1701,14 @@ int cal_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, int n
         L->dExt = dQc + c->A.lpad;
         L->next = nconv;
         for (int it = 0; it <= iters; ++it) {
+            if (nest.active) CAL_TRY(normest_async_poll(c, nest, false));
             const int st = lanczos_step(c, 0);
             if (st < 0) return st;
             if (st == CAL_WARN_BREAKDOWN) return set_error(c, CAL_WARN_BREAKDOWN, "restart: inner CA-Lanczos breakdown");
+        }
+        if (nest.active) {
+            CAL_TRY(normest_async_finish(c, nest, &norm_A));
+            tol = tol_rel * norm_A;
         }
         // eig(T(1:m,1:m)), beta = T(m+1,m) (:105-107); unit-norm eigenvectors
         std::vector<double> Tm((size_t)m * m), wr(m), wi(m), V((size_t)m * m);

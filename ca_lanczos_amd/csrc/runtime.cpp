@@ -923,6 +923,9 @@ void cal_destroy(cal_ctx* c) {
     if (c->d_zbuf) hipFree(c->d_zbuf);
     if (c->d_tsqrv) hipFree(c->d_tsqrv);
     if (c->d_fold) hipFree(c->d_fold);
+    if (c->pbw.d) hipFree(c->pbw.d);
+    if (c->pbw.h) hipHostFree(c->pbw.h);
+    if (c->pbw.ev) hipEventDestroy(c->pbw.ev);
     if (c->h_pub) hipHostFree(c->h_pub);
     if (c->aux_stream) hipStreamDestroy(c->aux_stream);
     if (c->d_nest) hipFree(c->d_nest);

@@ -197,3 +197,25 @@ print(json.dumps(dict(inr=[int(i0["num_restarts"]), int(i1["num_restarts"])],
     assert abs(res["inr"][0] - res["inr"][1]) <= 2, res
     assert res["ie"] <= 1e-10 and res["re"] <= 1e-10, res
     assert res["ien"] == [6, 6] and res["ren"][0] == res["ren"][1] >= 1, res
+
+
+@pytest.mark.parametrize("N,its", [(40, 120), (24, 64)])
+def test_full_passb_wide_gram_vs_separate(N, its):
+    """'full' orthogonalisation (ca_lanczos.m:197): the local block's pass B
+    also forms the next projection's Gram [Qp | Q_new | Qold]' Q_new
+    (k_passb_wide) instead of the separate wide Gram sweep
+    (CAL_TEST_PASSB_WIDE_OFF).  The Gram is summed in another order, so the
+    bar is the solver's: T within 1e-9 ||A||, the same reorth flags, and both
+    runs orthonormal to 1e-12 (orth_err of every iteration)."""
+    res = run_testhooks(r"""
+A = cal.matrices.laplacian_3d(%d)
+r = ref.matlab_rand(A.shape[0])
+a = cal.ca_lanczos_ex(A, r, 8, %d, "newton", "full")
+os.environ["CAL_TEST_PASSB_WIDE_OFF"] = "1"
+b = cal.ca_lanczos_ex(A, r, 8, %d, "newton", "full")
+print(json.dumps(dict(dT=float(np.max(np.abs(a.T - b.T))), fa=[int(f) for f in a.reorth], fb=[int(f) for f in b.reorth],
+                      oa=float(np.max(a.orth_err)), ob=float(np.max(b.orth_err)), t=int(a.info["t"]))))
+""" % (N, its, its))
+    assert res["dT"] <= 1e-9 * 12.0, res
+    assert res["fa"] == res["fb"], res
+    assert res["oa"] < 1e-12 and res["ob"] < 1e-12, res

@@ -1095,8 +1095,9 @@ def test_production_library_has_no_test_hooks(cal, ref):
 
 @pytest.mark.parametrize("fmt", ["auto", "csr"])
 def test_impl_restart_normest_async_matches_sync(cal, ref, fmt):
-    """The implicit restart runs normest(A) on its own stream beside the
-    Newton prologue and the first CA blocks (lanczos.cpp normest_async_*);
+    """The implicit and the explicit restart run normest(A) on its own stream
+    beside the Newton prologue and the first CA blocks (lanczos.cpp
+    normest_async_*);
     'periodic' CA-Lanczos runs the synchronous normest_dev.  Same kernels in
     the same order: the same norm to the bit, in the matrix's own SpMV format
     and forced to CSR (the rescale in the gathers, mode 3); and the restart
@@ -1108,7 +1109,9 @@ def test_impl_restart_normest_async_matches_sync(cal, ref, fmt):
     p = cal.ca_lanczos_ex(A, r, 4, 40, "newton", "periodic", ctx=ctx)
     irl = cal.impl_restarted_ca_lanczos(A, r, 40, 6, 4, "newton", "full", 1e-8, ctx=ctx)
     irl2 = cal.impl_restarted_ca_lanczos(A, r, 40, 6, 4, "newton", "full", 1e-8, ctx=ctx)
+    rst = cal.restarted_ca_lanczos(A, r, 40, 4, 4, "newton", "local", 1e-8, ctx=ctx)  # the explicit restart too
     ctx.close()
+    assert rst["norm_A"] == p.info["norm_A"], (rst["norm_A"], p.info["norm_A"])
     assert p.info["norm_A"] > 0 and irl["norm_A"] == p.info["norm_A"], (irl["norm_A"], p.info["norm_A"])
     assert irl2["norm_A"] == irl["norm_A"] and irl2["num_restarts"] == irl["num_restarts"]
     assert np.array_equal(irl2["conv_eigs"], irl["conv_eigs"])

@@ -4,7 +4,7 @@
 set -o pipefail
 O=gpurun_out/r06/${TAG:-irl}
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests/test_gpu_hooks.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_ingest.py -k "normest or impl_restart or project_blocks or periodic or config5 or irl" -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_gpu_hooks.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_ingest.py -k "normest or restart or project_blocks or periodic or config5 or irl" -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 for rep in 1 2; do
 timeout -k 10 300 python bench.py --driver irl --workload circuit_1259 --no-cpu-baseline --steps 3 --warmup 1 > $O/irl.$rep.json 2> $O/irl.$rep.err || exit $?
