@@ -3212,9 +3212,6 @@ hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, co
 // group's Qold loads in flight during the current group's MFMAs.  Partials
 // entry-major: entry j (16 NTW) + a (a = A column, j < 8) of block b at
 // partial[entry * nblocks + b].  gate: as k_rowapply's.
-#ifndef CAL_PBW_PREFETCH
-#define CAL_PBW_PREFETCH 0
-#endif
 template <int NTW, bool NTS>
 __global__ __launch_bounds__(256) void k_passb_wide(ColList P, const double* __restrict__ M, OutList Y, Panel Qold,
                                                     int64_t n, double* __restrict__ partial,
@@ -3239,35 +3236,14 @@ __global__ __launch_bounds__(256) void k_passb_wide(ColList P, const double* __r
     const double* const* pc = P.p;
     double* const* yc = Y.p;
     const int64_t nch = (n + 255) / 256;
-#if CAL_PBW_PREFETCH
-    // the next chunk's W row loads fly during this chunk's Gram groups
-    double pn[WPMAX];
-    {
-        const int64_t r0 = (int64_t)blockIdx.x * 256 + tid;
-        const int64_t rr0 = r0 < n ? r0 : n - 1;
-#pragma unroll
-        for (int c = 0; c < WPMAX; ++c) pn[c] = pc[c][rr0];
-    }
-#endif
     for (int64_t ci = blockIdx.x; ci < nch; ci += gridDim.x) {
         asm volatile("" ::: "memory");
         const int64_t r = ci * 256 + tid;
         const bool in = r < n;
         const int64_t rr = in ? r : n - 1;
         double p[WPMAX];
-#if CAL_PBW_PREFETCH
-#pragma unroll
-        for (int c = 0; c < WPMAX; ++c) p[c] = pn[c];
-        if (ci + gridDim.x < nch) {
-            const int64_t r1 = (ci + gridDim.x) * 256 + tid;
-            const int64_t rr1 = r1 < n ? r1 : n - 1;
-#pragma unroll
-            for (int c = 0; c < WPMAX; ++c) pn[c] = pc[c][rr1];
-        }
-#else
 #pragma unroll
         for (int c = 0; c < WPMAX; ++c) p[c] = pc[c][rr];
-#endif
 #pragma unroll
         for (int c = 0; c < WPMAX; ++c) p[c] = in ? p[c] : 0.0;
         // Q1 = P M1, then Q_new = [P(0:9) | Q1] [M2p; M2y] (k_rowapply CHAIN)
@@ -3324,17 +3300,15 @@ __global__ __launch_bounds__(256) void k_passb_wide(ColList P, const double* __r
         // [Qp | Q_new | Qold] through the same rows
 #pragma unroll
         for (int j = 0; j < MOUT; ++j) tw[lane * TLD + j] = y[j];
-        double nxt[2][16];  // the next two groups' Qold values (group t in slot t & 1)
+        double nxt[16];  // the next group's Qold values (two groups ahead measured slower: registers)
         auto load_old = [&](int t) {
-            if (t >= NTW) return;
 #pragma unroll
             for (int c = 0; c < 16; ++c) {
                 const int k = 16 * t + c - (WQ + MOUT);  // Qold column
-                nxt[t & 1][c] = (k >= 0 && k < wold && in) ? pcol(Qold, k)[rr] : 0.0;
+                nxt[c] = (k >= 0 && k < wold && in) ? pcol(Qold, k)[rr] : 0.0;
             }
         };
         load_old(1);
-        load_old(2);
         wave_lds_sync();
         double bv[16];
 #pragma unroll
@@ -3348,8 +3322,8 @@ __global__ __launch_bounds__(256) void k_passb_wide(ColList P, const double* __r
                 for (int c = 0; c < 16; ++c) a[c] = c < WQ ? p[c < WQ ? c : 0] : y[c >= WQ ? c - WQ : 0];
             } else {
 #pragma unroll
-                for (int c = 0; c < 16; ++c) a[c] = nxt[t & 1][c];
-                load_old(t + 2);
+                for (int c = 0; c < 16; ++c) a[c] = nxt[c];
+                if (t + 1 < NTW) load_old(t + 1);
             }
             if (t == 1) a[0] = y[7];  // column 16 = Q_new(:, 7)
 #pragma unroll
