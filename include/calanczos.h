@@ -225,7 +225,10 @@ int cal_compute_ritz_rnorm(cal_ctx* ctx, const double* Q, int k, const double* V
  * With diagnostics the iteration's rn / oe are computed late (rn one
  * iteration behind; oe of 'local' / 'full' runs of <= 128 columns at the
  * last step, from one Gram of Q): get() finishes whatever is pending, so
- * its rn / oe are always complete for the iterations run so far. */
+ * its rn / oe are always complete for the iterations run so far.  eig(T) of
+ * iteration k runs on a host worker thread and is joined one step later: a
+ * non-converging eig(T) is reported (CAL_ERR_NUMERIC) by step k+1 or by get(),
+ * after step k+1 has already extended T. */
 int cal_lanczos_begin(cal_ctx* ctx, const double* r, int s, int max_outer, const char* basis,
                       const char* orth);
 int cal_lanczos_step(cal_ctx* ctx, int diagnostics);
