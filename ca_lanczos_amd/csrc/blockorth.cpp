@@ -548,6 +548,7 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
         CAL_HIP(c, launch_passb_wide(cw, d_mbuf, ol, c->pbw.qold, n, pblocks, c->d_partial, gate, c->stream));
         timer_end(c, t);
         CAL_HIP_OTHER(c, launch_reduce(c->d_partial, pblocks, (int64_t)ent, c->pbw.d, c->stream));
+        CAL_TRY(allreduce_sum(c, c->pbw.d, (int64_t)ent));  // the slabs' Grams (every rank takes this branch)
         CAL_HIP_OTHER(c, hipMemcpyAsync(c->pbw.h, c->pbw.d, ent * sizeof(double), hipMemcpyDeviceToHost, c->stream));
         CAL_HIP(c, hipEventRecord(c->pbw.ev, c->stream));
         c->pbw.ntw = ntw;
