@@ -533,14 +533,15 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
         const size_t ent = (size_t)128 * ntw;
         const int pblocks = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, kRowGramBlocks));
         CAL_TRY(ensure_partial(c, (size_t)pblocks * ent));
-        if (ent > c->pbw.cap) {
+        if (ent > c->pbw.cap) {  // (1536 doubles at most: sized for the widest at once)
             if (c->pbw.d) CAL_HIP(c, hipFree(c->pbw.d));
             if (c->pbw.h) CAL_HIP(c, hipHostFree(c->pbw.h));
             c->pbw.d = c->pbw.h = nullptr;
             c->pbw.cap = 0;
-            CAL_HIP(c, scratch_malloc((void**)&c->pbw.d, ent * sizeof(double)));
-            CAL_HIP(c, hipHostMalloc((void**)&c->pbw.h, ent * sizeof(double), hipHostMallocDefault));
-            c->pbw.cap = ent;
+            const size_t cap = (size_t)128 * kPassbWideMaxTiles;
+            CAL_HIP(c, scratch_malloc((void**)&c->pbw.d, cap * sizeof(double)));
+            CAL_HIP(c, hipHostMalloc((void**)&c->pbw.h, cap * sizeof(double), hipHostMallocDefault));
+            c->pbw.cap = cap;
         }
         if (!c->pbw.ev) CAL_HIP(c, hipEventCreateWithFlags(&c->pbw.ev, hipEventDisableTiming));
         // bytes: pass B's, plus the Qold columns the Gram reads

@@ -47,7 +47,10 @@ static int grow(cal_ctx* c, double** p, size_t* cap, size_t need) {
     if (need <= *cap) return 0;
     if (*p) CAL_HIP(c, hipFree(*p));
     *p = nullptr;
-    size_t n = std::max(need, (size_t)4096);
+    // by half again at least: a Gram that widens every outer iteration ('full',
+    // 'selective', the restarts) reallocates O(log) times, not every other step
+    // (each reallocation synchronises the device and allocates: 0.3-0.5 ms)
+    size_t n = std::max({need, *cap + *cap / 2, (size_t)4096});
     CAL_HIP(c, scratch_malloc((void**)p, n * sizeof(double)));
     *cap = n;
     return 0;

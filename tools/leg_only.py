@@ -22,7 +22,7 @@ def main():
     K = int(os.environ.get("LEG_STEPS", "10"))
     out = []
     for _ in range(int(os.environ.get("LEG_REPS", "2"))):
-        leg = bench.timed_leg(ctx, r, 8, K, 2, "newton", os.environ.get("LEG_ORTH", "local"), None)
+        leg = bench.timed_leg(ctx, r, 8, K, int(os.environ.get("LEG_WARMUP", "2")), "newton", os.environ.get("LEG_ORTH", "local"), None)
         out.append({k: leg[k] for k in ("outer_iters_per_s", "ms_per_step", "kernel_ms_per_step", "kernel_share")})
     print(json.dumps(out))
 
