@@ -525,7 +525,8 @@ static int orth_device(cal_ctx* c, int64_t n, const Panel& Qp, const Panel& X, b
     // pass B: Q = [Qp | W M1] M2, one store -- with the 'full' projection's
     // Gram [Qp | Q | Qold]' Q when the caller asked for it (k_passb_wide)
     const bool pbw = c->pbw.want && w == 9 && m == 8 && WP == 17 && MO == 8 &&
-                     passb_wide_tiles(c->pbw.qold.total) <= kPassbWideMaxTiles && Qp.nseg == 1;
+                     passb_wide_tiles(c->pbw.qold.total) <= kPassbWideMaxTiles && Qp.nseg == 1 &&
+                     c->pbw.qold.nseg <= 1;
     c->pbw.want = false;
     c->pbw.ready = false;
     if (pbw) {

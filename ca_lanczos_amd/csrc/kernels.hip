@@ -3213,7 +3213,8 @@ hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, co
 // entry-major: entry j (16 NTW) + a (a = A column, j < 8) of block b at
 // partial[entry * nblocks + b].  gate: as k_rowapply's.
 template <int NTW, bool NTS>
-__global__ __launch_bounds__(256) void k_passb_wide(ColList P, const double* __restrict__ M, OutList Y, Panel Qold,
+__global__ __launch_bounds__(256) void k_passb_wide(ColList P, const double* __restrict__ M, OutList Y,
+                                                    const double* __restrict__ qold, int64_t ldq, int wold,
                                                     int64_t n, double* __restrict__ partial,
                                                     const double* __restrict__ gate) {
     constexpr int WPMAX = 17, MOUT = 8, WQ = 9;
@@ -3229,7 +3230,6 @@ __global__ __launch_bounds__(256) void k_passb_wide(ColList P, const double* __r
     for (int e = tid; e < MSZ; e += 256) Ms[e] = M[e];
     __syncthreads();
     double* const tw = lds + wave * WTILE;
-    const int wold = Qold.total;
     d4 acc[NTW];
 #pragma unroll
     for (int t = 0; t < NTW; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
@@ -3305,7 +3305,7 @@ __global__ __launch_bounds__(256) void k_passb_wide(ColList P, const double* __r
 #pragma unroll
             for (int c = 0; c < 16; ++c) {
                 const int k = 16 * t + c - (WQ + MOUT);  // Qold column
-                nxt[c] = (k >= 0 && k < wold && in) ? pcol(Qold, k)[rr] : 0.0;
+                nxt[c] = (k >= 0 && k < wold && in) ? qold[(int64_t)k * ldq + rr] : 0.0;
             }
         };
         load_old(1);
@@ -3368,13 +3368,19 @@ int passb_wide_tiles(int wold) { return (9 + 8 + wold + 15) / 16; }
 
 hipError_t launch_passb_wide(const ColList& P, const double* dM, const OutList& Y, const Panel& Qold, int64_t n,
                              int blocks, double* partial, const double* gate, hipStream_t st) {
+    if (Qold.total > 0 && Qold.nseg != 1) return hipErrorInvalidValue;  // one column block (Q(:,1:(k-2)s))
     const int ntw = passb_wide_tiles(Qold.total);
+    const double* qold = Qold.total > 0 ? Qold.ptr[0] : nullptr;
+    const int64_t ldq = Qold.total > 0 ? Qold.ld[0] : 0;
+    const int wold = Qold.total;
     const bool nts = (int64_t)n * 8 * (17 + 8) > ((int64_t)256 << 20);  // as launch_rowapply's pass B
     dim3 g(blocks), b(256);
 #define CAL_PBW(T)                                                                                              \
     case T:                                                                                                     \
-        if (nts) hipLaunchKernelGGL((k_passb_wide<T, true>), g, b, 0, st, P, dM, Y, Qold, n, partial, gate);  \
-        else hipLaunchKernelGGL((k_passb_wide<T, false>), g, b, 0, st, P, dM, Y, Qold, n, partial, gate);     \
+        if (nts) hipLaunchKernelGGL((k_passb_wide<T, true>), g, b, 0, st, P, dM, Y, qold, ldq, wold, n, partial, \
+                                    gate);                                                                      \
+        else hipLaunchKernelGGL((k_passb_wide<T, false>), g, b, 0, st, P, dM, Y, qold, ldq, wold, n, partial, \
+                                gate);                                                                          \
         break;
     switch (ntw) {
         CAL_PBW(2)
