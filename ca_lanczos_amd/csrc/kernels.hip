@@ -3211,7 +3211,8 @@ hipError_t launch_rowapply(const ColList& P, const double* dM, int wp, int m, co
 // v_mfma_f64_16x16x4f64 with B = Q_new (columns 8..15 zero), the next
 // group's Qold loads in flight during the current group's MFMAs.  Partials
 // entry-major: entry j (16 NTW) + a (a = A column, j < 8) of block b at
-// partial[entry * nblocks + b].  gate: as k_rowapply's.
+// partial[entry * nblocks + b]; entries a >= 17 + wold are padding.  gate: as
+// k_rowapply's.
 template <int NTW, bool NTS>
 __global__ __launch_bounds__(256) void k_passb_wide(ColList P, const double* __restrict__ M, OutList Y,
                                                     const double* __restrict__ qold, int64_t ldq, int wold,
@@ -3301,11 +3302,18 @@ __global__ __launch_bounds__(256) void k_passb_wide(ColList P, const double* __r
 #pragma unroll
         for (int j = 0; j < MOUT; ++j) tw[lane * TLD + j] = y[j];
         double nxt[16];  // the next group's Qold values (two groups ahead measured slower: registers)
+        // unconditional loads of a valid row and a valid column, no select: a
+        // load under a condition became a branch per load, and a select right
+        // after the load a full vmcnt wait per load.  Rows past n have Q_new =
+        // 0, so their (finite) A values add nothing; the padding columns past
+        // Qold (clamped to its last column) give Gram entries a >= 17 + wold,
+        // which no caller reads.
         auto load_old = [&](int t) {
 #pragma unroll
             for (int c = 0; c < 16; ++c) {
-                const int k = 16 * t + c - (WQ + MOUT);  // Qold column
-                nxt[c] = (k >= 0 && k < wold && in) ? qold[(int64_t)k * ldq + rr] : 0.0;
+                const int k = 16 * t + c - (WQ + MOUT);  // Qold column (wave-uniform)
+                const int kc = k < 0 ? 0 : (k < wold ? k : wold - 1);
+                nxt[c] = qold[(int64_t)kc * ldq + rr];
             }
         };
         load_old(1);
@@ -3316,18 +3324,17 @@ __global__ __launch_bounds__(256) void k_passb_wide(ColList P, const double* __r
         wave_lds_sync();
 #pragma unroll
         for (int t = 0; t < NTW; ++t) {
-            double a[16];
+            // group t into the wave's rows first, then group t + 1's loads into
+            // the registers group t just left (loading first made the compiler
+            // wait for every load before reusing its register)
             if (t == 0) {  // [Qp (9) | Q_new (0:7)]
 #pragma unroll
-                for (int c = 0; c < 16; ++c) a[c] = c < WQ ? p[c < WQ ? c : 0] : y[c >= WQ ? c - WQ : 0];
+                for (int c = 0; c < 16; ++c) tw[lane * TLD + c] = c < WQ ? p[c < WQ ? c : 0] : y[c >= WQ ? c - WQ : 0];
             } else {
 #pragma unroll
-                for (int c = 0; c < 16; ++c) a[c] = nxt[c];
+                for (int c = 0; c < 16; ++c) tw[lane * TLD + c] = (t == 1 && c == 0) ? y[7] : nxt[c];  // col 16 = Q_new(:, 7)
                 if (t + 1 < NTW) load_old(t + 1);
             }
-            if (t == 1) a[0] = y[7];  // column 16 = Q_new(:, 7)
-#pragma unroll
-            for (int c = 0; c < 16; ++c) tw[lane * TLD + c] = a[c];
             wave_lds_sync();
 #pragma unroll
             for (int kk = 0; kk < 16; ++kk) acc[t] = mfma64(tw[(4 * kk + g) * TLD + c16], bv[kk], acc[t]);
@@ -3370,7 +3377,8 @@ hipError_t launch_passb_wide(const ColList& P, const double* dM, const OutList& 
                              int blocks, double* partial, const double* gate, hipStream_t st) {
     if (Qold.total > 0 && Qold.nseg != 1) return hipErrorInvalidValue;  // one column block (Q(:,1:(k-2)s))
     const int ntw = passb_wide_tiles(Qold.total);
-    const double* qold = Qold.total > 0 ? Qold.ptr[0] : nullptr;
+    // (no Qold: column 0 of P stands in; only padding columns read it)
+    const double* qold = Qold.total > 0 ? Qold.ptr[0] : P.p[0];
     const int64_t ldq = Qold.total > 0 ? Qold.ld[0] : 0;
     const int wold = Qold.total;
     const bool nts = (int64_t)n * 8 * (17 + 8) > ((int64_t)256 << 20);  // as launch_rowapply's pass B
