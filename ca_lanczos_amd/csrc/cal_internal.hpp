@@ -467,6 +467,7 @@ struct cal_ctx {
     std::string err;
     cal::DevMatrix A;
     bool has_A = false;
+    uint64_t A_gen = 0;  // matrix uploads so far (keys what was captured against A)
     int64_t stat_spmv_rows = 0;  // rows computed by SpMV launches (cal_comm_stats)
 
     // reduction scratch
@@ -552,6 +553,11 @@ struct cal_ctx {
     double* d_nest = nullptr;
     double* h_nest = nullptr;
     size_t nest_cap = 0;
+    // its chunks as replayed HIP graphs (one host launch per chunk, not ~50):
+    // [0] the first chunk, [1] the later ones; each valid for the key it was
+    // captured with (scratch, matrix arrays, sizes)
+    hipGraphExec_t nest_exec[2] = {nullptr, nullptr};
+    std::vector<int64_t> nest_key[2];
     // the test build only (CAL_TEST_HOOKS): R of ca_lanczos's first block
     // (normalize, ca_lanczos.m:176), read back by cal_test_first_block_R
     std::vector<double> test_R1;

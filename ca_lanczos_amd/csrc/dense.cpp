@@ -234,7 +234,9 @@ void svd(int m, const double* A, int lda, double* U, double* S, double* V) {
 // transformations accumulated (EISPACK tred2), then the implicit QL iteration
 // with Wilkinson-type shifts applied to the accumulated vectors (tql2).
 // O(n^3) with a small constant (0.6 ms at n = 60; the Jacobi sweeps it
-// replaces took 50 ms).  Ascending eigenvalues, orthonormal vectors.
+// replaces took 50 ms).  Ascending eigenvalues, orthonormal vectors; V =
+// NULL: the values alone (the same arithmetic on d and e, so the same bits,
+// without the O(n^3) accumulation and the rotations of the vectors).
 void eig_symmetric(int n, const double* A, int lda, double* w, double* V, int ldv) {
     if (n <= 0) return;
     std::vector<double> z((size_t)n * n), d(n, 0.0), e(n, 0.0);
@@ -284,6 +286,10 @@ void eig_symmetric(int n, const double* A, int lda, double* w, double* V, int ld
     d[0] = 0.0;
     e[0] = 0.0;
     for (int i = 0; i < n; ++i) {  // accumulate the transformations
+        if (!V) {  // values only: the diagonal, which the accumulation leaves as it is
+            d[i] = Z(i, i);
+            continue;
+        }
         const int l = i - 1;
         if (d[i] != 0.0) {
             for (int j = 0; j <= l; ++j) {
@@ -330,7 +336,7 @@ void eig_symmetric(int n, const double* A, int lda, double* w, double* V, int ld
                     r = (d[i] - g) * s + 2.0 * c * b;
                     d[i + 1] = g + (p = s * r);
                     g = c * r - b;
-                    for (int k = 0; k < n; ++k) {
+                    for (int k = 0; V && k < n; ++k) {
                         f = Z(k, i + 1);
                         Z(k, i + 1) = s * Z(k, i) + c * f;
                         Z(k, i) = c * Z(k, i) - s * f;
@@ -348,7 +354,7 @@ void eig_symmetric(int n, const double* A, int lda, double* w, double* V, int ld
     std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return d[x] < d[y]; });
     for (int j = 0; j < n; ++j) {
         w[j] = d[idx[j]];
-        for (int i = 0; i < n; ++i) V[i + (size_t)j * ldv] = Z(i, idx[j]);
+        for (int i = 0; V && i < n; ++i) V[i + (size_t)j * ldv] = Z(i, idx[j]);
     }
 }
 
@@ -722,48 +728,85 @@ bool eig_general(int n, const double* A, int lda, double* wr, double* wi, double
     return ok;
 }
 
-// One explicit shifted QR step on an upper-Hessenberg H (m x m): H - mu I =
-// QR, H <- RQ + mu I = Q'HQ, W (m x m) <- WQ, with Q the product of m-1
-// Givens rotations (O(m^2); the reference's qrstep forms the same Q, up to
-// column signs, by a dense Householder QR and two m^3 products).
-void hess_qrstep(int m, double* H, int ldh, double* W, int ldw, double mu) {
+// Explicit shifted QR steps on an upper-Hessenberg H (m x m), one per shift
+// mu[t]: H - mu I = QR, H <- RQ + mu I = Q'HQ, W (m x m) <- WQ, with Q the
+// product of m-1 Givens rotations (O(m^2) a step; the reference's qrstep
+// forms the same Q, up to column signs, by a dense Householder QR and two m^3
+// products).  W's rotations depend on H only through the (c, s) pairs, so
+// they are applied after all the H steps, eight rows at a time with the
+// rotated column carried in registers: every W entry sees the same
+// operations in the same order as when applied step by step (the same bits),
+// at a fraction of the loads and stores.
+void hess_qrsteps(int m, double* H, int ldh, double* W, int ldw, const double* mu, int count) {
+    if (m < 1 || count < 1) return;
     auto h = [&](int i, int j) -> double& { return H[i + (size_t)j * ldh]; };
-    std::vector<double> cs(m, 1.0), sn(m, 0.0);
-    for (int i = 0; i < m; ++i) h(i, i) -= mu;
-    for (int j = 0; j + 1 < m; ++j) {  // R = G'_{m-2} ... G'_0 (H - mu I)
-        const double a = h(j, j), b = h(j + 1, j);
-        double c = 1.0, s = 0.0;
-        if (b != 0.0) {
-            const double r = std::hypot(a, b);
-            c = a / r;
-            s = b / r;
+    const int nr = m - 1;
+    std::vector<double> cs((size_t)count * (nr > 0 ? nr : 1), 1.0), sn((size_t)count * (nr > 0 ? nr : 1), 0.0);
+    for (int t = 0; t < count; ++t) {
+        double* ct = cs.data() + (size_t)t * nr;
+        double* st = sn.data() + (size_t)t * nr;
+        for (int i = 0; i < m; ++i) h(i, i) -= mu[t];
+        for (int j = 0; j + 1 < m; ++j) {  // R = G'_{m-2} ... G'_0 (H - mu I)
+            const double a = h(j, j), b = h(j + 1, j);
+            double c = 1.0, s = 0.0;
+            if (b != 0.0) {
+                const double r = std::hypot(a, b);
+                c = a / r;
+                s = b / r;
+            }
+            ct[j] = c;
+            st[j] = s;
+            for (int col = j; col < m; ++col) {
+                const double x = h(j, col), y = h(j + 1, col);
+                h(j, col) = c * x + s * y;
+                h(j + 1, col) = c * y - s * x;
+            }
+            h(j + 1, j) = 0.0;
         }
-        cs[j] = c;
-        sn[j] = s;
-        for (int col = j; col < m; ++col) {
-            const double x = h(j, col), y = h(j + 1, col);
-            h(j, col) = c * x + s * y;
-            h(j + 1, col) = c * y - s * x;
+        for (int j = 0; j + 1 < m; ++j) {  // RQ, Q = G_0 ... G_{m-2}
+            const double c = ct[j], s = st[j];
+            for (int row = 0; row < std::min(j + 2, m); ++row) {
+                const double x = h(row, j), y = h(row, j + 1);
+                h(row, j) = c * x + s * y;
+                h(row, j + 1) = c * y - s * x;
+            }
         }
-        h(j + 1, j) = 0.0;
+        for (int i = 0; i < m; ++i) h(i, i) += mu[t];
     }
-    for (int j = 0; j + 1 < m; ++j) {  // RQ and WQ, Q = G_0 ... G_{m-2}
-        const double c = cs[j], s = sn[j];
-        for (int row = 0; row < std::min(j + 2, m); ++row) {
-            const double x = h(row, j), y = h(row, j + 1);
-            h(row, j) = c * x + s * y;
-            h(row, j + 1) = c * y - s * x;
-        }
-        double* wj = W + (size_t)j * ldw;
-        double* wj1 = W + (size_t)(j + 1) * ldw;
-        for (int row = 0; row < m; ++row) {
-            const double x = wj[row], y = wj1[row];
-            wj[row] = c * x + s * y;
-            wj1[row] = c * y - s * x;
+    if (nr < 1) return;
+    constexpr int RB = 8;
+    for (int r0 = 0; r0 < m; r0 += RB) {
+        const int rows = std::min(RB, m - r0);
+        for (int t = 0; t < count; ++t) {
+            const double* ct = cs.data() + (size_t)t * nr;
+            const double* st = sn.data() + (size_t)t * nr;
+            double a[RB];
+            for (int i = 0; i < rows; ++i) a[i] = W[r0 + i];
+            for (int j = 0; j < nr; ++j) {
+                const double c = ct[j], s = st[j];
+                double* wj = W + (size_t)j * ldw + r0;
+                const double* wj1 = W + (size_t)(j + 1) * ldw + r0;
+                if (rows == RB) {
+#pragma GCC unroll 8
+                    for (int i = 0; i < RB; ++i) {
+                        const double x = a[i], y = wj1[i];
+                        wj[i] = c * x + s * y;
+                        a[i] = c * y - s * x;
+                    }
+                } else {
+                    for (int i = 0; i < rows; ++i) {
+                        const double x = a[i], y = wj1[i];
+                        wj[i] = c * x + s * y;
+                        a[i] = c * y - s * x;
+                    }
+                }
+            }
+            for (int i = 0; i < rows; ++i) W[(size_t)nr * ldw + r0 + i] = a[i];
         }
     }
-    for (int i = 0; i < m; ++i) h(i, i) += mu;
 }
+
+void hess_qrstep(int m, double* H, int ldh, double* W, int ldw, double mu) { hess_qrsteps(m, H, ldh, W, ldw, &mu, 1); }
 
 void matlab_rand(std::mt19937& g, int64_t count, double* out) {
     for (int64_t i = 0; i < count; ++i) {

@@ -34,11 +34,15 @@ void svd(int m, const double* A, int lda, double* U, double* S, double* V);
 // columns j and j+1 hold the real and imaginary part of the eigenvector of
 // wr[j] + i wi[j].  Returns false if QR failed to converge.
 bool eig_general(int n, const double* A, int lda, double* wr, double* wi, double* V, int ldv);
-// Symmetric eigenproblem (Jacobi), ascending, orthonormal vectors.
+// Symmetric eigenproblem (tred2 + tql2), ascending, orthonormal vectors;
+// V = NULL computes the same values without the vectors.
 void eig_symmetric(int n, const double* A, int lda, double* w, double* V, int ldv);
 // One explicit shifted QR step on an upper-Hessenberg H: H <- Q'HQ,
 // W <- WQ with H - mu I = QR (Givens rotations; qrstep of the implicit restart).
 void hess_qrstep(int m, double* H, int ldh, double* W, int ldw, double mu);
+// count such steps, shifts mu[0..count) in order (W's rotations batched:
+// the same bits as count hess_qrstep calls)
+void hess_qrsteps(int m, double* H, int ldh, double* W, int ldw, const double* mu, int count);
 // `count` draws of MATLAB's rand from the MT19937 stream g (genrand_res53:
 // two 32-bit words per double)
 void matlab_rand(std::mt19937& g, int64_t count, double* out);

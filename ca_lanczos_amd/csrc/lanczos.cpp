@@ -252,26 +252,78 @@ struct NormestAsync {
 };
 }  // namespace
 
-static int normest_async_enqueue_chunk(cal_ctx* c, NormestAsync& J) {
+// One chunk's launches (kNestChunk iterations and the norms' copy to the
+// host), xnrm0 the first SpMV's divisor (null: x already rescaled).
+static hipError_t normest_chunk_launches(const cal_ctx* c, bool gather_div, const double* xnrm0, hipStream_t st) {
     const int64_t n = c->A.n_local;
     const int nb = dot_blocks(n);
     double* x = c->d_nest;
     double* y = x + n;
     double* part = y + n;
     double* d_nrm = part + 2 * (size_t)nb;  // [0] = x0'x0, then 2 per iteration of the chunk
-    const hipStream_t st = c->nest_stream;
-    for (int i = 0; i < kNestChunk; ++i) {
-        CAL_HIP(c, spmv_on_stream(c, x, y, J.xnrm ? 3 : 0, J.xnrm, st));  // Sx = S*x
-        CAL_HIP(c, spmv_on_stream(c, y, x, 0, nullptr, st));              // x = S'*Sx
+    const double* xnrm = xnrm0;
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < kNestChunk && e == hipSuccess; ++i) {
+        e = spmv_on_stream(c, x, y, xnrm ? 3 : 0, xnrm, st);     // Sx = S*x
+        if (e == hipSuccess) e = spmv_on_stream(c, y, x, 0, nullptr, st);  // x = S'*Sx
         double* dst = d_nrm + 1 + 2 * i;
-        if (J.gather_div) {
-            CAL_HIP(c, launch_normest_norms_only(x, y, n, part, dst, st));
-            J.xnrm = dst;
+        if (e != hipSuccess) break;
+        if (gather_div) {
+            e = launch_normest_norms_only(x, y, n, part, dst, st);
+            xnrm = dst;
         } else {
-            CAL_HIP(c, launch_normest_norms(x, y, n, part, dst, st));
+            e = launch_normest_norms(x, y, n, part, dst, st);
         }
     }
-    CAL_HIP(c, hipMemcpyAsync(c->h_nest, d_nrm, (1 + 2 * kNestChunk) * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(c->h_nest, d_nrm, (1 + 2 * kNestChunk) * sizeof(double), hipMemcpyDeviceToHost, st);
+    return e;
+}
+
+// The chunk as a replayed graph: the ~50 launches cost the host ~0.7 ms per
+// chunk, time in which the solver's stream (waiting for its next block's
+// launches) ran dry; one graph launch costs tens of us.  The first chunk
+// (kind 0) and the later ones (kind 1: the first SpMV divides by the previous
+// chunk's last norm) are captured once per context and re-captured when the
+// scratch or the matrix change.  Same kernels, same order: same bits.
+static int normest_chunk_graph(cal_ctx* c, const NormestAsync& J, int kind, hipStream_t st) {
+    const DevMatrix& A = c->A;
+    const std::vector<int64_t> key = {(int64_t)(intptr_t)c->d_nest, (int64_t)(intptr_t)A.rowptr,
+                                      (int64_t)(intptr_t)A.col,    (int64_t)(intptr_t)A.val,
+                                      (int64_t)(intptr_t)A.blk,    (int64_t)A.nblk,
+                                      (int64_t)A.nit,              (int64_t)A.use_pat,
+                                      (int64_t)A.ext_off,          A.n_local,
+                                      (int64_t)A.nnz,              (int64_t)J.gather_div,
+                                      (int64_t)c->A_gen};
+    if (!c->nest_exec[kind] || c->nest_key[kind] != key) {
+        if (c->nest_exec[kind]) CAL_HIP(c, hipGraphExecDestroy(c->nest_exec[kind]));
+        c->nest_exec[kind] = nullptr;
+        CAL_HIP(c, hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        const hipError_t e = normest_chunk_launches(c, J.gather_div, J.xnrm, st);
+        hipGraph_t g = nullptr;
+        const hipError_t e2 = hipStreamEndCapture(st, &g);
+        CAL_HIP(c, e);
+        CAL_HIP(c, e2);
+        const hipError_t e3 = hipGraphInstantiate(&c->nest_exec[kind], g, nullptr, nullptr, 0);
+        hipGraphDestroy(g);
+        CAL_HIP(c, e3);
+        c->nest_key[kind] = key;
+    }
+    CAL_HIP(c, hipGraphLaunch(c->nest_exec[kind], st));
+    return 0;
+}
+
+static int normest_async_enqueue_chunk(cal_ctx* c, NormestAsync& J) {
+    const int64_t n = c->A.n_local;
+    const int nb = dot_blocks(n);
+    double* d_nrm = c->d_nest + 2 * n + 2 * (size_t)nb;
+    const hipStream_t st = c->nest_stream;
+    if (test_switch("CAL_TEST_NEST_DIRECT")) {  // the test build's A/B: the launches themselves
+        CAL_HIP(c, normest_chunk_launches(c, J.gather_div, J.xnrm, st));
+    } else {
+        CAL_TRY(normest_chunk_graph(c, J, J.xnrm ? 1 : 0, st));
+    }
+    if (J.gather_div) J.xnrm = d_nrm + 1 + 2 * (kNestChunk - 1);
     timer_end_on(c, J.timer, st);  // re-recorded per chunk: the last one ends the span
     CAL_HIP(c, hipEventRecord(c->nest_event, st));
     J.chunk++;
@@ -1910,13 +1962,14 @@ int irl_block(cal_ctx* c, LanczosState& L, int nvecs, double* bprev) {
 
 // eigen-decomposition of the symmetric part of the leading m x m of T
 // (ascending, orthonormal vectors) -- the IRL's Ritz data
-void irl_sym_eig(const std::vector<double>& T, int ldt, int m, std::vector<double>& w, std::vector<double>& Y) {
+// (Y = NULL: the values alone -- the same values, without the vectors' cost)
+void irl_sym_eig(const std::vector<double>& T, int ldt, int m, std::vector<double>& w, std::vector<double>* Y) {
     std::vector<double> S((size_t)m * m);
     for (int j = 0; j < m; ++j)
         for (int i = 0; i < m; ++i) S[i + (size_t)j * m] = 0.5 * (T[i + (size_t)j * ldt] + T[j + (size_t)i * ldt]);
     w.resize(m);
-    Y.resize((size_t)m * m);
-    dense::eig_symmetric(m, S.data(), m, w.data(), Y.data(), m);
+    if (Y) Y->resize((size_t)m * m);
+    dense::eig_symmetric(m, S.data(), m, w.data(), Y ? Y->data() : nullptr, m);
 }
 
 // selectShifts 'largest' (impl_restarted_ca_lanczos.m:236-243): by modulus, descending (stable)
@@ -2024,17 +2077,19 @@ int cal_impl_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, 
         }
         const double beta_m = L->T[m + (size_t)(m - 1) * L->Tld];
         // exact shifts: the p smallest-modulus Ritz values of T_m (:96-107)
-        std::vector<double> H((size_t)m * m), W((size_t)m * m, 0.0), w, Ym;
+        std::vector<double> H((size_t)m * m), W((size_t)m * m, 0.0), w;
         for (int j = 0; j < m; ++j)
             for (int i = 0; i < m; ++i) H[i + (size_t)j * m] = L->T[i + (size_t)j * L->Tld];
-        irl_sym_eig(L->T, L->Tld, m, w, Ym);
+        irl_sym_eig(L->T, L->Tld, m, w, nullptr);  // the shifts need no vectors
         const std::vector<int> u = irl_order(w);
         // T_m is tridiagonal up to rounding: drop the sub-subdiagonal noise the
         // reference's first qrstep clean-up removes (:670-672)
         for (int j = 0; j < m; ++j)
             for (int i = j + 2; i < m; ++i) H[i + (size_t)j * m] = 0.0;
         for (int i = 0; i < m; ++i) W[i + (size_t)i * m] = 1.0;
-        for (int j = m; j > k; --j) dense::hess_qrstep(m, H.data(), m, W.data(), m, w[u[j - 1]]);
+        std::vector<double> mus;
+        for (int j = m; j > k; --j) mus.push_back(w[u[j - 1]]);
+        dense::hess_qrsteps(m, H.data(), m, W.data(), m, mus.data(), (int)mus.size());
         // [V_k | r] = [V_m | v_{m+1}] M with r = V_m W(:,k+1) H(k+1,k) + f_m W(m,k)
         std::vector<double> M((size_t)(m + 1) * (k + 1), 0.0);
         for (int j = 0; j < k; ++j)
@@ -2059,7 +2114,7 @@ int cal_impl_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, 
             for (int i = 0; i < k; ++i) L->T[i + (size_t)j * L->Tld] = H[i + (size_t)j * m];
         L->T[k + (size_t)(k - 1) * L->Tld] = bk;
         // convergence of the n_wanted largest-modulus Ritz pairs of T_k (:127-143)
-        irl_sym_eig(L->T, L->Tld, k, wk, Yk);
+        irl_sym_eig(L->T, L->Tld, k, wk, &Yk);
         const std::vector<int> ord = irl_order(wk);
         wanted.assign(ord.begin(), ord.begin() + std::min(n_wanted, k));
         converged = true;

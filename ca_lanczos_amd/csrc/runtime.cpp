@@ -548,6 +548,7 @@ int upload_matrix(cal_ctx* c, int64_t n_rows, int64_t ext_off, int64_t n_local, 
     }
     CAL_HIP(c, hipMemcpy(A.blk, blk.data(), blk.size() * sizeof(int), hipMemcpyHostToDevice));
     c->has_A = true;
+    c->A_gen++;
     return 0;
 }
 
@@ -931,6 +932,8 @@ void cal_destroy(cal_ctx* c) {
     if (c->pbw.ev) hipEventDestroy(c->pbw.ev);
     if (c->h_pub) hipHostFree(c->h_pub);
     if (c->aux_stream) hipStreamDestroy(c->aux_stream);
+    for (hipGraphExec_t& g : c->nest_exec)
+        if (g) hipGraphExecDestroy(g);
     if (c->d_nest) hipFree(c->d_nest);
     if (c->h_nest) hipHostFree(c->h_nest);
     if (c->nest_event) hipEventDestroy(c->nest_event);

@@ -128,6 +128,30 @@ int main() {
             std::printf("%d\n", st);
             put(H.data(), H.size());
             put(W.data(), W.size());
+        } else if (cmd == "eigsym") {  // vectors and values, then the values alone
+            int n;
+            std::cin >> n;
+            auto T = readv((size_t)n * n);
+            std::vector<double> w(n), w2(n), V((size_t)n * n);
+            cal::dense::eig_symmetric(n, T.data(), n, w.data(), V.data(), n);
+            cal::dense::eig_symmetric(n, T.data(), n, w2.data(), nullptr, n);
+            std::printf("0\n");
+            put(w.data(), n);
+            put(w2.data(), n);
+            put(V.data(), V.size());
+        } else if (cmd == "qrsteps") {  // count batched steps, then the same one at a time
+            int m, count;
+            std::cin >> m >> count;
+            auto mu = readv(count);
+            auto H = readv((size_t)m * m), W = readv((size_t)m * m);
+            auto H1 = H, W1 = W;
+            cal::dense::hess_qrsteps(m, H.data(), m, W.data(), m, mu.data(), count);
+            for (int t = 0; t < count; ++t) cal::dense::hess_qrstep(m, H1.data(), m, W1.data(), m, mu[t]);
+            std::printf("0\n");
+            put(H.data(), H.size());
+            put(W.data(), W.size());
+            put(H1.data(), H1.size());
+            put(W1.data(), W1.size());
         } else if (cmd == "tridiag") {
             int n;
             std::cin >> n;

@@ -161,6 +161,36 @@ print(json.dumps(dict(na=bool(p0.info["norm_A"] == p1.info["norm_A"] and p0.info
     assert all(res.values()), res
 
 
+@pytest.mark.parametrize("fmt", ["auto", "csr"])
+def test_normest_graph_vs_launches_bitexact(fmt):
+    """The asynchronous normest's chunks replayed as captured HIP graphs
+    (lanczos.cpp normest_chunk_graph) against the same launches issued one by
+    one (CAL_TEST_NEST_DIRECT): the same norm_A, restart count and
+    eigenvalues to the bit, over three solves on one context -- a matrix, a
+    second one of another size and format, the first again -- so each graph
+    is re-captured when the scratch or the matrix changes."""
+    res = run_testhooks(r"""
+mats = [cal.matrices.circuit_like(60, seed=3), cal.matrices.laplacian_3d(20)]
+fmt = %r
+outs = []
+for direct in (False, True):
+    if direct:
+        os.environ["CAL_TEST_NEST_DIRECT"] = "1"
+    ctx = cal.Context(spmv_format=None if fmt == "auto" else fmt)
+    row = []
+    for A in mats + mats[:1]:
+        ctx.set_matrix(A)
+        r = ref.matlab_rand(A.shape[0])
+        irl = cal.impl_restarted_ca_lanczos(A, r, 40, 6, 4, "newton", "full", 1e-8, ctx=ctx)
+        row.append([float(irl["norm_A"]), int(irl["num_restarts"]), [float(x) for x in irl["conv_eigs"]]])
+    ctx.close()
+    outs.append(row)
+print(json.dumps(dict(same=outs[0] == outs[1], na=[x[0] for x in outs[0]], nr=[x[1] for x in outs[0]])))
+""" % fmt)
+    assert res["same"], res
+    assert res["na"][0] == res["na"][2] and res["na"][0] != res["na"][1], res
+
+
 @pytest.mark.parametrize("switch", ["CAL_TEST_APPLY_GRAM_OFF", "CAL_TEST_SELFGRAM_OFF"])
 def test_project_blocks_fused_vs_unfused(switch):
     """project_blocks_async (blockorth.cpp): the update of block i fused with

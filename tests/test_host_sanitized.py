@@ -111,6 +111,36 @@ def test_eig_qrstep_tridiag(run, cal):
     assert np.array_equal(_f(out[k + 4]), w)
 
 
+def test_eig_values_only_and_batched_qrsteps(run):
+    """The implicit restart's host algebra (lanczos.cpp, impl_restarted_ca_lanczos.m:96-107):
+    eig_symmetric without vectors gives the same values, bit for bit, as with
+    them (the shifts need no vectors), and hess_qrsteps (W's rotations
+    batched after all the H steps, eight rows at a time) the same H and W as
+    the steps one at a time -- m = 1, 9 (a tail of one row), 60 (the config-5
+    m) with the exact shifts of the restart."""
+    rng = np.random.RandomState(11)
+    script, cases = "", []
+    for m in (1, 2, 9, 20, 60):
+        d, e = 4 + rng.rand(m), rng.rand(m - 1)
+        T = np.diag(d) + np.diag(e, 1) + np.diag(e, -1) + 1e-13 * np.triu(rng.rand(m, m), 2)
+        S = 0.5 * (T + T.T)
+        w = np.linalg.eigvalsh(S)
+        p = max(1, m - 12)
+        mu = w[:p]
+        H0 = np.tril(np.triu(T, -1))
+        script += "eigsym %d %s\n" % (m, _fmt(S))
+        script += "qrsteps %d %d %s %s %s\n" % (m, p, _fmt(mu), _fmt(H0 + np.triu(T, 2)), _fmt(np.eye(m)))
+        cases.append((m, S))
+    out = run(script)
+    for i, (m, S) in enumerate(cases):
+        o = out[9 * i: 9 * i + 9]
+        w, w2, V = _f(o[1]), _f(o[2]), _f(o[3]).reshape(m, m).T
+        assert np.array_equal(w, w2), m
+        assert np.max(np.abs(w - np.linalg.eigvalsh(S))) <= 1e-12 * 8, m
+        assert np.max(np.abs(V.T @ V - np.eye(m))) <= 1e-12, m
+        assert np.array_equal(_f(o[5]), _f(o[7])) and np.array_equal(_f(o[6]), _f(o[8])), m
+
+
 def test_dense_kernels(run):
     """Cholesky (and its failure on an indefinite Gram), triangular inverse
     and the Jacobi SVD of the s x s block algebra, m = 1..32."""
