@@ -2099,11 +2099,22 @@ int cal_impl_restarted_ca_lanczos(cal_ctx* c, const double* r, int max_lanczos, 
         M[m + (size_t)k * (m + 1)] = beta_m * W[(m - 1) + (size_t)(k - 1) * m];
         Panel P = panel();
         panel_add(P, L->col(0), ld, m + 1);
-        double* dW = work_col(c, 0);
-        PanelOut Y = panel_out(dW + c->A.lpad, ld, k + 1);
-        CAL_TRY(apply_host(c, n, P, M.data(), k + 1, &Y, nullptr, 0, nullptr));
-        CAL_HIP(c, hipMemcpyAsync(L->dQ, dW, (size_t)(k + 1) * ld * sizeof(double), hipMemcpyDeviceToDevice,
-                                  c->stream));
+        // in place when the apply is one row-parallel launch (<= 256 panel
+        // columns, <= 16 outputs: k_apply_stage / k_apply_rows read a row of
+        // [V_m | v_{m+1}] whole before writing it): no work panel and no copy
+        // back (≈ 58 us per restart).  Wider panels take the MFMA-tile apply
+        // and more outputs split into launches that would read what an
+        // earlier one wrote: those keep the work panel.
+        if (m + 1 <= 256 && k + 1 <= 16 && !test_switch("CAL_TEST_RESTART_COPY")) {
+            PanelOut Y = panel_out(L->col(0), ld, k + 1);
+            CAL_TRY(apply_host(c, n, P, M.data(), k + 1, &Y, nullptr, 0, nullptr));
+        } else {
+            double* dW = work_col(c, 0);
+            PanelOut Y = panel_out(dW + c->A.lpad, ld, k + 1);
+            CAL_TRY(apply_host(c, n, P, M.data(), k + 1, &Y, nullptr, 0, nullptr));
+            CAL_HIP(c, hipMemcpyAsync(L->dQ, dW, (size_t)(k + 1) * ld * sizeof(double), hipMemcpyDeviceToDevice,
+                                      c->stream));
+        }
         double rk2 = 0.0;
         CAL_TRY(dot_host(c, n, L->col(k), L->col(k), &rk2));
         const double bk = std::sqrt(rk2);

@@ -161,6 +161,32 @@ print(json.dumps(dict(na=bool(p0.info["norm_A"] == p1.info["norm_A"] and p0.info
     assert all(res.values()), res
 
 
+def test_irl_restart_apply_in_place_bitexact():
+    """The implicit restart's [V_k | r] = [V_m | v_{m+1}] M formed in place in
+    Q's first k + 1 columns (one row-parallel apply: every row read whole
+    before it is written) against the work panel and the copy back
+    (CAL_TEST_RESTART_COPY): the same restart count, eigenvalues and Ritz
+    vectors to the bit, on the circuit stand-in and on lap2d(40)."""
+    res = run_testhooks(r"""
+C = cal.matrices.circuit_like(60, seed=3)
+D = cal.matrices.laplacian_2d(40)
+outs = []
+for copy in (False, True):
+    if copy:
+        os.environ["CAL_TEST_RESTART_COPY"] = "1"
+    a = cal.impl_restarted_ca_lanczos(C, ref.matlab_rand(C.shape[0]), 40, 6, 4, "newton", "full", 1e-8)
+    b = cal.impl_restarted_ca_lanczos(D, ref.matlab_rand(D.shape[0]), 48, 8, 8, "newton", "full", 1e-8)
+    outs.append((a, b))
+(a0, b0), (a1, b1) = outs
+print(json.dumps(dict(nr=[int(a0["num_restarts"]), int(a1["num_restarts"]), int(b0["num_restarts"]), int(b1["num_restarts"])],
+                      e=bool(np.array_equal(a0["conv_eigs"], a1["conv_eigs"]) and np.array_equal(b0["conv_eigs"], b1["conv_eigs"])),
+                      q=bool(np.array_equal(a0["Q_conv"], a1["Q_conv"]) and np.array_equal(b0["Q_conv"], b1["Q_conv"])),
+                      conv=bool(a0["converged"] and b0["converged"]))))
+""")
+    assert res["nr"][0] == res["nr"][1] and res["nr"][2] == res["nr"][3], res
+    assert res["e"] and res["q"] and res["conv"], res
+
+
 @pytest.mark.parametrize("fmt", ["auto", "csr"])
 def test_normest_graph_vs_launches_bitexact(fmt):
     """The asynchronous normest's chunks replayed as captured HIP graphs
