@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <vector>
 
 namespace cal {
@@ -737,6 +738,8 @@ bool eig_general(int n, const double* A, int lda, double* wr, double* wi, double
 // rotated column carried in registers: every W entry sees the same
 // operations in the same order as when applied step by step (the same bits),
 // at a fraction of the loads and stores.
+typedef double v2d __attribute__((vector_size(16)));
+
 void hess_qrsteps(int m, double* H, int ldh, double* W, int ldw, const double* mu, int count) {
     if (m < 1 || count < 1) return;
     auto h = [&](int i, int j) -> double& { return H[i + (size_t)j * ldh]; };
@@ -756,10 +759,18 @@ void hess_qrsteps(int m, double* H, int ldh, double* W, int ldw, const double* m
             }
             ct[j] = c;
             st[j] = s;
+            // rows j, j+1 of a column are adjacent: one pair vector per column,
+            // [c x + s y, c y + (-s) x] -- (-s) x = -(s x) and a + (-b) = a - b
+            // exactly, so the same bits as the scalar rotation
+            const v2d cc = {c, c}, ss = {s, -s};
             for (int col = j; col < m; ++col) {
-                const double x = h(j, col), y = h(j + 1, col);
-                h(j, col) = c * x + s * y;
-                h(j + 1, col) = c * y - s * x;
+                double* hp = &h(j, col);
+                v2d v;
+                std::memcpy(&v, hp, sizeof v);
+                const v2d sw = {v[1], v[0]};
+                const v2d a = cc * v, b = ss * sw;
+                const v2d r = a + b;
+                std::memcpy(hp, &r, sizeof r);
             }
             h(j + 1, j) = 0.0;
         }
