@@ -614,6 +614,17 @@ def test_impl_restarted_diagonal(cal, ref):
     assert out["num_restarts"] == 14
 
 
+def test_impl_restarted_many_wanted_copy_path(cal, ref):
+    """14 wanted (k = 18 kept vectors): the restart's [V_k | r] has more than
+    16 outputs, so it is formed in the work panel and copied back (the in-place
+    path takes <= 16, lanczos.cpp); the top 14 diagonal entries and the
+    oracle's eigenvalues."""
+    import scipy.sparse as sp
+    a = ref.matlab_linspace(1.0, 1.0e4, 5000)
+    A = sp.csr_matrix(sp.diags(a))
+    _irl_check(cal, ref, A, np.ones(5000), 64, 14, 4, "newton", a[::-1], 1e-12, same_restarts=False)
+
+
 def test_impl_restarted_truncated_monomial(cal, ref):
     """m = 60 with s = 8 (first pass truncated from 64 vectors), monomial basis."""
     import scipy.sparse as sp
